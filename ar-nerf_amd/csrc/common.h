@@ -1,0 +1,70 @@
+// Shared device helpers for the gfx950 kernels of libngp_amd.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ngp_amd.h"
+
+#define NGP_SQRT3 1.73205080757f
+
+#define NGP_CHECK_ARG(cond)        \
+    do {                           \
+        if (!(cond)) return NGP_EINVAL; \
+    } while (0)
+
+static inline int ngp_launch_status() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? NGP_OK : (int)e;
+}
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+namespace ngp {
+
+// helper_math.h:280-283 clamp(f,a,b) = fmaxf(a, fminf(f,b)) -- keeps the
+// NaN behaviour of fminf/fmaxf that the marcher relies on.
+__device__ __forceinline__ float clampf(float f, float a, float b) { return fmaxf(a, fminf(f, b)); }
+
+// raymarching.cu:11-13
+__device__ __forceinline__ float calc_dt(float t, float esf, int max_samples, int grid_size, float scale) {
+    return clampf(t * esf, NGP_SQRT3 / max_samples, NGP_SQRT3 * 2 * scale / grid_size);
+}
+
+// raymarching.cu:19-23
+__device__ __forceinline__ int mip_from_pos(float x, float y, float z, int cascades) {
+    const float mx = fmaxf(fabsf(x), fmaxf(fabsf(y), fabsf(z)));
+    int exponent;
+    frexpf(mx, &exponent);
+    return min(cascades - 1, max(0, exponent + 1));
+}
+
+// raymarching.cu:29-32
+__device__ __forceinline__ int mip_from_dt(float dt, int grid_size, int cascades) {
+    int exponent;
+    frexpf(dt * grid_size, &exponent);
+    return min(cascades - 1, max(0, exponent));
+}
+
+// raymarching.cu:35-50: 3-D Morton code, x in bit 0 (same magic-number
+// spread as the reference so every int input maps identically).
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t morton3(uint32_t x, uint32_t y, uint32_t z) {
+    return spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
+}
+// inverse of one axis (raymarching.cu:52-60)
+__device__ __forceinline__ uint32_t compact3(uint32_t x) {
+    x &= 0x49249249u;
+    x = (x | (x >> 2)) & 0xc30c30c3u;
+    x = (x | (x >> 4)) & 0x0f00f00fu;
+    x = (x | (x >> 8)) & 0xff0000ffu;
+    x = (x | (x >> 16)) & 0x0000ffffu;
+    return x;
+}
+
+}  // namespace ngp

@@ -1,0 +1,169 @@
+// Volume-rendering compositing (forward, backward, test-time) for gfx950.
+// Replaces models/csrc/volumerendering.cu of the reference.
+//
+// One lane per ray (64-lane workgroups), front-to-back, with the same
+// early-termination rule (T <= T_threshold breaks BEFORE the count
+// increments, volumerendering.cu:40-41).  Unlike the reference, the kernels
+// write every output element themselves (zeros past termination), so the
+// caller never needs a zero-fill, and the backward keeps the running prefix
+// of dL_dws*ws in a register instead of a per-thread thrust scan
+// (volumerendering.cu:118-121) -- same left-to-right fp32 sum.
+#pragma clang fp contract(off)
+
+#include "common.h"
+
+namespace ngp {
+
+__global__ void __launch_bounds__(64) composite_fw_kernel(const float* __restrict__ sigmas,
+                                                          const float* __restrict__ rgbs,
+                                                          const float* __restrict__ deltas,
+                                                          const float* __restrict__ ts,
+                                                          const int64_t* __restrict__ rays_a, int64_t n_rays,
+                                                          float T_thr, int64_t* __restrict__ total_samples,
+                                                          float* __restrict__ opacity, float* __restrict__ depth,
+                                                          float* __restrict__ rgb, float* __restrict__ ws) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_rays) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+    float T = 1.0f, r = 0.f, g = 0.f, b = 0.f, d = 0.f, op = 0.f;
+    int64_t samples = 0;
+    while (samples < N) {
+        const int64_t s = start + samples;
+        const float a = 1.0f - __expf(-sigmas[s] * deltas[s]);
+        const float w = a * T;
+        r += w * rgbs[3 * s]; g += w * rgbs[3 * s + 1]; b += w * rgbs[3 * s + 2];
+        d += w * ts[s];
+        op += w;
+        ws[s] = w;
+        T *= 1.0f - a;
+        if (T <= T_thr) break;
+        samples++;
+    }
+    for (int64_t k = samples + 1; k < N; ++k) ws[start + k] = 0.f;
+    rgb[3 * ray] = r; rgb[3 * ray + 1] = g; rgb[3 * ray + 2] = b;
+    depth[ray] = d;
+    opacity[ray] = op;
+    total_samples[ray] = samples;
+}
+
+__global__ void __launch_bounds__(64) composite_bw_kernel(
+    const float* __restrict__ dL_dop, const float* __restrict__ dL_ddep, const float* __restrict__ dL_drgb,
+    const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ rgbs,
+    const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
+    const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ opacity,
+    const float* __restrict__ depth, const float* __restrict__ rgb, float T_thr, float* __restrict__ dL_dsig,
+    float* __restrict__ dL_drgbs) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_rays) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+    if (N <= 0) return;
+    // total of the inclusive scan of dL_dws*ws (volumerendering.cu:118-122)
+    float S = 0.f;
+    for (int64_t k = 0; k < N; ++k) S += dL_dws[start + k] * ws[start + k];
+    const float R = rgb[3 * ray], G = rgb[3 * ray + 1], B = rgb[3 * ray + 2];
+    const float O = opacity[ray], D = depth[ray];
+    const float gr = dL_drgb[3 * ray], gg = dL_drgb[3 * ray + 1], gb = dL_drgb[3 * ray + 2];
+    const float gop = dL_dop[ray], gdep = dL_ddep[ray];
+    float T = 1.0f, r = 0.f, g = 0.f, b = 0.f, d = 0.f, pre = 0.f;
+    int64_t samples = 0;
+    while (samples < N) {
+        const int64_t s = start + samples;
+        const float a = 1.0f - __expf(-sigmas[s] * deltas[s]);
+        const float w = a * T;
+        r += w * rgbs[3 * s]; g += w * rgbs[3 * s + 1]; b += w * rgbs[3 * s + 2];
+        d += w * ts[s];
+        T *= 1.0f - a;
+        pre += dL_dws[s] * ws[s];
+        dL_drgbs[3 * s] = gr * w;
+        dL_drgbs[3 * s + 1] = gg * w;
+        dL_drgbs[3 * s + 2] = gb * w;
+        dL_dsig[s] = deltas[s] * (gr * (rgbs[3 * s] * T - (R - r)) + gg * (rgbs[3 * s + 1] * T - (G - g)) +
+                                  gb * (rgbs[3 * s + 2] * T - (B - b)) + gop * (1 - O) +
+                                  gdep * (ts[s] * T - (D - d)) + T * dL_dws[s] - (S - pre));
+        if (T <= T_thr) break;
+        samples++;
+    }
+    for (int64_t k = samples + 1; k < N; ++k) {
+        const int64_t s = start + k;
+        dL_dsig[s] = 0.f;
+        dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
+    }
+}
+
+__global__ void __launch_bounds__(64) composite_test_kernel(const float* __restrict__ sigmas,
+                                                            const float* __restrict__ rgbs,
+                                                            const float* __restrict__ deltas,
+                                                            const float* __restrict__ ts, int64_t n_alive, int Ns,
+                                                            int64_t* __restrict__ alive, float T_thr,
+                                                            const int32_t* __restrict__ n_eff,
+                                                            float* __restrict__ opacity, float* __restrict__ depth,
+                                                            float* __restrict__ rgb) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_alive) return;
+    const int ne = n_eff[n];
+    if (ne == 0) { alive[n] = -1; return; }  // volumerendering.cu:221-224
+    const int64_t r = alive[n];
+    float op = opacity[r], d = depth[r], cr = rgb[3 * r], cg = rgb[3 * r + 1], cb = rgb[3 * r + 2];
+    float T = 1 - op;
+    for (int s = 0; s < ne; ++s) {
+        const int64_t o = n * (int64_t)Ns + s;
+        const float a = 1.0f - __expf(-sigmas[o] * deltas[o]);
+        const float w = a * T;
+        cr += w * rgbs[3 * o]; cg += w * rgbs[3 * o + 1]; cb += w * rgbs[3 * o + 2];
+        d += w * ts[o];
+        op += w;
+        T *= 1.0f - a;
+        if (T <= T_thr) { alive[n] = -1; break; }
+    }
+    rgb[3 * r] = cr; rgb[3 * r + 1] = cg; rgb[3 * r + 2] = cb;
+    depth[r] = d;
+    opacity[r] = op;
+}
+
+}  // namespace ngp
+
+using namespace ngp;
+
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+extern "C" {
+
+int ngp_composite_train_fw(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                           const int64_t* rays_a, int64_t n_rays, float T_threshold, int64_t* total_samples,
+                           float* opacity, float* depth, float* rgb, float* ws, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(rays_a && total_samples && opacity && depth && rgb);
+    composite_fw_kernel<<<nblk(n_rays, 64), 64, 0, as_stream(stream)>>>(sigmas, rgbs, deltas, ts, rays_a, n_rays,
+                                                                       T_threshold, total_samples, opacity, depth,
+                                                                       rgb, ws);
+    return ngp_launch_status();
+}
+
+int ngp_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drgb,
+                           const float* dL_dws, const float* sigmas, const float* rgbs, const float* ws,
+                           const float* deltas, const float* ts, const int64_t* rays_a, int64_t n_rays,
+                           const float* opacity, const float* depth, const float* rgb, float T_threshold,
+                           float* dL_dsigmas, float* dL_drgbs, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(dL_dopacity && dL_ddepth && dL_drgb && rays_a && opacity && depth && rgb);
+    composite_bw_kernel<<<nblk(n_rays, 64), 64, 0, as_stream(stream)>>>(
+        dL_dopacity, dL_ddepth, dL_drgb, dL_dws, sigmas, rgbs, ws, deltas, ts, rays_a, n_rays, opacity, depth, rgb,
+        T_threshold, dL_dsigmas, dL_drgbs);
+    return ngp_launch_status();
+}
+
+int ngp_composite_test_fw(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                          int64_t n_alive, int N_samples, int64_t* alive, float T_threshold, const int32_t* n_eff,
+                          float* opacity, float* depth, float* rgb, void* stream) {
+    NGP_CHECK_ARG(n_alive >= 0 && N_samples >= 1);
+    if (n_alive == 0) return NGP_OK;
+    NGP_CHECK_ARG(sigmas && rgbs && deltas && ts && alive && n_eff && opacity && depth && rgb);
+    composite_test_kernel<<<nblk(n_alive, 64), 64, 0, as_stream(stream)>>>(sigmas, rgbs, deltas, ts, n_alive,
+                                                                          N_samples, alive, T_threshold, n_eff,
+                                                                          opacity, depth, rgb);
+    return ngp_launch_status();
+}
+
+}  // extern "C"

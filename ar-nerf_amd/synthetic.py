@@ -1,0 +1,130 @@
+"""Seeded synthetic Lego-shaped workload (BASELINE.md "CPU-baseline plan",
+SURVEY.md §8d): no dataset or checkpoint is reachable, so the benchmark and
+the parity tests run on synthetic cameras, rays and occupancy of the exact
+shapes the reference trains on.
+
+* Camera: W x H pinhole, fx = fy = 0.5*W/tan(0.5*fov) (800 px -> 1111.111),
+  cx = W/2, cy = H/2; directions through pixel centres
+  (datasets/ray_utils.py:24-42, kornia create_meshgrid(H, W, False): u =
+  column, v = row, pixel index = v*W + u).
+* Poses: cameras on the upper hemisphere of radius 1.5 looking at the origin,
+  Blender convention converted to "right down front" like
+  datasets/nerf.py:70-73 (c2w[:, 1:3] *= -1).
+* Occupancy: a thin spherical shell |r - 0.3| < 2/128 plus 2 % random cells,
+  in Morton order, thresholded through packbits.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+
+def intrinsics(W: int, H: int, focal: float | None = None):
+    if focal is None:
+        focal = 0.5 * 800 / math.tan(0.5 * 0.6911112070083618) * (W / 800)  # Lego camera_angle_x
+    return torch.tensor([[focal, 0, W / 2], [0, focal, H / 2], [0, 0, 1]], dtype=torch.float32)
+
+
+def get_ray_directions(H: int, W: int, K: torch.Tensor) -> torch.Tensor:
+    """datasets/ray_utils.py:7-42 (random=False, flatten=True)."""
+    v, u = torch.meshgrid(torch.arange(H, dtype=torch.float32), torch.arange(W, dtype=torch.float32), indexing="ij")
+    fx, fy, cx, cy = K[0, 0], K[1, 1], K[0, 2], K[1, 2]
+    d = torch.stack([(u - cx + 0.5) / fx, (v - cy + 0.5) / fy, torch.ones_like(u)], -1)
+    return d.reshape(-1, 3)
+
+
+def make_poses(n: int = 100, radius: float = 1.5, seed: int = 0) -> torch.Tensor:
+    """(n,3,4) c2w on the upper hemisphere, looking at the origin."""
+    g = np.random.default_rng(seed)
+    poses = []
+    for _ in range(n):
+        theta = g.uniform(0, 2 * np.pi)
+        phi = g.uniform(0.1, 0.45 * np.pi)  # elevation
+        c = radius * np.array([np.cos(phi) * np.cos(theta), np.cos(phi) * np.sin(theta), np.sin(phi)])
+        back = c / np.linalg.norm(c)  # OpenGL camera looks along -z
+        right = np.cross(np.array([0.0, 0.0, 1.0]), back)
+        right /= np.linalg.norm(right)
+        up = np.cross(back, right)
+        c2w = np.stack([right, up, back, c], 1)  # Blender/OpenGL
+        c2w[:, 1:3] *= -1  # datasets/nerf.py:70-73 -> right, down, front
+        poses.append(c2w)
+    return torch.tensor(np.stack(poses), dtype=torch.float32)
+
+
+def morton3(x, y, z):
+    def spread(v):
+        v = v.astype(np.uint64)
+        v = (v * 0x00010001) & 0xFF0000FF
+        v = (v * 0x00000101) & 0x0F00F00F
+        v = (v * 0x00000011) & 0xC30C30C3
+        v = (v * 0x00000005) & 0x49249249
+        return v
+    return (spread(x) | (spread(y) << 1) | (spread(z) << 2)).astype(np.int64)
+
+
+def shell_density_grid(grid_size: int = 128, cascades: int = 1, scale: float = 0.5, radius: float = 0.3,
+                       rand_frac: float = 0.02, seed: int = 2) -> torch.Tensor:
+    """(cascades, G^3) f32 density grid in Morton order: 20 inside a thin
+    shell around the origin plus `rand_frac` random cells, 0 elsewhere."""
+    G = grid_size
+    g = np.random.default_rng(seed)
+    ax = np.arange(G)
+    X, Y, Z = np.meshgrid(ax, ax, ax, indexing="ij")
+    X, Y, Z = X.ravel(), Y.ravel(), Z.ravel()
+    idx = morton3(X, Y, Z)
+    grid = np.zeros((cascades, G ** 3), np.float32)
+    for c in range(cascades):
+        s = min(2.0 ** (c - 1), scale)
+        cx = ((X + 0.5) / G * 2 - 1) * s
+        cy = ((Y + 0.5) / G * 2 - 1) * s
+        cz = ((Z + 0.5) / G * 2 - 1) * s
+        r = np.sqrt(cx * cx + cy * cy + cz * cz)
+        occ = (np.abs(r - radius) < 2.0 / G) | (g.random(G ** 3) < rand_frac)
+        grid[c, idx] = np.where(occ, 20.0, 0.0)
+    return torch.from_numpy(grid)
+
+
+def packbits_cpu(grid: torch.Tensor, thr: float) -> torch.Tensor:
+    b = (grid.reshape(-1, 8) > thr).to(torch.uint8)
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8)
+    return (b * w).sum(1).to(torch.uint8)
+
+
+class SyntheticScene:
+    """Everything the training step needs, on the host."""
+
+    def __init__(self, W=800, H=800, n_images=100, scale=0.5, grid_size=128, seed=0):
+        self.W, self.H, self.scale, self.G = W, H, scale, grid_size
+        self.K = intrinsics(W, H)
+        self.directions = get_ray_directions(H, W, self.K)
+        self.poses = make_poses(n_images, seed=seed)
+        self.cascades = max(1 + int(np.ceil(np.log2(2 * scale))), 1)  # models/networks.py:27
+        self.density_grid = shell_density_grid(grid_size, self.cascades, scale)
+        self.bitfield = packbits_cpu(self.density_grid, 0.5)
+        g = np.random.default_rng(seed + 7)
+        # synthetic ground-truth colour per image/pixel is generated lazily
+        self._rgb_seed = int(g.integers(1 << 30))
+
+    def sample_batch(self, n_rays: int, gen: torch.Generator):
+        """datasets/base.py:25-31: uniform image and pixel indices."""
+        img = torch.randint(0, self.poses.shape[0], (n_rays,), generator=gen)
+        pix = torch.randint(0, self.W * self.H, (n_rays,), generator=gen)
+        return img, pix
+
+    def target_rgb(self, img: torch.Tensor, pix: torch.Tensor) -> torch.Tensor:
+        """Deterministic smooth pseudo-colour per (image, pixel)."""
+        u = (pix % self.W).float() / self.W
+        v = (pix // self.W).float() / self.H
+        t = img.float() / max(1, self.poses.shape[0])
+        return torch.stack([0.5 + 0.5 * torch.sin(6 * u + t), 0.5 + 0.5 * torch.cos(5 * v - t),
+                            0.5 + 0.5 * torch.sin(3 * (u + v))], -1)
+
+    def rays(self, img: torch.Tensor, pix: torch.Tensor):
+        """datasets/ray_utils.py:45-70 (host reference for tests)."""
+        P = self.poses[img]
+        d = self.directions[pix]
+        rays_d = torch.einsum("nc,nac->na", d, P[:, :, :3])
+        rays_o = P[:, :, 3].clone()
+        return rays_o, rays_d

@@ -1,0 +1,133 @@
+/*
+ * ngp_amd.h -- C-ABI of the MI355X-native Instant-NGP hot path
+ * (libngp_amd.so, built from the ar-nerf_amd/csrc .hip sources for gfx950).
+ *
+ * Every entry point takes plain device pointers + sizes and an opaque HIP
+ * stream (`void* stream` = hipStream_t; NULL = the null stream), launches
+ * asynchronously, never allocates or frees caller memory, never
+ * synchronises, and returns 0 on success, a negative NGP_E* code for a bad
+ * argument, or a positive hipError_t from the launch.  The Python layer
+ * (ar-nerf_amd/vren.py) allocates every buffer with the PyTorch caching
+ * allocator, exactly like the reference's `vren` extension allocates its
+ * outputs with torch::zeros.
+ *
+ * Each function names the reference interface it replaces (paths relative
+ * to the YessionCC/AR-NeRF tree).  The pybind module `vren`
+ * (models/csrc/binding.cpp:234-250) is replaced by the ngp_* functions
+ * below; tinycudann's NetworkWithInputEncoding / Encoding / Network
+ * (models/networks.py:37-78) by the ngp_field_* functions.
+ */
+#ifndef NGP_AMD_H
+#define NGP_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NGP_OK 0
+#define NGP_EINVAL (-1)      /* null pointer / non-positive size               */
+#define NGP_ERANGE (-2)      /* a size exceeds what the kernel supports        */
+
+/* Library build tag (gfx950 code object version string). */
+const char* ngp_version(void);
+
+/* ---------------------------------------------------------------- rays */
+/* Replaces vren.ray_aabb_intersect (binding.cpp:9-20 -> intersection.cu:59-100).
+ * rays_o/rays_d (n_rays,3) f32; centers/half_sizes (n_voxels,3) f32.
+ * Out: hit_cnt (n_rays) i32, hits_t (n_rays,max_hits,2) f32 (-1 = no hit),
+ * hits_voxel_idx (n_rays,max_hits) i64 (-1 = no hit); hits sorted by t1
+ * ascending exactly as the reference's torch::sort (misses first). */
+int ngp_ray_aabb_intersect(const float* rays_o, const float* rays_d, int64_t n_rays,
+                           const float* centers, const float* half_sizes, int n_voxels,
+                           int max_hits, int32_t* hit_cnt, float* hits_t, int64_t* hits_voxel_idx,
+                           void* stream);
+
+/* Fused training ray generation (datasets/ray_utils.py:7-70 get_ray_directions
+ * + get_rays, train.py:85-87 gathers) + AABB intersection + near clamp
+ * (models/rendering.py:29-31, NEAR_DISTANCE).  directions (HW,3) f32 camera
+ * space; poses (n_img,3,4) f32 c2w; img_idx/pix_idx (n_rays) i64.
+ * Out: rays_o, rays_d (n_rays,3) f32, hits_t (n_rays,2) f32. */
+int ngp_raygen_aabb(const float* directions, const float* poses, const int64_t* img_idx,
+                    const int64_t* pix_idx, int64_t n_rays, const float* center,
+                    const float* half_size, float near_distance, float* rays_o, float* rays_d,
+                    float* hits_t, void* stream);
+
+/* ------------------------------------------------- occupancy grid utils */
+/* Replaces vren.morton3D (binding.cpp:36-40 -> raymarching.cu:62-88). */
+int ngp_morton3d(const int32_t* coords, int64_t n, int32_t* indices, void* stream);
+/* Replaces vren.morton3D_invert (binding.cpp:43-47 -> raymarching.cu:90-119). */
+int ngp_morton3d_invert(const int32_t* indices, int64_t n, int32_t* coords, void* stream);
+/* Replaces vren.packbits (binding.cpp:26-33 -> raymarching.cu:122-161):
+ * bit i of byte n = (grid[8n+i] > threshold).  If threshold_dev != NULL the
+ * threshold is read from device memory (no host sync; see
+ * ngp_density_grid_ema) and `threshold` is ignored. */
+int ngp_packbits(const float* density_grid, int64_t n_bytes, float threshold,
+                 const float* threshold_dev, uint8_t* bitfield, void* stream);
+
+/* ------------------------------------------------------- ray marching */
+/* Replaces vren.raymarching_train (binding.cpp:50-67 -> raymarching.cu:166-332),
+ * split into count + write so that the layout is deterministic and exact-size.
+ * Pass 1: counts (n_rays) i32, rays_a (n_rays,3) i64 in RAY order
+ * (row r = [r, start_r, n_r], start = exclusive prefix sum), total (1) i64.
+ * hits_t is (n_rays,2) f32 (= the reference's hits_t[:,0]); noise (n_rays) f32
+ * in [0,1) perturbs the first sample (custom_functions.py:83). */
+int ngp_march_train_count(const float* rays_o, const float* rays_d, const float* hits_t,
+                          int64_t n_rays, const uint8_t* bitfield, int cascades, int grid_size,
+                          float scale, float exp_step_factor, const float* noise, int max_samples,
+                          int32_t* counts, int64_t* rays_a, int64_t* total, void* stream);
+/* Pass 2: writes xyzs, dirs (N,3), deltas, ts (N) f32 at rays_a starts. */
+int ngp_march_train_write(const float* rays_o, const float* rays_d, const float* hits_t,
+                          int64_t n_rays, const uint8_t* bitfield, int cascades, int grid_size,
+                          float scale, float exp_step_factor, const float* noise, int max_samples,
+                          const int64_t* rays_a, float* xyzs, float* dirs, float* deltas,
+                          float* ts, void* stream);
+
+/* Replaces vren.raymarching_test (binding.cpp:70-88 -> raymarching.cu:335-454).
+ * hits_t (n_rays_total,2) updated in place; alive (n_alive) i64.  Out:
+ * xyzs, dirs (n_alive,N_samples,3), deltas, ts (n_alive,N_samples) -- slots
+ * past the last sample are written 0 like the reference's torch::zeros --
+ * n_eff (n_alive) i32.  Keeps the reference quirk: calc_dt gets `cascades`
+ * as its scale (raymarching.cu:370,399). */
+int ngp_march_test(const float* rays_o, const float* rays_d, float* hits_t, const int64_t* alive,
+                   int64_t n_alive, const uint8_t* bitfield, int cascades, int grid_size,
+                   float scale, float exp_step_factor, int N_samples, int max_samples,
+                   float* xyzs, float* dirs, float* deltas, float* ts, int32_t* n_eff,
+                   void* stream);
+
+/* -------------------------------------------------------- compositing */
+/* Replaces vren.composite_train_fw (binding.cpp:91-101 -> volumerendering.cu:5-83).
+ * rays_a (n_rays,3) i64 (any row order); every output element is written
+ * (ws = 0 past early termination).  total_samples (n_rays) i64 per ray. */
+int ngp_composite_train_fw(const float* sigmas, const float* rgbs, const float* deltas,
+                           const float* ts, const int64_t* rays_a, int64_t n_rays, float T_threshold,
+                           int64_t* total_samples, float* opacity, float* depth, float* rgb,
+                           float* ws, void* stream);
+/* Replaces vren.composite_train_bw (binding.cpp:104-127 -> volumerendering.cu:86-201). */
+int ngp_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drgb,
+                           const float* dL_dws, const float* sigmas, const float* rgbs,
+                           const float* ws, const float* deltas, const float* ts,
+                           const int64_t* rays_a, int64_t n_rays, const float* opacity,
+                           const float* depth, const float* rgb, float T_threshold,
+                           float* dL_dsigmas, float* dL_drgbs, void* stream);
+/* Replaces vren.composite_test_fw (binding.cpp:130-151 -> volumerendering.cu:204-284).
+ * sigmas/deltas/ts (n_alive,N_samples), rgbs (n_alive,N_samples,3); alive,
+ * opacity, depth, rgb updated in place. */
+int ngp_composite_test_fw(const float* sigmas, const float* rgbs, const float* deltas,
+                          const float* ts, int64_t n_alive, int N_samples, int64_t* alive,
+                          float T_threshold, const int32_t* n_eff, float* opacity, float* depth,
+                          float* rgb, void* stream);
+
+/* --------------------------------------------- hash grid + fused MLPs */
+/* Level table of tcnn's Grid/Hash encoding as configured at
+ * models/networks.py:33-49 (host function; fp32 arithmetic like tcnn).
+ * Fills scales/res/sizes (L) and offsets (L+1); returns total entries. */
+uint32_t ngp_hashgrid_levels(int n_levels, int log2_hashmap_size, int base_resolution,
+                             float per_level_scale, float* scales, uint32_t* res,
+                             uint32_t* offsets, uint32_t* sizes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NGP_AMD_H */

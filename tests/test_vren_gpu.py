@@ -1,0 +1,169 @@
+"""GPU parity: libngp_amd.so (through the reference-shaped `vren`) vs the CPU
+oracle on the same seeded inputs.  Integer outputs (Morton codes, bitfields,
+per-ray sample counts, rays_a) and the marcher's fp32 sample positions are
+compared BIT-EXACTLY (both sides evaluate the reference's expressions with
+no FMA contraction); compositing within 1e-5 abs/rel (the reference itself
+uses __expf)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import synthetic as S
+import vren
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _scene_rays(n_rays, scale=0.5, seed=1, W=800):
+    sc = S.SyntheticScene(W=W, H=W, n_images=20, scale=scale)
+    gen = torch.Generator().manual_seed(seed)
+    img, pix = sc.sample_batch(n_rays, gen)
+    o, d = sc.rays(img, pix)
+    return sc, o.contiguous(), d.contiguous(), img, pix
+
+
+def _hits(o, d, scale):
+    c = torch.zeros(1, 3); h = torch.ones(1, 3) * scale
+    _, ht, _ = O.ray_aabb_intersect(o, d, c, h, 1)
+    ht = ht.clone()
+    m = (ht[:, 0, 0] >= 0) & (ht[:, 0, 0] < 0.01)
+    ht[m, 0, 0] = 0.01
+    return ht[:, 0].contiguous()
+
+
+def test_library_loads_on_gpu():
+    assert torch.cuda.is_available()
+    assert vren.lib().ngp_version().startswith(b"ngp_amd")
+
+
+@pytest.mark.parametrize("max_hits,nv", [(1, 1), (3, 4)])
+def test_ray_aabb_intersect(max_hits, nv):
+    g = torch.Generator().manual_seed(0)
+    o = (torch.rand(2000, 3, generator=g) - 0.5) * 4
+    d = torch.randn(2000, 3, generator=g)
+    d[:10, 0] = 0.0  # axis-parallel rays: inf/NaN slab handling
+    c = (torch.rand(nv, 3, generator=g) - 0.5)
+    h = torch.rand(nv, 3, generator=g) * 0.5 + 0.1
+    ref = O.ray_aabb_intersect(o, d, c, h, max_hits)
+    out = vren.ray_aabb_intersect(o.to(DEV), d.to(DEV), c.to(DEV), h.to(DEV), max_hits)
+    assert torch.equal(out[0].cpu(), ref[0])
+    assert torch.equal(out[1].cpu(), ref[1])
+    assert torch.equal(out[2].cpu(), ref[2])
+
+
+def test_raygen_aabb_matches_host_rays():
+    sc, o, d, img, pix = _scene_rays(8192)
+    center = torch.zeros(1, 3, device=DEV); half = torch.ones(1, 3, device=DEV) * 0.5
+    ro, rd, ht = vren.raygen_aabb(sc.directions.to(DEV), sc.poses.to(DEV), img.to(DEV), pix.to(DEV), center, half,
+                                  0.01)
+    assert torch.allclose(ro.cpu(), o, atol=0, rtol=0)
+    assert torch.allclose(rd.cpu(), d, atol=1e-6, rtol=1e-6)
+    ref = _hits(ro.cpu(), rd.cpu(), 0.5)  # same rays -> bit-exact AABB + clamp
+    assert torch.equal(ht.cpu(), ref)
+
+
+def test_morton_packbits():
+    g = torch.Generator().manual_seed(3)
+    coords = torch.randint(0, 128, (100000, 3), generator=g, dtype=torch.int32)
+    m = vren.morton3D(coords.to(DEV))
+    assert torch.equal(m.cpu(), O.morton3D(coords))
+    assert torch.equal(vren.morton3D_invert(m).cpu(), coords)
+    grid = torch.rand(6 * 128 ** 3 // 64 * 64, generator=g)
+    bf = torch.zeros(grid.numel() // 8, dtype=torch.uint8, device=DEV)
+    vren.packbits(grid.to(DEV), 0.7, bf)
+    ref = torch.zeros(grid.numel() // 8, dtype=torch.uint8)
+    O.packbits(grid, 0.7, ref)
+    assert torch.equal(bf.cpu(), ref)
+    thr = torch.tensor([0.3], device=DEV)
+    vren.packbits(grid.to(DEV), thr, bf)  # device-side threshold
+    O.packbits(grid, 0.3, ref)
+    assert torch.equal(bf.cpu(), ref)
+
+
+@pytest.mark.parametrize("scale,esf,n_rays,max_samples", [(0.5, 0.0, 8192, 1024), (16.0, 1 / 256, 4096, 1024),
+                                                         (0.5, 0.0, 3000, 7)])
+def test_march_train_bit_exact(scale, esf, n_rays, max_samples):
+    sc, o, d, _, _ = _scene_rays(n_rays, scale=scale, W=400)
+    ht = _hits(o, d, scale)
+    noise = torch.rand(n_rays, generator=torch.Generator().manual_seed(3))
+    bf = sc.bitfield
+    ref = O.raymarching_train(o, d, ht, bf, sc.cascades, scale, esf, noise, 128, max_samples)
+    out = vren.raymarching_train(o.to(DEV), d.to(DEV), ht.to(DEV), bf.to(DEV), sc.cascades, scale, esf,
+                                 noise.to(DEV), 128, max_samples)
+    assert int(out[5][0]) == int(ref[5][0]) and int(out[5][1]) == n_rays
+    assert int(ref[5][0]) > (n_rays if max_samples > 100 else n_rays // 10)  # the shell is actually hit
+    for a, b in zip(out[:5], ref[:5]):
+        assert torch.equal(a.cpu(), b)
+
+
+def test_march_train_empty_and_misses():
+    o = torch.tensor([[5.0, 5.0, 5.0]]); d = torch.tensor([[1.0, 0.0, 0.0]])
+    ht = torch.tensor([[-1.0, -1.0]])
+    bf = torch.full((128 ** 3 // 8,), 255, dtype=torch.uint8)
+    out = vren.raymarching_train(o.to(DEV), d.to(DEV), ht.to(DEV), bf.to(DEV), 1, 0.5, 0.0,
+                                 torch.zeros(1, device=DEV), 128, 1024)
+    assert int(out[5][0]) == 0 and out[1].shape == (0, 3)
+    assert out[0].cpu().tolist() == [[0, 0, 0]]
+
+
+def test_composite_train_fw_bw():
+    sc, o, d, _, _ = _scene_rays(4096, W=400)
+    ht = _hits(o, d, 0.5)
+    noise = torch.rand(4096, generator=torch.Generator().manual_seed(4))
+    rays_a, xyzs, dirs, deltas, ts, cnt = O.raymarching_train(o, d, ht, sc.bitfield, 1, 0.5, 0.0, noise, 128, 1024)
+    N = xyzs.shape[0]
+    g = torch.Generator().manual_seed(5)
+    sig = torch.rand(N, generator=g) * 200
+    rgbs = torch.rand(N, 3, generator=g)
+    ref = O.composite_train_fw(sig, rgbs, deltas, ts, rays_a, 1e-4)
+    D = lambda x: x.to(DEV)
+    out = vren.composite_train_fw(D(sig), D(rgbs), D(deltas), D(ts), D(rays_a), 1e-4)
+    assert (out[0].cpu() - ref[0]).abs().max() <= 1  # borderline T<=thr may flip one sample
+    assert (out[0].cpu() != ref[0]).float().mean() < 1e-3
+    for a, b in zip(out[1:], ref[1:]):
+        torch.testing.assert_close(a.cpu(), b, atol=1e-5, rtol=1e-4)
+    gop, gdep, grgb, gws = torch.randn(4096, generator=g), torch.randn(4096, generator=g), \
+        torch.randn(4096, 3, generator=g), torch.randn(N, generator=g)
+    refb = O.composite_train_bw(gop, gdep, grgb, gws, sig, rgbs, ref[4], deltas, ts, rays_a, ref[1], ref[2], ref[3],
+                                1e-4)
+    outb = vren.composite_train_bw(D(gop), D(gdep), D(grgb), D(gws), D(sig), D(rgbs), D(ref[4]), D(deltas), D(ts),
+                                   D(rays_a), D(ref[1]), D(ref[2]), D(ref[3]), 1e-4)
+    torch.testing.assert_close(outb[0].cpu(), refb[0], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(outb[1].cpu(), refb[1], atol=1e-5, rtol=1e-4)
+
+
+def test_march_test_and_composite_test():
+    sc, o, d, _, _ = _scene_rays(5000, W=400)
+    ht = _hits(o, d, 0.5)
+    alive = torch.arange(5000, dtype=torch.int64)[::2].contiguous()
+    ht_ref = ht.clone()
+    ref = O.raymarching_test(o, d, ht_ref, alive, sc.bitfield, 1, 0.5, 0.0, 128, 1024, 8)
+    ht_gpu = ht.to(DEV)
+    out = vren.raymarching_test(o.to(DEV), d.to(DEV), ht_gpu, alive.to(DEV), sc.bitfield.to(DEV), 1, 0.5, 0.0, 128,
+                                1024, 8)
+    for a, b in zip(out, ref):
+        assert torch.equal(a.cpu(), b)
+    assert torch.equal(ht_gpu.cpu(), ht_ref)
+    n = alive.numel()
+    g = torch.Generator().manual_seed(6)
+    sig = torch.rand(n, 8, generator=g) * 100; rgbs = torch.rand(n, 8, 3, generator=g)
+    op = torch.rand(5000, generator=g) * 0.5; dep = torch.zeros(5000); rgb = torch.zeros(5000, 3)
+    al_ref = alive.clone(); op_ref, dep_ref, rgb_ref = op.clone(), dep.clone(), rgb.clone()
+    O.composite_test_fw(sig, rgbs, ref[2], ref[3], ht_ref, al_ref, 1e-4, ref[4], op_ref, dep_ref, rgb_ref)
+    al_g, op_g, dep_g, rgb_g = alive.to(DEV), op.to(DEV), dep.to(DEV), rgb.to(DEV)
+    vren.composite_test_fw(sig.to(DEV), rgbs.to(DEV), out[2], out[3], ht_gpu, al_g, 1e-4, out[4], op_g, dep_g, rgb_g)
+    assert (al_g.cpu() != al_ref).sum() <= 2
+    torch.testing.assert_close(op_g.cpu(), op_ref, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rgb_g.cpu(), rgb_ref, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(dep_g.cpu(), dep_ref, atol=1e-5, rtol=1e-5)
+
+
+def test_check_input_errors_like_reference():
+    x = torch.zeros(4, 3)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        vren.morton3D(x.int())
+    y = torch.zeros(4, 6, dtype=torch.int32, device=DEV)[:, ::2]
+    with pytest.raises(RuntimeError, match="must be contiguous"):
+        vren.morton3D(y)
