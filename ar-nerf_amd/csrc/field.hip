@@ -1,0 +1,661 @@
+// Fused multires hash-grid encoding + tiny MLPs (density 32-64-16, colour
+// 32-64-64-16) on gfx950 MFMA.  Replaces tiny-cuda-nn's
+// NetworkWithInputEncoding / Encoding(SH4) / Network as the reference uses
+// them (models/networks.py:37-78, 95-146).
+//
+// Work decomposition (one 64-lane wave = one 16-sample column block):
+//   lane l -> sample s = l & 15 of the block, lane group g = l >> 4.
+//   Lane (s, g) gathers hash levels 4g..4g+3 of sample s (32 independent
+//   4-byte gathers of fp16x2 table entries), which lands the 8 encoding
+//   values enc[s][8g..8g+7] directly in the B-operand layout of
+//   v_mfma_f32_16x16x32_f16 (B[k = 8g + j][n = s]).  Every layer is computed
+//   transposed, Y^T = W X^T (M = output units, N = samples), so each MFMA's
+//   accumulator (rows 4g + r, column s) is re-packed in registers into the
+//   next layer's B operand; the K order of that operand is permuted and the
+//   weight columns are stored in LDS with the same permutation (P64/P32).
+//   Weights (10240 fp16) live in LDS for the whole persistent wave loop.
+// Numerics (tcnn storage points): fp16 params, fp32 interpolation weights
+// and feature accumulation (fmaf over corners in tcnn order), fp16 encoding,
+// fp32 MFMA accumulation, fp16 layer outputs, fp32 TruncExp / sigmoid.
+#pragma clang fp contract(off)
+
+#include "common.h"
+
+namespace ngp {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int L = 16;  // levels (x2 features = the 32-wide MLP input)
+// fp16 MLP buffer offsets (halfs), matrices row-major [out][in]
+constexpr int OW1 = 0, OW2 = 2048, OW3 = 3072, OW4 = 5120, OW5 = 9216;
+// LDS image of the forward weights (halfs): rows padded to 40 / 72 halfs
+constexpr int R32 = 40, R64 = 72;
+constexpr int SW1 = 0, SW2 = SW1 + 64 * R32, SW3 = SW2 + 16 * R64, SW4 = SW3 + 64 * R32, SW5 = SW4 + 64 * R64,
+              SWF = SW5 + 16 * R64;
+
+// K permutations matching the register re-pack of accumulator tiles:
+// step q, lane group g, element j <- hidden unit 32q + (j<4 ? 4g+j : 16+4g+j-4)
+__device__ __forceinline__ int P64(int kp) {
+    const int q = kp >> 5, g = (kp >> 3) & 3, j = kp & 7;
+    return 32 * q + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));
+}
+// colour-net input c = [SH(16), h(16)]: element j <- j<4 ? SH[4g+j] : h[4g+j-4]
+__device__ __forceinline__ int P32(int kp) {
+    const int g = kp >> 3, j = kp & 7;
+    return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4);
+}
+
+__device__ __forceinline__ f4 mfma32(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+
+struct GridArgs {
+    ngp_hashgrid_t g;
+    uint32_t dense_mask;  // bit l: level l indexes densely (res^3 <= size)
+    uint32_t pow2_mask;   // bit l: size_l is a power of two
+};
+
+struct LevelLds {
+    float scale[L];
+    uint32_t res[L], off[L], size[L];
+    uint32_t dense, pow2;
+};
+
+__device__ __forceinline__ void load_levels(const GridArgs& ga, LevelLds& lv) {
+    const int t = threadIdx.x;
+    if (t < L) {
+        lv.scale[t] = ga.g.scales[t];
+        lv.res[t] = ga.g.res[t];
+        lv.off[t] = ga.g.offsets[t];
+        lv.size[t] = ga.g.sizes[t];
+    }
+    if (t == 0) { lv.dense = ga.dense_mask; lv.pow2 = ga.pow2_mask; }
+}
+
+// tcnn grid_index for one corner (see oracle or_* restatement).
+__device__ __forceinline__ uint32_t corner_index(uint32_t px, uint32_t py, uint32_t pz, uint32_t res, uint32_t size,
+                                                 bool dense, bool pow2) {
+    uint32_t idx = dense ? (px + py * res + pz * (res * res)) : ((px * 1u) ^ (py * 2654435761u) ^ (pz * 805459861u));
+    if (pow2) idx &= size - 1u;
+    else if (idx >= size) idx %= size;
+    return idx;
+}
+
+// Hash-encode levels 4g..4g+3 of one sample -> 8 fp16 values (enc[8g..8g+7]).
+__device__ __forceinline__ h8 encode4(const float in[3], int g, const LevelLds& lv, const uint32_t* __restrict__ table) {
+    h8 e;
+#pragma unroll
+    for (int jl = 0; jl < 4; ++jl) {
+        const int l = 4 * g + jl;
+        const float sc = lv.scale[l];
+        const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
+        const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
+        float pos[3];
+        uint32_t pg[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float p = fmaf(sc, in[d], 0.5f);
+            const float fl = floorf(p);
+            pg[d] = (uint32_t)(int)fl;
+            pos[d] = p - fl;
+        }
+        uint32_t v[8];
+        float w[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            float wt = 1.0f;
+            uint32_t q[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                if (c & (1 << d)) { wt *= pos[d]; q[d] = pg[d] + 1; }
+                else { wt *= 1 - pos[d]; q[d] = pg[d]; }
+            }
+            w[c] = wt;
+            v[c] = table[off + corner_index(q[0], q[1], q[2], res, size, dense, pow2)];
+        }
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const _Float16 f0 = __builtin_bit_cast(_Float16, (uint16_t)(v[c] & 0xffffu));
+            const _Float16 f1 = __builtin_bit_cast(_Float16, (uint16_t)(v[c] >> 16));
+            a0 = fmaf(w[c], (float)f0, a0);
+            a1 = fmaf(w[c], (float)f1, a1);
+        }
+        e[2 * jl] = (_Float16)a0;
+        e[2 * jl + 1] = (_Float16)a1;
+    }
+    return e;
+}
+
+__device__ __forceinline__ void load_x01(const float* __restrict__ xyzs, int64_t i, bool valid, const GridArgs& ga,
+                                         float in[3]) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float x = valid ? xyzs[3 * i + d] : 0.0f;
+        // models/networks.py:104
+        in[d] = (x - ga.g.xyz_min[d]) / (ga.g.xyz_max[d] - ga.g.xyz_min[d]);
+    }
+}
+
+// tcnn SphericalHarmonics degree 4 of (d/|d|+1)/2 (models/networks.py:144-145),
+// returning the 4 values SH[4g..4g+3] this lane group needs.
+__device__ __forceinline__ void sh4_select(float dx, float dy, float dz, int g, float out[4]) {
+    const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float x = ((dx / nrm + 1) / 2) * 2.f - 1.f;
+    const float y = ((dy / nrm + 1) / 2) * 2.f - 1.f;
+    const float z = ((dz / nrm + 1) / 2) * 2.f - 1.f;
+    const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+    float o[16];
+    o[0] = 0.28209479177387814f;
+    o[1] = -0.48860251190291987f * y;
+    o[2] = 0.48860251190291987f * z;
+    o[3] = -0.48860251190291987f * x;
+    o[4] = 1.0925484305920792f * xy;
+    o[5] = -1.0925484305920792f * yz;
+    o[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+    o[7] = -1.0925484305920792f * xz;
+    o[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+    o[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+    o[10] = 2.8906114426405538f * xy * z;
+    o[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+    o[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+    o[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+    o[14] = 1.4453057213202769f * z * (x2 - y2);
+    o[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        out[r] = g == 0 ? o[r] : g == 1 ? o[4 + r] : g == 2 ? o[8 + r] : o[12 + r];
+}
+
+__device__ __forceinline__ h8 pack(h4 a, h4 b) { return h8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
+__device__ __forceinline__ h4 relu_h(f4 c) {
+    return h4{(_Float16)fmaxf(c[0], 0.f), (_Float16)fmaxf(c[1], 0.f), (_Float16)fmaxf(c[2], 0.f),
+              (_Float16)fmaxf(c[3], 0.f)};
+}
+__device__ __forceinline__ h4 to_h(f4 c) { return h4{(_Float16)c[0], (_Float16)c[1], (_Float16)c[2], (_Float16)c[3]}; }
+__device__ __forceinline__ h8 lds8(const _Float16* p) { return *reinterpret_cast<const h8*>(p); }
+
+// Load the forward weight image (permuted columns, padded rows) into LDS.
+__device__ __forceinline__ void load_fwd_weights(const _Float16* __restrict__ mlp, _Float16* sw, bool color) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    for (int i = t; i < 64 * 32; i += nt) sw[SW1 + (i >> 5) * R32 + (i & 31)] = mlp[OW1 + i];
+    for (int i = t; i < 16 * 64; i += nt) sw[SW2 + (i >> 6) * R64 + (i & 63)] = mlp[OW2 + (i >> 6) * 64 + P64(i & 63)];
+    if (!color) return;
+    for (int i = t; i < 64 * 32; i += nt) sw[SW3 + (i >> 5) * R32 + (i & 31)] = mlp[OW3 + (i >> 5) * 32 + P32(i & 31)];
+    for (int i = t; i < 64 * 64; i += nt) sw[SW4 + (i >> 6) * R64 + (i & 63)] = mlp[OW4 + (i >> 6) * 64 + P64(i & 63)];
+    for (int i = t; i < 16 * 64; i += nt) sw[SW5 + (i >> 6) * R64 + (i & 63)] = mlp[OW5 + (i >> 6) * 64 + P64(i & 63)];
+}
+
+// Density net on one column block: returns h (rows 4g+r of sample s) and
+// the four relu'd hidden tiles.
+__device__ __forceinline__ h4 density_net(h8 e, const _Float16* sw, int s, int g, h4 h1[4]) {
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) h1[t] = relu_h(mfma32(lds8(sw + SW1 + (16 * t + s) * R32 + 8 * g), e, z));
+    f4 c = z;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) c = mfma32(lds8(sw + SW2 + s * R64 + 32 * q + 8 * g), pack(h1[2 * q], h1[2 * q + 1]), c);
+    return to_h(c);
+}
+
+__device__ __forceinline__ h4 color_net(h8 cin, const _Float16* sw, int s, int g, h4 h3[4], h4 h4v[4]) {
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) h3[t] = relu_h(mfma32(lds8(sw + SW3 + (16 * t + s) * R32 + 8 * g), cin, z));
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        f4 c = z;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+            c = mfma32(lds8(sw + SW4 + (16 * t + s) * R64 + 32 * q + 8 * g), pack(h3[2 * q], h3[2 * q + 1]), c);
+        h4v[t] = relu_h(c);
+    }
+    f4 c = z;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) c = mfma32(lds8(sw + SW5 + s * R64 + 32 * q + 8 * g), pack(h4v[2 * q], h4v[2 * q + 1]), c);
+    return to_h(c);
+}
+
+__device__ __forceinline__ float sigmoid_h(_Float16 o) {
+    return (float)(_Float16)(1.0f / (1.0f + expf(-(float)o)));
+}
+
+template <bool COLOR>
+__global__ void __launch_bounds__(256) field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
+                                                        int64_t n, const int64_t* __restrict__ n_dev, GridArgs ga,
+                                                        const uint32_t* __restrict__ table,
+                                                        const _Float16* __restrict__ mlp, float* __restrict__ sigmas,
+                                                        float* __restrict__ rgbs, _Float16* __restrict__ enc_out,
+                                                        _Float16* __restrict__ h_out) {
+    __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
+    __shared__ LevelLds lv;
+    load_fwd_weights(mlp, sw, COLOR);
+    load_levels(ga, lv);
+    __syncthreads();
+    const int64_t N = n_dev ? *n_dev : n;
+    const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16; base < N; base += nw * 16) {
+        const int64_t i = base + s;
+        const bool valid = i < N;
+        float in[3];
+        load_x01(xyzs, i, valid, ga, in);
+        const h8 e = encode4(in, g, lv, table);
+        h4 h1[4];
+        const h4 hh = density_net(e, sw, s, g, h1);
+        if (valid) {
+            if (enc_out) *reinterpret_cast<h8*>(enc_out + i * 32 + 8 * g) = e;
+            if (h_out) *reinterpret_cast<h4*>(h_out + i * 16 + 4 * g) = hh;
+            if (g == 0) sigmas[i] = expf((float)hh[0]);  // TruncExp forward (custom_functions.py:165-167)
+        }
+        if constexpr (COLOR) {
+            const float dx = valid ? dirs[3 * i] : 0.f, dy = valid ? dirs[3 * i + 1] : 0.f,
+                        dz = valid ? dirs[3 * i + 2] : 1.f;
+            float sh[4];
+            sh4_select(dx, dy, dz, g, sh);
+            const h8 cin = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3], hh[0], hh[1], hh[2], hh[3]};
+            h4 h3[4], h4v[4];
+            const h4 o = color_net(cin, sw, s, g, h3, h4v);
+            if (valid && g == 0) {
+                rgbs[3 * i] = sigmoid_h(o[0]);
+                rgbs[3 * i + 1] = sigmoid_h(o[1]);
+                rgbs[3 * i + 2] = sigmoid_h(o[2]);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ backward
+// Kernel A: MLP backward.  Recomputes the forward from the saved encoding
+// (MFMA, cheap), back-propagates with v_mfma_f32_16x16x16_f16 (whose B
+// operand layout B[k = 4g + j][n = s] IS the accumulator layout, so every
+// gradient tile chains in registers), writes dL/denc (n,32) f32, and sums
+// the weight gradients dW = sum_s G[o][s] H[i][s] in 40 register tiles over
+// the persistent wave loop (operands transposed through a per-wave LDS
+// scratch).  Gradient operands are scaled per stage by a power of two chosen
+// from the wave's max |g| before the fp16 cast and unscaled exactly in fp32
+// (tcnn's role of a loss scale, without a global scale to tune).
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f4 mfma16(h4 a, h4 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ h4 lds4(const _Float16* p) { return *reinterpret_cast<const h4*>(p); }
+
+constexpr int RT16 = 20, RT64 = 68;  // transposed-weight rows: 16 / 64 halfs + pad
+constexpr int BT5 = SWF, BT4 = BT5 + 64 * RT16, BT3 = BT4 + 64 * RT64, BT2 = BT3 + 16 * RT64, BT1 = BT2 + 64 * RT16,
+              BTE = BT1 + 32 * RT64;
+constexpr int TROW = 20, TTILE = 16 * TROW, NT = 30;  // per-wave transpose scratch: 30 tiles [16][20]
+constexpr int SCR = (BTE + 7) & ~7, SCRW = NT * TTILE, BWD_LDS_HALFS = SCR + 4 * SCRW;
+// scratch tile ids
+constexpr int T_DO = 0, T_DA4 = 1, T_DA3 = 5, T_DH = 9, T_DA1 = 10, T_H4 = 14, T_H3 = 18, T_C = 22, T_H1 = 24, T_E = 28;
+constexpr int NACC = 40;
+
+__device__ __forceinline__ void load_bwd_weights(const _Float16* __restrict__ mlp, _Float16* sw) {
+    const int t = threadIdx.x, nt = blockDim.x;
+    // W5T[i][o] = W5[o][i] (64 x 16); W4T (64 x 64); W3hT[i][o] = W3[o][16+i] (16 x 64);
+    // W2T[i][o] = W2[o][i] (64 x 16); W1T[i][o] = W1[o][i] (32 x 64)
+    for (int e = t; e < 64 * 16; e += nt) { const int i = e >> 4, o = e & 15; sw[BT5 + i * RT16 + o] = mlp[OW5 + o * 64 + i]; }
+    for (int e = t; e < 64 * 64; e += nt) { const int i = e >> 6, o = e & 63; sw[BT4 + i * RT64 + o] = mlp[OW4 + o * 64 + i]; }
+    for (int e = t; e < 16 * 64; e += nt) { const int i = e >> 6, o = e & 63; sw[BT3 + i * RT64 + o] = mlp[OW3 + o * 32 + 16 + i]; }
+    for (int e = t; e < 64 * 16; e += nt) { const int i = e >> 4, o = e & 15; sw[BT2 + i * RT16 + o] = mlp[OW2 + o * 64 + i]; }
+    for (int e = t; e < 32 * 64; e += nt) { const int i = e >> 6, o = e & 63; sw[BT1 + i * RT64 + o] = mlp[OW1 + o * 32 + i]; }
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float max4(f4 v) { return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))); }
+// power of two s.t. maxabs * s < 2^14 (fp16-safe, full mantissa for the max)
+__device__ __forceinline__ float pow2_scale(float maxabs) {
+    int e;
+    frexpf(maxabs, &e);
+    e = min(max(14 - e, -100), 100);
+    return ldexpf(1.0f, e);
+}
+__device__ __forceinline__ h4 scaled_h(f4 v, float sc) {
+    return h4{(_Float16)(v[0] * sc), (_Float16)(v[1] * sc), (_Float16)(v[2] * sc), (_Float16)(v[3] * sc)};
+}
+__device__ __forceinline__ f4 mask_relu(f4 g, h4 act) {
+    return f4{act[0] > (_Float16)0 ? g[0] : 0.f, act[1] > (_Float16)0 ? g[1] : 0.f, act[2] > (_Float16)0 ? g[2] : 0.f,
+              act[3] > (_Float16)0 ? g[3] : 0.f};
+}
+__device__ __forceinline__ void put_tile(_Float16* T, h4 v, int s, int g) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) T[(4 * g + r) * TROW + s] = v[r];
+}
+__device__ __forceinline__ h4 get_tile(const _Float16* T, int s, int g) { return lds4(T + s * TROW + 4 * g); }
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+}
+
+// accumulator tile k -> (matrix offset, in_dim, o0, i0)
+__device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& o0, int& i0) {
+    if (k < 4) { ow = OW5; in_dim = 64; o0 = 0; i0 = 16 * k; return; }
+    k -= 4;
+    if (k < 16) { ow = OW4; in_dim = 64; o0 = 16 * (k >> 2); i0 = 16 * (k & 3); return; }
+    k -= 16;
+    if (k < 8) { ow = OW3; in_dim = 32; o0 = 16 * (k >> 1); i0 = 16 * (k & 1); return; }
+    k -= 8;
+    if (k < 4) { ow = OW2; in_dim = 64; o0 = 0; i0 = 16 * k; return; }
+    k -= 4;
+    ow = OW1; in_dim = 32; o0 = 16 * (k >> 1); i0 = 16 * (k & 1);
+}
+
+__global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
+    const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const _Float16* __restrict__ enc,
+    const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
+    float* __restrict__ denc, float* __restrict__ grad_mlp) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+    _Float16* sw = smem;
+    load_fwd_weights(mlp, sw, true);
+    load_bwd_weights(mlp, sw);
+    __syncthreads();
+    const int64_t N = n_dev ? *n_dev : n;
+    const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
+    _Float16* scr = smem + SCR + wid * SCRW;
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    f4 acc[NACC];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) acc[k] = z;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wid) * 16; base < N; base += nw * 16) {
+        const int64_t i = base + s;
+        const bool valid = i < N;
+        h8 e = {0, 0, 0, 0, 0, 0, 0, 0};
+        float dx = 0.f, dy = 0.f, dz = 1.f, dsig = 0.f, gr[3] = {0.f, 0.f, 0.f};
+        if (valid) {
+            e = *reinterpret_cast<const h8*>(enc + i * 32 + 8 * g);
+            dx = dirs[3 * i]; dy = dirs[3 * i + 1]; dz = dirs[3 * i + 2];
+            dsig = dL_dsig[i];
+            gr[0] = dL_drgb[3 * i]; gr[1] = dL_drgb[3 * i + 1]; gr[2] = dL_drgb[3 * i + 2];
+        }
+        // ---- forward recompute
+        h4 h1[4];
+        const h4 hh = density_net(e, sw, s, g, h1);
+        float sh[4];
+        sh4_select(dx, dy, dz, g, sh);
+        const h4 shh = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3]};
+        const h8 cin = pack(shh, hh);
+        h4 h3[4], h4v[4];
+        const h4 o = color_net(cin, sw, s, g, h3, h4v);
+        // ---- output layer: sigmoid backward on rows 0..2
+        f4 dout = z;
+        if (g == 0) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const float y = 1.0f / (1.0f + expf(-(float)o[r]));
+                dout[r] = gr[r] * (y * (1.0f - y));
+            }
+        }
+        const float sc_o = pow2_scale(wave_max(max4(dout))), is_o = 1.0f / sc_o;
+        const h4 do_h = scaled_h(dout, sc_o);
+        // ---- dh4 = W5^T do
+        f4 da4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da4[t] = mask_relu(mfma16(lds4(sw + BT5 + (16 * t + s) * RT16 + 4 * g), do_h, z) * is_o, h4v[t]);
+        float m = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da4[t]));
+        const float sc_4 = pow2_scale(wave_max(m)), is_4 = 1.0f / sc_4;
+        h4 da4h[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da4h[t] = scaled_h(da4[t], sc_4);
+        // ---- dh3 = W4^T da4
+        f4 da3[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            f4 c = z;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT4 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da4h[kt], c);
+            da3[t] = mask_relu(c * is_4, h3[t]);
+        }
+        m = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da3[t]));
+        const float sc_3 = pow2_scale(wave_max(m)), is_3 = 1.0f / sc_3;
+        h4 da3h[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da3h[t] = scaled_h(da3[t], sc_3);
+        // ---- d h (colour-net input, h part) = W3h^T da3, + TruncExp backward
+        f4 dh = z;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) dh = mfma16(lds4(sw + BT3 + s * RT64 + 16 * kt + 4 * g), da3h[kt], dh);
+        dh = dh * is_3;
+        if (g == 0) dh[0] += dsig * expf(fminf(fmaxf((float)hh[0], -15.f), 15.f));  // custom_functions.py:169-173
+        const float sc_h = pow2_scale(wave_max(max4(dh))), is_h = 1.0f / sc_h;
+        const h4 dhh = scaled_h(dh, sc_h);
+        // ---- dh1 = W2^T dh
+        f4 da1[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da1[t] = mask_relu(mfma16(lds4(sw + BT2 + (16 * t + s) * RT16 + 4 * g), dhh, z) * is_h, h1[t]);
+        m = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da1[t]));
+        const float sc_1 = pow2_scale(wave_max(m)), is_1 = 1.0f / sc_1;
+        h4 da1h[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da1h[t] = scaled_h(da1[t], sc_1);
+        // ---- dL/denc = W1^T da1 (rows 16t + 4g + r of sample s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            f4 c = z;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT1 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da1h[kt], c);
+            c = c * is_1;
+            if (valid) *reinterpret_cast<f4*>(denc + i * 32 + 16 * t + 4 * g) = c;
+        }
+        // ---- weight gradients: transpose operands through LDS, K = 16 samples
+        wave_sync_lds();  // previous iteration's reads are done
+        put_tile(scr + T_DO * TTILE, do_h, s, g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            put_tile(scr + (T_DA4 + t) * TTILE, da4h[t], s, g);
+            put_tile(scr + (T_DA3 + t) * TTILE, da3h[t], s, g);
+            put_tile(scr + (T_DA1 + t) * TTILE, da1h[t], s, g);
+            put_tile(scr + (T_H4 + t) * TTILE, h4v[t], s, g);
+            put_tile(scr + (T_H3 + t) * TTILE, h3[t], s, g);
+            put_tile(scr + (T_H1 + t) * TTILE, h1[t], s, g);
+        }
+        put_tile(scr + T_DH * TTILE, dhh, s, g);
+        put_tile(scr + T_C * TTILE, shh, s, g);
+        put_tile(scr + (T_C + 1) * TTILE, hh, s, g);
+        {   // enc fragment: lane holds enc[8g + j] of sample s
+            _Float16* Te = scr + (T_E + (g >> 1)) * TTILE;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) Te[(8 * (g & 1) + j) * TROW + s] = e[j];
+        }
+        wave_sync_lds();
+        int k = 0;
+        const h4 gdo = get_tile(scr + T_DO * TTILE, s, g);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt, ++k) acc[k] += mfma16(gdo, get_tile(scr + (T_H4 + nt) * TTILE, s, g), z) * is_o;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const h4 ga = get_tile(scr + (T_DA4 + mt) * TTILE, s, g);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt, ++k) acc[k] += mfma16(ga, get_tile(scr + (T_H3 + nt) * TTILE, s, g), z) * is_4;
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const h4 ga = get_tile(scr + (T_DA3 + mt) * TTILE, s, g);
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt, ++k) acc[k] += mfma16(ga, get_tile(scr + (T_C + nt) * TTILE, s, g), z) * is_3;
+        }
+        const h4 gdh = get_tile(scr + T_DH * TTILE, s, g);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt, ++k) acc[k] += mfma16(gdh, get_tile(scr + (T_H1 + nt) * TTILE, s, g), z) * is_h;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+            const h4 ga = get_tile(scr + (T_DA1 + mt) * TTILE, s, g);
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt, ++k) acc[k] += mfma16(ga, get_tile(scr + (T_E + nt) * TTILE, s, g), z) * is_1;
+        }
+    }
+    // ---- block reduction of the 40 tiles in LDS (fp32), then one global add each
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem + SCR);
+    for (int e = threadIdx.x; e < NACC * 256; e += blockDim.x) red[e] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NACC; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(&red[k * 256 + (4 * g + r) * 16 + s], acc[k][r]);
+    __syncthreads();
+    for (int e = threadIdx.x; e < NACC * 256; e += blockDim.x) {
+        const int k = e >> 8, row = (e >> 4) & 15, col = e & 15;
+        int ow, in_dim, o0, i0;
+        acc_tile_info(k, ow, in_dim, o0, i0);
+        atomicAdd(&grad_mlp[ow + (o0 + row) * in_dim + i0 + col], red[e]);
+    }
+}
+
+// Kernel B: hash-table gradient scatter.  Lane = sample (64 consecutive
+// samples per wave, i.e. runs of samples along one ray), loop over the 16
+// levels x 8 corners.  Consecutive samples of a ray share coarse-level
+// cells, so equal indices in adjacent lanes are first summed with a
+// segmented suffix scan inside the wave and only each run's head issues the
+// two fp32 atomics (dL/dtable[e][f] += w_c * dL/denc[2l+f]).
+__global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__ xyzs, int64_t n,
+                                                       const int64_t* __restrict__ n_dev, GridArgs ga,
+                                                       const float* __restrict__ denc, float* __restrict__ grad) {
+    __shared__ LevelLds lv;
+    load_levels(ga, lv);
+    __syncthreads();
+    const int64_t N = n_dev ? *n_dev : n;
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < N; base += nw * 64) {
+        const int64_t i = base + lane;
+        const bool valid = i < N;
+        float in[3];
+        load_x01(xyzs, i, valid, ga, in);
+#pragma unroll 1
+        for (int l = 0; l < L; ++l) {
+            float2 gd = valid ? *reinterpret_cast<const float2*>(denc + i * 32 + 2 * l) : make_float2(0.f, 0.f);
+            const float sc = lv.scale[l];
+            const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
+            const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
+            float pos[3];
+            uint32_t pg[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const float p = fmaf(sc, in[d], 0.5f);
+                const float fl = floorf(p);
+                pg[d] = (uint32_t)(int)fl;
+                pos[d] = p - fl;
+            }
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                float wt = 1.0f;
+                uint32_t q[3];
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    if (c & (1 << d)) { wt *= pos[d]; q[d] = pg[d] + 1; }
+                    else { wt *= 1 - pos[d]; q[d] = pg[d]; }
+                }
+                const uint32_t idx = valid ? off + corner_index(q[0], q[1], q[2], res, size, dense, pow2) : 0xffffffffu;
+                float v0 = wt * gd.x, v1 = wt * gd.y;
+                const uint32_t prev = __shfl_up(idx, 1, 64);
+                const bool head = lane == 0 || prev != idx;
+                const uint64_t heads = __ballot(head);
+                if (heads != ~0ull) {  // some lanes continue a run: segmented suffix sum
+#pragma unroll
+                    for (int off2 = 1; off2 < 64; off2 <<= 1) {
+                        const float o0 = __shfl_down(v0, off2, 64), o1 = __shfl_down(v1, off2, 64);
+                        const uint64_t after = lane < 63 ? (heads >> (lane + 1)) : 0ull;
+                        const bool in_seg = lane + off2 < 64 && (after & ((1ull << off2) - 1ull)) == 0;
+                        if (in_seg) { v0 += o0; v1 += o1; }
+                    }
+                }
+                if (head && valid) {
+                    atomicAdd(&grad[2 * (size_t)idx], v0);
+                    atomicAdd(&grad[2 * (size_t)idx + 1], v1);
+                }
+            }
+        }
+    }
+}
+
+static int grid_args(const ngp_hashgrid_t* grid, GridArgs& ga) {
+    if (!grid || grid->n_levels != L) return NGP_ERANGE;
+    ga.g = *grid;
+    ga.dense_mask = 0;
+    ga.pow2_mask = 0;
+    for (int l = 0; l < L; ++l) {
+        const uint64_t r = grid->res[l];
+        if (r * r * r <= (uint64_t)grid->sizes[l]) ga.dense_mask |= 1u << l;
+        if ((grid->sizes[l] & (grid->sizes[l] - 1u)) == 0) ga.pow2_mask |= 1u << l;
+        if (grid->sizes[l] == 0) return NGP_EINVAL;
+    }
+    return NGP_OK;
+}
+
+static unsigned persistent_blocks(int64_t n, int samples_per_block, unsigned cap) {
+    int64_t b = (n + samples_per_block - 1) / samples_per_block;
+    if (b < 1) b = 1;
+    return (unsigned)(b < cap ? b : cap);
+}
+
+}  // namespace ngp
+
+using namespace ngp;
+
+extern "C" {
+
+int ngp_field_forward(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
+                      const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16, float* sigmas,
+                      float* rgbs, void* enc_f16, void* h_f16, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && dirs && table_f16 && mlp_f16 && sigmas && rgbs);
+    field_fwd_kernel<true><<<persistent_blocks(n, 64, 4096), 256, 0, as_stream(stream)>>>(
+        xyzs, dirs, n, n_dev, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16, sigmas, rgbs,
+        (_Float16*)enc_f16, (_Float16*)h_f16);
+    return ngp_launch_status();
+}
+
+int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
+                        const void* table_f16, const void* mlp_f16, float* sigmas, void* h_f16, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && table_f16 && mlp_f16 && sigmas);
+    field_fwd_kernel<false><<<persistent_blocks(n, 64, 4096), 256, 0, as_stream(stream)>>>(
+        xyzs, nullptr, n, n_dev, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16, sigmas, nullptr, nullptr,
+        (_Float16*)h_f16);
+    return ngp_launch_status();
+}
+
+int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
+                       const ngp_hashgrid_t* grid, const void* enc_f16, const void* mlp_f16,
+                       const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
+                       float* grad_table, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && dirs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp && grad_table);
+    static bool attr_set = false;
+    const size_t lds = (size_t)BWD_LDS_HALFS * sizeof(_Float16);
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)field_bwd_mlp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return NGP_ERANGE;
+        attr_set = true;
+    }
+    hipStream_t s = as_stream(stream);
+    field_bwd_mlp_kernel<<<persistent_blocks(n, 64, 256), 256, lds, s>>>(
+        dirs, n, n_dev, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp);
+    st = ngp_launch_status();
+    if (st) return st;
+    hash_bwd_kernel<<<persistent_blocks(n, 256, 4096), 256, 0, s>>>(xyzs, n, n_dev, ga, denc_ws, grad_table);
+    return ngp_launch_status();
+}
+
+}  // extern "C"

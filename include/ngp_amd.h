@@ -127,6 +127,54 @@ uint32_t ngp_hashgrid_levels(int n_levels, int log2_hashmap_size, int base_resol
                              float per_level_scale, float* scales, uint32_t* res,
                              uint32_t* offsets, uint32_t* sizes);
 
+/* Hash-grid description passed by value to the field kernels.  Only the
+ * reference's configuration is supported on the GPU: 16 levels x 2 features
+ * (a 32-wide MLP input), any log2T / base resolution / per-level scale. */
+#define NGP_MAX_LEVELS 16
+typedef struct {
+    int n_levels;                       /* must be 16 */
+    float scales[NGP_MAX_LEVELS];
+    uint32_t res[NGP_MAX_LEVELS];
+    uint32_t offsets[NGP_MAX_LEVELS + 1];
+    uint32_t sizes[NGP_MAX_LEVELS];
+    float xyz_min[3], xyz_max[3];        /* models/networks.py:22-23 */
+} ngp_hashgrid_t;
+
+/* MLP weights, fp16, one contiguous buffer of NGP_MLP_PARAMS halfs, each
+ * matrix row-major [out][in] (tcnn FullyFusedMLP layout, no biases):
+ *   W1 64x32, W2 16x64   density net  (xyz_encoder's MLP, networks.py:50-56)
+ *   W3 64x32, W4 64x64, W5 16x64 (rows 3..15 padding)  rgb_net (networks.py:68-78) */
+#define NGP_MLP_PARAMS 10240
+
+/* Replaces tcnn NetworkWithInputEncoding + Encoding(SH4) + Network as used by
+ * NGP.forward (models/networks.py:133-146), fused: per sample
+ *   x01 = (x - xyz_min)/(xyz_max - xyz_min); enc = hash(x01) (32, fp16)
+ *   h = W2 relu(W1 enc) (16, fp16); sigma = exp(h[0]) (TruncExp, fp32)
+ *   rgb = sigmoid(W5 relu(W4 relu(W3 [SH4(d/|d|), h])))[0:3]
+ * xyzs, dirs (n,3) f32; table_f16 (entries,2) fp16; mlp_f16 as above.
+ * Out: sigmas (n) f32, rgbs (n,3) f32 (fp16 values), optional enc_f16 (n,32)
+ * (saved for the backward) and h_f16 (n,16).  If n_dev != NULL the sample
+ * count is read from device memory (n = capacity, for graph capture). */
+int ngp_field_forward(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
+                      const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
+                      float* sigmas, float* rgbs, void* enc_f16, void* h_f16, void* stream);
+
+/* NGP.density (models/networks.py:95-108): hash + density MLP only.
+ * Out: sigmas (n) f32, optional h_f16 (n,16). */
+int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
+                        const void* table_f16, const void* mlp_f16, float* sigmas, void* h_f16,
+                        void* stream);
+
+/* Backward of ngp_field_forward (tcnn's backward for the three modules +
+ * TruncExp.backward, custom_functions.py:169-173).  enc_f16 is the forward's
+ * saved encoding; dL_dsigmas (n) f32, dL_drgbs (n,3) f32.  denc_ws (n,32) f32
+ * is scratch (receives dL/denc).  ACCUMULATES (+=) into grad_mlp
+ * (NGP_MLP_PARAMS f32, layout of mlp_f16) and grad_table ((entries,2) f32). */
+int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
+                       const ngp_hashgrid_t* grid, const void* enc_f16, const void* mlp_f16,
+                       const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
+                       float* grad_table, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
