@@ -1,0 +1,248 @@
+// Training-step kernels around the field: fused compositing + loss +
+// compositing backward, fused Adam with the fp16 shadow write and gradient
+// zeroing, and the occupancy-grid EMA / threshold / scatter of the
+// density-grid update.  Replaces (train.py:174-200, losses.py:63-82,
+// apex FusedAdam at train.py:146, models/networks.py:252-281).
+#pragma clang fp contract(off)
+
+#include "common.h"
+
+namespace ngp {
+
+// ------------------------------------------------------ composite + loss
+// One lane per ray.  Pass 1 = composite_train_fw (volumerendering.cu:5-44);
+// then the background blend (models/rendering.py:287-296) and NeRFLoss
+// (losses.py:63-82: rgb loss of type `loss_type`, opacity entropy, depth
+// term) with its analytic gradient; pass 2 = composite_train_bw
+// (volumerendering.cu:86-150) with dL/dws = 0 (no distortion loss).
+// Per-ray outputs: rgb (after bg), opacity, depth, loss contribution
+// (already divided by the batch means' denominators).
+struct LossArgs {
+    int loss_type;  // 0 raw (default, opt.py:34), 1 mse (upstream ngp_pl), 2 log, 3 tanh
+    float lambda_opacity, lambda_depth, depth_scale, inv_n_rays, T_thr;
+};
+
+__device__ __forceinline__ void rgb_loss(int type, float x, float y, float& l, float& dldx) {
+    switch (type) {
+        case 0: {  // (x - y)/(x.detach() + 1e-3), squared
+            const float den = x + 1e-3f, d = (x - y) / den;
+            l = d * d; dldx = 2.f * d / den; break;
+        }
+        case 1: { const float d = x - y; l = d * d; dldx = 2.f * d; break; }
+        case 2: {
+            const float u = logf((0.2935f + x) / (0.2935f + y)) * 0.7607f;
+            l = u * u; dldx = 2.f * u * 0.7607f / (0.2935f + x); break;
+        }
+        default: {
+            const float tx = tanhf(x), u = tx - tanhf(y);
+            l = u * u; dldx = 2.f * u * (1.f - tx * tx); break;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(64) composite_loss_kernel(
+    const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
+    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
+    const float* __restrict__ bg, LossArgs la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
+    float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
+    float* __restrict__ out_loss, int64_t* __restrict__ vr_samples) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_rays) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+    // ---- forward
+    float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
+    int64_t samples = 0;
+    while (samples < N) {
+        const int64_t s = start + samples;
+        const float a = 1.0f - __expf(-sigmas[s] * deltas[s]);
+        const float w = a * T;
+        R += w * rgbs[3 * s]; G += w * rgbs[3 * s + 1]; B += w * rgbs[3 * s + 2];
+        D += w * ts[s];
+        O += w;
+        T *= 1.0f - a;
+        if (T <= la.T_thr) break;
+        samples++;
+    }
+    // ---- background + loss (mean over rays*3 for rgb, over rays otherwise)
+    const float bgc[3] = {bg[0], bg[1], bg[2]};
+    const float xc[3] = {R + bgc[0] * (1 - O), G + bgc[1] * (1 - O), B + bgc[2] * (1 - O)};
+    float loss = 0.f, g[3], gop = 0.f;
+    const float inv3n = la.inv_n_rays / 3.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float l, d;
+        rgb_loss(la.loss_type, xc[c], gt[3 * ray + c], l, d);
+        loss += l * inv3n;
+        g[c] = d * inv3n;
+        gop -= g[c] * bgc[c];
+    }
+    const float o = O + 1e-10f;
+    loss += la.lambda_opacity * (-o * logf(o)) * la.inv_n_rays;
+    gop += la.lambda_opacity * (-(logf(o) + 1.f)) * la.inv_n_rays;
+    float gdep = 0.f;
+    if (la.lambda_depth != 0.f) {
+        const float v = D / la.depth_scale + 1e-10f;
+        loss += -la.lambda_depth * logf(fminf(v, 1.0f)) * la.inv_n_rays;
+        if (v < 1.0f) gdep = -la.lambda_depth / v / la.depth_scale * la.inv_n_rays;
+    }
+    out_rgb[3 * ray] = xc[0]; out_rgb[3 * ray + 1] = xc[1]; out_rgb[3 * ray + 2] = xc[2];
+    out_op[ray] = O;
+    out_depth[ray] = D;
+    out_loss[ray] = loss;
+    if (vr_samples) atomicAdd((unsigned long long*)vr_samples, (unsigned long long)samples);
+    // ---- backward (dL/dws = 0)
+    float Tb = 1.0f, r = 0.f, gg = 0.f, b = 0.f, d = 0.f;
+    int64_t k = 0;
+    while (k < N) {
+        const int64_t s = start + k;
+        const float a = 1.0f - __expf(-sigmas[s] * deltas[s]);
+        const float w = a * Tb;
+        r += w * rgbs[3 * s]; gg += w * rgbs[3 * s + 1]; b += w * rgbs[3 * s + 2];
+        d += w * ts[s];
+        Tb *= 1.0f - a;
+        dL_drgbs[3 * s] = g[0] * w; dL_drgbs[3 * s + 1] = g[1] * w; dL_drgbs[3 * s + 2] = g[2] * w;
+        dL_dsig[s] = deltas[s] * (g[0] * (rgbs[3 * s] * Tb - (R - r)) + g[1] * (rgbs[3 * s + 1] * Tb - (G - gg)) +
+                                  g[2] * (rgbs[3 * s + 2] * Tb - (B - b)) + gop * (1 - O) + gdep * (ts[s] * Tb - (D - d)));
+        if (Tb <= la.T_thr) break;
+        k++;
+    }
+    for (int64_t q = k + 1; q < N; ++q) {
+        const int64_t s = start + q;
+        dL_dsig[s] = 0.f;
+        dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
+    }
+}
+
+// ------------------------------------------------------------------ Adam
+// apex FusedAdam, adam_w_mode with weight_decay 0 == Adam (train.py:146):
+//   m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
+//   p -= lr * (m / bc1) / (sqrt(v / bc2) + eps)
+// g = grad * grad_scale (1/world_size after an all-reduce SUM).  Writes the
+// fp16 shadow the kernels read and zeroes the gradient for the next step.
+// 4 params per lane, 16-B loads/stores.
+__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ grad, float* __restrict__ m,
+                                                   float* __restrict__ v, _Float16* __restrict__ p16, int64_t n4,
+                                                   float lr, float b1, float b2, float eps, float bc1, float bc2,
+                                                   float grad_scale, int zero_grad) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 P = reinterpret_cast<float4*>(p)[i], Gd = reinterpret_cast<float4*>(grad)[i];
+        float4 M = reinterpret_cast<float4*>(m)[i], V = reinterpret_cast<float4*>(v)[i];
+        float* pp = &P.x; float* gp = &Gd.x; float* mp = &M.x; float* vp = &V.x;
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 out;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float gk = gp[k] * grad_scale;
+            mp[k] = b1 * mp[k] + (1 - b1) * gk;
+            vp[k] = b2 * vp[k] + (1 - b2) * gk * gk;
+            const float denom = sqrtf(vp[k] / bc2) + eps;
+            pp[k] = pp[k] - lr * ((mp[k] / bc1) / denom);
+            out[k] = (_Float16)pp[k];
+        }
+        reinterpret_cast<float4*>(p)[i] = P;
+        reinterpret_cast<float4*>(m)[i] = M;
+        reinterpret_cast<float4*>(v)[i] = V;
+        reinterpret_cast<h4*>(p16)[i] = out;
+        if (zero_grad) reinterpret_cast<float4*>(grad)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+// --------------------------------------------------- occupancy grid update
+// density_grid_tmp[c, idx] = sigma (models/networks.py:268); duplicates keep
+// the max (the reference's last-writer-wins is order-undefined on a GPU).
+// sigma >= 0, so an unsigned-int max on the fp32 bits is a float max.
+__global__ void scatter_max_kernel(const int64_t* __restrict__ idx, const float* __restrict__ sig, int64_t n,
+                                   float* __restrict__ tmp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    atomicMax(reinterpret_cast<unsigned int*>(tmp) + idx[i], __float_as_uint(fmaxf(sig[i], 0.f)));
+}
+
+// models/networks.py:273-278: grid = where(grid<0, grid, max(grid*decay, tmp));
+// accumulates sum and count of grid > 0 for the mean.
+__global__ void __launch_bounds__(256) grid_ema_kernel(float* __restrict__ grid, const float* __restrict__ tmp, int64_t n,
+                                                       float decay, float* __restrict__ sum_cnt) {
+    float s = 0.f, c = 0.f;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float gv = grid[i];
+        const float nv = gv < 0 ? gv : fmaxf(gv * decay, tmp[i]);
+        grid[i] = nv;
+        if (nv > 0) { s += nv; c += 1.f; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o, 64); c += __shfl_xor(c, o, 64); }
+    if ((threadIdx.x & 63) == 0) { atomicAdd(sum_cnt, s); atomicAdd(sum_cnt + 1, c); }
+}
+
+// threshold = min(mean(grid[grid>0]), thr_max)  (models/networks.py:278-281)
+__global__ void grid_threshold_kernel(const float* __restrict__ sum_cnt, float thr_max, float* __restrict__ thr) {
+    // Python's min(nan, x) is nan (mean of an empty selection), and packbits
+    // against a NaN threshold clears every bit -- reproduce that exactly.
+    const float nan = __int_as_float(0x7fc00000);
+    const float mean = sum_cnt[1] > 0 ? sum_cnt[0] / sum_cnt[1] : nan;
+    thr[0] = sum_cnt[1] > 0 ? fminf(mean, thr_max) : nan;
+    thr[1] = mean;
+}
+
+}  // namespace ngp
+
+using namespace ngp;
+
+extern "C" {
+
+int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                       const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg, int loss_type,
+                       float lambda_opacity, float lambda_depth, float depth_scale, float T_threshold,
+                       float* dL_dsigmas, float* dL_drgbs, float* out_rgb, float* out_opacity, float* out_depth,
+                       float* out_loss, int64_t* vr_samples, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && loss_type >= 0 && loss_type <= 3 && depth_scale > 0);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(rays_a && rgb_gt && bg && out_rgb && out_opacity && out_depth && out_loss);
+    LossArgs la{loss_type, lambda_opacity, lambda_depth, depth_scale, 1.0f / (float)n_rays, T_threshold};
+    composite_loss_kernel<<<(unsigned)((n_rays + 63) / 64), 64, 0, as_stream(stream)>>>(
+        sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
+        out_depth, out_loss, vr_samples);
+    return ngp_launch_status();
+}
+
+int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16, int64_t n,
+                  float lr, float beta1, float beta2, float eps, int64_t step, float grad_scale, int zero_grad,
+                  void* stream) {
+    NGP_CHECK_ARG(n >= 0 && step >= 1);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && params_f16);
+    if (n % 4 != 0) return NGP_ERANGE;
+    const float bc1 = 1.0f - powf(beta1, (float)step), bc2 = 1.0f - powf(beta2, (float)step);
+    const int64_t n4 = n / 4;
+    int64_t blocks = (n4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
+                                                                 (_Float16*)params_f16, n4, lr, beta1, beta2, eps, bc1,
+                                                                 bc2, grad_scale, zero_grad);
+    return ngp_launch_status();
+}
+
+int ngp_density_scatter_max(const int64_t* indices, const float* sigmas, int64_t n, float* grid_tmp, void* stream) {
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(indices && sigmas && grid_tmp);
+    scatter_max_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(indices, sigmas, n, grid_tmp);
+    return ngp_launch_status();
+}
+
+int ngp_density_grid_ema(float* density_grid, const float* grid_tmp, int64_t n, float decay, float thr_max,
+                         float* sum_cnt_ws, float* threshold_out, void* stream) {
+    NGP_CHECK_ARG(n > 0 && density_grid && grid_tmp && sum_cnt_ws && threshold_out);
+    hipStream_t s = as_stream(stream);
+    hipError_t e = hipMemsetAsync(sum_cnt_ws, 0, 2 * sizeof(float), s);
+    if (e != hipSuccess) return (int)e;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    grid_ema_kernel<<<(unsigned)blocks, 256, 0, s>>>(density_grid, grid_tmp, n, decay, sum_cnt_ws);
+    grid_threshold_kernel<<<1, 1, 0, s>>>(sum_cnt_ws, thr_max, threshold_out);
+    return ngp_launch_status();
+}
+
+}  // extern "C"

@@ -128,3 +128,58 @@ class SyntheticScene:
         rays_d = torch.einsum("nc,nac->na", d, P[:, :, :3])
         rays_o = P[:, :, 3].clone()
         return rays_o, rays_d
+
+
+class AnalyticScene(SyntheticScene):
+    """SyntheticScene whose ground truth is an analytic object, so training
+    has a consistent target and the occupancy grid converges onto a surface
+    the way it does on Lego: an opaque sphere (radius 0.3) plus a box, with
+    procedural colours, on a white background (Blender scenes are composited
+    on white, datasets/nerf.py read_image)."""
+
+    SPHERE_R = 0.3
+    BOX_MIN = torch.tensor([-0.42, -0.12, -0.40])
+    BOX_MAX = torch.tensor([-0.18, 0.18, 0.05])
+
+    def gt_rgb_rays(self, rays_o: torch.Tensor, rays_d: torch.Tensor) -> torch.Tensor:
+        o, d = rays_o.double(), rays_d.double()
+        dn = d / d.norm(dim=1, keepdim=True)
+        inf = torch.full((o.shape[0],), float("inf"), dtype=torch.float64, device=o.device)
+        # sphere
+        b = (o * dn).sum(1)
+        c = (o * o).sum(1) - self.SPHERE_R ** 2
+        disc = b * b - c
+        ts = torch.where(disc > 0, -b - torch.sqrt(disc.clamp(min=0)), inf)
+        ts = torch.where(ts > 0, ts, inf)
+        # box (slabs)
+        bmin, bmax = self.BOX_MIN.double().to(o.device), self.BOX_MAX.double().to(o.device)
+        inv = 1.0 / dn
+        t0, t1 = (bmin - o) * inv, (bmax - o) * inv
+        tn = torch.minimum(t0, t1).max(1).values
+        tf = torch.maximum(t0, t1).min(1).values
+        tb = torch.where((tn < tf) & (tn > 0), tn, inf)
+        hit_s = ts <= tb
+        t = torch.minimum(ts, tb)
+        p = o + t[:, None] * dn
+        n_s = p / self.SPHERE_R
+        col_s = 0.5 + 0.45 * torch.stack([torch.sin(7 * p[:, 0]) * n_s[:, 2], torch.cos(9 * p[:, 1]),
+                                          torch.sin(5 * (p[:, 2] + p[:, 0]))], 1)
+        checker = ((torch.floor(p[:, 0] * 20) + torch.floor(p[:, 1] * 20) + torch.floor(p[:, 2] * 20)) % 2)
+        col_b = torch.stack([0.8 - 0.5 * checker, 0.3 + 0.4 * checker, 0.2 + 0.1 * checker], 1)
+        col = torch.where(hit_s[:, None], col_s, col_b)
+        hit = torch.isfinite(t)
+        col = torch.where(hit[:, None], col, torch.ones_like(col))
+        return col.clamp(0, 1).float()
+
+    def gt_images(self, device="cpu", chunk=1 << 20) -> torch.Tensor:
+        """(n_images, H*W, 3) uint8 ground truth for every view."""
+        n, HW = self.poses.shape[0], self.H * self.W
+        out = torch.empty(n, HW, 3, dtype=torch.uint8, device=device)
+        dirs = self.directions.to(device)
+        for i in range(n):
+            P = self.poses[i].to(device)
+            for s in range(0, HW, chunk):
+                d = dirs[s:s + chunk] @ P[:, :3].t()
+                o = P[:, 3].expand_as(d)
+                out[i, s:s + chunk] = (self.gt_rgb_rays(o, d) * 255 + 0.5).to(torch.uint8)
+        return out

@@ -1,0 +1,276 @@
+"""The reference's training step (train.py NeRFSystem, Lightning + apex +
+tcnn + vren) as a chain of libngp_amd.so kernels on one MI355X per process.
+
+One step (train.py:174-200), all on the current HIP stream, no host sync:
+  raygen_aabb (ray_utils.get_rays + RayAABBIntersector + near clamp)
+  -> march_train_count / scan / write (RayMarcher; sample count stays on device)
+  -> field_forward (hash grid + density MLP + SH + colour MLP)
+  -> composite_loss (VolumeRenderer fw + bg blend + NeRFLoss + VolumeRenderer bw)
+  -> field_backward (MLP backward + hash scatter)
+  -> [all_reduce(grad) over RCCL when world_size > 1]  (DDP, train.py:288)
+  -> adam_step (FusedAdam + fp16 shadow + grad zeroing)
+and every `update_interval` steps the occupancy update
+(models/networks.py:252-281) before the batch (train.py:175-178).
+
+Per-sample buffers are allocated once at capacity n_rays * max_samples; the
+kernels read the live sample count from device memory.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+import hashgrid as HG
+import vren
+
+MAX_SAMPLES = 1024  # models/rendering.py:9
+NEAR_DISTANCE = 0.01  # models/rendering.py:10
+LOSS_TYPES = {"raw": 0, "mse": 1, "log": 2, "tanh": 3}
+
+
+def _p(t):
+    return HG._ptr(t)
+
+
+class NGPTrainer:
+    def __init__(self, scale=0.5, batch_size=8192, lr=1e-2, num_epochs=30, steps_per_epoch=1000, loss="raw",
+                 lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
+                 update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
+                 device="cuda", process_group=None):
+        self.dev = torch.device(device)
+        self.scale = float(scale)
+        self.batch_size = batch_size
+        self.lr0, self.num_epochs, self.steps_per_epoch = lr, num_epochs, steps_per_epoch
+        self.loss_type = LOSS_TYPES[loss]
+        self.lambda_opacity, self.lambda_depth = lambda_opacity, lambda_depth
+        self.random_bg = random_bg
+        # train.py:104-105
+        self.esf = exp_step_factor if exp_step_factor is not None else (1 / 256 if scale > 0.5 else 0.0)
+        self.G = grid_size
+        self.cascades = max(1 + int(np.ceil(np.log2(2 * scale))), 1)  # models/networks.py:27
+        self.update_interval, self.warmup_steps, self.max_samples = update_interval, warmup_steps, max_samples
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        dev = self.dev
+        # ---- field parameters: fp32 master, fp16 shadow, Adam state, grad
+        self.grid = HG.HashGrid(scale)
+        self.params = HG.init_params(self.grid, seed=seed, device=dev)
+        self.params16 = self.params.half()
+        self.grad = torch.zeros_like(self.params)
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+        self.global_step = 0
+        # ---- occupancy (models/networks.py:20-30, train.py:78-82)
+        self.center = torch.zeros(1, 3, device=dev)
+        self.half_size = torch.ones(1, 3, device=dev) * scale
+        self.density_grid = torch.zeros(self.cascades, self.G ** 3, device=dev)
+        self.density_bitfield = torch.zeros(self.cascades * self.G ** 3 // 8, dtype=torch.uint8, device=dev)
+        ax = torch.arange(self.G, dtype=torch.int32, device=dev)
+        self.grid_coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3).contiguous()
+        self.all_indices = vren.morton3D(self.grid_coords).long()
+        self._sum_cnt = torch.zeros(2, device=dev)
+        self.threshold = torch.zeros(2, device=dev)
+        # ---- per-step buffers
+        R = batch_size
+        if sample_capacity is not None:  # never let a ray overflow the sample buffers
+            self.max_samples = max_samples = max(1, min(max_samples, sample_capacity // R))
+        cap = R * max_samples
+        self.cap = cap
+        f = dict(device=dev, dtype=torch.float32)
+        self.rays_o, self.rays_d, self.hits_t = torch.empty(R, 3, **f), torch.empty(R, 3, **f), torch.empty(R, 2, **f)
+        self.noise = torch.empty(R, **f)
+        self.counts = torch.empty(R, dtype=torch.int32, device=dev)
+        self.rays_a = torch.empty(R, 3, dtype=torch.int64, device=dev)
+        self.n_samples = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.xyzs, self.dirs = torch.empty(cap, 3, **f), torch.empty(cap, 3, **f)
+        self.deltas, self.ts = torch.empty(cap, **f), torch.empty(cap, **f)
+        self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
+        self.enc = torch.empty(cap, 32, dtype=torch.float16, device=dev)
+        self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
+        self.denc = torch.empty(cap, 32, **f)
+        self.out_rgb, self.out_op = torch.empty(R, 3, **f), torch.empty(R, **f)
+        self.out_depth, self.out_loss = torch.empty(R, **f), torch.empty(R, **f)
+        self.vr_samples = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.bg = torch.ones(3, **f) if self.esf == 0 else torch.zeros(3, **f)  # models/rendering.py:287-296
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(1000 + seed + self.rank)
+        self.L = vren.lib()
+        HG._lib()
+        self.field_events = None  # (start, end) torch.cuda.Event pair around field_forward (bench roofline)
+
+    # ------------------------------------------------------------ schedule
+    def lr(self):
+        """CosineAnnealingLR(T_max=num_epochs, eta_min=lr/30), stepped per epoch (train.py:149-151)."""
+        e = self.global_step // self.steps_per_epoch
+        eta_min = self.lr0 / 30
+        return eta_min + (self.lr0 - eta_min) * (1 + math.cos(math.pi * e / self.num_epochs)) / 2
+
+    # ------------------------------------------------------ occupancy grid
+    @torch.no_grad()
+    def mark_invisible_cells(self, K, poses, img_wh, chunk=64 ** 3):
+        """models/networks.py:209-250 (once, before training)."""
+        K, poses = K.to(self.dev), poses.to(self.dev)
+        N_cams = poses.shape[0]
+        w2c_R = poses[:, :3, :3].transpose(1, 2)
+        w2c_T = -w2c_R @ poses[:, :3, 3:]
+        for c in range(self.cascades):
+            indices, coords = self.all_indices, self.grid_coords
+            for i in range(0, len(indices), chunk):
+                xyzs = coords[i:i + chunk] / (self.G - 1) * 2 - 1
+                s = min(2 ** (c - 1), self.scale)
+                half_grid_size = s / self.G
+                xyzs_w = (xyzs * (s - half_grid_size)).T
+                xyzs_c = w2c_R @ xyzs_w + w2c_T
+                uvd = K @ xyzs_c
+                uv = uvd[:, :2] / uvd[:, 2:]
+                in_image = (uvd[:, 2] >= 0) & (uv[:, 0] >= 0) & (uv[:, 0] < img_wh[0]) & (uv[:, 1] >= 0) & \
+                           (uv[:, 1] < img_wh[1])
+                covered_by_cam = (uvd[:, 2] >= NEAR_DISTANCE) & in_image
+                count = covered_by_cam.sum(0) / N_cams
+                too_near_to_any_cam = ((uvd[:, 2] < NEAR_DISTANCE) & in_image).any(0)
+                valid_mask = (count > 0) & (~too_near_to_any_cam)
+                self.density_grid[c, indices[i:i + chunk]] = torch.where(valid_mask, 0., -1.)
+
+    @torch.no_grad()
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95):
+        """models/networks.py:252-281.  Multi-GPU: each rank evaluates its 1/world
+        share of the cells and the cell maxima are combined with one MAX
+        all-reduce, so every rank packs an identical bitfield."""
+        C, G = self.cascades, self.G
+        tmp = torch.zeros_like(self.density_grid)
+        for c in range(C):
+            if warmup:  # get_all_cells (networks.py:167-179)
+                indices, coords = self.all_indices, self.grid_coords
+            else:  # sample_uniform_and_occupied_cells (networks.py:181-207)
+                M = G ** 3 // 4
+                coords1 = torch.randint(G, (M, 3), dtype=torch.int32, device=self.dev, generator=self.gen)
+                indices1 = vren.morton3D(coords1).long()
+                indices2 = torch.nonzero(self.density_grid[c] > density_threshold)[:, 0]
+                if len(indices2) > 0:
+                    rand_idx = torch.randint(len(indices2), (M,), device=self.dev, generator=self.gen)
+                    indices2 = indices2[rand_idx]
+                coords2 = vren.morton3D_invert(indices2.int().contiguous())
+                indices = torch.cat([indices1, indices2])
+                coords = torch.cat([coords1, coords2])
+            if self.world > 1:  # shard the cells
+                n = indices.shape[0]
+                lo, hi = n * self.rank // self.world, n * (self.rank + 1) // self.world
+                indices, coords = indices[lo:hi], coords[lo:hi]
+            s = min(2 ** (c - 1), self.scale)
+            half_grid_size = s / G
+            xyzs_w = (coords / (G - 1) * 2 - 1) * (s - half_grid_size)
+            xyzs_w += (torch.rand(xyzs_w.shape, device=self.dev, generator=self.gen) * 2 - 1) * half_grid_size
+            sig, _ = HG.density_forward(xyzs_w.float().contiguous(), self.grid, self.params16)
+            flat = (indices + c * G ** 3).contiguous()
+            vren._ok(self.L.ngp_density_scatter_max(_p(flat), _p(sig), flat.shape[0], _p(tmp), vren._stream()),
+                     "density_scatter_max")
+        if self.world > 1:
+            dist.all_reduce(tmp, op=dist.ReduceOp.MAX, group=self.pg)
+        st = self.L.ngp_density_grid_ema(_p(self.density_grid), _p(tmp), self.density_grid.numel(),
+                                         ctypes_float(decay), ctypes_float(density_threshold), _p(self._sum_cnt),
+                                         _p(self.threshold), vren._stream())
+        vren._ok(st, "density_grid_ema")
+        if self.world > 1:  # identical threshold on every rank
+            dist.broadcast(self.threshold, src=0, group=self.pg)
+        vren.packbits(self.density_grid, self.threshold[:1], self.density_bitfield)
+
+    # ---------------------------------------------------------------- step
+    def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses):
+        """One training step on a batch (train.py:174-200).  img/pix (R) i64,
+        rgb_gt (R,3) f32, directions (HW,3), poses (n_img,3,4), all on device."""
+        L, s = self.L, vren._stream()
+        if self.global_step % self.update_interval == 0:
+            self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=self.global_step < self.warmup_steps)
+        R = img_idxs.shape[0]
+        assert R == self.batch_size
+        vren._ok(L.ngp_raygen_aabb(_p(directions), _p(poses), _p(img_idxs), _p(pix_idxs), R, _p(self.center),
+                                   _p(self.half_size), ctypes_float(NEAR_DISTANCE), _p(self.rays_o), _p(self.rays_d),
+                                   _p(self.hits_t), s), "raygen")
+        torch.rand(R, out=self.noise, generator=self.gen)  # custom_functions.py:83
+        vren._ok(L.ngp_march_train_count(_p(self.rays_o), _p(self.rays_d), _p(self.hits_t), R, _p(self.density_bitfield),
+                                         self.cascades, self.G, ctypes_float(self.scale), ctypes_float(self.esf),
+                                         _p(self.noise), self.max_samples, _p(self.counts), _p(self.rays_a),
+                                         _p(self.n_samples), s), "march_count")
+        vren._ok(L.ngp_march_train_write(_p(self.rays_o), _p(self.rays_d), _p(self.hits_t), R, _p(self.density_bitfield),
+                                         self.cascades, self.G, ctypes_float(self.scale), ctypes_float(self.esf),
+                                         _p(self.noise), self.max_samples, _p(self.rays_a), _p(self.xyzs),
+                                         _p(self.dirs), _p(self.deltas), _p(self.ts), s), "march_write")
+        HGL = HG._lib()
+        if self.field_events is not None:
+            self.field_events[0].record()
+        vren._ok(HGL.ngp_field_forward(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples),
+                                       HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
+                                       _p(self.params16), _p(self.sigmas), _p(self.rgbs), _p(self.enc), None, s),
+                 "field_forward")
+        if self.field_events is not None:
+            self.field_events[1].record()
+        bg = torch.rand(3, device=self.dev, generator=self.gen) if self.random_bg else self.bg
+        vren._ok(L.ngp_composite_loss(_p(self.sigmas), _p(self.rgbs), _p(self.deltas), _p(self.ts), _p(self.rays_a), R,
+                                      _p(rgb_gt), _p(bg), self.loss_type, ctypes_float(self.lambda_opacity),
+                                      ctypes_float(self.lambda_depth), ctypes_float(self.scale), ctypes_float(1e-4),
+                                      _p(self.dsig), _p(self.drgb), _p(self.out_rgb), _p(self.out_op),
+                                      _p(self.out_depth), _p(self.out_loss), _p(self.vr_samples), s), "composite_loss")
+        vren._ok(HGL.ngp_field_backward(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples),
+                                        HG.ctypes.byref(self.grid.desc), _p(self.enc), _p(self.params16),
+                                        _p(self.dsig), _p(self.drgb), _p(self.denc), _p(self.grad),
+                                        _p(self.grad[HG.MLP_PARAMS:]), s), "field_backward")
+        if self.world > 1:
+            dist.all_reduce(self.grad, group=self.pg)  # DDP gradient all-reduce (RCCL)
+        self.global_step += 1
+        vren._ok(L.ngp_adam_step(_p(self.params), _p(self.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
+                                 _p(self.params16), self.params.numel(), ctypes_float(self.lr()), ctypes_float(0.9),
+                                 ctypes_float(0.999), ctypes_float(1e-15), self.global_step,
+                                 ctypes_float(1.0 / self.world), 1, s), "adam")
+        return self.out_loss
+
+    # ---------------------------------------------------- test-time render
+    @torch.no_grad()
+    def render(self, rays_o, rays_d, T_threshold=1e-4, max_samples=MAX_SAMPLES, bg=0.0):
+        """__render_rays_test (models/rendering.py:162-253) on the native kernels."""
+        N_rays = rays_o.shape[0]
+        dev = self.dev
+        _, hits_t, _ = vren.ray_aabb_intersect(rays_o, rays_d, self.center, self.half_size, 1)
+        m = (hits_t[:, 0, 0] >= 0) & (hits_t[:, 0, 0] < NEAR_DISTANCE)
+        hits_t[m, 0, 0] = NEAR_DISTANCE
+        ht = hits_t[:, 0]
+        opacity = torch.zeros(N_rays, device=dev)
+        depth = torch.zeros(N_rays, device=dev)
+        rgb = torch.zeros(N_rays, 3, device=dev)
+        samples = total = 0
+        alive = torch.arange(N_rays, device=dev)
+        min_samples = 1 if self.esf == 0 else 4
+        while samples < max_samples:
+            N_alive = len(alive)
+            if N_alive == 0:
+                break
+            Ns = max(min(N_rays // N_alive, 64), min_samples)
+            samples += Ns
+            xyzs, dirs, deltas, ts, neff = vren.raymarching_test(rays_o, rays_d, ht, alive, self.density_bitfield,
+                                                                 self.cascades, self.scale, self.esf, self.G,
+                                                                 MAX_SAMPLES, Ns)
+            total += int(neff.sum())
+            xyzs = xyzs.reshape(-1, 3)
+            dirs = dirs.reshape(-1, 3)
+            valid = ~torch.all(dirs == 0, dim=1)
+            if valid.sum() == 0:
+                break
+            sig = torch.zeros(len(xyzs), device=dev)
+            rgbs = torch.zeros(len(xyzs), 3, device=dev)
+            sv, rv, _, _ = HG.field_forward(xyzs[valid].contiguous(), dirs[valid].contiguous(), self.grid,
+                                            self.params16, save_enc=False)
+            sig[valid] = sv
+            rgbs[valid] = rv
+            vren.composite_test_fw(sig.view(-1, Ns), rgbs.view(-1, Ns, 3), deltas, ts, ht, alive, T_threshold, neff,
+                                   opacity, depth, rgb)
+            alive = alive[alive >= 0].contiguous()
+        rgb = rgb + bg * (1 - opacity)[:, None]
+        return {"rgb": rgb, "opacity": opacity, "depth": depth, "total_samples": total}
+
+
+def ctypes_float(x):
+    return HG.c_float(float(x))

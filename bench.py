@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Training-throughput benchmark of the MI355X-native Instant-NGP hot path.
+
+Metric (BASELINE.json): training rays/s on Lego-shaped 8192-ray batches
+(L=16, T=2^19 hash, 64-wide MLPs, 128^3 occupancy grid, fp16 field), one
+process per GPU, each rank drawing its own 8192-ray batch (the reference's
+Lightning DDP semantics, train.py:288) -> weak scaling, value = all ranks'
+rays / max-over-ranks wall time.
+
+Workload: no dataset is reachable, so the scene is analytic
+(synthetic.AnalyticScene: 100 800x800 views of an opaque sphere + box on
+white, Lego camera intrinsics); the model is first trained for --pretrain
+steps (setup, untimed) so the occupancy grid and samples/ray are in the
+steady state of real training, then --warmup untimed and --steps timed FULL
+training steps (occupancy update every 16 steps, ray generation, marching,
+field fwd/bwd, compositing + loss, [RCCL all-reduce], Adam).
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
+torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the env).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "ar-nerf_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import hashgrid as HG  # noqa: E402
+import synthetic as S  # noqa: E402
+from trainer import NGPTrainer  # noqa: E402
+
+with open(os.path.join(ROOT, "BASELINE.json")) as f:
+    BASELINE = json.load(f)
+
+# Algorithmic bytes per sample of the roofline kernel (field forward:
+# 16 levels x 8 corners x fp16x2 gathered + xyz + dir read + fp16 encoding,
+# sigma and rgb written).  See DESIGN.md "Measurement".
+FIELD_FWD_BYTES_PER_SAMPLE = 16 * 8 * 4 + 12 + 12 + 64 + 4 + 12
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--pretrain", type=int, default=400, help="untimed setup training steps (steady-state occupancy)")
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--scale", type=float, default=0.5)
+    ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--images", type=int, default=100)
+    ap.add_argument("--psnr-views", type=int, default=2)
+    ap.add_argument("--psnr-res", type=int, default=400)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--quiet", action="store_true")
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def psnr_eval(trainer, scene, n_views, res, seed=123):
+    """Test PSNR on held-out analytic views (black test background like
+    models/rendering.py:240 would need a black GT; the analytic GT is on
+    white, so the white background is blended: bg=1)."""
+    sc = S.AnalyticScene(W=res, H=res, n_images=n_views, scale=scene.scale, seed=seed)
+    psnrs = []
+    for i in range(n_views):
+        P = sc.poses[i].cuda()
+        d = (sc.directions.cuda() @ P[:, :3].t()).contiguous()
+        o = P[:, 3].expand_as(d).contiguous()
+        out = trainer.render(o, d, bg=1.0)
+        gt = sc.gt_rgb_rays(o, d)
+        mse = torch.mean((out["rgb"].clamp(0, 1) - gt) ** 2).item()
+        psnrs.append(-10 * math.log10(max(mse, 1e-12)))
+    return sum(psnrs) / len(psnrs)
+
+
+def cpu_baseline(trainer, scene, gt_images, budget_s, batch):
+    """The oracle (oracle/, CPU restatement) timed on this host on the same
+    workload: full training steps on 8192-ray batches from the same model
+    state, as many as fit ~budget_s (at least 1)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # test/baseline infrastructure only
+    threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(threads)
+    ot = O.OracleTrainer(trainer.params, scene.scale, trainer.density_bitfield, trainer.cascades)
+    gen = torch.Generator().manual_seed(77)
+    c = torch.zeros(1, 3); h = torch.ones(1, 3) * scene.scale
+    steps, t_total, samples = 0, 0.0, 0
+    while steps < 5 and (steps == 0 or t_total < budget_s):
+        img, pix = scene.sample_batch(batch, gen)
+        o, d = scene.rays(img, pix)
+        _, ht, _ = O.ray_aabb_intersect(o, d, c, h, 1)
+        ht = ht[:, 0].contiguous()
+        ht[(ht[:, 0] >= 0) & (ht[:, 0] < 0.01), 0] = 0.01
+        gt = gt_images[img, pix].float().cpu() / 255
+        noise = torch.rand(batch, generator=gen)
+        t0 = time.perf_counter()
+        _, n = ot.step(o.contiguous(), d.contiguous(), ht, gt, noise, torch.ones(3))
+        t_total += time.perf_counter() - t0
+        steps += 1
+        samples += n
+    return {"value": round(batch * steps / t_total, 1), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} full training step(s) of the {batch}-ray batch on the oracle "
+                      f"(C march/composite/hash + torch fp32 MLP autograd + C Adam over all params), "
+                      f"{samples / max(1, steps) / batch:.1f} samples/ray, {t_total:.1f} s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    torch.manual_seed(0)
+    scene = S.AnalyticScene(W=args.res, H=args.res, n_images=args.images, scale=args.scale)
+    gt_images = scene.gt_images(device=dev)  # (n_img, HW, 3) u8, resident in HBM
+    directions = scene.directions.to(dev).contiguous()
+    poses = scene.poses.to(dev).contiguous()
+    trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev)
+    trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + rank)
+    HW, n_img = scene.W * scene.H, scene.poses.shape[0]
+    R = args.batch
+
+    def batch():
+        img = torch.randint(0, n_img, (R,), device=dev, generator=gen)
+        pix = torch.randint(0, HW, (R,), device=dev, generator=gen)
+        rgb = gt_images[img, pix].float().div_(255)
+        return img, pix, rgb
+
+    t0 = time.time()
+    for i in range(args.pretrain):
+        img, pix, rgb = batch()
+        trainer.step(img, pix, rgb, directions, poses)
+    torch.cuda.synchronize()
+    log(rank, f"[bench] pretrain {args.pretrain} steps in {time.time() - t0:.1f}s, "
+              f"samples last batch {int(trainer.n_samples.item())}")
+    for i in range(args.warmup):
+        img, pix, rgb = batch()
+        trainer.step(img, pix, rgb, directions, poses)
+    # ---- timed region
+    n_samples_acc = torch.zeros(1, dtype=torch.int64, device=dev)
+    trainer.vr_samples.zero_()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    trainer.timing_events = None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        img, pix, rgb = batch()
+        trainer.field_events = ev[i]
+        trainer.step(img, pix, rgb, directions, poses)
+        n_samples_acc += trainer.n_samples
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_el = time.perf_counter() - t_start
+    trainer.field_events = None
+    t_max = torch.tensor([t_el], device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    t_el = float(t_max.item())
+    total_rays = R * args.steps * world
+    value = total_rays / t_el
+    samples = int(n_samples_acc.item())
+    fwd_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    samples_per_step = samples / args.steps
+    achieved = samples_per_step * FIELD_FWD_BYTES_PER_SAMPLE / (fwd_ms * 1e-3) / 1e9
+    rm_s = samples / (R * args.steps)
+    vr_s = int(trainer.vr_samples.item()) / (R * args.steps)
+    loss = float(trainer.out_loss.sum().item())
+    psnr = psnr_eval(trainer, scene, args.psnr_views, args.psnr_res) if (rank == 0 and args.psnr_views > 0) else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(trainer, scene, gt_images, args.cpu_budget_s, R)
+    if rank == 0:
+        out = {
+            "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_el / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16/fp32",
+            "data": "synthetic (analytic sphere+box scene, 100 views 800x800, Lego intrinsics; random-init weights "
+                    f"trained {args.pretrain} setup steps)",
+            "config": {"workload": "lego-shaped training step: 8192 rays/rank, scale 0.5, 128^3 grid, L=16 F=2 "
+                                   "T=2^19 hash, 64-wide MLPs, raw loss, Adam lr 1e-2",
+                       "batch_rays_per_gpu": R, "global_batch_rays": R * world, "pretrain_steps": args.pretrain,
+                       "rm_samples_per_ray": round(rm_s, 2), "vr_samples_per_ray": round(vr_s, 2),
+                       "parallelism": f"dp{world}", "last_loss": round(loss, 5),
+                       "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
+            "roofline": {"kernel": "field_fwd (hash encode + fused MLPs)", "bound": "hbm",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_sample": FIELD_FWD_BYTES_PER_SAMPLE, "avg_launch_ms": round(fwd_ms, 4),
+                         "samples_per_launch": round(samples_per_step, 1)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

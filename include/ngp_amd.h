@@ -175,6 +175,41 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
                        const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
                        float* grad_table, void* stream);
 
+/* ------------------------------------------------------ training step */
+/* Fused compositing + NeRFLoss + compositing backward for one training batch:
+ * composite_train_fw (volumerendering.cu:5-44), background blend
+ * (models/rendering.py:287-296, bg = 3 device floats), NeRFLoss
+ * (losses.py:63-82; loss_type 0 raw (default), 1 mse, 2 log, 3 tanh;
+ * opacity entropy lambda_opacity; depth term lambda_depth with depth_scale)
+ * and composite_train_bw with dL/dws = 0.  rgb_gt (n_rays,3).
+ * Out: dL_dsigmas (N), dL_drgbs (N,3); per ray out_rgb (n_rays,3) (after bg),
+ * out_opacity, out_depth, out_loss (n_rays; sum = the batch loss);
+ * vr_samples (1) i64 += composited samples (nullable). */
+int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                       const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg,
+                       int loss_type, float lambda_opacity, float lambda_depth, float depth_scale,
+                       float T_threshold, float* dL_dsigmas, float* dL_drgbs, float* out_rgb,
+                       float* out_opacity, float* out_depth, float* out_loss, int64_t* vr_samples,
+                       void* stream);
+
+/* apex FusedAdam step (train.py:146; weight decay 0) over n (multiple of 4)
+ * fp32 params with grad *= grad_scale, bias corrections for `step` (1-based);
+ * writes the fp16 shadow params_f16 and, if zero_grad, zeroes grads. */
+int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16,
+                  int64_t n, float lr, float beta1, float beta2, float eps, int64_t step,
+                  float grad_scale, int zero_grad, void* stream);
+
+/* Occupancy update (models/networks.py:252-281).  scatter_max: grid_tmp[idx[i]]
+ * = max(grid_tmp[idx[i]], sigmas[i]) (flat cascade*G^3 indices, sigmas >= 0).
+ * grid_ema: grid = where(grid<0, grid, max(grid*decay, tmp)) in place, then
+ * threshold_out[0] = min(mean(grid[grid>0]), thr_max) (NaN if none, as in
+ * Python), threshold_out[1] = the mean; feed threshold_out to ngp_packbits'
+ * threshold_dev.  sum_cnt_ws: 2 floats of scratch. */
+int ngp_density_scatter_max(const int64_t* indices, const float* sigmas, int64_t n, float* grid_tmp,
+                            void* stream);
+int ngp_density_grid_ema(float* density_grid, const float* grid_tmp, int64_t n, float decay,
+                         float thr_max, float* sum_cnt_ws, float* threshold_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

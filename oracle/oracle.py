@@ -424,3 +424,65 @@ class tcnn_stub:
             if self.act == "Sigmoid":
                 out = rh(torch.sigmoid(out))
             return out.half()
+
+
+# ------------------------------------------------ CPU training step (baseline)
+class _VolumeRendererCPU(torch.autograd.Function):
+    """custom_functions.py:115-159 on the oracle kernels."""
+
+    @staticmethod
+    def forward(ctx, sigmas, rgbs, deltas, ts, rays_a, T_threshold):
+        tot, op, dep, rgb, ws = composite_train_fw(sigmas, rgbs, deltas, ts, rays_a, T_threshold)
+        ctx.save_for_backward(sigmas, rgbs, deltas, ts, rays_a, op, dep, rgb, ws)
+        ctx.T = T_threshold
+        return tot.sum(), op, dep, rgb, ws
+
+    @staticmethod
+    def backward(ctx, dtot, dop, ddep, drgb, dws):
+        sigmas, rgbs, deltas, ts, rays_a, op, dep, rgb, ws = ctx.saved_tensors
+        dsig, drgbs = composite_train_bw(dop, ddep, drgb, dws, sigmas, rgbs, ws, deltas, ts, rays_a, op, dep, rgb,
+                                         ctx.T)
+        return dsig, drgbs, None, None, None, None
+
+
+def nerf_loss_raw(rgb, gt, opacity, lambda_opacity=1e-3):
+    """losses.py:63-82 with the default 'raw' rgb loss and depth weight 0."""
+    d_rgb = ((rgb - gt) / (rgb.detach() + 1e-3)) ** 2
+    o = opacity + 1e-10
+    d_op = lambda_opacity * (-o * torch.log(o))
+    return d_rgb.mean() + d_op.mean()
+
+
+class OracleTrainer:
+    """One reference training step (train.py:174-200 + FusedAdam) on the CPU
+    oracle: march (C), field (torch MLP with fp16 storage points + C hash),
+    VolumeRenderer fw/bw (C), NeRFLoss (torch), autograd, Adam (C)."""
+
+    def __init__(self, flat_params, scale, bitfield, cascades, grid_size=128, lr=1e-2):
+        self.field = OracleNGPField(scale=scale, table_init=0.0)
+        nd = self.field.n_dens
+        flat = flat_params.detach().float().cpu()
+        with torch.no_grad():
+            self.field.xyz_params.copy_(torch.cat([flat[:nd], flat[10240:]]))
+            self.field.rgb_params.copy_(flat[nd:10240])
+        self.scale, self.cascades, self.G, self.lr = scale, cascades, grid_size, lr
+        self.bitfield = bitfield.cpu().contiguous()
+        self.state = {p: (torch.zeros_like(p), torch.zeros_like(p)) for p in (self.field.xyz_params,
+                                                                             self.field.rgb_params)}
+        self.t = 0
+
+    def step(self, rays_o, rays_d, hits_t, rgb_gt, noise, bg):
+        rays_a, xyzs, dirs, deltas, ts, cnt = raymarching_train(rays_o, rays_d, hits_t, self.bitfield, self.cascades,
+                                                                self.scale, 0.0, noise, self.G, 1024)
+        sig, rgbs = self.field(xyzs, dirs)
+        vr, op, dep, rgb, ws = _VolumeRendererCPU.apply(sig, rgbs.contiguous(), deltas, ts, rays_a, 1e-4)
+        rgb = rgb + bg * (1 - op)[:, None]
+        loss = nerf_loss_raw(rgb, rgb_gt, op)
+        for p in self.state:
+            p.grad = None
+        loss.backward()
+        self.t += 1
+        for p, (m, v) in self.state.items():
+            g = p.grad if p.grad is not None else torch.zeros_like(p)
+            adam_(p.data, g.contiguous(), m, v, self.lr, self.t)
+        return float(loss), int(cnt[0])
