@@ -511,12 +511,16 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
     }
 }
 
-// Kernel B: hash-table gradient scatter.  Lane = sample (64 consecutive
-// samples per wave, i.e. runs of samples along one ray), loop over the 16
-// levels x 8 corners.  Consecutive samples of a ray share coarse-level
-// cells, so equal indices in adjacent lanes are first summed with a
-// segmented suffix scan inside the wave and only each run's head issues the
-// two fp32 atomics (dL/dtable[e][f] += w_c * dL/denc[2l+f]).
+// Kernel B: hash-table gradient scatter, dL/dtable[e][f] += w_c * dL/denc[2l+f].
+// Lane map: 16 consecutive samples per wave, 4 lanes per sample:
+//   lane = 4*s + 2*cx + f  (cx = the corner's x bit, f = feature).
+// One wave instruction then carries, per sample, the x-adjacent corner pair
+// x both features: 4 floats that sit in 16 contiguous bytes whenever the two
+// entries are neighbours (dense levels; hashed levels when px is even, since
+// the x term of the hash is px*1), so the atomics leave as one request per
+// sample instead of four scattered ones.  Samples of one ray are consecutive,
+// so equal indices of the same (cx, f) at lane stride 4 are first summed by a
+// segmented suffix scan; only each run's head issues its fp32 atomic.
 __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__ xyzs, int64_t n,
                                                        const int64_t* __restrict__ n_dev, GridArgs ga,
                                                        const float* __restrict__ denc, float* __restrict__ grad) {
@@ -524,16 +528,16 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
     load_levels(ga, lv);
     __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, s = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < N; base += nw * 64) {
-        const int64_t i = base + lane;
+    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16; base < N; base += nw * 16) {
+        const int64_t i = base + s;
         const bool valid = i < N;
         float in[3];
         load_x01(xyzs, i, valid, ga, in);
 #pragma unroll 1
         for (int l = 0; l < L; ++l) {
-            float2 gd = valid ? *reinterpret_cast<const float2*>(denc + i * 32 + 2 * l) : make_float2(0.f, 0.f);
+            const float gd = valid ? denc[i * 32 + 2 * l + f] : 0.f;
             const float sc = lv.scale[l];
             const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
             const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
@@ -546,33 +550,31 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
                 pg[d] = (uint32_t)(int)fl;
                 pos[d] = p - fl;
             }
+            // corner c = cx | (cy<<1) | (cz<<2); weight product in tcnn's d order
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
+            for (int yz = 0; yz < 4; ++yz) {
+                const int cy = yz & 1, cz = yz >> 1;
                 float wt = 1.0f;
-                uint32_t q[3];
-#pragma unroll
-                for (int d = 0; d < 3; ++d) {
-                    if (c & (1 << d)) { wt *= pos[d]; q[d] = pg[d] + 1; }
-                    else { wt *= 1 - pos[d]; q[d] = pg[d]; }
-                }
-                const uint32_t idx = valid ? off + corner_index(q[0], q[1], q[2], res, size, dense, pow2) : 0xffffffffu;
-                float v0 = wt * gd.x, v1 = wt * gd.y;
-                const uint32_t prev = __shfl_up(idx, 1, 64);
-                const bool head = lane == 0 || prev != idx;
+                wt *= cx ? pos[0] : 1 - pos[0];
+                wt *= cy ? pos[1] : 1 - pos[1];
+                wt *= cz ? pos[2] : 1 - pos[2];
+                const uint32_t idx = valid ? off + corner_index(pg[0] + cx, pg[1] + cy, pg[2] + cz, res, size, dense, pow2)
+                                           : 0xffffffffu;
+                float v = wt * gd;
+                const uint32_t prev = __shfl_up(idx, 4, 64);
+                const bool head = lane < 4 || prev != idx;
                 const uint64_t heads = __ballot(head);
-                if (heads != ~0ull) {  // some lanes continue a run: segmented suffix sum
+                if (heads != ~0ull) {  // some runs: segmented suffix sum at lane stride 4
 #pragma unroll
-                    for (int off2 = 1; off2 < 64; off2 <<= 1) {
-                        const float o0 = __shfl_down(v0, off2, 64), o1 = __shfl_down(v1, off2, 64);
-                        const uint64_t after = lane < 63 ? (heads >> (lane + 1)) : 0ull;
-                        const bool in_seg = lane + off2 < 64 && (after & ((1ull << off2) - 1ull)) == 0;
-                        if (in_seg) { v0 += o0; v1 += o1; }
+                    for (int o4 = 4; o4 < 64; o4 <<= 1) {
+                        const float ov = __shfl_down(v, o4, 64);
+                        // lanes lane+4, lane+8, ..., lane+o4 must all continue the run
+                        const uint64_t span = (0x1111111111111111ull & ((2ull << o4) - 1ull)) & ~1ull;
+                        const bool in_seg = lane + o4 < 64 && (heads & (span << lane)) == 0;
+                        if (in_seg) v += ov;
                     }
                 }
-                if (head && valid) {
-                    atomicAdd(&grad[2 * (size_t)idx], v0);
-                    atomicAdd(&grad[2 * (size_t)idx + 1], v1);
-                }
+                if (head && valid) atomicAdd(&grad[2 * (size_t)idx + f], v);
             }
         }
     }
@@ -633,6 +635,38 @@ int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, cons
     return ngp_launch_status();
 }
 
+int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const void* enc_f16,
+                           const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws,
+                           float* grad_mlp, void* stream) {
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(dirs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp);
+    static bool attr_set = false;
+    const size_t lds = (size_t)BWD_LDS_HALFS * sizeof(_Float16);
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)field_bwd_mlp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds) != hipSuccess)
+            return NGP_ERANGE;
+        attr_set = true;
+    }
+    field_bwd_mlp_kernel<<<persistent_blocks(n, 64, 256), 256, lds, as_stream(stream)>>>(
+        dirs, n, n_dev, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp);
+    return ngp_launch_status();
+}
+
+int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
+                      const float* denc, float* grad_table, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && denc && grad_table);
+    hash_bwd_kernel<<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, ga, denc,
+                                                                                  grad_table);
+    return ngp_launch_status();
+}
+
 int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
                        const ngp_hashgrid_t* grid, const void* enc_f16, const void* mlp_f16,
                        const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
@@ -640,22 +674,9 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
-    NGP_CHECK_ARG(n >= 0);
-    if (n == 0) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && dirs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp && grad_table);
-    static bool attr_set = false;
-    const size_t lds = (size_t)BWD_LDS_HALFS * sizeof(_Float16);
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)field_bwd_mlp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return NGP_ERANGE;
-        attr_set = true;
-    }
-    hipStream_t s = as_stream(stream);
-    field_bwd_mlp_kernel<<<persistent_blocks(n, 64, 256), 256, lds, s>>>(
-        dirs, n, n_dev, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp);
-    st = ngp_launch_status();
+    st = ngp_field_backward_mlp(dirs, n, n_dev, enc_f16, mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp, stream);
     if (st) return st;
-    hash_bwd_kernel<<<persistent_blocks(n, 256, 4096), 256, 0, s>>>(xyzs, n, n_dev, ga, denc_ws, grad_table);
-    return ngp_launch_status();
+    return ngp_hash_backward(xyzs, n, n_dev, grid, denc_ws, grad_table, stream);
 }
 
 }  // extern "C"

@@ -101,7 +101,8 @@ class NGPTrainer:
         self.gen.manual_seed(1000 + seed + self.rank)
         self.L = vren.lib()
         HG._lib()
-        self.field_events = None  # (start, end) torch.cuda.Event pair around field_forward (bench roofline)
+        # {"field_fwd"|"mlp_bwd"|"hash_bwd": (start, end) torch.cuda.Event} around those launches (bench)
+        self.kernel_events = None
 
     # ------------------------------------------------------------ schedule
     def lr(self):
@@ -201,24 +202,33 @@ class NGPTrainer:
                                          _p(self.noise), self.max_samples, _p(self.rays_a), _p(self.xyzs),
                                          _p(self.dirs), _p(self.deltas), _p(self.ts), s), "march_write")
         HGL = HG._lib()
-        if self.field_events is not None:
-            self.field_events[0].record()
+        if self.kernel_events is not None:
+            self.kernel_events["field_fwd"][0].record()
         vren._ok(HGL.ngp_field_forward(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples),
                                        HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
                                        _p(self.params16), _p(self.sigmas), _p(self.rgbs), _p(self.enc), None, s),
                  "field_forward")
-        if self.field_events is not None:
-            self.field_events[1].record()
+        if self.kernel_events is not None:
+            self.kernel_events["field_fwd"][1].record()
         bg = torch.rand(3, device=self.dev, generator=self.gen) if self.random_bg else self.bg
         vren._ok(L.ngp_composite_loss(_p(self.sigmas), _p(self.rgbs), _p(self.deltas), _p(self.ts), _p(self.rays_a), R,
                                       _p(rgb_gt), _p(bg), self.loss_type, ctypes_float(self.lambda_opacity),
                                       ctypes_float(self.lambda_depth), ctypes_float(self.scale), ctypes_float(1e-4),
                                       _p(self.dsig), _p(self.drgb), _p(self.out_rgb), _p(self.out_op),
                                       _p(self.out_depth), _p(self.out_loss), _p(self.vr_samples), s), "composite_loss")
-        vren._ok(HGL.ngp_field_backward(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples),
-                                        HG.ctypes.byref(self.grid.desc), _p(self.enc), _p(self.params16),
-                                        _p(self.dsig), _p(self.drgb), _p(self.denc), _p(self.grad),
-                                        _p(self.grad[HG.MLP_PARAMS:]), s), "field_backward")
+        ev = self.kernel_events
+        if ev is not None:
+            ev["mlp_bwd"][0].record()
+        vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_samples), _p(self.enc),
+                                            _p(self.params16), _p(self.dsig), _p(self.drgb), _p(self.denc),
+                                            _p(self.grad), s), "field_backward_mlp")
+        if ev is not None:
+            ev["mlp_bwd"][1].record()
+            ev["hash_bwd"][0].record()
+        vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_samples), HG.ctypes.byref(self.grid.desc),
+                                       _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
+        if ev is not None:
+            ev["hash_bwd"][1].record()
         if self.world > 1:
             dist.all_reduce(self.grad, group=self.pg)  # DDP gradient all-reduce (RCCL)
         self.global_step += 1

@@ -40,11 +40,22 @@ from trainer import NGPTrainer  # noqa: E402
 with open(os.path.join(ROOT, "BASELINE.json")) as f:
     BASELINE = json.load(f)
 
-# Algorithmic bytes per sample of the roofline kernel (field forward:
-# 16 levels x 8 corners x fp16x2 gathered + xyz + dir read + fp16 encoding,
-# sigma and rgb written).  See DESIGN.md "Measurement".
-FIELD_FWD_BYTES_PER_SAMPLE = 16 * 8 * 4 + 12 + 12 + 64 + 4 + 12
-HBM_PEAK_GBS = 8000.0
+# Algorithmic work per marched sample of the three per-sample kernels
+# (DESIGN.md "Measurement"):
+#  field_fwd: 16 levels x 8 corners x fp16x2 gathered + xyz + dir read,
+#             fp16 encoding (64 B), sigma + rgb (16 B) written      -> bytes
+#  hash_bwd : xyz (12 B) + dL/denc fp32 (128 B) read + read-modify-write of
+#             16 x 8 x 2 fp32 table gradients (2 x 1024 B)           -> bytes
+#  mlp_bwd  : forward recompute + dX + dW of the 32-64-16 / 32-64-64-16 MLPs
+#             (16-row output layer as computed)                      -> FLOPs
+KERNEL_WORK = {
+    "field_fwd": ("hbm", 16 * 8 * 4 + 12 + 12 + 64 + 4 + 12, "GB/s"),
+    "hash_bwd": ("hbm", 12 + 128 + 2 * 16 * 8 * 2 * 4, "GB/s"),
+    "mlp_bwd": ("mfma", 2 * (32 * 64 + 64 * 16 + 32 * 64 + 64 * 64 + 64 * 16)
+                + 2 * (16 * 64 + 64 * 64 + 64 * 16 + 16 * 64 + 64 * 32)
+                + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32), "TFLOP/s"),
+}
+PEAK = {"hbm": 8000.0, "mfma": 2500.0}  # MI355X: HBM3E GB/s; dense fp16 MFMA TFLOP/s
 
 
 def parse():
@@ -52,7 +63,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--pretrain", type=int, default=400, help="untimed setup training steps (steady-state occupancy)")
+    ap.add_argument("--pretrain", type=int, default=2000, help="untimed setup training steps (steady-state occupancy)")
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--scale", type=float, default=0.5)
     ap.add_argument("--res", type=int, default=800)
@@ -166,22 +177,23 @@ def main():
     # ---- timed region
     n_samples_acc = torch.zeros(1, dtype=torch.int64, device=dev)
     trainer.vr_samples.zero_()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    trainer.timing_events = None
+    names = list(KERNEL_WORK)
+    ev = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in names}
+          for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for i in range(args.steps):
         img, pix, rgb = batch()
-        trainer.field_events = ev[i]
+        trainer.kernel_events = ev[i]
         trainer.step(img, pix, rgb, directions, poses)
         n_samples_acc += trainer.n_samples
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t_el = time.perf_counter() - t_start
-    trainer.field_events = None
+    trainer.kernel_events = None
     t_max = torch.tensor([t_el], device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -189,9 +201,16 @@ def main():
     total_rays = R * args.steps * world
     value = total_rays / t_el
     samples = int(n_samples_acc.item())
-    fwd_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     samples_per_step = samples / args.steps
-    achieved = samples_per_step * FIELD_FWD_BYTES_PER_SAMPLE / (fwd_ms * 1e-3) / 1e9
+    kernels = {}
+    for k in names:
+        ms = sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / args.steps
+        bound, per_sample, unit = KERNEL_WORK[k]
+        achieved = samples_per_step * per_sample / (ms * 1e-3) / (1e9 if bound == "hbm" else 1e12)
+        kernels[k] = {"bound": bound, "achieved": round(achieved, 2), "peak": PEAK[bound], "unit": unit,
+                      "frac": round(achieved / PEAK[bound], 4), "avg_launch_ms": round(ms, 4),
+                      "work_per_sample": per_sample}
+    dominant = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
     rm_s = samples / (R * args.steps)
     vr_s = int(trainer.vr_samples.item()) / (R * args.steps)
     loss = float(trainer.out_loss.sum().item())
@@ -212,11 +231,10 @@ def main():
                        "rm_samples_per_ray": round(rm_s, 2), "vr_samples_per_ray": round(vr_s, 2),
                        "parallelism": f"dp{world}", "last_loss": round(loss, 5),
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
-            "roofline": {"kernel": "field_fwd (hash encode + fused MLPs)", "bound": "hbm",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_sample": FIELD_FWD_BYTES_PER_SAMPLE, "avg_launch_ms": round(fwd_ms, 4),
-                         "samples_per_launch": round(samples_per_step, 1)},
+            "roofline": dict(kernel=dominant, traffic=None, samples_per_launch=round(samples_per_step, 1),
+                             **kernels[dominant]),
+            "kernels": kernels,
+            "ms_per_step_breakdown_note": "kernels = HIP-event averages over the timed steps",
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -175,6 +175,15 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
                        const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
                        float* grad_table, void* stream);
 
+/* The two halves of ngp_field_backward as separate launches (so each can be
+ * timed / overlapped): the MLP backward (writes dL/denc to denc_ws, += grad_mlp)
+ * and the hash-table scatter (+= grad_table from denc). */
+int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const void* enc_f16,
+                           const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs,
+                           float* denc_ws, float* grad_mlp, void* stream);
+int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
+                      const float* denc, float* grad_table, void* stream);
+
 /* ------------------------------------------------------ training step */
 /* Fused compositing + NeRFLoss + compositing backward for one training batch:
  * composite_train_fw (volumerendering.cu:5-44), background blend
