@@ -298,6 +298,67 @@ __global__ void __launch_bounds__(64) march_write_kernel(const float* __restrict
     }
 }
 
+// Single-pass training march: the walk of raymarching.cu:200-234 run once,
+// each occupied sample's (t, dt) stored in the ray's own slot range
+// [r*max_samples, r*max_samples + n_r).  The reference's second walk
+// (:243-279) re-derives exactly these first n_r samples, so storing them is
+// equivalent and halves the latency-bound marching.
+__global__ void __launch_bounds__(64) march_slots_kernel(const float* __restrict__ rays_o,
+                                                         const float* __restrict__ rays_d,
+                                                         const float* __restrict__ hits_t, int64_t n_rays,
+                                                         const float* __restrict__ noise, MarchParams p,
+                                                         int32_t* __restrict__ counts, float* __restrict__ slot_t,
+                                                         float* __restrict__ slot_dt) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    float o[3], d[3], dinv[3];
+    load_ray(rays_o, rays_d, r, o, d, dinv);
+    const float t2 = hits_t[2 * r + 1];
+    float t = start_t(hits_t, noise, r, p);
+    int N = 0;
+    float x, y, z, dt;
+    float* st = slot_t + r * (int64_t)p.max_samples;
+    float* sd = slot_dt + r * (int64_t)p.max_samples;
+    while (0 <= t && t < t2 && N < p.max_samples) {
+        const float tc = t;
+        if (march_step(t, o, d, dinv, p, x, y, z, dt)) {
+            st[N] = tc;
+            sd[N] = dt;
+            N++;
+        }
+    }
+    counts[r] = N;
+}
+
+// Dense ray-ordered outputs from the slots: one wave per ray, lanes over the
+// ray's samples (coalesced 12-B / 4-B stores).  xyz = o + t*d is the same
+// fp32 expression march_step evaluates (no contraction): bit-identical.
+__global__ void __launch_bounds__(256) march_compact_kernel(const float* __restrict__ rays_o,
+                                                            const float* __restrict__ rays_d,
+                                                            const int64_t* __restrict__ rays_a, int64_t n_rays,
+                                                            const float* __restrict__ slot_t,
+                                                            const float* __restrict__ slot_dt, int max_samples,
+                                                            float* __restrict__ xyzs, float* __restrict__ dirs,
+                                                            float* __restrict__ deltas, float* __restrict__ ts) {
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= n_rays) return;
+    const int64_t start = rays_a[3 * r + 1];
+    const int N = (int)rays_a[3 * r + 2];
+    const float o0 = rays_o[3 * r], o1 = rays_o[3 * r + 1], o2 = rays_o[3 * r + 2];
+    const float d0 = rays_d[3 * r], d1 = rays_d[3 * r + 1], d2 = rays_d[3 * r + 2];
+    const float* st = slot_t + r * (int64_t)max_samples;
+    const float* sd = slot_dt + r * (int64_t)max_samples;
+    for (int k = lane; k < N; k += 64) {
+        const float t = st[k];
+        const int64_t s = start + k;
+        xyzs[3 * s] = o0 + t * d0; xyzs[3 * s + 1] = o1 + t * d1; xyzs[3 * s + 2] = o2 + t * d2;
+        dirs[3 * s] = d0; dirs[3 * s + 1] = d1; dirs[3 * s + 2] = d2;
+        ts[s] = t;
+        deltas[s] = sd[k];
+    }
+}
+
 // raymarching.cu:335-404 (test time), zero-filling unused slots itself.
 __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict__ rays_o,
                                                         const float* __restrict__ rays_d,
@@ -433,6 +494,35 @@ int ngp_march_train_write(const float* rays_o, const float* rays_d, const float*
     NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && rays_a && xyzs && dirs && deltas && ts);
     march_write_kernel<<<nblk(n_rays, 64), 64, 0, as_stream(stream)>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
                                                                       rays_a, xyzs, dirs, deltas, ts);
+    return ngp_launch_status();
+}
+
+int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float* hits_t, int64_t n_rays,
+                          const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
+                          const float* noise, int max_samples, int32_t* counts, int64_t* rays_a, int64_t* total,
+                          float* slot_t, float* slot_dt, void* stream) {
+    MarchParams p;
+    int st = march_params(bitfield, cascades, grid_size, scale, exp_step_factor, max_samples, p);
+    if (st) return st;
+    NGP_CHECK_ARG(n_rays >= 0 && total && rays_a && counts);
+    hipStream_t s = as_stream(stream);
+    if (n_rays > 0) {
+        NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && slot_t && slot_dt);
+        march_slots_kernel<<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t,
+                                                           slot_dt);
+    }
+    scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total);
+    return ngp_launch_status();
+}
+
+int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int64_t* rays_a, int64_t n_rays,
+                            const float* slot_t, const float* slot_dt, int max_samples, float* xyzs, float* dirs,
+                            float* deltas, float* ts, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && max_samples >= 1);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(rays_o && rays_d && rays_a && slot_t && slot_dt && xyzs && dirs && deltas && ts);
+    march_compact_kernel<<<nblk(n_rays, 4), 256, 0, as_stream(stream)>>>(rays_o, rays_d, rays_a, n_rays, slot_t,
+                                                                        slot_dt, max_samples, xyzs, dirs, deltas, ts);
     return ngp_launch_status();
 }
 

@@ -40,6 +40,24 @@ __device__ __forceinline__ void rgb_loss(int type, float x, float y, float& l, f
     }
 }
 
+// Samples are consumed in chunks of CH: the loads of a chunk are issued
+// together (their addresses do not depend on the running transmittance), the
+// arithmetic then runs strictly in sample order with the reference's break.
+constexpr int CH = 8;
+struct SampleChunk {
+    float sg[CH], dl[CH], cr[CH], cg[CH], cb[CH], tt[CH];
+};
+__device__ __forceinline__ void load_chunk(SampleChunk& c, const float* __restrict__ sigmas,
+                                           const float* __restrict__ rgbs, const float* __restrict__ deltas,
+                                           const float* __restrict__ ts, int64_t s0, int64_t cnt) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+        const int64_t s = s0 + (j < cnt ? j : 0);
+        c.sg[j] = sigmas[s]; c.dl[j] = deltas[s]; c.tt[j] = ts[s];
+        c.cr[j] = rgbs[3 * s]; c.cg[j] = rgbs[3 * s + 1]; c.cb[j] = rgbs[3 * s + 2];
+    }
+}
+
 __global__ void __launch_bounds__(64) composite_loss_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
@@ -49,19 +67,26 @@ __global__ void __launch_bounds__(64) composite_loss_kernel(
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= n_rays) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
-    // ---- forward
+    // ---- forward (volumerendering.cu:24-43)
     float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
     int64_t samples = 0;
-    while (samples < N) {
-        const int64_t s = start + samples;
-        const float a = 1.0f - __expf(-sigmas[s] * deltas[s]);
-        const float w = a * T;
-        R += w * rgbs[3 * s]; G += w * rgbs[3 * s + 1]; B += w * rgbs[3 * s + 2];
-        D += w * ts[s];
-        O += w;
-        T *= 1.0f - a;
-        if (T <= la.T_thr) break;
-        samples++;
+    bool done = false;
+    SampleChunk c;
+    for (int64_t k0 = 0; k0 < N && !done; k0 += CH) {
+        const int64_t cnt = N - k0 < CH ? N - k0 : CH;
+        load_chunk(c, sigmas, rgbs, deltas, ts, start + k0, cnt);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            if (j >= cnt || done) break;
+            const float a = 1.0f - __expf(-c.sg[j] * c.dl[j]);
+            const float w = a * T;
+            R += w * c.cr[j]; G += w * c.cg[j]; B += w * c.cb[j];
+            D += w * c.tt[j];
+            O += w;
+            T *= 1.0f - a;
+            if (T <= la.T_thr) { done = true; break; }
+            samples++;
+        }
     }
     // ---- background + loss (mean over rays*3 for rgb, over rays otherwise)
     const float bgc[3] = {bg[0], bg[1], bg[2]};
@@ -69,12 +94,12 @@ __global__ void __launch_bounds__(64) composite_loss_kernel(
     float loss = 0.f, g[3], gop = 0.f;
     const float inv3n = la.inv_n_rays / 3.0f;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
+    for (int q = 0; q < 3; ++q) {
         float l, d;
-        rgb_loss(la.loss_type, xc[c], gt[3 * ray + c], l, d);
+        rgb_loss(la.loss_type, xc[q], gt[3 * ray + q], l, d);
         loss += l * inv3n;
-        g[c] = d * inv3n;
-        gop -= g[c] * bgc[c];
+        g[q] = d * inv3n;
+        gop -= g[q] * bgc[q];
     }
     const float o = O + 1e-10f;
     loss += la.lambda_opacity * (-o * logf(o)) * la.inv_n_rays;
@@ -90,26 +115,39 @@ __global__ void __launch_bounds__(64) composite_loss_kernel(
     out_depth[ray] = D;
     out_loss[ray] = loss;
     if (vr_samples) atomicAdd((unsigned long long*)vr_samples, (unsigned long long)samples);
-    // ---- backward (dL/dws = 0)
+    // ---- backward, dL/dws = 0 (volumerendering.cu:124-149); the samples past
+    // the terminating one (index `samples`) get zero gradient.
+    const float gs = gop * (1 - O);
     float Tb = 1.0f, r = 0.f, gg = 0.f, b = 0.f, d = 0.f;
-    int64_t k = 0;
-    while (k < N) {
-        const int64_t s = start + k;
-        const float a = 1.0f - __expf(-sigmas[s] * deltas[s]);
-        const float w = a * Tb;
-        r += w * rgbs[3 * s]; gg += w * rgbs[3 * s + 1]; b += w * rgbs[3 * s + 2];
-        d += w * ts[s];
-        Tb *= 1.0f - a;
-        dL_drgbs[3 * s] = g[0] * w; dL_drgbs[3 * s + 1] = g[1] * w; dL_drgbs[3 * s + 2] = g[2] * w;
-        dL_dsig[s] = deltas[s] * (g[0] * (rgbs[3 * s] * Tb - (R - r)) + g[1] * (rgbs[3 * s + 1] * Tb - (G - gg)) +
-                                  g[2] * (rgbs[3 * s + 2] * Tb - (B - b)) + gop * (1 - O) + gdep * (ts[s] * Tb - (D - d)));
-        if (Tb <= la.T_thr) break;
-        k++;
-    }
-    for (int64_t q = k + 1; q < N; ++q) {
-        const int64_t s = start + q;
-        dL_dsig[s] = 0.f;
-        dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
+    for (int64_t k0 = 0; k0 < N; k0 += CH) {
+        const int64_t cnt = N - k0 < CH ? N - k0 : CH;
+        if (k0 > samples) {  // past termination: zero-fill
+            for (int64_t j = 0; j < cnt; ++j) {
+                const int64_t s = start + k0 + j;
+                dL_dsig[s] = 0.f;
+                dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
+            }
+            continue;
+        }
+        load_chunk(c, sigmas, rgbs, deltas, ts, start + k0, cnt);
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            if (j >= cnt) break;
+            const int64_t k = k0 + j, s = start + k;
+            if (k > samples) {
+                dL_dsig[s] = 0.f;
+                dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
+                continue;
+            }
+            const float a = 1.0f - __expf(-c.sg[j] * c.dl[j]);
+            const float w = a * Tb;
+            r += w * c.cr[j]; gg += w * c.cg[j]; b += w * c.cb[j];
+            d += w * c.tt[j];
+            Tb *= 1.0f - a;
+            dL_drgbs[3 * s] = g[0] * w; dL_drgbs[3 * s + 1] = g[1] * w; dL_drgbs[3 * s + 2] = g[2] * w;
+            dL_dsig[s] = c.dl[j] * (g[0] * (c.cr[j] * Tb - (R - r)) + g[1] * (c.cg[j] * Tb - (G - gg)) +
+                                    g[2] * (c.cb[j] * Tb - (B - b)) + gs + gdep * (c.tt[j] * Tb - (D - d)));
+        }
     }
 }
 

@@ -89,6 +89,7 @@ class NGPTrainer:
         self.n_samples = torch.zeros(1, dtype=torch.int64, device=dev)
         self.xyzs, self.dirs = torch.empty(cap, 3, **f), torch.empty(cap, 3, **f)
         self.deltas, self.ts = torch.empty(cap, **f), torch.empty(cap, **f)
+        self.slot_t, self.slot_dt = torch.empty(cap, **f), torch.empty(cap, **f)  # per-ray sample slots
         self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         self.enc = torch.empty(cap, 32, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
@@ -181,7 +182,7 @@ class NGPTrainer:
         vren.packbits(self.density_grid, self.threshold[:1], self.density_bitfield)
 
     # ---------------------------------------------------------------- step
-    def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses):
+    def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True):
         """One training step on a batch (train.py:174-200).  img/pix (R) i64,
         rgb_gt (R,3) f32, directions (HW,3), poses (n_img,3,4), all on device."""
         L, s = self.L, vren._stream()
@@ -192,15 +193,18 @@ class NGPTrainer:
         vren._ok(L.ngp_raygen_aabb(_p(directions), _p(poses), _p(img_idxs), _p(pix_idxs), R, _p(self.center),
                                    _p(self.half_size), ctypes_float(NEAR_DISTANCE), _p(self.rays_o), _p(self.rays_d),
                                    _p(self.hits_t), s), "raygen")
-        torch.rand(R, out=self.noise, generator=self.gen)  # custom_functions.py:83
-        vren._ok(L.ngp_march_train_count(_p(self.rays_o), _p(self.rays_d), _p(self.hits_t), R, _p(self.density_bitfield),
-                                         self.cascades, self.G, ctypes_float(self.scale), ctypes_float(self.esf),
-                                         _p(self.noise), self.max_samples, _p(self.counts), _p(self.rays_a),
-                                         _p(self.n_samples), s), "march_count")
-        vren._ok(L.ngp_march_train_write(_p(self.rays_o), _p(self.rays_d), _p(self.hits_t), R, _p(self.density_bitfield),
-                                         self.cascades, self.G, ctypes_float(self.scale), ctypes_float(self.esf),
-                                         _p(self.noise), self.max_samples, _p(self.rays_a), _p(self.xyzs),
-                                         _p(self.dirs), _p(self.deltas), _p(self.ts), s), "march_write")
+        if noise is None:
+            torch.rand(R, out=self.noise, generator=self.gen)  # custom_functions.py:83
+        else:
+            self.noise.copy_(noise)
+        vren._ok(L.ngp_march_train_slots(_p(self.rays_o), _p(self.rays_d), _p(self.hits_t), R,
+                                         _p(self.density_bitfield), self.cascades, self.G, ctypes_float(self.scale),
+                                         ctypes_float(self.esf), _p(self.noise), self.max_samples, _p(self.counts),
+                                         _p(self.rays_a), _p(self.n_samples), _p(self.slot_t), _p(self.slot_dt), s),
+                 "march_slots")
+        vren._ok(L.ngp_march_train_compact(_p(self.rays_o), _p(self.rays_d), _p(self.rays_a), R, _p(self.slot_t),
+                                           _p(self.slot_dt), self.max_samples, _p(self.xyzs), _p(self.dirs),
+                                           _p(self.deltas), _p(self.ts), s), "march_compact")
         HGL = HG._lib()
         if self.kernel_events is not None:
             self.kernel_events["field_fwd"][0].record()
@@ -231,6 +235,8 @@ class NGPTrainer:
             ev["hash_bwd"][1].record()
         if self.world > 1:
             dist.all_reduce(self.grad, group=self.pg)  # DDP gradient all-reduce (RCCL)
+        if not apply_adam:  # (tests) leave the summed gradient in self.grad
+            return self.out_loss
         self.global_step += 1
         vren._ok(L.ngp_adam_step(_p(self.params), _p(self.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
                                  _p(self.params16), self.params.numel(), ctypes_float(self.lr()), ctypes_float(0.9),

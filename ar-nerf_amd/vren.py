@@ -45,6 +45,9 @@ def _declare(L):
         "ngp_march_train_count": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, vp, c_int, vp, vp, vp, vp],
         "ngp_march_train_write": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, vp, c_int, vp, vp, vp, vp,
                                   vp, vp],
+        "ngp_march_train_slots": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, vp, c_int, vp, vp, vp, vp,
+                                  vp, vp],
+        "ngp_march_train_compact": [vp, vp, vp, c_int64, vp, vp, c_int, vp, vp, vp, vp, vp],
         "ngp_march_test": [vp, vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, c_int, c_int, vp, vp, vp, vp,
                            vp, vp],
         "ngp_composite_train_fw": [vp, vp, vp, vp, vp, c_int64, c_float, vp, vp, vp, vp, vp, vp],
@@ -196,21 +199,35 @@ def march_train_write(rays_o, rays_d, hits_t, density_bitfield, cascades, scale,
 def raymarching_train(rays_o, rays_d, hits_t, density_bitfield, cascades, scale, exp_step_factor, noise,
                       grid_size, max_samples):
     """raymarching.cu:283-332 -> [rays_a, xyzs, dirs, deltas, ts, counter].
-    counter = [total_samples, n_rays] (int32, like the reference's).  One host
-    sync to size the outputs (the reference syncs on counter[0] slicing,
-    custom_functions.py:91-96)."""
-    counts, rays_a, total = march_train_count(rays_o, rays_d, hits_t, density_bitfield, cascades, scale,
-                                              exp_step_factor, noise, grid_size, max_samples)
-    N = int(total.item())
+    counter = [total_samples, n_rays] (int32, like the reference's).  Single
+    walk per ray into slot scratch, then one host sync to size the outputs
+    (the reference syncs on counter[0] slicing, custom_functions.py:91-96)."""
+    n = rays_o.shape[0]
     dev = rays_o.device
+    counts = torch.empty(n, dtype=torch.int32, device=dev)
+    rays_a = torch.empty(n, 3, dtype=torch.int64, device=dev)
+    total = torch.empty(1, dtype=torch.int64, device=dev)
+    slot_t = torch.empty(n * int(max_samples), device=dev)
+    slot_dt = torch.empty(n * int(max_samples), device=dev)
+    po, pd = _check("rays_o", rays_o, torch.float32), _check("rays_d", rays_d, torch.float32)
+    _ok(lib().ngp_march_train_slots(po, pd, _check("hits_t", hits_t, torch.float32), n,
+                                    _check("density_bitfield", density_bitfield, torch.uint8), int(cascades),
+                                    int(grid_size), float(scale), float(exp_step_factor),
+                                    _check("noise", noise, torch.float32), int(max_samples),
+                                    c_void_p(counts.data_ptr()), c_void_p(rays_a.data_ptr()),
+                                    c_void_p(total.data_ptr()), c_void_p(slot_t.data_ptr()),
+                                    c_void_p(slot_dt.data_ptr()), _stream()), "march_train_slots")
+    N = int(total.item())
     xyzs = torch.empty(N, 3, device=dev)
     dirs = torch.empty(N, 3, device=dev)
     deltas = torch.empty(N, device=dev)
     ts = torch.empty(N, device=dev)
     if N > 0:
-        march_train_write(rays_o, rays_d, hits_t, density_bitfield, cascades, scale, exp_step_factor, noise,
-                          grid_size, max_samples, rays_a, xyzs, dirs, deltas, ts)
-    counter = torch.stack([total[0].to(torch.int32), torch.full_like(total[0], rays_o.shape[0], dtype=torch.int32)])
+        _ok(lib().ngp_march_train_compact(po, pd, c_void_p(rays_a.data_ptr()), n, c_void_p(slot_t.data_ptr()),
+                                          c_void_p(slot_dt.data_ptr()), int(max_samples), c_void_p(xyzs.data_ptr()),
+                                          c_void_p(dirs.data_ptr()), c_void_p(deltas.data_ptr()),
+                                          c_void_p(ts.data_ptr()), _stream()), "march_train_compact")
+    counter = torch.stack([total[0].to(torch.int32), torch.full_like(total[0], n, dtype=torch.int32)])
     return [rays_a, xyzs, dirs, deltas, ts, counter]
 
 

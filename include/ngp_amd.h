@@ -84,6 +84,20 @@ int ngp_march_train_write(const float* rays_o, const float* rays_d, const float*
                           const int64_t* rays_a, float* xyzs, float* dirs, float* deltas,
                           float* ts, void* stream);
 
+/* Single-pass variant of the two calls above (same outputs, bit-identical):
+ * ngp_march_train_slots walks each ray ONCE, storing its samples' (t, dt) in
+ * caller scratch slot_t/slot_dt (n_rays*max_samples f32 each) and producing
+ * counts/rays_a/total; ngp_march_train_compact then writes the dense
+ * ray-ordered xyzs/dirs/deltas/ts (capacity >= total). */
+int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float* hits_t,
+                          int64_t n_rays, const uint8_t* bitfield, int cascades, int grid_size,
+                          float scale, float exp_step_factor, const float* noise, int max_samples,
+                          int32_t* counts, int64_t* rays_a, int64_t* total, float* slot_t,
+                          float* slot_dt, void* stream);
+int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int64_t* rays_a,
+                            int64_t n_rays, const float* slot_t, const float* slot_dt, int max_samples,
+                            float* xyzs, float* dirs, float* deltas, float* ts, void* stream);
+
 /* Replaces vren.raymarching_test (binding.cpp:70-88 -> raymarching.cu:335-454).
  * hits_t (n_rays_total,2) updated in place; alive (n_alive) i64.  Out:
  * xyzs, dirs (n_alive,N_samples,3), deltas, ts (n_alive,N_samples) -- slots

@@ -471,7 +471,17 @@ class OracleTrainer:
                                                                              self.field.rgb_params)}
         self.t = 0
 
-    def step(self, rays_o, rays_d, hits_t, rgb_gt, noise, bg):
+    def flat_grad(self):
+        nd = self.field.n_dens
+        gx, gr = self.field.xyz_params.grad, self.field.rgb_params.grad
+        return torch.cat([gx[:nd], gr, gx[nd:]])
+
+    def flat_params(self):
+        nd = self.field.n_dens
+        px, pr = self.field.xyz_params.detach(), self.field.rgb_params.detach()
+        return torch.cat([px[:nd], pr, px[nd:]])
+
+    def step(self, rays_o, rays_d, hits_t, rgb_gt, noise, bg, apply_adam=True):
         rays_a, xyzs, dirs, deltas, ts, cnt = raymarching_train(rays_o, rays_d, hits_t, self.bitfield, self.cascades,
                                                                 self.scale, 0.0, noise, self.G, 1024)
         sig, rgbs = self.field(xyzs, dirs)
@@ -481,8 +491,11 @@ class OracleTrainer:
         for p in self.state:
             p.grad = None
         loss.backward()
+        self.last = dict(rays_a=rays_a, rgb=rgb.detach(), opacity=op.detach(), depth=dep.detach(), vr=int(vr))
+        if not apply_adam:
+            return float(loss.detach()), int(cnt[0])
         self.t += 1
         for p, (m, v) in self.state.items():
             g = p.grad if p.grad is not None else torch.zeros_like(p)
             adam_(p.data, g.contiguous(), m, v, self.lr, self.t)
-        return float(loss), int(cnt[0])
+        return float(loss.detach()), int(cnt[0])
