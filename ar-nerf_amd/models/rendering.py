@@ -1,0 +1,139 @@
+"""Drop-in for the reference's models/rendering.py:1-319 (render,
+__render_rays_train, __render_rays_test) on the MI355X kernels."""
+import torch
+
+import vren
+from .custom_functions import RayAABBIntersector, RayMarcher, VolumeRenderer
+
+MAX_SAMPLES = 1024
+NEAR_DISTANCE = 0.01
+
+
+@torch.amp.autocast("cuda")
+def render(model, rays_o, rays_d, **kwargs):
+    """models/rendering.py:13-54: AABB intersection + near clamp, then the
+    train or test render function; optional to_cpu / to_numpy."""
+    rays_o = rays_o.contiguous()
+    rays_d = rays_d.contiguous()
+    _, hits_t, _ = RayAABBIntersector.apply(rays_o, rays_d, model.center, model.half_size, 1)
+    hits_t[(hits_t[:, 0, 0] >= 0) & (hits_t[:, 0, 0] < NEAR_DISTANCE), 0, 0] = NEAR_DISTANCE
+    render_func = __render_rays_test if kwargs.get('test_time', False) else __render_rays_train
+    mesh_depth_map = kwargs.get('mesh_depth_map', None)
+    if mesh_depth_map is not None:  # rendering.py:38-44
+        valid_depth = mesh_depth_map >= 1e-6
+        hits_t_s = hits_t[valid_depth]
+        update_min = torch.min(hits_t_s[:, 0, 1], mesh_depth_map[valid_depth])
+        update_min = torch.max(update_min, hits_t_s[:, 0, 0])
+        hits_t[valid_depth, 0, 1] = update_min
+    results = render_func(model, rays_o, rays_d, hits_t, **kwargs)
+    for k, v in results.items():
+        if kwargs.get('to_cpu', False):
+            v = v.cpu()
+            if kwargs.get('to_numpy', False):
+                v = v.numpy()
+        results[k] = v
+    return results
+
+
+def _background(kwargs, rays_d, default):
+    if kwargs.get('SH_bkg', None) is not None:
+        raise NotImplementedError("SH_bkg belongs to the AR-insertion app (insert/), out of scope")
+    im = kwargs.get('IM_bkg', None)
+    return im if im is not None else default
+
+
+@torch.no_grad()
+def __render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
+    """models/rendering.py:162-253 (grows samples per alive ray, composites
+    until T < T_threshold; black background by default)."""
+    exp_step_factor = kwargs.get('exp_step_factor', 0.)
+    results = {}
+    N_rays = len(rays_o)
+    device = rays_o.device
+    opacity = torch.zeros(N_rays, device=device)
+    depth = torch.zeros(N_rays, device=device)
+    rgb = torch.zeros(N_rays, 3, device=device)
+    samples = total_samples = 0
+    alive_indices = torch.arange(N_rays, device=device)
+    min_samples = 1 if exp_step_factor == 0 else 4
+    ht = hits_t[:, 0]
+    while samples < kwargs.get('max_samples', MAX_SAMPLES):
+        N_alive = len(alive_indices)
+        if N_alive == 0:
+            break
+        N_samples = max(min(N_rays // N_alive, 64), min_samples)
+        samples += N_samples
+        xyzs, dirs, deltas, ts, N_eff_samples = vren.raymarching_test(
+            rays_o, rays_d, ht, alive_indices, model.density_bitfield, model.cascades, model.scale, exp_step_factor,
+            model.grid_size, MAX_SAMPLES, N_samples)
+        total_samples += N_eff_samples.sum()
+        xyzs = xyzs.reshape(-1, 3)
+        dirs = dirs.reshape(-1, 3)
+        valid_mask = ~torch.all(dirs == 0, dim=1)
+        if valid_mask.sum() == 0:
+            break
+        sigmas = torch.zeros(len(xyzs), device=device)
+        rgbs = torch.zeros(len(xyzs), 3, device=device)
+        xyzs = xyzs[valid_mask]
+        dirs = dirs[valid_mask]
+        pts_num = xyzs.shape[0]
+        val_batch_size = kwargs.get('val_batch_size', pts_num)
+        sig_res, rgb_res = [], []
+        for i in range(0, pts_num, val_batch_size):
+            s, c = model(xyzs[i:i + val_batch_size], dirs[i:i + val_batch_size], **kwargs)
+            sig_res.append(s)
+            rgb_res.append(c)
+        sigmas[valid_mask] = torch.cat(sig_res, 0).float()
+        rgbs[valid_mask] = torch.cat(rgb_res, 0).float()
+        sigmas = sigmas.view(-1, N_samples)
+        rgbs = rgbs.view(-1, N_samples, 3)
+        vren.composite_test_fw(sigmas, rgbs, deltas, ts, ht, alive_indices, kwargs.get('T_threshold', 1e-4),
+                               N_eff_samples, opacity, depth, rgb)
+        alive_indices = alive_indices[alive_indices >= 0].contiguous()
+    results['opacity'] = opacity
+    results['depth'] = depth
+    results['rgb'] = rgb
+    results['total_samples'] = total_samples
+    rgb_bg = _background(kwargs, rays_d, torch.zeros(3, device=device))
+    if kwargs.get('blend_bkg', True):
+        results['rgb'] += rgb_bg * (1 - opacity)[:, None]
+    return results
+
+
+def __render_rays_train(model, rays_o, rays_d, hits_t, **kwargs):
+    """models/rendering.py:255-298."""
+    exp_step_factor = kwargs.get('exp_step_factor', 0.)
+    results = {}
+    (rays_a, xyzs, dirs, results['deltas'], results['ts'], results['rm_samples']) = RayMarcher.apply(
+        rays_o, rays_d, hits_t[:, 0], model.density_bitfield, model.cascades, model.scale, exp_step_factor,
+        model.grid_size, MAX_SAMPLES)
+    for k, v in kwargs.items():  # supply additional inputs, repeated per ray
+        if isinstance(v, torch.Tensor):
+            kwargs[k] = torch.repeat_interleave(v[rays_a[:, 0]], rays_a[:, 2], 0)
+    sigmas, rgbs = model(xyzs, dirs, **kwargs)
+    (results['vr_samples'], results['opacity'], results['depth'], results['rgb'], results['ws']) = \
+        VolumeRenderer.apply(sigmas, rgbs.contiguous(), results['deltas'], results['ts'], rays_a,
+                             kwargs.get('T_threshold', 1e-4))
+    results['rays_a'] = rays_a
+    if kwargs.get('random_bg', False):
+        rgb_bg = torch.rand(3, device=rays_o.device)
+    elif exp_step_factor == 0:  # synthetic
+        rgb_bg = torch.ones(3, device=rays_o.device)
+    else:  # real
+        rgb_bg = torch.zeros(3, device=rays_o.device)
+    results['rgb'] = results['rgb'] + rgb_bg * (1 - results['opacity'])[:, None]
+    return results
+
+
+@torch.no_grad()
+def render_surface_rgb(model, pts, rays_d, **kwargs):
+    """models/rendering.py:314-319."""
+    H, W, _ = pts.shape
+    _, rgbs = model(pts.reshape(-1, 3).contiguous(), rays_d.reshape(-1, 3).contiguous(), **kwargs)
+    return rgbs.reshape(H, W, 3)
+
+
+def render_surface_normal(model, pts, **kwargs):
+    """models/rendering.py:300-312 needs dsigma/dx through the hash grid
+    (input gradient); a 'next' item."""
+    raise NotImplementedError("hash-grid input gradient (render_surface_normal) is not implemented yet")

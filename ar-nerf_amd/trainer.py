@@ -24,6 +24,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+import ddp
 import hashgrid as HG
 import vren
 
@@ -159,10 +160,8 @@ class NGPTrainer:
                 coords2 = vren.morton3D_invert(indices2.int().contiguous())
                 indices = torch.cat([indices1, indices2])
                 coords = torch.cat([coords1, coords2])
-            if self.world > 1:  # shard the cells
-                n = indices.shape[0]
-                lo, hi = n * self.rank // self.world, n * (self.rank + 1) // self.world
-                indices, coords = indices[lo:hi], coords[lo:hi]
+            if self.world > 1:  # each rank evaluates its share of the cells
+                indices, coords = ddp.shard_cells(indices, coords, self.rank, self.world)
             s = min(2 ** (c - 1), self.scale)
             half_grid_size = s / G
             xyzs_w = (coords / (G - 1) * 2 - 1) * (s - half_grid_size)
@@ -171,14 +170,12 @@ class NGPTrainer:
             flat = (indices + c * G ** 3).contiguous()
             vren._ok(self.L.ngp_density_scatter_max(_p(flat), _p(sig), flat.shape[0], _p(tmp), vren._stream()),
                      "density_scatter_max")
-        if self.world > 1:
-            dist.all_reduce(tmp, op=dist.ReduceOp.MAX, group=self.pg)
+        ddp.combine_density_tmp_(tmp, self.pg)
         st = self.L.ngp_density_grid_ema(_p(self.density_grid), _p(tmp), self.density_grid.numel(),
                                          ctypes_float(decay), ctypes_float(density_threshold), _p(self._sum_cnt),
                                          _p(self.threshold), vren._stream())
         vren._ok(st, "density_grid_ema")
-        if self.world > 1:  # identical threshold on every rank
-            dist.broadcast(self.threshold, src=0, group=self.pg)
+        ddp.sync_threshold_(self.threshold, self.pg)  # identical threshold on every rank
         vren.packbits(self.density_grid, self.threshold[:1], self.density_bitfield)
 
     # ---------------------------------------------------------------- step
@@ -233,8 +230,7 @@ class NGPTrainer:
                                        _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
         if ev is not None:
             ev["hash_bwd"][1].record()
-        if self.world > 1:
-            dist.all_reduce(self.grad, group=self.pg)  # DDP gradient all-reduce (RCCL)
+        ddp.allreduce_grad_(self.grad, self.pg)  # DDP gradient all-reduce (RCCL over xGMI)
         if not apply_adam:  # (tests) leave the summed gradient in self.grad
             return self.out_loss
         self.global_step += 1

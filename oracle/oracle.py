@@ -66,6 +66,10 @@ def lib():
         L.or_sh4.argtypes = [c_int, vp, vp]
         L.or_sh4_unit01.argtypes = [c_int, vp, vp]
         L.or_adam.argtypes = [c_int64, vp, vp, vp, vp, c_float, c_float, c_float, c_float, c_float, c_float]
+        L.or_calc_dt.argtypes = [c_float, c_float, c_int, c_int, c_float]
+        L.or_calc_dt.restype = c_float
+        L.or_mip_from_pos.argtypes = [c_float, c_float, c_float, c_int]
+        L.or_mip_from_dt.argtypes = [c_float, c_int, c_int]
         L.or_f32_to_f16.argtypes = [c_float]
         L.or_f32_to_f16.restype = ctypes.c_uint16
         _lib = L

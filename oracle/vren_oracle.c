@@ -577,3 +577,10 @@ void or_adam(int64_t n, float* p, const float* g, float* m, float* v, float lr, 
 
 /* keep rh() referenced for builds that only use part of the file */
 float or_round_half(float f) { return rh(f); }
+
+/* Exported for known-answer tests only. */
+float or_calc_dt(float t, float esf, int max_samples, int grid_size, float scale) {
+    return calc_dt(t, esf, max_samples, grid_size, scale);
+}
+int or_mip_from_pos(float x, float y, float z, int cascades) { return mip_from_pos(x, y, z, cascades); }
+int or_mip_from_dt(float dt, int grid_size, int cascades) { return mip_from_dt(dt, grid_size, cascades); }

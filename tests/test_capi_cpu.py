@@ -1,0 +1,63 @@
+"""The C-ABI library loads on a GPU-less host and exports every entry point
+include/ngp_amd.h declares; argument checks fail loudly like the
+reference's CHECK_INPUT (no compute is launched here)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+import hashgrid as HG
+import oracle as O
+import vren
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    hdr = open(os.path.join(ROOT, "include", "ngp_amd.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(ngp_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def test_header_declares_the_vren_surface():
+    names = _declared()
+    for n in ("ngp_ray_aabb_intersect", "ngp_morton3d", "ngp_morton3d_invert", "ngp_packbits",
+              "ngp_march_train_count", "ngp_march_train_write", "ngp_march_test", "ngp_composite_train_fw",
+              "ngp_composite_train_bw", "ngp_composite_test_fw", "ngp_field_forward", "ngp_field_backward"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = vren.lib()
+    missing = [n for n in _declared() if not hasattr(L, n)]
+    assert not missing, missing
+    assert L.ngp_version().startswith(b"ngp_amd")
+
+
+def test_library_levels_equal_oracle_levels():
+    for scale in (0.5, 16.0):
+        g = HG.HashGrid(scale)
+        spec = O.HashGridSpec(16, 19, 16, scale=scale)
+        assert g.resolutions == spec.res.tolist() and g.offsets == spec.offsets.tolist()
+        assert list(g.desc.scales)[:16] == spec.scales.tolist()
+
+
+def test_cpu_tensors_are_rejected_like_check_input():
+    x = torch.zeros(4, 3)
+    with pytest.raises(RuntimeError, match="rays_o must be a CUDA tensor"):
+        vren.ray_aabb_intersect(x, x, torch.zeros(1, 3), torch.ones(1, 3), 1)
+    with pytest.raises(RuntimeError, match="coords must be a CUDA tensor"):
+        vren.morton3D(x.int())
+
+
+def test_bad_arguments_return_einval():
+    L = vren.lib()
+    # null pointers with a non-zero size: rejected before any launch
+    assert L.ngp_morton3d(None, 10, None, None) == -1
+    assert L.ngp_composite_train_fw(None, None, None, None, None, 5, 1e-4, None, None, None, None, None, None) == -1
+    assert L.ngp_march_test(None, None, None, None, 1, None, 1, 128, 0.5, 0.0, 1, 1024, None, None, None, None, None,
+                            None) == -1
+    # zero-size calls are no-ops
+    assert L.ngp_morton3d(None, 0, None, None) == 0

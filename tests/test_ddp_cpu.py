@@ -1,0 +1,82 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the data-parallel
+pieces used by trainer.NGPTrainer (ar-nerf_amd/ddp.py)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import ddp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {}
+        # 1) gradient all-reduce == sum of the ranks' gradients
+        g = torch.arange(10, dtype=torch.float32) * (rank + 1)
+        ddp.allreduce_grad_(g)
+        out["grad"] = g
+        # 2) sharded occupancy evaluation + MAX combine == single-process result
+        n = 1000
+        idx = torch.randperm(4096, generator=torch.Generator().manual_seed(0))[:n]
+        coords = torch.stack([idx % 16, (idx // 16) % 16, idx // 256], 1)
+        si, sc = ddp.shard_cells(idx, coords, rank, world)
+        tmp = torch.zeros(4096)
+        tmp[si] = torch.sin(si.float()).abs() + sc.sum(1).float() * 1e-3
+        ddp.combine_density_tmp_(tmp)
+        out["tmp"] = tmp
+        # 3) threshold broadcast from rank 0
+        thr = torch.tensor([1.0 + rank, 2.0])
+        ddp.sync_threshold_(thr)
+        out["thr"] = thr
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_pieces_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    base = torch.arange(10, dtype=torch.float32)
+    for r in range(2):
+        torch.testing.assert_close(res[r]["grad"], base * 3)
+        assert res[r]["thr"].tolist() == [1.0, 2.0]
+    idx = torch.randperm(4096, generator=torch.Generator().manual_seed(0))[:1000]
+    coords = torch.stack([idx % 16, (idx // 16) % 16, idx // 256], 1)
+    full = torch.zeros(4096)
+    full[idx] = torch.sin(idx.float()).abs() + coords.sum(1).float() * 1e-3
+    torch.testing.assert_close(res[0]["tmp"], full)
+    assert torch.equal(res[0]["tmp"], res[1]["tmp"])
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (2_097_152, 8), (7, 8)])
+def test_shard_range_covers_exactly_once(n, world):
+    seen = []
+    for r in range(world):
+        lo, hi = ddp.shard_range(n, r, world)
+        seen += list(range(lo, hi)) if n < 100 else [lo, hi]
+    if n < 100:
+        assert sorted(seen) == list(range(n))
+    else:
+        assert seen[0] == 0 and seen[-1] == n and all(seen[2 * i + 1] == seen[2 * i + 2] for i in range(world - 1))
