@@ -344,7 +344,8 @@ __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& 
 }
 
 __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
-    const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const _Float16* __restrict__ enc,
+    const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
+    const _Float16* __restrict__ enc,
     const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
     float* __restrict__ denc, float* __restrict__ grad_mlp) {
     extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
@@ -361,8 +362,9 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
     for (int k = 0; k < NACC; ++k) acc[k] = z;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wid) * 16; base < N; base += nw * 16) {
-        const int64_t i = base + s;
-        const bool valid = i < N;
+        const int64_t j = base + s;  // compact position (denc row)
+        const bool valid = j < N;
+        const int64_t i = valid && sidx ? (int64_t)sidx[j] : j;  // sample
         h8 e = {0, 0, 0, 0, 0, 0, 0, 0};
         float dx = 0.f, dy = 0.f, dz = 1.f, dsig = 0.f, gr[3] = {0.f, 0.f, 0.f};
         if (valid) {
@@ -444,7 +446,7 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT1 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da1h[kt], c);
             c = c * is_1;
-            if (valid) *reinterpret_cast<f4*>(denc + i * 32 + 16 * t + 4 * g) = c;
+            if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
         }
         // ---- weight gradients: transpose operands through LDS, K = 16 samples
         wave_sync_lds();  // previous iteration's reads are done
@@ -522,7 +524,8 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
 // so equal indices of the same (cx, f) at lane stride 4 are first summed by a
 // segmented suffix scan; only each run's head issues its fp32 atomic.
 __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__ xyzs, int64_t n,
-                                                       const int64_t* __restrict__ n_dev, GridArgs ga,
+                                                       const int64_t* __restrict__ n_dev,
+                                                       const int32_t* __restrict__ sidx, GridArgs ga,
                                                        const float* __restrict__ denc, float* __restrict__ grad) {
     __shared__ LevelLds lv;
     load_levels(ga, lv);
@@ -531,13 +534,14 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
     const int lane = threadIdx.x & 63, s = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16; base < N; base += nw * 16) {
-        const int64_t i = base + s;
-        const bool valid = i < N;
+        const int64_t j = base + s;  // compact position (denc row)
+        const bool valid = j < N;
+        const int64_t i = valid && sidx ? (int64_t)sidx[j] : j;  // sample
         float in[3];
         load_x01(xyzs, i, valid, ga, in);
 #pragma unroll 1
         for (int l = 0; l < L; ++l) {
-            const float gd = valid ? denc[i * 32 + 2 * l + f] : 0.f;
+            const float gd = valid ? denc[j * 32 + 2 * l + f] : 0.f;
             const float sc = lv.scale[l];
             const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
             const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
@@ -635,7 +639,8 @@ int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, cons
     return ngp_launch_status();
 }
 
-int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const void* enc_f16,
+int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                           const void* enc_f16,
                            const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws,
                            float* grad_mlp, void* stream) {
     NGP_CHECK_ARG(n >= 0);
@@ -650,20 +655,21 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
         attr_set = true;
     }
     field_bwd_mlp_kernel<<<persistent_blocks(n, 64, 256), 256, lds, as_stream(stream)>>>(
-        dirs, n, n_dev, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp);
+        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
+        grad_mlp);
     return ngp_launch_status();
 }
 
-int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
-                      const float* denc, float* grad_table, void* stream) {
+int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                      const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && denc && grad_table);
-    hash_bwd_kernel<<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, ga, denc,
-                                                                                  grad_table);
+    hash_bwd_kernel<<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga,
+                                                                                  denc, grad_table);
     return ngp_launch_status();
 }
 
@@ -674,9 +680,10 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
-    st = ngp_field_backward_mlp(dirs, n, n_dev, enc_f16, mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp, stream);
+    st = ngp_field_backward_mlp(dirs, n, n_dev, nullptr, enc_f16, mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp,
+                                stream);
     if (st) return st;
-    return ngp_hash_backward(xyzs, n, n_dev, grid, denc_ws, grad_table, stream);
+    return ngp_hash_backward(xyzs, n, n_dev, nullptr, grid, denc_ws, grad_table, stream);
 }
 
 }  // extern "C"

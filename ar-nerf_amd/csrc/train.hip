@@ -63,7 +63,7 @@ __global__ void __launch_bounds__(64) composite_loss_kernel(
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
     const float* __restrict__ bg, LossArgs la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
     float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
-    float* __restrict__ out_loss, int64_t* __restrict__ vr_samples) {
+    float* __restrict__ out_loss, int64_t* __restrict__ vr_samples, int32_t* __restrict__ n_active) {
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= n_rays) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
@@ -115,6 +115,9 @@ __global__ void __launch_bounds__(64) composite_loss_kernel(
     out_depth[ray] = D;
     out_loss[ray] = loss;
     if (vr_samples) atomicAdd((unsigned long long*)vr_samples, (unsigned long long)samples);
+    // samples past the terminating one get exactly zero gradient below, so
+    // the field backward only needs the first n_active samples of this row
+    if (n_active) n_active[n] = (int32_t)(done ? samples + 1 : N);
     // ---- backward, dL/dws = 0 (volumerendering.cu:124-149); the samples past
     // the terminating one (index `samples`) get zero gradient.
     const float gs = gop * (1 - O);
@@ -224,6 +227,71 @@ __global__ void grid_threshold_kernel(const float* __restrict__ sum_cnt, float t
     thr[1] = mean;
 }
 
+// ---------------------------------------------------- active-sample map
+// Exclusive scan of the per-row active counts (one 1024-lane workgroup) and
+// the compacted index map sample_idx[j] = rays_a[row].start + k for the
+// first n_active[row] samples of every row (one wave per row).
+__global__ void __launch_bounds__(1024) active_scan_kernel(const int32_t* __restrict__ n_active, int64_t n_rows,
+                                                           int64_t* __restrict__ act_start,
+                                                           int64_t* __restrict__ total) {
+    __shared__ int64_t wave_sums[16];
+    __shared__ int64_t carry_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    constexpr int PER = 8;
+    for (int64_t base = 0; base < n_rows; base += 1024 * PER) {
+        int64_t v[PER], local = 0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int64_t i = base + (int64_t)tid * PER + k;
+            v[k] = i < n_rows ? n_active[i] : 0;
+            local += v[k];
+        }
+        int64_t incl = local;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wave_sums[wid] = incl;
+        __syncthreads();
+        if (wid == 0) {
+            int64_t ws = lane < 16 ? wave_sums[lane] : 0;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                const int64_t y = __shfl_up(ws, off, 64);
+                if (lane >= off) ws += y;
+            }
+            if (lane < 16) wave_sums[lane] = ws;
+        }
+        __syncthreads();
+        int64_t run = carry_s + (wid > 0 ? wave_sums[wid - 1] : 0) + incl - local;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int64_t i = base + (int64_t)tid * PER + k;
+            if (i < n_rows) act_start[i] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        if (tid == 1023) carry_s = run;
+        __syncthreads();
+    }
+    if (tid == 0) *total = carry_s;
+}
+
+__global__ void __launch_bounds__(256) active_map_kernel(const int32_t* __restrict__ n_active,
+                                                         const int64_t* __restrict__ rays_a,
+                                                         const int64_t* __restrict__ act_start, int64_t n_rows,
+                                                         int32_t* __restrict__ sample_idx) {
+    const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (r >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int na = n_active[r];
+    const int64_t src = rays_a[3 * r + 1], dst = act_start[r];
+    for (int k = lane; k < na; k += 64) sample_idx[dst + k] = (int32_t)(src + k);
+}
+
 }  // namespace ngp
 
 using namespace ngp;
@@ -234,14 +302,14 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
                        const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg, int loss_type,
                        float lambda_opacity, float lambda_depth, float depth_scale, float T_threshold,
                        float* dL_dsigmas, float* dL_drgbs, float* out_rgb, float* out_opacity, float* out_depth,
-                       float* out_loss, int64_t* vr_samples, void* stream) {
+                       float* out_loss, int64_t* vr_samples, int32_t* n_active, void* stream) {
     NGP_CHECK_ARG(n_rays >= 0 && loss_type >= 0 && loss_type <= 3 && depth_scale > 0);
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_a && rgb_gt && bg && out_rgb && out_opacity && out_depth && out_loss);
     LossArgs la{loss_type, lambda_opacity, lambda_depth, depth_scale, 1.0f / (float)n_rays, T_threshold};
     composite_loss_kernel<<<(unsigned)((n_rays + 63) / 64), 64, 0, as_stream(stream)>>>(
         sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
-        out_depth, out_loss, vr_samples);
+        out_depth, out_loss, vr_samples, n_active);
     return ngp_launch_status();
 }
 
@@ -280,6 +348,18 @@ int ngp_density_grid_ema(float* density_grid, const float* grid_tmp, int64_t n, 
     if (blocks > 2048) blocks = 2048;
     grid_ema_kernel<<<(unsigned)blocks, 256, 0, s>>>(density_grid, grid_tmp, n, decay, sum_cnt_ws);
     grid_threshold_kernel<<<1, 1, 0, s>>>(sum_cnt_ws, thr_max, threshold_out);
+    return ngp_launch_status();
+}
+
+int ngp_active_samples(const int32_t* n_active, const int64_t* rays_a, int64_t n_rows, int64_t* act_start_ws,
+                       int64_t* n_active_total, int32_t* sample_idx, void* stream) {
+    NGP_CHECK_ARG(n_rows >= 0 && n_active_total);
+    hipStream_t s = as_stream(stream);
+    if (n_rows > 0) NGP_CHECK_ARG(n_active && rays_a && act_start_ws && sample_idx);
+    active_scan_kernel<<<1, 1024, 0, s>>>(n_active, n_rows, act_start_ws, n_active_total);
+    if (n_rows > 0)
+        active_map_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, s>>>(n_active, rays_a, act_start_ws, n_rows,
+                                                                      sample_idx);
     return ngp_launch_status();
 }
 

@@ -43,8 +43,8 @@ def _lib():
         L.ngp_field_forward.argtypes = [vp, vp, c_int64, vp, P, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_density_forward.argtypes = [vp, c_int64, vp, P, vp, vp, vp, vp, vp]
         L.ngp_field_backward.argtypes = [vp, vp, c_int64, vp, P, vp, vp, vp, vp, vp, vp, vp, vp]
-        L.ngp_field_backward_mlp.argtypes = [vp, c_int64, vp, vp, vp, vp, vp, vp, vp, vp]
-        L.ngp_hash_backward.argtypes = [vp, c_int64, vp, P, vp, vp, vp]
+        L.ngp_field_backward_mlp.argtypes = [vp, c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.ngp_hash_backward.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
         for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_field_backward, L.ngp_field_backward_mlp,
                   L.ngp_hash_backward):
             f.restype = c_int

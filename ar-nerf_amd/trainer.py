@@ -98,6 +98,11 @@ class NGPTrainer:
         self.out_rgb, self.out_op = torch.empty(R, 3, **f), torch.empty(R, **f)
         self.out_depth, self.out_loss = torch.empty(R, **f), torch.empty(R, **f)
         self.vr_samples = torch.zeros(1, dtype=torch.int64, device=dev)
+        # gradient-carrying samples (up to each ray's termination): index map
+        self.n_active = torch.empty(R, dtype=torch.int32, device=dev)
+        self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
+        self.n_active_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.sample_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         self.bg = torch.ones(3, **f) if self.esf == 0 else torch.zeros(3, **f)  # models/rendering.py:287-296
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(1000 + seed + self.rank)
@@ -216,17 +221,22 @@ class NGPTrainer:
                                       _p(rgb_gt), _p(bg), self.loss_type, ctypes_float(self.lambda_opacity),
                                       ctypes_float(self.lambda_depth), ctypes_float(self.scale), ctypes_float(1e-4),
                                       _p(self.dsig), _p(self.drgb), _p(self.out_rgb), _p(self.out_op),
-                                      _p(self.out_depth), _p(self.out_loss), _p(self.vr_samples), s), "composite_loss")
+                                      _p(self.out_depth), _p(self.out_loss), _p(self.vr_samples), _p(self.n_active),
+                                      s), "composite_loss")
+        vren._ok(L.ngp_active_samples(_p(self.n_active), _p(self.rays_a), R, _p(self.act_start),
+                                      _p(self.n_active_total), _p(self.sample_idx), s), "active_samples")
         ev = self.kernel_events
         if ev is not None:
             ev["mlp_bwd"][0].record()
-        vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_samples), _p(self.enc),
+        vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                                            _p(self.enc),
                                             _p(self.params16), _p(self.dsig), _p(self.drgb), _p(self.denc),
                                             _p(self.grad), s), "field_backward_mlp")
         if ev is not None:
             ev["mlp_bwd"][1].record()
             ev["hash_bwd"][0].record()
-        vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_samples), HG.ctypes.byref(self.grid.desc),
+        vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                                       HG.ctypes.byref(self.grid.desc),
                                        _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
         if ev is not None:
             ev["hash_bwd"][1].record()

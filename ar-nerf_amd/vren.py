@@ -54,7 +54,8 @@ def _declare(L):
         "ngp_composite_train_bw": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, c_int64, vp, vp, vp, c_float, vp, vp, vp],
         "ngp_composite_test_fw": [vp, vp, vp, vp, c_int64, c_int, vp, c_float, vp, vp, vp, vp, vp],
         "ngp_composite_loss": [vp, vp, vp, vp, vp, c_int64, vp, vp, c_int, c_float, c_float, c_float, c_float, vp,
-                               vp, vp, vp, vp, vp, vp, vp],
+                               vp, vp, vp, vp, vp, vp, vp, vp],
+        "ngp_active_samples": [vp, vp, c_int64, vp, vp, vp, vp],
         "ngp_adam_step": [vp, vp, vp, vp, vp, c_int64, c_float, c_float, c_float, c_float, c_int64, c_float, c_int,
                           vp],
         "ngp_density_scatter_max": [vp, vp, c_int64, vp, vp],

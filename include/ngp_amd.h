@@ -191,12 +191,14 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
 
 /* The two halves of ngp_field_backward as separate launches (so each can be
  * timed / overlapped): the MLP backward (writes dL/denc to denc_ws, += grad_mlp)
- * and the hash-table scatter (+= grad_table from denc). */
-int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const void* enc_f16,
-                           const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs,
-                           float* denc_ws, float* grad_mlp, void* stream);
-int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
-                      const float* denc, float* grad_table, void* stream);
+ * and the hash-table scatter (+= grad_table from denc).  sample_idx (nullable):
+ * process only the samples sample_idx[0..n) (compact row j of denc_ws <->
+ * sample sample_idx[j]); see ngp_active_samples. */
+int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                           const void* enc_f16, const void* mlp_f16, const float* dL_dsigmas,
+                           const float* dL_drgbs, float* denc_ws, float* grad_mlp, void* stream);
+int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                      const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* stream);
 
 /* ------------------------------------------------------ training step */
 /* Fused compositing + NeRFLoss + compositing backward for one training batch:
@@ -207,12 +209,21 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
  * and composite_train_bw with dL/dws = 0.  rgb_gt (n_rays,3).
  * Out: dL_dsigmas (N), dL_drgbs (N,3); per ray out_rgb (n_rays,3) (after bg),
  * out_opacity, out_depth, out_loss (n_rays; sum = the batch loss);
- * vr_samples (1) i64 += composited samples (nullable). */
+ * vr_samples (1) i64 += composited samples (nullable); n_active (n_rays) i32
+ * (nullable) = samples of each row that can carry gradient (up to and
+ * including the terminating one; all later ones get exactly 0). */
 int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
                        const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg,
                        int loss_type, float lambda_opacity, float lambda_depth, float depth_scale,
                        float T_threshold, float* dL_dsigmas, float* dL_drgbs, float* out_rgb,
                        float* out_opacity, float* out_depth, float* out_loss, int64_t* vr_samples,
+                       int32_t* n_active, void* stream);
+
+/* Compacted list of the gradient-carrying samples: act_start_ws (n_rows) i64
+ * scratch, n_active_total (1) i64, sample_idx (>= total) i32 with
+ * sample_idx[act_start[r] + k] = rays_a[r].start + k, k < n_active[r]. */
+int ngp_active_samples(const int32_t* n_active, const int64_t* rays_a, int64_t n_rows,
+                       int64_t* act_start_ws, int64_t* n_active_total, int32_t* sample_idx,
                        void* stream);
 
 /* apex FusedAdam step (train.py:146; weight decay 0) over n (multiple of 4)
