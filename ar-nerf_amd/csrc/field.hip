@@ -361,18 +361,35 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
 #pragma unroll
     for (int k = 0; k < NACC; ++k) acc[k] = z;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wid) * 16; base < N; base += nw * 16) {
+    // per-sample inputs of the NEXT column block are loaded while this one
+    // computes (one wave per SIMD: nothing else would hide the latency)
+    struct In {
+        h8 e;
+        float dx, dy, dz, dsig, gr[3];
+    };
+    auto load_in = [&](int64_t b, In& x) {
+        const int64_t jj = b + s;
+        x.e = h8{0, 0, 0, 0, 0, 0, 0, 0};
+        x.dx = 0.f; x.dy = 0.f; x.dz = 1.f; x.dsig = 0.f; x.gr[0] = x.gr[1] = x.gr[2] = 0.f;
+        if (jj < N) {
+            const int64_t ii = sidx ? (int64_t)sidx[jj] : jj;
+            x.e = *reinterpret_cast<const h8*>(enc + ii * 32 + 8 * g);
+            x.dx = dirs[3 * ii]; x.dy = dirs[3 * ii + 1]; x.dz = dirs[3 * ii + 2];
+            x.dsig = dL_dsig[ii];
+            x.gr[0] = dL_drgb[3 * ii]; x.gr[1] = dL_drgb[3 * ii + 1]; x.gr[2] = dL_drgb[3 * ii + 2];
+        }
+    };
+    int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wid) * 16;
+    In cur;
+    load_in(base, cur);
+    for (; base < N; base += nw * 16) {
+        In nxt;
+        load_in(base + nw * 16, nxt);
         const int64_t j = base + s;  // compact position (denc row)
         const bool valid = j < N;
-        const int64_t i = valid && sidx ? (int64_t)sidx[j] : j;  // sample
-        h8 e = {0, 0, 0, 0, 0, 0, 0, 0};
-        float dx = 0.f, dy = 0.f, dz = 1.f, dsig = 0.f, gr[3] = {0.f, 0.f, 0.f};
-        if (valid) {
-            e = *reinterpret_cast<const h8*>(enc + i * 32 + 8 * g);
-            dx = dirs[3 * i]; dy = dirs[3 * i + 1]; dz = dirs[3 * i + 2];
-            dsig = dL_dsig[i];
-            gr[0] = dL_drgb[3 * i]; gr[1] = dL_drgb[3 * i + 1]; gr[2] = dL_drgb[3 * i + 2];
-        }
+        const h8 e = cur.e;
+        const float dx = cur.dx, dy = cur.dy, dz = cur.dz, dsig = cur.dsig;
+        const float gr[3] = {cur.gr[0], cur.gr[1], cur.gr[2]};
         // ---- forward recompute
         h4 h1[4];
         const h4 hh = density_net(e, sw, s, g, h1);
@@ -494,6 +511,7 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
 #pragma unroll
             for (int nt = 0; nt < 2; ++nt, ++k) acc[k] += mfma16(ga, get_tile(scr + (T_E + nt) * TTILE, s, g), z) * is_1;
         }
+        cur = nxt;
     }
     // ---- block reduction of the 40 tiles in LDS (fp32), then one global add each
     __syncthreads();

@@ -144,30 +144,62 @@ struct MarchParams {
 // One step of the reference's occupancy walk (raymarching.cu:205-233):
 // returns true and advances t by dt if the sample at t is occupied,
 // otherwise jumps t over the empty voxel with repeated calc_dt steps.
+// SIMPLE = (cascades == 1 && esf == 0): then mip == 0, mip_bound ==
+// min(0.5, scale) and dt == sqrt(3)/max_samples exactly (the general
+// expressions fold to these constants), so the compiler drops frexp /
+// scalbn / the division per step -- same values, bit for bit.
+// `wcache` holds the 64-bit bitfield word (a Morton-aligned 4x4x4 block of
+// cells) last loaded by this lane; consecutive samples along a ray mostly
+// stay in the same block, so most occupancy tests need no memory access.
+struct WordCache {
+    uint32_t idx = 0xffffffffu;
+    uint64_t word = 0;
+};
+
+template <bool SIMPLE>
 __device__ __forceinline__ bool march_step(float& t, const float o[3], const float d[3], const float dinv[3],
-                                           const MarchParams& p, float& x, float& y, float& z, float& dt) {
+                                           const MarchParams& p, float& x, float& y, float& z, float& dt,
+                                           WordCache& wc) {
     const uint32_t G = (uint32_t)p.grid_size;
     const uint32_t grid_size3 = G * G * G;
     const float grid_size_inv = 1.0f / p.grid_size;
     x = o[0] + t * d[0]; y = o[1] + t * d[1]; z = o[2] + t * d[2];
-    dt = calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
-    const int mip = max(mip_from_pos(x, y, z, p.cascades), mip_from_dt(dt, p.grid_size, p.cascades));
-    const float mip_bound = fminf(scalbnf(1.0f, mip - 1), p.scale);
-    const float mip_bound_inv = 1 / mip_bound;
+    int mip;
+    float mip_bound, mip_bound_inv;
+    if constexpr (SIMPLE) {
+        dt = NGP_SQRT3 / p.max_samples;  // = clamp(t*0, sqrt3/max, 2 sqrt3 scale/G), t finite
+        mip = 0;
+        mip_bound = fminf(0.5f, p.scale);
+        mip_bound_inv = 1 / mip_bound;
+    } else {
+        dt = calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
+        mip = max(mip_from_pos(x, y, z, p.cascades), mip_from_dt(dt, p.grid_size, p.cascades));
+        mip_bound = fminf(scalbnf(1.0f, mip - 1), p.scale);
+        mip_bound_inv = 1 / mip_bound;
+    }
     const float gm1 = p.grid_size - 1.0f;
     const int nx = (int)clampf(0.5f * (x * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
     const int ny = (int)clampf(0.5f * (y * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
     const int nz = (int)clampf(0.5f * (z * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
     const uint32_t idx = (uint32_t)mip * grid_size3 + morton3((uint32_t)nx, (uint32_t)ny, (uint32_t)nz);
-    const bool occ = (p.bitfield[idx / 8] >> (idx % 8)) & 1u;
+    const uint32_t wi = idx >> 6;
+    if (wi != wc.idx) {  // bitfield is (C*G^3/8) bytes, G^3 a multiple of 64 for G >= 4
+        wc.word = reinterpret_cast<const uint64_t*>(p.bitfield)[wi];
+        wc.idx = wi;
+    }
+    const bool occ = (wc.word >> (idx & 63u)) & 1ull;
     if (occ) { t += dt; return true; }
     const float tx = (((nx + 0.5f + 0.5f * copysignf(1.0f, d[0])) * grid_size_inv * 2 - 1) * mip_bound - x) * dinv[0];
     const float ty = (((ny + 0.5f + 0.5f * copysignf(1.0f, d[1])) * grid_size_inv * 2 - 1) * mip_bound - y) * dinv[1];
     const float tz = (((nz + 0.5f + 0.5f * copysignf(1.0f, d[2])) * grid_size_inv * 2 - 1) * mip_bound - z) * dinv[2];
     const float t_target = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
-    do {
-        t += calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
-    } while (t < t_target);
+    if constexpr (SIMPLE) {
+        do { t += dt; } while (t < t_target);
+    } else {
+        do {
+            t += calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
+        } while (t < t_target);
+    }
     return false;
 }
 
@@ -192,6 +224,7 @@ __device__ __forceinline__ float start_t(const float* hits_t, const float* noise
 }
 
 // Pass 1 (raymarching.cu:200-234)
+template <bool SIMPLE>
 __global__ void __launch_bounds__(64) march_count_kernel(const float* __restrict__ rays_o,
                                                          const float* __restrict__ rays_d,
                                                          const float* __restrict__ hits_t, int64_t n_rays,
@@ -205,7 +238,8 @@ __global__ void __launch_bounds__(64) march_count_kernel(const float* __restrict
     float t = start_t(hits_t, noise, r, p);
     int N = 0;
     float x, y, z, dt;
-    while (0 <= t && t < t2 && N < p.max_samples) N += march_step(t, o, d, dinv, p, x, y, z, dt) ? 1 : 0;
+    WordCache wc;
+    while (0 <= t && t < t2 && N < p.max_samples) N += march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc) ? 1 : 0;
     counts[r] = N;
 }
 
@@ -267,6 +301,7 @@ __global__ void __launch_bounds__(1024) scan_rays_kernel(const int32_t* __restri
 }
 
 // Pass 2 (raymarching.cu:236-279) at the scanned starts.
+template <bool SIMPLE>
 __global__ void __launch_bounds__(64) march_write_kernel(const float* __restrict__ rays_o,
                                                          const float* __restrict__ rays_d,
                                                          const float* __restrict__ hits_t, int64_t n_rays,
@@ -285,9 +320,10 @@ __global__ void __launch_bounds__(64) march_write_kernel(const float* __restrict
     float t = start_t(hits_t, noise, r, p);
     int samples = 0;
     float x, y, z, dt;
+    WordCache wc;
     while (t < t2 && samples < N) {
         const float tc = t;
-        if (march_step(t, o, d, dinv, p, x, y, z, dt)) {
+        if (march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc)) {
             const int64_t s = start + samples;
             xyzs[3 * s] = x; xyzs[3 * s + 1] = y; xyzs[3 * s + 2] = z;
             dirs[3 * s] = d[0]; dirs[3 * s + 1] = d[1]; dirs[3 * s + 2] = d[2];
@@ -303,6 +339,7 @@ __global__ void __launch_bounds__(64) march_write_kernel(const float* __restrict
 // [r*max_samples, r*max_samples + n_r).  The reference's second walk
 // (:243-279) re-derives exactly these first n_r samples, so storing them is
 // equivalent and halves the latency-bound marching.
+template <bool SIMPLE>
 __global__ void __launch_bounds__(64) march_slots_kernel(const float* __restrict__ rays_o,
                                                          const float* __restrict__ rays_d,
                                                          const float* __restrict__ hits_t, int64_t n_rays,
@@ -319,9 +356,10 @@ __global__ void __launch_bounds__(64) march_slots_kernel(const float* __restrict
     float x, y, z, dt;
     float* st = slot_t + r * (int64_t)p.max_samples;
     float* sd = slot_dt + r * (int64_t)p.max_samples;
+    WordCache wc;
     while (0 <= t && t < t2 && N < p.max_samples) {
         const float tc = t;
-        if (march_step(t, o, d, dinv, p, x, y, z, dt)) {
+        if (march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc)) {
             st[N] = tc;
             sd[N] = dt;
             N++;
@@ -360,6 +398,7 @@ __global__ void __launch_bounds__(256) march_compact_kernel(const float* __restr
 }
 
 // raymarching.cu:335-404 (test time), zero-filling unused slots itself.
+template <bool SIMPLE>
 __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict__ rays_o,
                                                         const float* __restrict__ rays_d,
                                                         float* __restrict__ hits_t,
@@ -377,9 +416,10 @@ __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict_
     int s = 0;
     float x, y, z, dt;
     const int64_t base = n * (int64_t)N_samples;
+    WordCache wc;
     while (t < t2 && s < N_samples) {
         const float tc = t;
-        if (march_step(t, o, d, dinv, p, x, y, z, dt)) {
+        if (march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc)) {
             const int64_t q = base + s;
             xyzs[3 * q] = x; xyzs[3 * q + 1] = y; xyzs[3 * q + 2] = z;
             dirs[3 * q] = d[0]; dirs[3 * q + 1] = d[1]; dirs[3 * q + 2] = d[2];
@@ -457,9 +497,15 @@ int ngp_packbits(const float* density_grid, int64_t n_bytes, float threshold, co
     return ngp_launch_status();
 }
 
+// cascades == 1 and esf == 0 (the Lego configuration): see march_step.
+// Also requires the bitfield to be 8-byte aligned for the word loads (torch
+// allocations are).  dt_scale must be >= 0 so the constant-dt fold holds.
+static bool march_simple(const MarchParams& p) { return p.cascades == 1 && p.esf == 0.0f && p.dt_scale >= 0.0f; }
+
 static int march_params(const uint8_t* bf, int cascades, int grid_size, float scale, float esf, int max_samples,
                         MarchParams& p) {
-    if (!bf || cascades < 1 || grid_size < 1 || grid_size > 1024 || max_samples < 1) return NGP_EINVAL;
+    if (!bf || cascades < 1 || grid_size < 4 || grid_size > 1024 || max_samples < 1) return NGP_EINVAL;
+    if (((uintptr_t)bf & 7u) != 0) return NGP_EINVAL;  // 64-bit word loads
     p.bitfield = bf; p.cascades = cascades; p.grid_size = grid_size; p.max_samples = max_samples;
     p.scale = scale; p.esf = esf; p.dt_scale = scale;
     return NGP_OK;
@@ -476,7 +522,8 @@ int ngp_march_train_count(const float* rays_o, const float* rays_d, const float*
     hipStream_t s = as_stream(stream);
     if (n_rays > 0) {
         NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise);
-        march_count_kernel<<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts);
+        if (march_simple(p)) march_count_kernel<true><<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts);
+        else march_count_kernel<false><<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts);
     }
     scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total);
     return ngp_launch_status();
@@ -492,8 +539,12 @@ int ngp_march_train_write(const float* rays_o, const float* rays_d, const float*
     NGP_CHECK_ARG(n_rays >= 0);
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && rays_a && xyzs && dirs && deltas && ts);
-    march_write_kernel<<<nblk(n_rays, 64), 64, 0, as_stream(stream)>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
-                                                                      rays_a, xyzs, dirs, deltas, ts);
+    if (march_simple(p))
+        march_write_kernel<true><<<nblk(n_rays, 64), 64, 0, as_stream(stream)>>>(rays_o, rays_d, hits_t, n_rays, noise,
+                                                                                p, rays_a, xyzs, dirs, deltas, ts);
+    else
+        march_write_kernel<false><<<nblk(n_rays, 64), 64, 0, as_stream(stream)>>>(rays_o, rays_d, hits_t, n_rays,
+                                                                                 noise, p, rays_a, xyzs, dirs, deltas, ts);
     return ngp_launch_status();
 }
 
@@ -508,8 +559,12 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
     hipStream_t s = as_stream(stream);
     if (n_rays > 0) {
         NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && slot_t && slot_dt);
-        march_slots_kernel<<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t,
-                                                           slot_dt);
+        if (march_simple(p))
+            march_slots_kernel<true><<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts,
+                                                                     slot_t, slot_dt);
+        else
+            march_slots_kernel<false><<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts,
+                                                                      slot_t, slot_dt);
     }
     scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total);
     return ngp_launch_status();
@@ -537,8 +592,14 @@ int ngp_march_test(const float* rays_o, const float* rays_d, float* hits_t, cons
     NGP_CHECK_ARG(n_alive >= 0 && N_samples >= 1);
     if (n_alive == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_o && rays_d && hits_t && alive && xyzs && dirs && deltas && ts && n_eff);
-    march_test_kernel<<<nblk(n_alive, 64), 64, 0, as_stream(stream)>>>(rays_o, rays_d, hits_t, alive, n_alive, p,
-                                                                      N_samples, xyzs, dirs, deltas, ts, n_eff);
+    // test-time dt uses `cascades` as its scale: SIMPLE only needs esf == 0 and
+    // cascades == 1, where calc_dt is the constant minimum either way.
+    if (march_simple(p))
+        march_test_kernel<true><<<nblk(n_alive, 64), 64, 0, as_stream(stream)>>>(
+            rays_o, rays_d, hits_t, alive, n_alive, p, N_samples, xyzs, dirs, deltas, ts, n_eff);
+    else
+        march_test_kernel<false><<<nblk(n_alive, 64), 64, 0, as_stream(stream)>>>(
+            rays_o, rays_d, hits_t, alive, n_alive, p, N_samples, xyzs, dirs, deltas, ts, n_eff);
     return ngp_launch_status();
 }
 

@@ -118,30 +118,20 @@ __global__ void __launch_bounds__(64) composite_loss_kernel(
     // samples past the terminating one get exactly zero gradient below, so
     // the field backward only needs the first n_active samples of this row
     if (n_active) n_active[n] = (int32_t)(done ? samples + 1 : N);
-    // ---- backward, dL/dws = 0 (volumerendering.cu:124-149); the samples past
-    // the terminating one (index `samples`) get zero gradient.
+    // ---- backward, dL/dws = 0 (volumerendering.cu:124-149) over the first
+    // n_active samples.  Samples past the terminating one carry exactly zero
+    // gradient in the reference; the field backward skips them (sample map),
+    // so their dL_dsig/dL_drgbs entries are left unwritten here.
     const float gs = gop * (1 - O);
+    const int64_t na = done ? samples + 1 : N;
     float Tb = 1.0f, r = 0.f, gg = 0.f, b = 0.f, d = 0.f;
-    for (int64_t k0 = 0; k0 < N; k0 += CH) {
-        const int64_t cnt = N - k0 < CH ? N - k0 : CH;
-        if (k0 > samples) {  // past termination: zero-fill
-            for (int64_t j = 0; j < cnt; ++j) {
-                const int64_t s = start + k0 + j;
-                dL_dsig[s] = 0.f;
-                dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
-            }
-            continue;
-        }
+    for (int64_t k0 = 0; k0 < na; k0 += CH) {
+        const int64_t cnt = na - k0 < CH ? na - k0 : CH;
         load_chunk(c, sigmas, rgbs, deltas, ts, start + k0, cnt);
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             if (j >= cnt) break;
-            const int64_t k = k0 + j, s = start + k;
-            if (k > samples) {
-                dL_dsig[s] = 0.f;
-                dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
-                continue;
-            }
+            const int64_t s = start + k0 + j;
             const float a = 1.0f - __expf(-c.sg[j] * c.dl[j]);
             const float w = a * Tb;
             r += w * c.cr[j]; gg += w * c.cg[j]; b += w * c.cb[j];

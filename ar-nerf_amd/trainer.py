@@ -183,13 +183,21 @@ class NGPTrainer:
         ddp.sync_threshold_(self.threshold, self.pg)  # identical threshold on every rank
         vren.packbits(self.density_grid, self.threshold[:1], self.density_bitfield)
 
+    def _ev(self, name, i):
+        ev = self.kernel_events
+        if ev is not None and name in ev:
+            ev[name][i].record()
+
     # ---------------------------------------------------------------- step
     def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True):
         """One training step on a batch (train.py:174-200).  img/pix (R) i64,
         rgb_gt (R,3) f32, directions (HW,3), poses (n_img,3,4), all on device."""
         L, s = self.L, vren._stream()
+        self._ev("occupancy_update", 0)
         if self.global_step % self.update_interval == 0:
             self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=self.global_step < self.warmup_steps)
+        self._ev("occupancy_update", 1)
+        self._ev("raygen_march", 0)
         R = img_idxs.shape[0]
         assert R == self.batch_size
         vren._ok(L.ngp_raygen_aabb(_p(directions), _p(poses), _p(img_idxs), _p(pix_idxs), R, _p(self.center),
@@ -207,6 +215,7 @@ class NGPTrainer:
         vren._ok(L.ngp_march_train_compact(_p(self.rays_o), _p(self.rays_d), _p(self.rays_a), R, _p(self.slot_t),
                                            _p(self.slot_dt), self.max_samples, _p(self.xyzs), _p(self.dirs),
                                            _p(self.deltas), _p(self.ts), s), "march_compact")
+        self._ev("raygen_march", 1)
         HGL = HG._lib()
         if self.kernel_events is not None:
             self.kernel_events["field_fwd"][0].record()
@@ -217,6 +226,7 @@ class NGPTrainer:
         if self.kernel_events is not None:
             self.kernel_events["field_fwd"][1].record()
         bg = torch.rand(3, device=self.dev, generator=self.gen) if self.random_bg else self.bg
+        self._ev("composite_loss", 0)
         vren._ok(L.ngp_composite_loss(_p(self.sigmas), _p(self.rgbs), _p(self.deltas), _p(self.ts), _p(self.rays_a), R,
                                       _p(rgb_gt), _p(bg), self.loss_type, ctypes_float(self.lambda_opacity),
                                       ctypes_float(self.lambda_depth), ctypes_float(self.scale), ctypes_float(1e-4),
@@ -225,6 +235,7 @@ class NGPTrainer:
                                       s), "composite_loss")
         vren._ok(L.ngp_active_samples(_p(self.n_active), _p(self.rays_a), R, _p(self.act_start),
                                       _p(self.n_active_total), _p(self.sample_idx), s), "active_samples")
+        self._ev("composite_loss", 1)
         ev = self.kernel_events
         if ev is not None:
             ev["mlp_bwd"][0].record()
@@ -240,14 +251,18 @@ class NGPTrainer:
                                        _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
         if ev is not None:
             ev["hash_bwd"][1].record()
+        self._ev("allreduce", 0)
         ddp.allreduce_grad_(self.grad, self.pg)  # DDP gradient all-reduce (RCCL over xGMI)
+        self._ev("allreduce", 1)
         if not apply_adam:  # (tests) leave the summed gradient in self.grad
             return self.out_loss
         self.global_step += 1
+        self._ev("adam", 0)
         vren._ok(L.ngp_adam_step(_p(self.params), _p(self.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
                                  _p(self.params16), self.params.numel(), ctypes_float(self.lr()), ctypes_float(0.9),
                                  ctypes_float(0.999), ctypes_float(1e-15), self.global_step,
                                  ctypes_float(1.0 / self.world), 1, s), "adam")
+        self._ev("adam", 1)
         return self.out_loss
 
     # ---------------------------------------------------- test-time render

@@ -179,7 +179,8 @@ def main():
     n_active_acc = torch.zeros(1, dtype=torch.int64, device=dev)
     trainer.vr_samples.zero_()
     names = list(KERNEL_WORK)
-    ev = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in names}
+    stages = ["occupancy_update", "raygen_march", "composite_loss", "allreduce", "adam"]
+    ev = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in names + stages}
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -216,6 +217,7 @@ def main():
                       "frac": round(achieved / PEAK[bound], 4), "avg_launch_ms": round(ms, 4),
                       "work_per_sample": per_sample, "samples_per_launch": round(units, 1)}
     dominant = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
+    stage_ms = {k: round(sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / args.steps, 4) for k in stages}
     rm_s = samples / (R * args.steps)
     vr_s = int(trainer.vr_samples.item()) / (R * args.steps)
     loss = float(trainer.out_loss.sum().item())
@@ -238,6 +240,7 @@ def main():
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
             "roofline": dict(kernel=dominant, traffic=None, **kernels[dominant]),
             "kernels": kernels,
+            "stage_ms": stage_ms,
             "ms_per_step_breakdown_note": "kernels = HIP-event averages over the timed steps",
             "cpu_baseline": cpu,
         }

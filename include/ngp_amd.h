@@ -207,7 +207,9 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
  * (losses.py:63-82; loss_type 0 raw (default), 1 mse, 2 log, 3 tanh;
  * opacity entropy lambda_opacity; depth term lambda_depth with depth_scale)
  * and composite_train_bw with dL/dws = 0.  rgb_gt (n_rays,3).
- * Out: dL_dsigmas (N), dL_drgbs (N,3); per ray out_rgb (n_rays,3) (after bg),
+ * Out: dL_dsigmas (N), dL_drgbs (N,3) for each row's first n_active samples
+ * (later entries are left unwritten: their gradient is exactly zero); per
+ * ray out_rgb (n_rays,3) (after bg),
  * out_opacity, out_depth, out_loss (n_rays; sum = the batch loss);
  * vr_samples (1) i64 += composited samples (nullable); n_active (n_rays) i32
  * (nullable) = samples of each row that can carry gradient (up to and
