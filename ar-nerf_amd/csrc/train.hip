@@ -144,6 +144,125 @@ __global__ void __launch_bounds__(64) composite_loss_kernel(
     }
 }
 
+// Wave-per-ray variant (the one the C-ABI launches).  Lane k of the wave
+// owns sample k0+k of a 64-sample chunk: loads are coalesced and 8192 rays
+// become 8192 waves (the lane-per-ray kernel above fills only 128).
+// * T follows the reference's strictly sequential recurrence T *= 1 - a
+//   (volumerendering.cu:38-41) through a readlane loop, so the termination
+//   index is exactly the sequential one;
+// * the colour / depth / opacity sums and the backward's inclusive prefixes
+//   are wave reductions / scans (fp32 reassociation only);
+// * w and T-after of every composited sample are parked in dL_drgbs[3s],
+//   dL_drgbs[3s+1] between the two passes (overwritten by the backward).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_incl_scan(float v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float y = __shfl_up(v, o, 64);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(256) composite_loss_wave_kernel(
+    const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
+    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
+    const float* __restrict__ bg, LossArgs la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
+    float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
+    float* __restrict__ out_loss, int64_t* __restrict__ vr_samples, int32_t* __restrict__ n_active) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (n >= n_rays) return;  // wave-uniform
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+    // ---- forward
+    float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
+    int64_t samples = 0, na = 0;
+    bool done = false;
+    for (int64_t k0 = 0; k0 < N && !done; k0 += 64) {
+        const int cnt = (int)(N - k0 < 64 ? N - k0 : 64);
+        const bool in = lane < cnt;
+        const int64_t s = start + k0 + lane;
+        float sg = 0.f, dl = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, tt = 0.f;
+        if (in) {
+            sg = sigmas[s]; dl = deltas[s]; tt = ts[s];
+            cr = rgbs[3 * s]; cg = rgbs[3 * s + 1]; cb = rgbs[3 * s + 2];
+        }
+        const float a = 1.0f - __expf(-sg * dl);
+        const float om = 1.0f - a;
+        float Tk = 0.f;
+        int stop = cnt;
+        for (int j = 0; j < cnt; ++j) {
+            const float omj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(om), j));
+            if (lane == j) Tk = T;
+            T *= omj;
+            if (T <= la.T_thr) { stop = j + 1; done = true; break; }
+        }
+        const bool act = lane < stop;
+        const float w = act ? a * Tk : 0.f;
+        if (act) { dL_drgbs[3 * s] = w; dL_drgbs[3 * s + 1] = Tk * om; }
+        R += wave_sum(w * cr); G += wave_sum(w * cg); B += wave_sum(w * cb);
+        D += wave_sum(w * tt); O += wave_sum(w);
+        samples += done ? stop - 1 : stop;
+        na += stop;
+    }
+    // ---- background + loss (wave-uniform)
+    const float bgc[3] = {bg[0], bg[1], bg[2]};
+    const float xc[3] = {R + bgc[0] * (1 - O), G + bgc[1] * (1 - O), B + bgc[2] * (1 - O)};
+    float loss = 0.f, g[3], gop = 0.f;
+    const float inv3n = la.inv_n_rays / 3.0f;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        float l, d;
+        rgb_loss(la.loss_type, xc[q], gt[3 * ray + q], l, d);
+        loss += l * inv3n;
+        g[q] = d * inv3n;
+        gop -= g[q] * bgc[q];
+    }
+    const float o = O + 1e-10f;
+    loss += la.lambda_opacity * (-o * logf(o)) * la.inv_n_rays;
+    gop += la.lambda_opacity * (-(logf(o) + 1.f)) * la.inv_n_rays;
+    float gdep = 0.f;
+    if (la.lambda_depth != 0.f) {
+        const float v = D / la.depth_scale + 1e-10f;
+        loss += -la.lambda_depth * logf(fminf(v, 1.0f)) * la.inv_n_rays;
+        if (v < 1.0f) gdep = -la.lambda_depth / v / la.depth_scale * la.inv_n_rays;
+    }
+    if (lane == 0) {
+        out_rgb[3 * ray] = xc[0]; out_rgb[3 * ray + 1] = xc[1]; out_rgb[3 * ray + 2] = xc[2];
+        out_op[ray] = O;
+        out_depth[ray] = D;
+        out_loss[ray] = loss;
+        if (vr_samples) atomicAdd((unsigned long long*)vr_samples, (unsigned long long)samples);
+        if (n_active) n_active[n] = (int32_t)na;
+    }
+    // ---- backward over the na composited samples (dL/dws = 0)
+    const float gs = gop * (1 - O);
+    float rc = 0.f, gc = 0.f, bc = 0.f, dc = 0.f;
+    for (int64_t k0 = 0; k0 < na; k0 += 64) {
+        const int cnt = (int)(na - k0 < 64 ? na - k0 : 64);
+        const bool in = lane < cnt;
+        const int64_t s = start + k0 + lane;
+        float dl = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, tt = 0.f, w = 0.f, Ta = 0.f;
+        if (in) {
+            dl = deltas[s]; tt = ts[s];
+            cr = rgbs[3 * s]; cg = rgbs[3 * s + 1]; cb = rgbs[3 * s + 2];
+            w = dL_drgbs[3 * s]; Ta = dL_drgbs[3 * s + 1];
+        }
+        const float pr = rc + wave_incl_scan(w * cr, lane), pg = gc + wave_incl_scan(w * cg, lane);
+        const float pb = bc + wave_incl_scan(w * cb, lane), pd = dc + wave_incl_scan(w * tt, lane);
+        if (in) {
+            dL_drgbs[3 * s] = g[0] * w; dL_drgbs[3 * s + 1] = g[1] * w; dL_drgbs[3 * s + 2] = g[2] * w;
+            dL_dsig[s] = dl * (g[0] * (cr * Ta - (R - pr)) + g[1] * (cg * Ta - (G - pg)) +
+                               g[2] * (cb * Ta - (B - pb)) + gs + gdep * (tt * Ta - (D - pd)));
+        }
+        rc = __shfl(pr, 63, 64); gc = __shfl(pg, 63, 64); bc = __shfl(pb, 63, 64); dc = __shfl(pd, 63, 64);
+    }
+}
+
 // ------------------------------------------------------------------ Adam
 // apex FusedAdam, adam_w_mode with weight_decay 0 == Adam (train.py:146):
 //   m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2
@@ -297,7 +416,7 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_a && rgb_gt && bg && out_rgb && out_opacity && out_depth && out_loss);
     LossArgs la{loss_type, lambda_opacity, lambda_depth, depth_scale, 1.0f / (float)n_rays, T_threshold};
-    composite_loss_kernel<<<(unsigned)((n_rays + 63) / 64), 64, 0, as_stream(stream)>>>(
+    composite_loss_wave_kernel<<<(unsigned)((n_rays + 3) / 4), 256, 0, as_stream(stream)>>>(
         sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
         out_depth, out_loss, vr_samples, n_active);
     return ngp_launch_status();

@@ -83,14 +83,14 @@ class NGPTrainer:
         cap = R * max_samples
         self.cap = cap
         f = dict(device=dev, dtype=torch.float32)
-        self.rays_o, self.rays_d, self.hits_t = torch.empty(R, 3, **f), torch.empty(R, 3, **f), torch.empty(R, 2, **f)
-        self.noise = torch.empty(R, **f)
-        self.counts = torch.empty(R, dtype=torch.int32, device=dev)
-        self.rays_a = torch.empty(R, 3, dtype=torch.int64, device=dev)
-        self.n_samples = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.xyzs, self.dirs = torch.empty(cap, 3, **f), torch.empty(cap, 3, **f)
-        self.deltas, self.ts = torch.empty(cap, **f), torch.empty(cap, **f)
-        self.slot_t, self.slot_dt = torch.empty(cap, **f), torch.empty(cap, **f)  # per-ray sample slots
+        # Two sets of ray / march buffers: the next batch is marched on a side
+        # stream while the current batch's field, loss, backward and Adam run.
+        self.msets = [self._march_buffers(R, cap, f) for _ in range(2)]
+        self.cur = 0
+        self.march_stream = torch.cuda.Stream(device=dev)
+        self._pending = None  # (set index, event) of a batch marched ahead
+        self.n_prefetched = 0
+        self._bind(self.msets[0])
         self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         self.enc = torch.empty(cap, 32, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
@@ -110,6 +110,20 @@ class NGPTrainer:
         HG._lib()
         # {"field_fwd"|"mlp_bwd"|"hash_bwd": (start, end) torch.cuda.Event} around those launches (bench)
         self.kernel_events = None
+
+    @staticmethod
+    def _march_buffers(R, cap, f):
+        dev = f["device"]
+        return dict(rays_o=torch.empty(R, 3, **f), rays_d=torch.empty(R, 3, **f), hits_t=torch.empty(R, 2, **f),
+                    noise=torch.empty(R, **f), counts=torch.empty(R, dtype=torch.int32, device=dev),
+                    rays_a=torch.empty(R, 3, dtype=torch.int64, device=dev),
+                    n_samples=torch.zeros(1, dtype=torch.int64, device=dev),
+                    xyzs=torch.empty(cap, 3, **f), dirs=torch.empty(cap, 3, **f), deltas=torch.empty(cap, **f),
+                    ts=torch.empty(cap, **f), slot_t=torch.empty(cap, **f), slot_dt=torch.empty(cap, **f))
+
+    def _bind(self, m):
+        for k, v in m.items():
+            setattr(self, k, v)
 
     # ------------------------------------------------------------ schedule
     def lr(self):
@@ -183,13 +197,64 @@ class NGPTrainer:
         ddp.sync_threshold_(self.threshold, self.pg)  # identical threshold on every rank
         vren.packbits(self.density_grid, self.threshold[:1], self.density_bitfield)
 
+    def _march(self, k, img_idxs, pix_idxs, directions, poses, noise, stream):
+        """Ray generation + AABB + single-pass march of one batch into buffer set k."""
+        m = self.msets[k]
+        L, R = self.L, img_idxs.shape[0]
+        evs = self.kernel_events.get("march_side") if self.kernel_events is not None else None
+        side = stream is self.march_stream
+        with torch.cuda.stream(stream):
+            if evs is not None and side:
+                evs[0].record(stream)
+            s = HG.c_void_p(stream.cuda_stream)
+            vren._ok(L.ngp_raygen_aabb(_p(directions), _p(poses), _p(img_idxs), _p(pix_idxs), R, _p(self.center),
+                                       _p(self.half_size), ctypes_float(NEAR_DISTANCE), _p(m["rays_o"]),
+                                       _p(m["rays_d"]), _p(m["hits_t"]), s), "raygen")
+            if noise is None:
+                torch.rand(R, out=m["noise"], generator=self.gen)  # custom_functions.py:83
+            else:
+                m["noise"].copy_(noise)
+            vren._ok(L.ngp_march_train_slots(_p(m["rays_o"]), _p(m["rays_d"]), _p(m["hits_t"]), R,
+                                             _p(self.density_bitfield), self.cascades, self.G,
+                                             ctypes_float(self.scale), ctypes_float(self.esf), _p(m["noise"]),
+                                             self.max_samples, _p(m["counts"]), _p(m["rays_a"]),
+                                             _p(m["n_samples"]), _p(m["slot_t"]), _p(m["slot_dt"]), s), "march_slots")
+            vren._ok(L.ngp_march_train_compact(_p(m["rays_o"]), _p(m["rays_d"]), _p(m["rays_a"]), R,
+                                               _p(m["slot_t"]), _p(m["slot_dt"]), self.max_samples, _p(m["xyzs"]),
+                                               _p(m["dirs"]), _p(m["deltas"]), _p(m["ts"]), s), "march_compact")
+            if evs is not None and side:
+                evs[1].record(stream)
+
+    def prefetch(self, img_idxs, pix_idxs, directions, poses, noise=None):
+        """March the NEXT batch into the idle buffer set on the side stream so
+        it overlaps the current step's field / loss / backward / Adam.  Called
+        by step() once the current set is bound: everything the side stream
+        needs (the next batch's indices, the bitfield, the idle set's last
+        readers = the previous step's backward) is already enqueued on the
+        main stream, which one event captures.  Skipped when the next step
+        begins with an occupancy update: that batch must see the new bitfield.
+        (Callers that edit density_bitfield between steps must not pass
+        next_batch.)"""
+        if self._pending is not None or (self.global_step + 1) % self.update_interval == 0:
+            return False
+        k = 1 - self.cur
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream())
+        self.march_stream.wait_event(ready)
+        self._march(k, img_idxs, pix_idxs, directions, poses, noise, self.march_stream)
+        ev = torch.cuda.Event()
+        ev.record(self.march_stream)
+        self._pending = (k, ev)
+        self.n_prefetched += 1
+        return True
+
     def _ev(self, name, i):
         ev = self.kernel_events
         if ev is not None and name in ev:
             ev[name][i].record()
 
     # ---------------------------------------------------------------- step
-    def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True):
+    def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True, next_batch=None):
         """One training step on a batch (train.py:174-200).  img/pix (R) i64,
         rgb_gt (R,3) f32, directions (HW,3), poses (n_img,3,4), all on device."""
         L, s = self.L, vren._stream()
@@ -200,22 +265,18 @@ class NGPTrainer:
         self._ev("raygen_march", 0)
         R = img_idxs.shape[0]
         assert R == self.batch_size
-        vren._ok(L.ngp_raygen_aabb(_p(directions), _p(poses), _p(img_idxs), _p(pix_idxs), R, _p(self.center),
-                                   _p(self.half_size), ctypes_float(NEAR_DISTANCE), _p(self.rays_o), _p(self.rays_d),
-                                   _p(self.hits_t), s), "raygen")
-        if noise is None:
-            torch.rand(R, out=self.noise, generator=self.gen)  # custom_functions.py:83
+        if self._pending is not None:  # this batch was marched ahead on the side stream
+            k, ev = self._pending
+            self._pending = None
+            self.cur = k
+            torch.cuda.current_stream().wait_event(ev)
         else:
-            self.noise.copy_(noise)
-        vren._ok(L.ngp_march_train_slots(_p(self.rays_o), _p(self.rays_d), _p(self.hits_t), R,
-                                         _p(self.density_bitfield), self.cascades, self.G, ctypes_float(self.scale),
-                                         ctypes_float(self.esf), _p(self.noise), self.max_samples, _p(self.counts),
-                                         _p(self.rays_a), _p(self.n_samples), _p(self.slot_t), _p(self.slot_dt), s),
-                 "march_slots")
-        vren._ok(L.ngp_march_train_compact(_p(self.rays_o), _p(self.rays_d), _p(self.rays_a), R, _p(self.slot_t),
-                                           _p(self.slot_dt), self.max_samples, _p(self.xyzs), _p(self.dirs),
-                                           _p(self.deltas), _p(self.ts), s), "march_compact")
+            self._march(self.cur, img_idxs, pix_idxs, directions, poses, noise, torch.cuda.current_stream())
+        self._bind(self.msets[self.cur])
         self._ev("raygen_march", 1)
+        if next_batch is not None and apply_adam:
+            self.prefetch(*next_batch, directions, poses)
+        s = vren._stream()
         HGL = HG._lib()
         if self.kernel_events is not None:
             self.kernel_events["field_fwd"][0].record()

@@ -142,6 +142,14 @@ def cpu_baseline(trainer, scene, gt_images, budget_s, batch):
                       f"{samples / max(1, steps) / batch:.1f} samples/ray, {t_total:.1f} s"}
 
 
+def _recorded(event):
+    try:
+        event.elapsed_time(event)
+        return True
+    except (RuntimeError, ValueError):
+        return False
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -164,34 +172,43 @@ def main():
         rgb = gt_images[img, pix].float().div_(255)
         return img, pix, rgb
 
+    def run(n, events=None):
+        """n training steps; batch i+1 is marched on the side stream during
+        step i (trainer.prefetch).  The last step does not prefetch, so every
+        march of the n batches happens inside this call."""
+        cur = batch()
+        for i in range(n):
+            nxt = batch() if i + 1 < n else None
+            if events is not None:
+                trainer.kernel_events = events[i]
+            trainer.step(*cur, directions, poses, next_batch=None if nxt is None else nxt[:2])
+            if events is not None:
+                n_samples_acc.add_(trainer.n_samples)
+                n_active_acc.add_(trainer.n_active_total)
+            cur = nxt
+
+    n_samples_acc = torch.zeros(1, dtype=torch.int64, device=dev)
+    n_active_acc = torch.zeros(1, dtype=torch.int64, device=dev)
     t0 = time.time()
-    for i in range(args.pretrain):
-        img, pix, rgb = batch()
-        trainer.step(img, pix, rgb, directions, poses)
+    run(args.pretrain)
     torch.cuda.synchronize()
     log(rank, f"[bench] pretrain {args.pretrain} steps in {time.time() - t0:.1f}s, "
               f"samples last batch {int(trainer.n_samples.item())}")
-    for i in range(args.warmup):
-        img, pix, rgb = batch()
-        trainer.step(img, pix, rgb, directions, poses)
+    run(args.warmup)
     # ---- timed region
-    n_samples_acc = torch.zeros(1, dtype=torch.int64, device=dev)
-    n_active_acc = torch.zeros(1, dtype=torch.int64, device=dev)
     trainer.vr_samples.zero_()
     names = list(KERNEL_WORK)
-    stages = ["occupancy_update", "raygen_march", "composite_loss", "allreduce", "adam"]
+    # raygen_march = inline march on the main stream (steps after an occupancy
+    # update); march_side = the next batch's march on the side stream, which
+    # overlaps the step's compute (averaged over the steps that launched one)
+    stages = ["occupancy_update", "raygen_march", "march_side", "composite_loss", "allreduce", "adam"]
     ev = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in names + stages}
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for i in range(args.steps):
-        img, pix, rgb = batch()
-        trainer.kernel_events = ev[i]
-        trainer.step(img, pix, rgb, directions, poses)
-        n_samples_acc += trainer.n_samples
-        n_active_acc += trainer.n_active_total
+    run(args.steps, ev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -217,7 +234,10 @@ def main():
                       "frac": round(achieved / PEAK[bound], 4), "avg_launch_ms": round(ms, 4),
                       "work_per_sample": per_sample, "samples_per_launch": round(units, 1)}
     dominant = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
-    stage_ms = {k: round(sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / args.steps, 4) for k in stages}
+    stage_ms = {k: round(sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / args.steps, 4)
+                for k in stages if k != "march_side"}
+    side = [e["march_side"][0].elapsed_time(e["march_side"][1]) for e in ev if _recorded(e["march_side"][1])]
+    stage_ms["march_side"] = round(sum(side) / max(len(side), 1), 4)
     rm_s = samples / (R * args.steps)
     vr_s = int(trainer.vr_samples.item()) / (R * args.steps)
     loss = float(trainer.out_loss.sum().item())

@@ -83,3 +83,37 @@ def test_training_loss_decreases():
         losses.append(float(tr.step(img, pix, gt_img[img, pix].float() / 255, dirs, poses).sum()))
     assert all(torch.isfinite(torch.tensor(losses)))
     assert sum(losses[-20:]) / 20 < 0.5 * sum(losses[:20]) / 20
+
+
+def test_prefetched_march_matches_inline():
+    """Marching batch i+1 on the side stream during step i (next_batch=) gives
+    the same batches as marching inline: identical sample counts and rays_a
+    on every step before the occupancy update (the march is bit-exact and the
+    noise is drawn in the same generator order), the same losses after."""
+    sc = S.AnalyticScene(W=200, H=200, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    batches = []
+    for _ in range(20):
+        img = torch.randint(0, 10, (4096,), device=DEV, generator=gen)
+        pix = torch.randint(0, 200 * 200, (4096,), device=DEV, generator=gen)
+        batches.append((img, pix, gt_img[img, pix].float() / 255))
+    runs = []
+    for prefetch in (False, True):
+        _, tr, _, _, _ = _setup(R=4096)
+        counts, losses, rays_a = [], [], []
+        for i, (img, pix, rgb) in enumerate(batches):
+            nxt = batches[i + 1][:2] if prefetch and i + 1 < len(batches) else None
+            loss = tr.step(img, pix, rgb, dirs, poses, next_batch=nxt)
+            counts.append(int(tr.n_samples.item()))
+            losses.append(float(loss.sum()))
+            rays_a.append(tr.rays_a.clone())
+        runs.append((counts, losses, rays_a, tr.n_prefetched))
+    (c0, l0, a0, p0), (c1, l1, a1, p1) = runs
+    assert p0 == 0 and p1 >= 15
+    upd = 16 - 1  # global_step starts at 1: step index 15 runs the occupancy update
+    assert c0[:upd] == c1[:upd]
+    assert all(torch.equal(x, y) for x, y in zip(a0[:upd], a1[:upd]))
+    for x, y in zip(l0, l1):
+        assert abs(x - y) <= 2e-2 * abs(x)
