@@ -19,6 +19,19 @@ static inline int ngp_launch_status() {
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Workgroups of `kernel` that fit on the whole device at once (occupancy x
+// CUs): the grid of a persistent kernel, so per-block prologues (LDS weight
+// images) are paid once per resident block, not once per tile.
+template <typename K>
+static unsigned resident_blocks(K kernel, int threads, size_t dyn_lds) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, dyn_lds) != hipSuccess || per_cu < 1)
+        return 256;
+    return (unsigned)(per_cu * cus);
+}
+
 namespace ngp {
 
 // helper_math.h:280-283 clamp(f,a,b) = fmaxf(a, fminf(f,b)) -- keeps the

@@ -20,6 +20,7 @@
 #pragma clang fp contract(off)
 
 #include "common.h"
+#include "grid.h"
 
 namespace ngp {
 
@@ -27,7 +28,6 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int L = 16;  // levels (x2 features = the 32-wide MLP input)
 // fp16 MLP buffer offsets (halfs), matrices row-major [out][in]
 constexpr int OW1 = 0, OW2 = 2048, OW3 = 3072, OW4 = 5120, OW5 = 9216;
 // LDS image of the forward weights (halfs): rows padded to 40 / 72 halfs
@@ -49,37 +49,10 @@ __device__ __forceinline__ int P32(int kp) {
 
 __device__ __forceinline__ f4 mfma32(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
 
-struct GridArgs {
-    ngp_hashgrid_t g;
-    uint32_t dense_mask;  // bit l: level l indexes densely (res^3 <= size)
-    uint32_t pow2_mask;   // bit l: size_l is a power of two
+struct __attribute__((aligned(4))) u2a4 {
+    uint32_t x, y;
+    __device__ operator uint2() const { return make_uint2(x, y); }
 };
-
-struct LevelLds {
-    float scale[L];
-    uint32_t res[L], off[L], size[L];
-    uint32_t dense, pow2;
-};
-
-__device__ __forceinline__ void load_levels(const GridArgs& ga, LevelLds& lv) {
-    const int t = threadIdx.x;
-    if (t < L) {
-        lv.scale[t] = ga.g.scales[t];
-        lv.res[t] = ga.g.res[t];
-        lv.off[t] = ga.g.offsets[t];
-        lv.size[t] = ga.g.sizes[t];
-    }
-    if (t == 0) { lv.dense = ga.dense_mask; lv.pow2 = ga.pow2_mask; }
-}
-
-// tcnn grid_index for one corner (see oracle or_* restatement).
-__device__ __forceinline__ uint32_t corner_index(uint32_t px, uint32_t py, uint32_t pz, uint32_t res, uint32_t size,
-                                                 bool dense, bool pow2) {
-    uint32_t idx = dense ? (px + py * res + pz * (res * res)) : ((px * 1u) ^ (py * 2654435761u) ^ (pz * 805459861u));
-    if (pow2) idx &= size - 1u;
-    else if (idx >= size) idx %= size;
-    return idx;
-}
 
 // Hash-encode levels 4g..4g+3 of one sample -> 8 fp16 values (enc[8g..8g+7]).
 __device__ __forceinline__ h8 encode4(const float in[3], int g, const LevelLds& lv, const uint32_t* __restrict__ table) {
@@ -104,14 +77,28 @@ __device__ __forceinline__ h8 encode4(const float in[3], int g, const LevelLds& 
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             float wt = 1.0f;
-            uint32_t q[3];
 #pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                if (c & (1 << d)) { wt *= pos[d]; q[d] = pg[d] + 1; }
-                else { wt *= 1 - pos[d]; q[d] = pg[d]; }
-            }
+            for (int d = 0; d < 3; ++d) wt *= (c & (1 << d)) ? pos[d] : 1 - pos[d];
             w[c] = wt;
-            v[c] = table[off + corner_index(q[0], q[1], q[2], res, size, dense, pow2)];
+        }
+        // x-adjacent corner pairs: one 8-byte load when the two entries are
+        // neighbours (always on dense levels; on hashed levels when px is
+        // even, the x term of the hash being px*1), else two 4-byte loads.
+#pragma unroll
+        for (int yz = 0; yz < 4; ++yz) {
+            const uint32_t qy = pg[1] + (yz & 1), qz = pg[2] + (yz >> 1);
+            const uint32_t i0 = corner_index(pg[0], qy, qz, res, size, dense, pow2);
+            const uint32_t i1 = corner_index(pg[0] + 1, qy, qz, res, size, dense, pow2);
+            const uint32_t lo = min(i0, i1), hi = max(i0, i1);
+            const bool adj = hi - lo == 1u;
+            // adjacent: the (4-byte aligned) pair at lo; else the aligned pair
+            // holding lo (level sizes are even, so it stays inside the level)
+            const uint2 pr = *reinterpret_cast<const u2a4*>(table + off + (adj ? lo : (lo & ~1u)));
+            const uint32_t vlo = adj ? pr.x : ((lo & 1u) ? pr.y : pr.x);
+            uint32_t vhi = pr.y;
+            if (!adj) vhi = table[off + hi];
+            v[2 * yz] = i0 < i1 ? vlo : vhi;
+            v[2 * yz + 1] = i0 < i1 ? vhi : vlo;
         }
         float a0 = 0.f, a1 = 0.f;
 #pragma unroll
@@ -125,16 +112,6 @@ __device__ __forceinline__ h8 encode4(const float in[3], int g, const LevelLds& 
         e[2 * jl + 1] = (_Float16)a1;
     }
     return e;
-}
-
-__device__ __forceinline__ void load_x01(const float* __restrict__ xyzs, int64_t i, bool valid, const GridArgs& ga,
-                                         float in[3]) {
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        const float x = valid ? xyzs[3 * i + d] : 0.0f;
-        // models/networks.py:104
-        in[d] = (x - ga.g.xyz_min[d]) / (ga.g.xyz_max[d] - ga.g.xyz_min[d]);
-    }
 }
 
 // tcnn SphericalHarmonics degree 4 of (d/|d|+1)/2 (models/networks.py:144-145),
@@ -175,7 +152,17 @@ __device__ __forceinline__ h4 relu_h(f4 c) {
 __device__ __forceinline__ h4 to_h(f4 c) { return h4{(_Float16)c[0], (_Float16)c[1], (_Float16)c[2], (_Float16)c[3]}; }
 __device__ __forceinline__ h8 lds8(const _Float16* p) { return *reinterpret_cast<const h8*>(p); }
 
-// Load the forward weight image (permuted columns, padded rows) into LDS.
+// Stage the raw fp16 MLP buffer (row-major, 20 KB) into LDS with coalesced
+// 16-byte loads; the permuted / transposed images are then built LDS->LDS
+// (strided 2-byte global reads there were latency-bound: one wave per SIMD).
+__device__ __forceinline__ void stage_raw_weights(const _Float16* __restrict__ mlp, _Float16* raw) {
+    const h8* src = reinterpret_cast<const h8*>(mlp);
+    h8* dst = reinterpret_cast<h8*>(raw);
+    for (int i = threadIdx.x; i < NGP_MLP_PARAMS / 8; i += blockDim.x) dst[i] = src[i];
+}
+
+// Build the forward weight image (permuted columns, padded rows) in LDS from
+// the staged raw buffer.
 __device__ __forceinline__ void load_fwd_weights(const _Float16* __restrict__ mlp, _Float16* sw, bool color) {
     const int t = threadIdx.x, nt = blockDim.x;
     for (int i = t; i < 64 * 32; i += nt) sw[SW1 + (i >> 5) * R32 + (i & 31)] = mlp[OW1 + i];
@@ -228,9 +215,12 @@ __global__ void __launch_bounds__(256) field_fwd_kernel(const float* __restrict_
                                                         float* __restrict__ rgbs, _Float16* __restrict__ enc_out,
                                                         _Float16* __restrict__ h_out) {
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
+    __shared__ __attribute__((aligned(16))) _Float16 raw[NGP_MLP_PARAMS];
     __shared__ LevelLds lv;
-    load_fwd_weights(mlp, sw, COLOR);
+    stage_raw_weights(mlp, raw);
     load_levels(ga, lv);
+    __syncthreads();
+    load_fwd_weights(raw, sw, COLOR);
     __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
@@ -282,7 +272,10 @@ __device__ __forceinline__ h4 lds4(const _Float16* p) { return *reinterpret_cast
 constexpr int RT16 = 20, RT64 = 68;  // transposed-weight rows: 16 / 64 halfs + pad
 constexpr int BT5 = SWF, BT4 = BT5 + 64 * RT16, BT3 = BT4 + 64 * RT64, BT2 = BT3 + 16 * RT64, BT1 = BT2 + 64 * RT16,
               BTE = BT1 + 32 * RT64;
-constexpr int TROW = 20, TTILE = 16 * TROW, NT = 30;  // per-wave transpose scratch: 30 tiles [16][20]
+// per-wave transpose scratch: 30 tiles, each a [sample][unit] 16x16 fp16 image
+// (32-byte rows: the packed 8-byte stores and the ds_read_b64_tr_b16 reads
+// of a 32-lane half both cover 64 distinct banks)
+constexpr int TROW = 16, TTILE = 16 * TROW, NT = 30;
 constexpr int SCR = (BTE + 7) & ~7, SCRW = NT * TTILE, BWD_LDS_HALFS = SCR + 4 * SCRW;
 // scratch tile ids
 constexpr int T_DO = 0, T_DA4 = 1, T_DA3 = 5, T_DH = 9, T_DA1 = 10, T_H4 = 14, T_H3 = 18, T_C = 22, T_H1 = 24, T_E = 28;
@@ -299,10 +292,21 @@ __device__ __forceinline__ void load_bwd_weights(const _Float16* __restrict__ ml
     for (int e = t; e < 32 * 64; e += nt) { const int i = e >> 6, o = e & 63; sw[BT1 + i * RT64 + o] = mlp[OW1 + o * 32 + i]; }
 }
 
+// max over the wave: DPP row rotates inside each 16-lane row, then the four
+// row maxima through scalar readlanes (no LDS round trips)
+#define NGP_DPP_ROR(v, n) \
+    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + (n), 0xf, 0xf, false))
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    v = fmaxf(v, NGP_DPP_ROR(v, 1));
+    v = fmaxf(v, NGP_DPP_ROR(v, 2));
+    v = fmaxf(v, NGP_DPP_ROR(v, 4));
+    v = fmaxf(v, NGP_DPP_ROR(v, 8));
+    const int iv = __builtin_bit_cast(int, v);
+    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 0));
+    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 16));
+    const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 32));
+    const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 48));
+    return fmaxf(fmaxf(a, b), fmaxf(c, d));
 }
 __device__ __forceinline__ float max4(f4 v) { return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))); }
 // power of two s.t. maxabs * s < 2^14 (fp16-safe, full mantissa for the max)
@@ -319,11 +323,19 @@ __device__ __forceinline__ f4 mask_relu(f4 g, h4 act) {
     return f4{act[0] > (_Float16)0 ? g[0] : 0.f, act[1] > (_Float16)0 ? g[1] : 0.f, act[2] > (_Float16)0 ? g[2] : 0.f,
               act[3] > (_Float16)0 ? g[3] : 0.f};
 }
+// Accumulator tile X[4g + r][s] (lane (s, g)) -> image row s, units 4g..4g+3.
 __device__ __forceinline__ void put_tile(_Float16* T, h4 v, int s, int g) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) T[(4 * g + r) * TROW + s] = v[r];
+    *reinterpret_cast<h4*>(T + s * TROW + 4 * g) = v;
 }
-__device__ __forceinline__ h4 get_tile(const _Float16* T, int s, int g) { return lds4(T + s * TROW + 4 * g); }
+// Transposed read: lane (u = s, g) receives X[u][4g + q], q = 0..3, i.e. the
+// K = sample fragment of the 16x16x16 operand.  Lane 4q+p of each 16-lane
+// group addresses image row 4g+q, units 4p..4p+3 (= T + 4*lane).
+typedef __fp16 hp4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+__device__ __forceinline__ h4 get_tile(const _Float16* T, int s, int g) {
+    const _Float16* a = T + 64 * g + 4 * s;
+    return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                                      (__attribute__((address_space(3))) hp4*)(const_cast<_Float16*>(a))));
+}
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -350,8 +362,11 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
     float* __restrict__ denc, float* __restrict__ grad_mlp) {
     extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
     _Float16* sw = smem;
-    load_fwd_weights(mlp, sw, true);
-    load_bwd_weights(mlp, sw);
+    _Float16* raw = smem + SCR;  // the per-wave scratch is free until the loop
+    stage_raw_weights(mlp, raw);
+    __syncthreads();
+    load_fwd_weights(raw, sw, true);
+    load_bwd_weights(raw, sw);
     __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
@@ -480,11 +495,8 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
         put_tile(scr + T_DH * TTILE, dhh, s, g);
         put_tile(scr + T_C * TTILE, shh, s, g);
         put_tile(scr + (T_C + 1) * TTILE, hh, s, g);
-        {   // enc fragment: lane holds enc[8g + j] of sample s
-            _Float16* Te = scr + (T_E + (g >> 1)) * TTILE;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) Te[(8 * (g & 1) + j) * TROW + s] = e[j];
-        }
+        // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
+        *reinterpret_cast<h8*>(scr + (T_E + (g >> 1)) * TTILE + s * TROW + 8 * (g & 1)) = e;
         wave_sync_lds();
         int k = 0;
         const h4 gdo = get_tile(scr + T_DO * TTILE, s, g);
@@ -541,10 +553,15 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
 // sample instead of four scattered ones.  Samples of one ray are consecutive,
 // so equal indices of the same (cx, f) at lane stride 4 are first summed by a
 // segmented suffix scan; only each run's head issues its fp32 atomic.
+// MODE != 0 and a level range other than [0, L) are diagnostic variants used
+// only by scripts/diag (1: no atomics, 2: plain stores, 3: no run merge).
+template <int MODE>
 __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__ xyzs, int64_t n,
                                                        const int64_t* __restrict__ n_dev,
                                                        const int32_t* __restrict__ sidx, GridArgs ga,
-                                                       const float* __restrict__ denc, float* __restrict__ grad) {
+                                                       const float* __restrict__ denc, float* __restrict__ grad,
+                                                       int lo, int hi) {
+    float sink = 0.f;
     __shared__ LevelLds lv;
     load_levels(ga, lv);
     __syncthreads();
@@ -558,7 +575,7 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
         float in[3];
         load_x01(xyzs, i, valid, ga, in);
 #pragma unroll 1
-        for (int l = 0; l < L; ++l) {
+        for (int l = lo; l < hi; ++l) {
             const float gd = valid ? denc[j * 32 + 2 * l + f] : 0.f;
             const float sc = lv.scale[l];
             const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
@@ -586,7 +603,7 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
                 const uint32_t prev = __shfl_up(idx, 4, 64);
                 const bool head = lane < 4 || prev != idx;
                 const uint64_t heads = __ballot(head);
-                if (heads != ~0ull) {  // some runs: segmented suffix sum at lane stride 4
+                if (MODE != 3 && heads != ~0ull) {  // some runs: segmented suffix sum at lane stride 4
 #pragma unroll
                     for (int o4 = 4; o4 < 64; o4 <<= 1) {
                         const float ov = __shfl_down(v, o4, 64);
@@ -596,30 +613,13 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
                         if (in_seg) v += ov;
                     }
                 }
-                if (head && valid) atomicAdd(&grad[2 * (size_t)idx + f], v);
+                if (MODE == 1) sink += head && valid ? v : 0.f;
+                else if (MODE == 2) { if ((head || MODE == 3) && valid) grad[2 * (size_t)idx + f] = v; }
+                else if ((head || MODE == 3) && valid) atomicAdd(&grad[2 * (size_t)idx + f], v);
             }
         }
     }
-}
-
-static int grid_args(const ngp_hashgrid_t* grid, GridArgs& ga) {
-    if (!grid || grid->n_levels != L) return NGP_ERANGE;
-    ga.g = *grid;
-    ga.dense_mask = 0;
-    ga.pow2_mask = 0;
-    for (int l = 0; l < L; ++l) {
-        const uint64_t r = grid->res[l];
-        if (r * r * r <= (uint64_t)grid->sizes[l]) ga.dense_mask |= 1u << l;
-        if ((grid->sizes[l] & (grid->sizes[l] - 1u)) == 0) ga.pow2_mask |= 1u << l;
-        if (grid->sizes[l] == 0) return NGP_EINVAL;
-    }
-    return NGP_OK;
-}
-
-static unsigned persistent_blocks(int64_t n, int samples_per_block, unsigned cap) {
-    int64_t b = (n + samples_per_block - 1) / samples_per_block;
-    if (b < 1) b = 1;
-    return (unsigned)(b < cap ? b : cap);
+    if (MODE == 1 && sink == 1234.5f) grad[threadIdx.x] = sink;
 }
 
 }  // namespace ngp
@@ -637,7 +637,9 @@ int ngp_field_forward(const float* xyzs, const float* dirs, int64_t n, const int
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && dirs && table_f16 && mlp_f16 && sigmas && rgbs);
-    field_fwd_kernel<true><<<persistent_blocks(n, 64, 4096), 256, 0, as_stream(stream)>>>(
+    NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
+    static const unsigned cap = resident_blocks(field_fwd_kernel<true>, 256, 0);
+    field_fwd_kernel<true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
         xyzs, dirs, n, n_dev, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16, sigmas, rgbs,
         (_Float16*)enc_f16, (_Float16*)h_f16);
     return ngp_launch_status();
@@ -651,7 +653,9 @@ int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, cons
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && table_f16 && mlp_f16 && sigmas);
-    field_fwd_kernel<false><<<persistent_blocks(n, 64, 4096), 256, 0, as_stream(stream)>>>(
+    NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
+    static const unsigned cap = resident_blocks(field_fwd_kernel<false>, 256, 0);
+    field_fwd_kernel<false><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
         xyzs, nullptr, n, n_dev, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16, sigmas, nullptr, nullptr,
         (_Float16*)h_f16);
     return ngp_launch_status();
@@ -664,6 +668,7 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(dirs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp);
+    NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
     static bool attr_set = false;
     const size_t lds = (size_t)BWD_LDS_HALFS * sizeof(_Float16);
     if (!attr_set) {
@@ -686,8 +691,8 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && denc && grad_table);
-    hash_bwd_kernel<<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga,
-                                                                                  denc, grad_table);
+    hash_bwd_kernel<0><<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx,
+                                                                                     ga, denc, grad_table, 0, L);
     return ngp_launch_status();
 }
 

@@ -1,0 +1,418 @@
+// Binned hash-table backward: dL/dtable without per-sample memory-side
+// atomics.  Same result as hash_bwd_kernel (field.hip) / tcnn's
+// kernel_grid_backward (the `params.grad` that models/networks.py's
+// xyz_encoder receives), up to fp32 rounding/summation order.
+//
+// Why: gfx950 float atomics execute at the memory side, one 64-byte request
+// per touched segment (MI355X_MICROARCH.md "Global float atomics"); the hash
+// backward touches ~4 random 16-byte segments per (sample, level), so the
+// atomic form runs at the chip's atomic request rate (~20 G/s), far below HBM
+// speed.  Here every gradient contribution is moved twice at HBM speed as a
+// 16-byte record, summed in LDS, and each table range is written once.
+//
+//   bucket  = (level l, range of BENT consecutive entries of level l)
+//   record  = one (sample, level, y/z corner) = the x-adjacent corner pair:
+//             {key = i0 | i1 << 14 | flags, fx, a0, a1} (16 B): i0/i1 are
+//             the two corners' entry offsets inside the bucket,
+//             a_f = (w_y * w_z) * dL/denc[2l + f]; corner x+c receives
+//             (c ? fx : 1 - fx) * a_f.
+//   1 count  (hash_count_kernel): records per (tile of TILE samples, bucket),
+//            LDS counters, one row per tile -- no global atomics.
+//   2 scan   (hash_scan_kernel): per bucket, exclusive prefix over tiles.
+//   3 plan   (hash_plan_kernel): bucket regions (prefix of bucket totals)
+//            and pass-B work items (chunks of <= CH records per bucket).
+//   4 write  (hash_write_kernel): recompute each record and store it at its
+//            slot of the bucket's contiguous region (counting sort).
+//   5 accum  (hash_accum_kernel): one workgroup per chunk streams its records
+//            into an LDS image of the range (BENT x 2 fp32 = 128 KB) and
+//            writes it out once: a read-add-store when it is the bucket's
+//            only chunk and nothing was added to the range directly, else
+//            atomic adds of the non-zero entries.
+// A dense-level pair split by a bucket boundary adds its x+1 corner with a
+// global atomic (and flags the bucket); samples beyond the workspace capacity
+// take the per-sample atomic path (and flag every bucket): exact either way.
+#pragma clang fp contract(off)
+
+#include "common.h"
+#include "grid.h"
+
+namespace ngp {
+
+constexpr int BSHIFT = 14, BENT = 1 << BSHIFT;  // entries per bucket
+constexpr int NBL = 32;                          // bucket slots per level (2^19 / BENT)
+constexpr int NSLOT = L * NBL;                   // (level, bucket) slots per tile row
+constexpr int MAXB = 512;                        // buckets over all levels
+constexpr int TILE = 256;                        // samples per count/write tile
+constexpr int RPT = TILE * 4 / 256;              // records per thread per level
+constexpr uint32_t CH = 32768;                   // records per pass-5 chunk
+constexpr uint32_t F_C0 = 1u << 28;              // record carries corner x only (pair split)
+
+struct BinArgs {
+    uint32_t bbase[L + 1];  // first bucket of level l
+    int64_t tiles_cap;      // tiles the workspace holds
+};
+
+struct BinWs {
+    uint32_t* fb;      // [MAXB + 1]: 1 if direct adds hit bucket b; [MAXB]: a tile spilled
+    uint32_t* tot;     // [MAXB] records per bucket
+    uint32_t* rstart;  // [MAXB + 1] bucket region starts
+    uint32_t* items;   // [MAXB + 1] chunk prefix
+    uint32_t* ofs;     // [tiles_cap][NSLOT] counts, then exclusive offsets over tiles
+    uint4* rec;        // [tiles_cap * TILE * 4 * L]
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static size_t bin_ws_bytes(int64_t tiles, BinWs* w, void* base) {
+    const size_t o_fb = 0, o_tot = align256((MAXB + 1) * 4), o_rs = o_tot + align256(MAXB * 4),
+                 o_it = o_rs + align256((MAXB + 1) * 4), o_ofs = o_it + align256((MAXB + 1) * 4);
+    const size_t o_rec = align256(o_ofs + (size_t)tiles * NSLOT * 4);
+    const size_t total = o_rec + (size_t)tiles * TILE * 4 * L * sizeof(uint4);
+    if (w) {
+        char* b = reinterpret_cast<char*>(base);
+        w->fb = reinterpret_cast<uint32_t*>(b + o_fb);
+        w->tot = reinterpret_cast<uint32_t*>(b + o_tot);
+        w->rstart = reinterpret_cast<uint32_t*>(b + o_rs);
+        w->items = reinterpret_cast<uint32_t*>(b + o_it);
+        w->ofs = reinterpret_cast<uint32_t*>(b + o_ofs);
+        w->rec = reinterpret_cast<uint4*>(b + o_rec);
+    }
+    return total;
+}
+
+__device__ __forceinline__ void add_pair_direct(float* __restrict__ grad, uint32_t e, float w, float a0, float a1) {
+    atomicAdd(grad + 2 * (size_t)e, w * a0);
+    atomicAdd(grad + 2 * (size_t)e + 1, w * a1);
+}
+
+// One record of sample (in, gd) at level l, y/z corner (cy, cz): the two
+// x-adjacent corners' entries of the level and the factors of their weights.
+struct Rec {
+    uint32_t e0, e1;
+    float fx, a0, a1;
+};
+
+__device__ __forceinline__ Rec make_rec(const float in[3], float2 gd, int cy, int cz, const LevelLds& lv, int l) {
+    const float sc = lv.scale[l];
+    const uint32_t res = lv.res[l], size = lv.size[l];
+    const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
+    float pos[3];
+    uint32_t pg[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float p = fmaf(sc, in[d], 0.5f);
+        const float fl = floorf(p);
+        pg[d] = (uint32_t)(int)fl;
+        pos[d] = p - fl;
+    }
+    const float wyz = (cy ? pos[1] : 1 - pos[1]) * (cz ? pos[2] : 1 - pos[2]);
+    Rec r;
+    r.fx = pos[0];
+    r.a0 = wyz * gd.x;
+    r.a1 = wyz * gd.y;
+    r.e0 = corner_index(pg[0], pg[1] + cy, pg[2] + cz, res, size, dense, pow2);
+    r.e1 = corner_index(pg[0] + 1, pg[1] + cy, pg[2] + cz, res, size, dense, pow2);
+    return r;
+}
+
+__device__ __forceinline__ void tile_inputs(const float* __restrict__ xyzs, const int32_t* __restrict__ sidx,
+                                            const GridArgs& ga, int64_t j0, int64_t N, float in[RPT][3],
+                                            bool valid[RPT]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+        const int64_t j = j0 + k * 64 + (t >> 2);
+        valid[k] = j < N;
+        const int64_t i = valid[k] && sidx ? (int64_t)sidx[j] : j;
+        load_x01(xyzs, i, valid[k], ga, in[k]);
+    }
+}
+
+__global__ void __launch_bounds__(256) hash_count_kernel(const float* __restrict__ xyzs, int64_t n,
+                                                         const int64_t* __restrict__ n_dev,
+                                                         const int32_t* __restrict__ sidx, GridArgs ga, BinArgs ba,
+                                                         BinWs ws) {
+    __shared__ LevelLds lv;
+    __shared__ uint32_t cnt[NSLOT];
+    load_levels(ga, lv);
+    const int64_t N = n_dev ? *n_dev : n;
+    const int64_t ntiles = min((N + TILE - 1) / TILE, ba.tiles_cap);
+    const int t = threadIdx.x, yz = t & 3, cy = yz & 1, cz = yz >> 1;
+    const float2 g0 = make_float2(0.f, 0.f);
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        for (int i = t; i < NSLOT; i += 256) cnt[i] = 0;
+        __syncthreads();
+        float in[RPT][3];
+        bool valid[RPT];
+        tile_inputs(xyzs, sidx, ga, tile * TILE, N, in, valid);
+#pragma unroll 1
+        for (int l = 0; l < L; ++l) {
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) {
+                if (!valid[k]) continue;
+                const Rec r = make_rec(in[k], g0, cy, cz, lv, l);
+                atomicAdd(&cnt[l * NBL + (r.e0 >> BSHIFT)], 1u);
+            }
+        }
+        __syncthreads();
+        uint32_t* row = ws.ofs + (size_t)tile * NSLOT;
+        for (int i = t; i < NSLOT; i += 256) row[i] = cnt[i];
+        __syncthreads();
+    }
+}
+
+// one workgroup per (level, bucket) slot: exclusive prefix over tiles in place
+__global__ void __launch_bounds__(256) hash_scan_kernel(const int64_t* __restrict__ n_dev, int64_t n, BinArgs ba,
+                                                        BinWs ws) {
+    __shared__ uint32_t wsum[4];
+    const int slot = blockIdx.x, l = slot / NBL, lb = slot % NBL;
+    if (lb >= (int)(ba.bbase[l + 1] - ba.bbase[l])) return;
+    const int64_t N = n_dev ? *n_dev : n;
+    const int64_t ntiles = min((N + TILE - 1) / TILE, ba.tiles_cap);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    uint32_t carry = 0;
+    for (int64_t c0 = 0; c0 < ntiles; c0 += 256) {
+        const int64_t tile = c0 + t;
+        uint32_t* p = ws.ofs + (size_t)tile * NSLOT + slot;
+        const uint32_t v = tile < ntiles ? *p : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint32_t before = carry;
+        for (int i = 0; i < w; ++i) before += wsum[i];
+        const uint32_t blk = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (tile < ntiles) *p = before + x - v;
+        carry += blk;
+        __syncthreads();
+    }
+    if (t == 0) ws.tot[ba.bbase[l] + lb] = carry;
+}
+
+// bucket regions + chunk items (one workgroup of MAXB threads)
+__global__ void __launch_bounds__(MAXB) hash_plan_kernel(uint32_t nbt, BinWs ws) {
+    __shared__ uint32_t a[MAXB], c[MAXB];
+    const uint32_t b = threadIdx.x;
+    const uint32_t tot = b < nbt ? ws.tot[b] : 0u;
+    a[b] = tot;
+    c[b] = (tot + CH - 1) / CH;
+    __syncthreads();
+    for (uint32_t o = 1; o < MAXB; o <<= 1) {  // Hillis-Steele inclusive scans
+        const uint32_t va = b >= o ? a[b - o] : 0u, vc = b >= o ? c[b - o] : 0u;
+        __syncthreads();
+        a[b] += va;
+        c[b] += vc;
+        __syncthreads();
+    }
+    ws.rstart[b + 1] = a[b];
+    ws.items[b + 1] = c[b];
+    if (b == 0) { ws.rstart[0] = 0; ws.items[0] = 0; }
+}
+
+__global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict__ xyzs, int64_t n,
+                                                         const int64_t* __restrict__ n_dev,
+                                                         const int32_t* __restrict__ sidx, GridArgs ga, BinArgs ba,
+                                                         const float* __restrict__ denc, float* __restrict__ grad,
+                                                         BinWs ws) {
+    __shared__ LevelLds lv;
+    __shared__ uint32_t base[NSLOT];
+    load_levels(ga, lv);
+    const int64_t N = n_dev ? *n_dev : n;
+    const int64_t ntiles = (N + TILE - 1) / TILE;
+    const int t = threadIdx.x, yz = t & 3, cy = yz & 1, cz = yz >> 1;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const bool spill = tile >= ba.tiles_cap;  // no room: per-sample atomics for this tile
+        if (spill && t == 0) ws.fb[MAXB] = 1u;
+        if (!spill) {
+            const uint32_t* row = ws.ofs + (size_t)tile * NSLOT;
+            for (int i = t; i < NSLOT; i += 256) {
+                const int l = i / NBL, lb = i % NBL;
+                base[i] = lb < (int)(ba.bbase[l + 1] - ba.bbase[l]) ? ws.rstart[ba.bbase[l] + lb] + row[i] : 0u;
+            }
+        }
+        __syncthreads();
+        float in[RPT][3];
+        bool valid[RPT];
+        const int64_t j0 = tile * TILE;
+        tile_inputs(xyzs, sidx, ga, j0, N, in, valid);
+        float2 gd[RPT], gn[RPT];
+#pragma unroll
+        for (int k = 0; k < RPT; ++k)
+            gd[k] = valid[k] ? *reinterpret_cast<const float2*>(denc + (j0 + k * 64 + (t >> 2)) * 32) : float2{0.f, 0.f};
+#pragma unroll 1
+        for (int l = 0; l < L; ++l) {
+#pragma unroll
+            for (int k = 0; k < RPT; ++k)  // next level's dL/denc, loaded ahead
+                gn[k] = valid[k] && l + 1 < L
+                            ? *reinterpret_cast<const float2*>(denc + (j0 + k * 64 + (t >> 2)) * 32 + 2 * (l + 1))
+                            : float2{0.f, 0.f};
+            const uint32_t off = lv.off[l];
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) {
+                if (!valid[k]) continue;
+                const Rec r = make_rec(in[k], gd[k], cy, cz, lv, l);
+                if (spill) {
+                    add_pair_direct(grad, off + r.e0, 1 - r.fx, r.a0, r.a1);
+                    add_pair_direct(grad, off + r.e1, r.fx, r.a0, r.a1);
+                    continue;
+                }
+                const uint32_t b0 = r.e0 >> BSHIFT, b1 = r.e1 >> BSHIFT;
+                uint32_t key = (r.e0 & (BENT - 1)) | ((r.e1 & (BENT - 1)) << BSHIFT);
+                if (b1 != b0) {  // pair split by a bucket boundary: corner x+1 goes direct
+                    key |= F_C0;
+                    add_pair_direct(grad, off + r.e1, r.fx, r.a0, r.a1);
+                    ws.fb[ba.bbase[l] + b1] = 1u;  // idempotent flag
+                }
+                const uint32_t dst = atomicAdd(&base[l * NBL + b0], 1u);
+                ws.rec[dst] = make_uint4(key, __float_as_uint(r.fx), __float_as_uint(r.a0), __float_as_uint(r.a1));
+            }
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) gd[k] = gn[k];
+        }
+        __syncthreads();
+    }
+}
+
+// MODE != 0: diagnostic variants for scripts/diag (1: no LDS adds, 2: no
+// flush, 3: neither)
+template <int MODE>
+__global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
+                                                          float* __restrict__ grad, BinWs ws) {
+    extern __shared__ __attribute__((aligned(16))) float img[];  // [BENT][2]
+    const uint32_t total = ws.items[nbt];
+    const int t = threadIdx.x;
+    const bool overflow = ws.fb[MAXB] != 0;
+    for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
+        uint32_t lo = 0, hi = nbt;  // bucket b: items[b] <= it < items[b + 1]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ws.items[mid] <= it) lo = mid; else hi = mid;
+        }
+        const uint32_t b = lo, c = it - ws.items[b], nch = ws.items[b + 1] - ws.items[b];
+        int l = 0;
+        while (l < L - 1 && b >= ba.bbase[l + 1]) ++l;
+        const uint32_t lb = b - ba.bbase[l];
+        const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
+        for (uint32_t e = t; e < 2 * BENT / 4; e += blockDim.x)
+            reinterpret_cast<float4*>(img)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        __syncthreads();
+        const uint32_t r0 = ws.rstart[b] + c * CH, r1 = min(ws.rstart[b + 1], r0 + CH);
+        constexpr int U = 4;  // records in flight per thread
+        for (uint32_t q0 = r0 + t; q0 < r1; q0 += U * blockDim.x) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t q = q0 + u * blockDim.x;
+                v[u] = q < r1 ? ws.rec[q] : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t key = v[u].x, i0 = key & (BENT - 1), i1 = (key >> BSHIFT) & (BENT - 1);
+                const float fx = __uint_as_float(v[u].y), a0 = __uint_as_float(v[u].z), a1 = __uint_as_float(v[u].w);
+                if (a0 == 0.f && a1 == 0.f) continue;  // padding (or a zero gradient: adds nothing)
+                const float w0 = 1 - fx;
+                if (MODE & 1) {
+                    if (w0 * a0 + fx * a1 == 1234.5f) img[i0 ^ i1] = 1.f;
+                    continue;
+                }
+                atomicAdd(&img[2 * i0], w0 * a0);
+                atomicAdd(&img[2 * i0 + 1], w0 * a1);
+                if (!(key & F_C0)) {
+                    atomicAdd(&img[2 * i1], fx * a0);
+                    atomicAdd(&img[2 * i1 + 1], fx * a1);
+                }
+            }
+        }
+        __syncthreads();
+        float* g = grad + 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
+        const bool own = nch == 1 && !overflow && ws.fb[b] == 0;
+        for (uint32_t e = t; e < ((MODE & 2) ? 0u : 2 * ne / 4); e += blockDim.x) {
+            const float4 v = reinterpret_cast<const float4*>(img)[e];
+            if (own) {  // sole writer of this range: read-add-store keeps the += contract
+                float4 o = reinterpret_cast<const float4*>(g)[e];
+                o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+                reinterpret_cast<float4*>(g)[e] = o;
+            } else {
+                if (v.x != 0.f) atomicAdd(g + 4 * e, v.x);
+                if (v.y != 0.f) atomicAdd(g + 4 * e + 1, v.y);
+                if (v.z != 0.f) atomicAdd(g + 4 * e + 2, v.z);
+                if (v.w != 0.f) atomicAdd(g + 4 * e + 3, v.w);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+static int bin_args(const ngp_hashgrid_t* grid, int64_t tiles_cap, BinArgs& ba, uint32_t& nbt) {
+    uint32_t b = 0;
+    for (int l = 0; l < L; ++l) {
+        ba.bbase[l] = b;
+        const uint32_t nb = (grid->sizes[l] + BENT - 1) >> BSHIFT;
+        if (nb > (uint32_t)NBL) return NGP_ERANGE;
+        if (grid->offsets[l] & 1u) return NGP_EINVAL;  // flush rows are 16-byte aligned
+        b += nb;
+    }
+    ba.bbase[L] = b;
+    ba.tiles_cap = tiles_cap;
+    nbt = b;
+    return b <= (uint32_t)MAXB ? NGP_OK : NGP_ERANGE;
+}
+
+}  // namespace ngp
+
+using namespace ngp;
+
+extern "C" {
+
+size_t ngp_hash_backward_binned_workspace(int64_t max_samples) {
+    if (max_samples <= 0) return 0;
+    return bin_ws_bytes((max_samples + TILE - 1) / TILE, nullptr, nullptr);
+}
+
+int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                             const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                             int64_t max_samples, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0 && max_samples > 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && denc && grad_table && workspace);
+    NGP_CHECK_ARG(((uintptr_t)workspace & 255) == 0 && ((uintptr_t)denc & 7) == 0 &&
+                  ((uintptr_t)grad_table & 15) == 0);
+    const int64_t tiles_cap = (max_samples + TILE - 1) / TILE;
+    // record slots are uint32-indexed
+    NGP_CHECK_ARG(tiles_cap * TILE * 4 * L < (int64_t)0xffffffffLL);
+    BinArgs ba;
+    uint32_t nbt;
+    st = bin_args(grid, tiles_cap, ba, nbt);
+    if (st) return st;
+    BinWs ws;
+    bin_ws_bytes(tiles_cap, &ws, workspace);
+    hipStream_t s = as_stream(stream);
+    if (hipMemsetAsync(ws.fb, 0, (MAXB + 1) * sizeof(uint32_t), s) != hipSuccess) return ngp_launch_status();
+    static const unsigned capC = resident_blocks(hash_count_kernel, 256, 0);
+    static const unsigned capW = resident_blocks(hash_write_kernel, 256, 0);
+    hash_count_kernel<<<persistent_blocks(n, TILE, capC), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, ws);
+    hash_scan_kernel<<<NSLOT, 256, 0, s>>>(n_dev, n, ba, ws);
+    hash_plan_kernel<<<1, MAXB, 0, s>>>(nbt, ws);
+    hash_write_kernel<<<persistent_blocks(n, TILE, capW), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, denc,
+                                                                       grad_table, ws);
+    static bool attr = false;
+    const size_t lds = (size_t)BENT * 2 * sizeof(float);
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)hash_accum_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds) != hipSuccess)
+            return NGP_ERANGE;
+        attr = true;
+    }
+    static const unsigned capB = resident_blocks(hash_accum_kernel<0>, 1024, lds);
+    hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws);
+    return ngp_launch_status();
+}
+
+}  // extern "C"

@@ -45,8 +45,11 @@ def _lib():
         L.ngp_field_backward.argtypes = [vp, vp, c_int64, vp, P, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_backward_mlp.argtypes = [vp, c_int64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_hash_backward.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
+        L.ngp_hash_backward_binned.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, vp]
+        L.ngp_hash_backward_binned_workspace.argtypes = [c_int64]
+        L.ngp_hash_backward_binned_workspace.restype = ctypes.c_size_t
         for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_field_backward, L.ngp_field_backward_mlp,
-                  L.ngp_hash_backward):
+                  L.ngp_hash_backward, L.ngp_hash_backward_binned):
             f.restype = c_int
         _declared = True
     return L

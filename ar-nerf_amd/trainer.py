@@ -41,7 +41,7 @@ class NGPTrainer:
     def __init__(self, scale=0.5, batch_size=8192, lr=1e-2, num_epochs=30, steps_per_epoch=1000, loss="raw",
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
-                 device="cuda", process_group=None):
+                 device="cuda", process_group=None, hash_backward="atomic", bin_samples_per_ray=128):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
@@ -103,6 +103,14 @@ class NGPTrainer:
         self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
         self.n_active_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.sample_idx = torch.empty(cap, dtype=torch.int32, device=dev)
+        # binned hash backward: workspace for bin_samples_per_ray gradient-
+        # carrying samples per ray on average (1 KiB each; the rest take the
+        # atomic path, still exact)
+        self.hash_backward = hash_backward
+        if hash_backward == "binned":
+            self.bin_max_samples = R * bin_samples_per_ray
+            nbytes = HG._lib().ngp_hash_backward_binned_workspace(self.bin_max_samples)
+            self.bin_ws = torch.empty((nbytes + 255) // 256, 64, dtype=torch.int32, device=dev)
         self.bg = torch.ones(3, **f) if self.esf == 0 else torch.zeros(3, **f)  # models/rendering.py:287-296
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(1000 + seed + self.rank)
@@ -307,9 +315,15 @@ class NGPTrainer:
         if ev is not None:
             ev["mlp_bwd"][1].record()
             ev["hash_bwd"][0].record()
-        vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                                       HG.ctypes.byref(self.grid.desc),
-                                       _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
+        if self.hash_backward == "binned":
+            vren._ok(HGL.ngp_hash_backward_binned(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                  _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
+                                                  _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
+                                                  s), "hash_backward_binned")
+        else:
+            vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                                           HG.ctypes.byref(self.grid.desc),
+                                           _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
         if ev is not None:
             ev["hash_bwd"][1].record()
         self._ev("allreduce", 0)

@@ -200,6 +200,18 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
 int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                       const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* stream);
 
+/* Binned form of ngp_hash_backward (same gradient up to fp32 summation order):
+ * records per (level, 16384-entry range) are staged in `workspace`, then each
+ * range is summed in LDS and written once -- no per-sample global atomics
+ * (DESIGN.md "hash backward").  max_samples = samples the workspace holds
+ * (1 KiB each; samples beyond it take the atomic path, still exact);
+ * workspace = ngp_hash_backward_binned_workspace(max_samples) bytes,
+ * 256-byte aligned device memory.  Replaces the same tcnn grid backward. */
+size_t ngp_hash_backward_binned_workspace(int64_t max_samples);
+int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                             const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                             int64_t max_samples, void* stream);
+
 /* ------------------------------------------------------ training step */
 /* Fused compositing + NeRFLoss + compositing backward for one training batch:
  * composite_train_fw (volumerendering.cu:5-44), background blend

@@ -124,3 +124,40 @@ def test_field_autograd_function():
     (sig.sum() * 1e-3 + rgb.sum()).backward()
     assert params.grad is not None and torch.isfinite(params.grad).all()
     assert params.grad[:HG.MLP_PARAMS].abs().sum() > 0
+
+
+@pytest.mark.parametrize("scale", [0.5, 16.0])
+@pytest.mark.parametrize("level_cap", [1 << 20, 3000])  # max_samples of the workspace
+def test_hash_backward_binned_matches_atomic(scale, level_cap):
+    """ngp_hash_backward_binned (records + LDS range sums) == ngp_hash_backward
+    (per-sample atomics) up to fp32 summation order, through a sample_idx
+    subset, onto a non-zero gradient (+= contract).  max_samples=3000 sends
+    most tiles through the overflow path (direct atomics)."""
+    x, _ = _points(40000, scale, seed=3)
+    n = x.shape[0]
+    grid = HG.HashGrid(scale)
+    g = torch.Generator().manual_seed(5)
+    sidx = torch.randperm(n, generator=g)[: n * 3 // 4].sort().values.to(torch.int32)
+    m = sidx.numel()
+    denc = (torch.randn(m, 32, generator=g) * 1e-2).to(DEV)
+    x, sidx = x.to(DEV), sidx.to(DEV)
+    n_dev = torch.tensor([m], dtype=torch.int64, device=DEV)
+    base = torch.randn(grid.n_entries * 2, generator=g).to(DEV)
+    L = HG._lib()
+    p = lambda t: vren.c_void_p(t.data_ptr())  # noqa: E731
+    ref = base.clone()
+    vren._ok(L.ngp_hash_backward(p(x), n, p(n_dev), p(sidx), HG.ctypes.byref(grid.desc), p(denc), p(ref),
+                                 vren._stream()), "hash_backward")
+    ws = torch.empty((L.ngp_hash_backward_binned_workspace(level_cap) + 255) // 256, 64, dtype=torch.int32,
+                     device=DEV)
+    out = base.clone()
+    for _ in range(2):  # the workspace is reusable: counters reset per call
+        out.copy_(base)
+        vren._ok(L.ngp_hash_backward_binned(p(x), n, p(n_dev), p(sidx), HG.ctypes.byref(grid.desc), p(denc), p(out),
+                                            p(ws), level_cap, vren._stream()), "hash_backward_binned")
+    torch.cuda.synchronize()
+    d_ref, d_out = (ref - base).cpu().double(), (out - base).cpu().double()
+    assert float(d_ref.abs().max()) > 0
+    assert _rel(d_out, d_ref) < 5e-5  # product order (1-fx)*((wy*wz)*g) vs ((wx*wy)*wz)*g + sum order
+    # rtol: a coarse entry sums thousands of terms in another order
+    torch.testing.assert_close(out.cpu(), ref.cpu(), rtol=1e-4, atol=1e-6 * float(d_ref.abs().max()))
