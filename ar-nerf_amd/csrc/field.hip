@@ -525,21 +525,28 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
         }
         cur = nxt;
     }
-    // ---- block reduction of the 40 tiles in LDS (fp32), then one global add each
-    __syncthreads();
+    // ---- block reduction of the 40 tiles, then one global add per weight.
+    // Plain LDS stores of each wave's tiles + a 4-way sum, CHK tiles at a
+    // time (ds_add_f32 costs ~3 cycles per lane on gfx950: 160 per thread
+    // were ~50 us per launch).
+    constexpr int CHK = 10;
+    static_assert(NACC % CHK == 0 && 4 * CHK * 256 * 4 <= 4 * SCRW * 2, "reduction chunk exceeds the scratch");
     float* red = reinterpret_cast<float*>(smem + SCR);
-    for (int e = threadIdx.x; e < NACC * 256; e += blockDim.x) red[e] = 0.f;
-    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < NACC; ++k)
+    for (int c0 = 0; c0 < NACC; c0 += CHK) {
+        __syncthreads();  // previous chunk's reads (or the loop's scratch use) are done
 #pragma unroll
-        for (int r = 0; r < 4; ++r) atomicAdd(&red[k * 256 + (4 * g + r) * 16 + s], acc[k][r]);
-    __syncthreads();
-    for (int e = threadIdx.x; e < NACC * 256; e += blockDim.x) {
-        const int k = e >> 8, row = (e >> 4) & 15, col = e & 15;
-        int ow, in_dim, o0, i0;
-        acc_tile_info(k, ow, in_dim, o0, i0);
-        atomicAdd(&grad_mlp[ow + (o0 + row) * in_dim + i0 + col], red[e]);
+        for (int k = 0; k < CHK; ++k)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[(wid * CHK + k) * 256 + (4 * g + r) * 16 + s] = acc[c0 + k][r];
+        __syncthreads();
+        for (int e = threadIdx.x; e < CHK * 256; e += blockDim.x) {
+            const float v = (red[e] + red[CHK * 256 + e]) + (red[2 * CHK * 256 + e] + red[3 * CHK * 256 + e]);
+            const int k = c0 + (e >> 8), row = (e >> 4) & 15, col = e & 15;
+            int ow, in_dim, o0, i0;
+            acc_tile_info(k, ow, in_dim, o0, i0);
+            atomicAdd(&grad_mlp[ow + (o0 + row) * in_dim + i0 + col], v);
+        }
     }
 }
 
@@ -693,6 +700,20 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
     NGP_CHECK_ARG(xyzs && denc && grad_table);
     hash_bwd_kernel<0><<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx,
                                                                                      ga, denc, grad_table, 0, L);
+    return ngp_launch_status();
+}
+
+int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                             const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
+                             int level_hi, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0 && 0 <= level_lo && level_lo <= level_hi && level_hi <= L);
+    if (n == 0 || level_lo == level_hi) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && denc && grad_table);
+    hash_bwd_kernel<0><<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(
+        xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
     return ngp_launch_status();
 }
 

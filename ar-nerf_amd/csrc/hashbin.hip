@@ -12,7 +12,7 @@
 //
 //   bucket  = (level l, range of BENT consecutive entries of level l)
 //   record  = one (sample, level, y/z corner) = the x-adjacent corner pair:
-//             {key = i0 | i1 << 14 | flags, fx, a0, a1} (16 B): i0/i1 are
+//             {key = i0 | i1 << 13 | flags, fx, a0, a1} (16 B): i0/i1 are
 //             the two corners' entry offsets inside the bucket,
 //             a_f = (w_y * w_z) * dL/denc[2l + f]; corner x+c receives
 //             (c ? fx : 1 - fx) * a_f.
@@ -24,7 +24,9 @@
 //   4 write  (hash_write_kernel): recompute each record and store it at its
 //            slot of the bucket's contiguous region (counting sort).
 //   5 accum  (hash_accum_kernel): one workgroup per chunk streams its records
-//            into an LDS image of the range (BENT x 2 fp32 = 128 KB) and
+//            into an fp64 LDS image of the range (BENT x 2 x 8 B = 128 KB;
+//            ds_add_f64 runs ~9x the rate of ds_add_f32 on gfx950, measured
+//            by scripts/diag/lds_atomics.py) and
 //            writes it out once: a read-add-store when it is the bucket's
 //            only chunk and nothing was added to the range directly, else
 //            atomic adds of the non-zero entries.
@@ -38,16 +40,17 @@
 
 namespace ngp {
 
-constexpr int BSHIFT = 14, BENT = 1 << BSHIFT;  // entries per bucket
-constexpr int NBL = 32;                          // bucket slots per level (2^19 / BENT)
+constexpr int BSHIFT = 13, BENT = 1 << BSHIFT;  // entries per bucket (fp64 LDS image: 128 KB)
+constexpr int NBL = 64;                          // bucket slots per level (2^19 / BENT)
 constexpr int NSLOT = L * NBL;                   // (level, bucket) slots per tile row
-constexpr int MAXB = 512;                        // buckets over all levels
+constexpr int MAXB = 1024;                       // buckets over all levels
 constexpr int TILE = 256;                        // samples per count/write tile
 constexpr int RPT = TILE * 4 / 256;              // records per thread per level
 constexpr uint32_t CH = 32768;                   // records per pass-5 chunk
 constexpr uint32_t F_C0 = 1u << 28;              // record carries corner x only (pair split)
 
 struct BinArgs {
+    int lo;                 // levels [lo, L) are binned (the others have no buckets)
     uint32_t bbase[L + 1];  // first bucket of level l
     int64_t tiles_cap;      // tiles the workspace holds
 };
@@ -57,7 +60,7 @@ struct BinWs {
     uint32_t* tot;     // [MAXB] records per bucket
     uint32_t* rstart;  // [MAXB + 1] bucket region starts
     uint32_t* items;   // [MAXB + 1] chunk prefix
-    uint32_t* ofs;     // [tiles_cap][NSLOT] counts, then exclusive offsets over tiles
+    uint32_t* ofs;     // [NSLOT][tiles_cap] counts, then exclusive offsets over tiles
     uint4* rec;        // [tiles_cap * TILE * 4 * L]
 };
 
@@ -146,7 +149,7 @@ __global__ void __launch_bounds__(256) hash_count_kernel(const float* __restrict
         bool valid[RPT];
         tile_inputs(xyzs, sidx, ga, tile * TILE, N, in, valid);
 #pragma unroll 1
-        for (int l = 0; l < L; ++l) {
+        for (int l = ba.lo; l < L; ++l) {
 #pragma unroll
             for (int k = 0; k < RPT; ++k) {
                 if (!valid[k]) continue;
@@ -155,8 +158,7 @@ __global__ void __launch_bounds__(256) hash_count_kernel(const float* __restrict
             }
         }
         __syncthreads();
-        uint32_t* row = ws.ofs + (size_t)tile * NSLOT;
-        for (int i = t; i < NSLOT; i += 256) row[i] = cnt[i];
+        for (int i = t; i < NSLOT; i += 256) ws.ofs[(size_t)i * ba.tiles_cap + tile] = cnt[i];
         __syncthreads();
     }
 }
@@ -173,7 +175,7 @@ __global__ void __launch_bounds__(256) hash_scan_kernel(const int64_t* __restric
     uint32_t carry = 0;
     for (int64_t c0 = 0; c0 < ntiles; c0 += 256) {
         const int64_t tile = c0 + t;
-        uint32_t* p = ws.ofs + (size_t)tile * NSLOT + slot;
+        uint32_t* p = ws.ofs + (size_t)slot * ba.tiles_cap + tile;
         const uint32_t v = tile < ntiles ? *p : 0u;
         uint32_t x = v;
 #pragma unroll
@@ -213,13 +215,21 @@ __global__ void __launch_bounds__(MAXB) hash_plan_kernel(uint32_t nbt, BinWs ws)
     if (b == 0) { ws.rstart[0] = 0; ws.items[0] = 0; }
 }
 
+// MODE bits: 2 = store each record from registers at its rank (the product
+// path: measured faster than staging a level's records in LDS and writing
+// bucket runs, MODE 0); 1 (no record stores) and 4 (no LDS rank atomics) are
+// diagnostic variants for scripts/diag.
+template <int MODE>
 __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict__ xyzs, int64_t n,
                                                          const int64_t* __restrict__ n_dev,
                                                          const int32_t* __restrict__ sidx, GridArgs ga, BinArgs ba,
                                                          const float* __restrict__ denc, float* __restrict__ grad,
                                                          BinWs ws) {
     __shared__ LevelLds lv;
-    __shared__ uint32_t base[NSLOT];
+    __shared__ uint32_t base[NSLOT];          // this tile's first slot in each bucket region
+    __shared__ uint32_t hist[NBL], loff[NBL + 1];
+    __shared__ uint4 stage[TILE * 4];         // one level's records, sorted by bucket
+    __shared__ uint8_t sbk[TILE * 4];
     load_levels(ga, lv);
     const int64_t N = n_dev ? *n_dev : n;
     const int64_t ntiles = (N + TILE - 1) / TILE;
@@ -228,13 +238,13 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
         const bool spill = tile >= ba.tiles_cap;  // no room: per-sample atomics for this tile
         if (spill && t == 0) ws.fb[MAXB] = 1u;
         if (!spill) {
-            const uint32_t* row = ws.ofs + (size_t)tile * NSLOT;
             for (int i = t; i < NSLOT; i += 256) {
                 const int l = i / NBL, lb = i % NBL;
-                base[i] = lb < (int)(ba.bbase[l + 1] - ba.bbase[l]) ? ws.rstart[ba.bbase[l] + lb] + row[i] : 0u;
+                base[i] = lb < (int)(ba.bbase[l + 1] - ba.bbase[l])
+                              ? ws.rstart[ba.bbase[l] + lb] + ws.ofs[(size_t)i * ba.tiles_cap + tile]
+                              : 0u;
             }
         }
-        __syncthreads();
         float in[RPT][3];
         bool valid[RPT];
         const int64_t j0 = tile * TILE;
@@ -242,17 +252,23 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
         float2 gd[RPT], gn[RPT];
 #pragma unroll
         for (int k = 0; k < RPT; ++k)
-            gd[k] = valid[k] ? *reinterpret_cast<const float2*>(denc + (j0 + k * 64 + (t >> 2)) * 32) : float2{0.f, 0.f};
+            gd[k] = valid[k] ? *reinterpret_cast<const float2*>(denc + (j0 + k * 64 + (t >> 2)) * 32 + 2 * ba.lo)
+                             : float2{0.f, 0.f};
 #pragma unroll 1
-        for (int l = 0; l < L; ++l) {
+        for (int l = ba.lo; l < L; ++l) {
+            if (t < NBL) hist[t] = 0;
+            __syncthreads();  // also: base[] ready; previous level's stage[] reads done
 #pragma unroll
             for (int k = 0; k < RPT; ++k)  // next level's dL/denc, loaded ahead
                 gn[k] = valid[k] && l + 1 < L
                             ? *reinterpret_cast<const float2*>(denc + (j0 + k * 64 + (t >> 2)) * 32 + 2 * (l + 1))
                             : float2{0.f, 0.f};
             const uint32_t off = lv.off[l];
+            uint4 rec[RPT];
+            uint32_t slot[RPT];  // bucket << 16 | rank in the tile's run, or ~0u
 #pragma unroll
             for (int k = 0; k < RPT; ++k) {
+                slot[k] = ~0u;
                 if (!valid[k]) continue;
                 const Rec r = make_rec(in[k], gd[k], cy, cz, lv, l);
                 if (spill) {
@@ -267,11 +283,47 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
                     add_pair_direct(grad, off + r.e1, r.fx, r.a0, r.a1);
                     ws.fb[ba.bbase[l] + b1] = 1u;  // idempotent flag
                 }
-                const uint32_t dst = atomicAdd(&base[l * NBL + b0], 1u);
-                ws.rec[dst] = make_uint4(key, __float_as_uint(r.fx), __float_as_uint(r.a0), __float_as_uint(r.a1));
+                rec[k] = make_uint4(key, __float_as_uint(r.fx), __float_as_uint(r.a0), __float_as_uint(r.a1));
+                slot[k] = (b0 << 16) | ((MODE & 4) ? (uint32_t)(t & 15) : atomicAdd(&hist[b0], 1u));
             }
 #pragma unroll
             for (int k = 0; k < RPT; ++k) gd[k] = gn[k];
+            if (spill) continue;
+            if (MODE & 2) {
+#pragma unroll
+                for (int k = 0; k < RPT; ++k)
+                    if (slot[k] != ~0u && !(MODE & 1))
+                        ws.rec[base[l * NBL + (slot[k] >> 16)] + (slot[k] & 0xffffu)] = rec[k];
+                continue;
+            }
+            __syncthreads();
+            if (t < 64) {  // exclusive scan of the tile's per-bucket counts (NBL = 64 = one wave)
+                const uint32_t h = hist[t];
+                uint32_t x = h;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(x, o, 64);
+                    if (t >= o) x += y;
+                }
+                loff[t] = x - h;
+                if (t == 63) loff[NBL] = x;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < RPT; ++k) {
+                if (slot[k] == ~0u) continue;
+                const uint32_t bb = slot[k] >> 16, r = loff[bb] + (slot[k] & 0xffffu);
+                stage[r] = rec[k];
+                sbk[r] = (uint8_t)bb;
+            }
+            __syncthreads();
+            // runs of one bucket are contiguous in both stage[] and the region
+            const uint32_t nrec = loff[NBL];
+            for (uint32_t r = t; r < nrec; r += 256) {
+                const uint32_t bb = sbk[r];
+                if (!(MODE & 1)) ws.rec[base[l * NBL + bb] + (r - loff[bb])] = stage[r];
+                else if (stage[r].x == 0xdeadbeefu) ws.fb[0] = 2u;  // keeps the staging live
+            }
         }
         __syncthreads();
     }
@@ -282,9 +334,9 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
 template <int MODE>
 __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
                                                           float* __restrict__ grad, BinWs ws) {
-    extern __shared__ __attribute__((aligned(16))) float img[];  // [BENT][2]
+    extern __shared__ __attribute__((aligned(16))) double img[];  // [2][BENT]: feature-major, 8-byte stride
     const uint32_t total = ws.items[nbt];
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63;
     const bool overflow = ws.fb[MAXB] != 0;
     for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
         uint32_t lo = 0, hi = nbt;  // bucket b: items[b] <= it < items[b + 1]
@@ -297,8 +349,8 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
         while (l < L - 1 && b >= ba.bbase[l + 1]) ++l;
         const uint32_t lb = b - ba.bbase[l];
         const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
-        for (uint32_t e = t; e < 2 * BENT / 4; e += blockDim.x)
-            reinterpret_cast<float4*>(img)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (uint32_t e = t; e < 2 * BENT / 2; e += blockDim.x)
+            reinterpret_cast<double2*>(img)[e] = make_double2(0.0, 0.0);
         __syncthreads();
         const uint32_t r0 = ws.rstart[b] + c * CH, r1 = min(ws.rstart[b + 1], r0 + CH);
         constexpr int U = 4;  // records in flight per thread
@@ -311,19 +363,44 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
+                const uint32_t q = q0 + u * blockDim.x;
                 const uint32_t key = v[u].x, i0 = key & (BENT - 1), i1 = (key >> BSHIFT) & (BENT - 1);
                 const float fx = __uint_as_float(v[u].y), a0 = __uint_as_float(v[u].z), a1 = __uint_as_float(v[u].w);
-                if (a0 == 0.f && a1 == 0.f) continue;  // padding (or a zero gradient: adds nothing)
                 const float w0 = 1 - fx;
                 if (MODE & 1) {
-                    if (w0 * a0 + fx * a1 == 1234.5f) img[i0 ^ i1] = 1.f;
+                    if (w0 * a0 + fx * a1 == 1234.5f) img[i0 ^ i1] = 1.0;  // keeps the loads live
                     continue;
                 }
-                atomicAdd(&img[2 * i0], w0 * a0);
-                atomicAdd(&img[2 * i0 + 1], w0 * a1);
-                if (!(key & F_C0)) {
-                    atomicAdd(&img[2 * i1], fx * a0);
-                    atomicAdd(&img[2 * i1 + 1], fx * a1);
+                // the fp32 products tcnn would add, summed in fp64
+                const bool c1 = !(key & F_C0);
+                double p00 = (double)(w0 * a0), p01 = (double)(w0 * a1);
+                double p10 = c1 ? (double)(fx * a0) : 0.0, p11 = c1 ? (double)(fx * a1) : 0.0;
+                // Runs: records 4 apart in a wave are the same y/z corner of
+                // consecutive samples (a ray's), which on coarse levels often
+                // share both entries -- sum such runs in registers first
+                // (segmented suffix sum at lane stride 4), one LDS add per run.
+                const bool pad = q >= r1;
+                const uint32_t kk = pad ? 0xf0000000u | lane : key;
+                const uint32_t prev = __shfl_up(kk, 4, 64);
+                const bool head = lane < 4 || prev != kk;
+                const uint64_t heads = __ballot(head);
+                if (heads != ~0ull) {
+#pragma unroll
+                    for (int o4 = 4; o4 < 64; o4 <<= 1) {
+                        const double d00 = __shfl_down(p00, o4, 64), d01 = __shfl_down(p01, o4, 64);
+                        const double d10 = __shfl_down(p10, o4, 64), d11 = __shfl_down(p11, o4, 64);
+                        const uint64_t span = (0x1111111111111111ull & ((2ull << o4) - 1ull)) & ~1ull;
+                        if (lane + o4 < 64 && (heads & (span << lane)) == 0) {
+                            p00 += d00; p01 += d01; p10 += d10; p11 += d11;
+                        }
+                    }
+                }
+                if (!head || pad) continue;
+                atomicAdd(&img[i0], p00);
+                atomicAdd(&img[BENT + i0], p01);
+                if (c1) {
+                    atomicAdd(&img[i1], p10);
+                    atomicAdd(&img[BENT + i1], p11);
                 }
             }
         }
@@ -331,7 +408,10 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
         float* g = grad + 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
         const bool own = nch == 1 && !overflow && ws.fb[b] == 0;
         for (uint32_t e = t; e < ((MODE & 2) ? 0u : 2 * ne / 4); e += blockDim.x) {
-            const float4 v = reinterpret_cast<const float4*>(img)[e];
+            // entries 2e, 2e+1 x features 0, 1 -> grad[4e .. 4e+3]
+            const double2 f0 = reinterpret_cast<const double2*>(img)[e];
+            const double2 f1 = reinterpret_cast<const double2*>(img + BENT)[e];
+            const float4 v = make_float4((float)f0.x, (float)f1.x, (float)f0.y, (float)f1.y);
             if (own) {  // sole writer of this range: read-add-store keeps the += contract
                 float4 o = reinterpret_cast<const float4*>(g)[e];
                 o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
@@ -347,11 +427,13 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
     }
 }
 
-static int bin_args(const ngp_hashgrid_t* grid, int64_t tiles_cap, BinArgs& ba, uint32_t& nbt) {
+static int bin_args(const ngp_hashgrid_t* grid, int64_t tiles_cap, int lo, BinArgs& ba, uint32_t& nbt) {
+    if (lo < 0 || lo >= L) return NGP_EINVAL;
+    ba.lo = lo;
     uint32_t b = 0;
     for (int l = 0; l < L; ++l) {
         ba.bbase[l] = b;
-        const uint32_t nb = (grid->sizes[l] + BENT - 1) >> BSHIFT;
+        const uint32_t nb = l < lo ? 0u : (grid->sizes[l] + BENT - 1) >> BSHIFT;
         if (nb > (uint32_t)NBL) return NGP_ERANGE;
         if (grid->offsets[l] & 1u) return NGP_EINVAL;  // flush rows are 16-byte aligned
         b += nb;
@@ -375,7 +457,7 @@ size_t ngp_hash_backward_binned_workspace(int64_t max_samples) {
 
 int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                             int64_t max_samples, void* stream) {
+                             int64_t max_samples, int level_lo, void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
@@ -389,21 +471,21 @@ int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev,
     NGP_CHECK_ARG(tiles_cap * TILE * 4 * L < (int64_t)0xffffffffLL);
     BinArgs ba;
     uint32_t nbt;
-    st = bin_args(grid, tiles_cap, ba, nbt);
+    st = bin_args(grid, tiles_cap, level_lo, ba, nbt);
     if (st) return st;
     BinWs ws;
     bin_ws_bytes(tiles_cap, &ws, workspace);
     hipStream_t s = as_stream(stream);
     if (hipMemsetAsync(ws.fb, 0, (MAXB + 1) * sizeof(uint32_t), s) != hipSuccess) return ngp_launch_status();
     static const unsigned capC = resident_blocks(hash_count_kernel, 256, 0);
-    static const unsigned capW = resident_blocks(hash_write_kernel, 256, 0);
+    static const unsigned capW = resident_blocks(hash_write_kernel<2>, 256, 0);
     hash_count_kernel<<<persistent_blocks(n, TILE, capC), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, ws);
     hash_scan_kernel<<<NSLOT, 256, 0, s>>>(n_dev, n, ba, ws);
     hash_plan_kernel<<<1, MAXB, 0, s>>>(nbt, ws);
-    hash_write_kernel<<<persistent_blocks(n, TILE, capW), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, denc,
+    hash_write_kernel<2><<<persistent_blocks(n, TILE, capW), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, denc,
                                                                        grad_table, ws);
     static bool attr = false;
-    const size_t lds = (size_t)BENT * 2 * sizeof(float);
+    const size_t lds = (size_t)BENT * 2 * sizeof(double);
     if (!attr) {
         if (hipFuncSetAttribute((const void*)hash_accum_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds) != hipSuccess)

@@ -10,7 +10,9 @@
 namespace ngp {
 
 // ------------------------------------------------------ composite + loss
-// One lane per ray.  Pass 1 = composite_train_fw (volumerendering.cu:5-44);
+// One wave per ray.  Pass 1 = composite_train_fw (volumerendering.cu:5-44),
+// the transmittance chain walked sample by sample in lane order (readlane)
+// with the reference's early break;
 // then the background blend (models/rendering.py:287-296) and NeRFLoss
 // (losses.py:63-82: rgb loss of type `loss_type`, opacity entropy, depth
 // term) with its analytic gradient; pass 2 = composite_train_bw
@@ -40,120 +42,8 @@ __device__ __forceinline__ void rgb_loss(int type, float x, float y, float& l, f
     }
 }
 
-// Samples are consumed in chunks of CH: the loads of a chunk are issued
-// together (their addresses do not depend on the running transmittance), the
-// arithmetic then runs strictly in sample order with the reference's break.
-constexpr int CH = 8;
-struct SampleChunk {
-    float sg[CH], dl[CH], cr[CH], cg[CH], cb[CH], tt[CH];
-};
-__device__ __forceinline__ void load_chunk(SampleChunk& c, const float* __restrict__ sigmas,
-                                           const float* __restrict__ rgbs, const float* __restrict__ deltas,
-                                           const float* __restrict__ ts, int64_t s0, int64_t cnt) {
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-        const int64_t s = s0 + (j < cnt ? j : 0);
-        c.sg[j] = sigmas[s]; c.dl[j] = deltas[s]; c.tt[j] = ts[s];
-        c.cr[j] = rgbs[3 * s]; c.cg[j] = rgbs[3 * s + 1]; c.cb[j] = rgbs[3 * s + 2];
-    }
-}
-
-__global__ void __launch_bounds__(64) composite_loss_kernel(
-    const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
-    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
-    const float* __restrict__ bg, LossArgs la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
-    float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
-    float* __restrict__ out_loss, int64_t* __restrict__ vr_samples, int32_t* __restrict__ n_active) {
-    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= n_rays) return;
-    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
-    // ---- forward (volumerendering.cu:24-43)
-    float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
-    int64_t samples = 0;
-    bool done = false;
-    SampleChunk c;
-    for (int64_t k0 = 0; k0 < N && !done; k0 += CH) {
-        const int64_t cnt = N - k0 < CH ? N - k0 : CH;
-        load_chunk(c, sigmas, rgbs, deltas, ts, start + k0, cnt);
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            if (j >= cnt || done) break;
-            const float a = 1.0f - __expf(-c.sg[j] * c.dl[j]);
-            const float w = a * T;
-            R += w * c.cr[j]; G += w * c.cg[j]; B += w * c.cb[j];
-            D += w * c.tt[j];
-            O += w;
-            T *= 1.0f - a;
-            if (T <= la.T_thr) { done = true; break; }
-            samples++;
-        }
-    }
-    // ---- background + loss (mean over rays*3 for rgb, over rays otherwise)
-    const float bgc[3] = {bg[0], bg[1], bg[2]};
-    const float xc[3] = {R + bgc[0] * (1 - O), G + bgc[1] * (1 - O), B + bgc[2] * (1 - O)};
-    float loss = 0.f, g[3], gop = 0.f;
-    const float inv3n = la.inv_n_rays / 3.0f;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        float l, d;
-        rgb_loss(la.loss_type, xc[q], gt[3 * ray + q], l, d);
-        loss += l * inv3n;
-        g[q] = d * inv3n;
-        gop -= g[q] * bgc[q];
-    }
-    const float o = O + 1e-10f;
-    loss += la.lambda_opacity * (-o * logf(o)) * la.inv_n_rays;
-    gop += la.lambda_opacity * (-(logf(o) + 1.f)) * la.inv_n_rays;
-    float gdep = 0.f;
-    if (la.lambda_depth != 0.f) {
-        const float v = D / la.depth_scale + 1e-10f;
-        loss += -la.lambda_depth * logf(fminf(v, 1.0f)) * la.inv_n_rays;
-        if (v < 1.0f) gdep = -la.lambda_depth / v / la.depth_scale * la.inv_n_rays;
-    }
-    out_rgb[3 * ray] = xc[0]; out_rgb[3 * ray + 1] = xc[1]; out_rgb[3 * ray + 2] = xc[2];
-    out_op[ray] = O;
-    out_depth[ray] = D;
-    out_loss[ray] = loss;
-    if (vr_samples) atomicAdd((unsigned long long*)vr_samples, (unsigned long long)samples);
-    // samples past the terminating one get exactly zero gradient below, so
-    // the field backward only needs the first n_active samples of this row
-    if (n_active) n_active[n] = (int32_t)(done ? samples + 1 : N);
-    // ---- backward, dL/dws = 0 (volumerendering.cu:124-149) over the first
-    // n_active samples.  Samples past the terminating one carry exactly zero
-    // gradient in the reference; the field backward skips them (sample map),
-    // so their dL_dsig/dL_drgbs entries are left unwritten here.
-    const float gs = gop * (1 - O);
-    const int64_t na = done ? samples + 1 : N;
-    float Tb = 1.0f, r = 0.f, gg = 0.f, b = 0.f, d = 0.f;
-    for (int64_t k0 = 0; k0 < na; k0 += CH) {
-        const int64_t cnt = na - k0 < CH ? na - k0 : CH;
-        load_chunk(c, sigmas, rgbs, deltas, ts, start + k0, cnt);
-#pragma unroll
-        for (int j = 0; j < CH; ++j) {
-            if (j >= cnt) break;
-            const int64_t s = start + k0 + j;
-            const float a = 1.0f - __expf(-c.sg[j] * c.dl[j]);
-            const float w = a * Tb;
-            r += w * c.cr[j]; gg += w * c.cg[j]; b += w * c.cb[j];
-            d += w * c.tt[j];
-            Tb *= 1.0f - a;
-            dL_drgbs[3 * s] = g[0] * w; dL_drgbs[3 * s + 1] = g[1] * w; dL_drgbs[3 * s + 2] = g[2] * w;
-            dL_dsig[s] = c.dl[j] * (g[0] * (c.cr[j] * Tb - (R - r)) + g[1] * (c.cg[j] * Tb - (G - gg)) +
-                                    g[2] * (c.cb[j] * Tb - (B - b)) + gs + gdep * (c.tt[j] * Tb - (D - d)));
-        }
-    }
-}
-
-// Wave-per-ray variant (the one the C-ABI launches).  Lane k of the wave
-// owns sample k0+k of a 64-sample chunk: loads are coalesced and 8192 rays
-// become 8192 waves (the lane-per-ray kernel above fills only 128).
-// * T follows the reference's strictly sequential recurrence T *= 1 - a
-//   (volumerendering.cu:38-41) through a readlane loop, so the termination
-//   index is exactly the sequential one;
-// * the colour / depth / opacity sums and the backward's inclusive prefixes
-//   are wave reductions / scans (fp32 reassociation only);
-// * w and T-after of every composited sample are parked in dL_drgbs[3s],
-//   dL_drgbs[3s+1] between the two passes (overwritten by the backward).
+// wave-wide sum / inclusive prefix sum (the reference's per-ray serial sums,
+// reassociated: fp32 sums over <= 64 lanes then carried chunk to chunk)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -168,15 +58,15 @@ __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
     return v;
 }
 
-__global__ void __launch_bounds__(256) composite_loss_wave_kernel(
-    const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
-    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
-    const float* __restrict__ bg, LossArgs la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
+// One row of rays_a on one wave; returns the composited sample count
+// (vr_samples' share of this ray).
+__device__ __forceinline__ int64_t composite_loss_ray(
+    int64_t n, const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
+    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, const float* __restrict__ gt,
+    const float* __restrict__ bg, const LossArgs& la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
     float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
-    float* __restrict__ out_loss, int64_t* __restrict__ vr_samples, int32_t* __restrict__ n_active) {
+    float* __restrict__ out_loss, int32_t* __restrict__ n_active) {
     const int lane = threadIdx.x & 63;
-    const int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (n >= n_rays) return;  // wave-uniform
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
     // ---- forward
     float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
@@ -236,7 +126,6 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
         out_op[ray] = O;
         out_depth[ray] = D;
         out_loss[ray] = loss;
-        if (vr_samples) atomicAdd((unsigned long long*)vr_samples, (unsigned long long)samples);
         if (n_active) n_active[n] = (int32_t)na;
     }
     // ---- backward over the na composited samples (dL/dws = 0)
@@ -261,6 +150,29 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
         }
         rc = __shfl(pr, 63, 64); gc = __shfl(pg, 63, 64); bc = __shfl(pb, 63, 64); dc = __shfl(pd, 63, 64);
     }
+    return samples;
+}
+
+// Waves stride over the rows; vr_samples is summed per block in LDS and added
+// with ONE global atomic per block (a per-ray atomic on one address
+// serialises at the memory side).
+__global__ void __launch_bounds__(256) composite_loss_wave_kernel(
+    const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
+    const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
+    const float* __restrict__ bg, LossArgs la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
+    float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
+    float* __restrict__ out_loss, int64_t* __restrict__ vr_samples, int32_t* __restrict__ n_active) {
+    __shared__ unsigned long long blk;
+    if (threadIdx.x == 0) blk = 0;
+    __syncthreads();
+    int64_t mine = 0;
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); n < n_rays; n += waves)
+        mine += composite_loss_ray(n, sigmas, rgbs, deltas, ts, rays_a, gt, bg, la, dL_dsig, dL_drgbs, out_rgb, out_op,
+                                   out_depth, out_loss, n_active);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&blk, (unsigned long long)mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && vr_samples && blk) atomicAdd((unsigned long long*)vr_samples, blk);
 }
 
 // ------------------------------------------------------------------ Adam
@@ -310,28 +222,38 @@ __global__ void scatter_max_kernel(const int64_t* __restrict__ idx, const float*
 }
 
 // models/networks.py:273-278: grid = where(grid<0, grid, max(grid*decay, tmp));
-// accumulates sum and count of grid > 0 for the mean.
+// accumulates sum and count of grid > 0 for the mean, in fp64 so the mean is
+// the correctly rounded one whatever the summation order: at initialisation
+// every cell holds sigma ~= 1 and the threshold (= that mean) splits them, so
+// a last-digit difference in an fp32 sum flips thousands of cells and sends
+// training down a different trajectory.
 __global__ void __launch_bounds__(256) grid_ema_kernel(float* __restrict__ grid, const float* __restrict__ tmp, int64_t n,
-                                                       float decay, float* __restrict__ sum_cnt) {
-    float s = 0.f, c = 0.f;
+                                                       float decay, double* __restrict__ sum_cnt) {
+    double s = 0.0, c = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const float gv = grid[i];
         const float nv = gv < 0 ? gv : fmaxf(gv * decay, tmp[i]);
         grid[i] = nv;
-        if (nv > 0) { s += nv; c += 1.f; }
+        if (nv > 0) { s += (double)nv; c += 1.0; }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { s += __shfl_xor(s, o, 64); c += __shfl_xor(c, o, 64); }
-    if ((threadIdx.x & 63) == 0) { atomicAdd(sum_cnt, s); atomicAdd(sum_cnt + 1, c); }
+    __shared__ double ws[2][4];  // one global add pair per block, not per wave
+    if ((threadIdx.x & 63) == 0) { ws[0][threadIdx.x >> 6] = s; ws[1][threadIdx.x >> 6] = c; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicAdd(sum_cnt, (ws[0][0] + ws[0][1]) + (ws[0][2] + ws[0][3]));
+        atomicAdd(sum_cnt + 1, (ws[1][0] + ws[1][1]) + (ws[1][2] + ws[1][3]));
+    }
 }
 
 // threshold = min(mean(grid[grid>0]), thr_max)  (models/networks.py:278-281)
-__global__ void grid_threshold_kernel(const float* __restrict__ sum_cnt, float thr_max, float* __restrict__ thr) {
+__global__ void grid_threshold_kernel(const double* __restrict__ sum_cnt, float thr_max, float* __restrict__ thr) {
     // Python's min(nan, x) is nan (mean of an empty selection), and packbits
     // against a NaN threshold clears every bit -- reproduce that exactly.
     const float nan = __int_as_float(0x7fc00000);
-    const float mean = sum_cnt[1] > 0 ? sum_cnt[0] / sum_cnt[1] : nan;
+    const float mean = sum_cnt[1] > 0 ? (float)(sum_cnt[0] / sum_cnt[1]) : nan;
     thr[0] = sum_cnt[1] > 0 ? fminf(mean, thr_max) : nan;
     thr[1] = mean;
 }
@@ -416,7 +338,7 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_a && rgb_gt && bg && out_rgb && out_opacity && out_depth && out_loss);
     LossArgs la{loss_type, lambda_opacity, lambda_depth, depth_scale, 1.0f / (float)n_rays, T_threshold};
-    composite_loss_wave_kernel<<<(unsigned)((n_rays + 3) / 4), 256, 0, as_stream(stream)>>>(
+    composite_loss_wave_kernel<<<(unsigned)std::min<int64_t>((n_rays + 3) / 4, 512), 256, 0, as_stream(stream)>>>(
         sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
         out_depth, out_loss, vr_samples, n_active);
     return ngp_launch_status();
@@ -448,15 +370,16 @@ int ngp_density_scatter_max(const int64_t* indices, const float* sigmas, int64_t
 }
 
 int ngp_density_grid_ema(float* density_grid, const float* grid_tmp, int64_t n, float decay, float thr_max,
-                         float* sum_cnt_ws, float* threshold_out, void* stream) {
+                         void* sum_cnt_ws, float* threshold_out, void* stream) {
     NGP_CHECK_ARG(n > 0 && density_grid && grid_tmp && sum_cnt_ws && threshold_out);
+    NGP_CHECK_ARG(((uintptr_t)sum_cnt_ws & 7) == 0);
     hipStream_t s = as_stream(stream);
-    hipError_t e = hipMemsetAsync(sum_cnt_ws, 0, 2 * sizeof(float), s);
+    hipError_t e = hipMemsetAsync(sum_cnt_ws, 0, 2 * sizeof(double), s);
     if (e != hipSuccess) return (int)e;
     int64_t blocks = (n + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
-    grid_ema_kernel<<<(unsigned)blocks, 256, 0, s>>>(density_grid, grid_tmp, n, decay, sum_cnt_ws);
-    grid_threshold_kernel<<<1, 1, 0, s>>>(sum_cnt_ws, thr_max, threshold_out);
+    if (blocks > 512) blocks = 512;
+    grid_ema_kernel<<<(unsigned)blocks, 256, 0, s>>>(density_grid, grid_tmp, n, decay, (double*)sum_cnt_ws);
+    grid_threshold_kernel<<<1, 1, 0, s>>>((const double*)sum_cnt_ws, thr_max, threshold_out);
     return ngp_launch_status();
 }
 

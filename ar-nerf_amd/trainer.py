@@ -41,7 +41,7 @@ class NGPTrainer:
     def __init__(self, scale=0.5, batch_size=8192, lr=1e-2, num_epochs=30, steps_per_epoch=1000, loss="raw",
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
-                 device="cuda", process_group=None, hash_backward="atomic", bin_samples_per_ray=128):
+                 device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=128, bin_level_lo=8):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
@@ -74,7 +74,7 @@ class NGPTrainer:
         ax = torch.arange(self.G, dtype=torch.int32, device=dev)
         self.grid_coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3).contiguous()
         self.all_indices = vren.morton3D(self.grid_coords).long()
-        self._sum_cnt = torch.zeros(2, device=dev)
+        self._sum_cnt = torch.zeros(2, dtype=torch.float64, device=dev)
         self.threshold = torch.zeros(2, device=dev)
         # ---- per-step buffers
         R = batch_size
@@ -106,8 +106,14 @@ class NGPTrainer:
         # binned hash backward: workspace for bin_samples_per_ray gradient-
         # carrying samples per ray on average (1 KiB each; the rest take the
         # atomic path, still exact)
+        # "atomic": per-sample fp32 atomics (ngp_hash_backward); "binned": all
+        # levels through the counting-sort path; "hybrid" (default): coarse
+        # levels [0, bin_level_lo) atomic -- their in-wave run merge keeps the
+        # requests few -- fine levels binned (DESIGN.md "hash backward").
+        assert hash_backward in ("atomic", "binned", "hybrid")
         self.hash_backward = hash_backward
-        if hash_backward == "binned":
+        self.bin_level_lo = 0 if hash_backward == "binned" else bin_level_lo
+        if hash_backward != "atomic":
             self.bin_max_samples = R * bin_samples_per_ray
             nbytes = HG._lib().ngp_hash_backward_binned_workspace(self.bin_max_samples)
             self.bin_ws = torch.empty((nbytes + 255) // 256, 64, dtype=torch.int32, device=dev)
@@ -315,11 +321,15 @@ class NGPTrainer:
         if ev is not None:
             ev["mlp_bwd"][1].record()
             ev["hash_bwd"][0].record()
-        if self.hash_backward == "binned":
+        if self.hash_backward != "atomic":
             vren._ok(HGL.ngp_hash_backward_binned(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
                                                   _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
-                                                  s), "hash_backward_binned")
+                                                  self.bin_level_lo, s), "hash_backward_binned")
+            vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                  _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
+                                                  _p(self.grad[HG.MLP_PARAMS:]), 0, self.bin_level_lo, s),
+                     "hash_backward_levels")
         else:
             vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
                                            HG.ctypes.byref(self.grid.desc),

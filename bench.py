@@ -73,6 +73,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--hash-backward", default="hybrid", choices=["hybrid", "binned", "atomic"])
     return ap.parse_args()
 
 
@@ -159,7 +160,7 @@ def main():
     gt_images = scene.gt_images(device=dev)  # (n_img, HW, 3) u8, resident in HBM
     directions = scene.directions.to(dev).contiguous()
     poses = scene.poses.to(dev).contiguous()
-    trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev)
+    trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward)
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
     gen = torch.Generator(device=dev)
     gen.manual_seed(1 + rank)
@@ -257,6 +258,7 @@ def main():
                        "batch_rays_per_gpu": R, "global_batch_rays": R * world, "pretrain_steps": args.pretrain,
                        "rm_samples_per_ray": round(rm_s, 2), "vr_samples_per_ray": round(vr_s, 2),
                        "parallelism": f"dp{world}", "last_loss": round(loss, 5),
+                       "hash_backward": args.hash_backward,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
             "roofline": dict(kernel=dominant, traffic=None, **kernels[dominant]),
             "kernels": kernels,

@@ -203,14 +203,20 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
 /* Binned form of ngp_hash_backward (same gradient up to fp32 summation order):
  * records per (level, 16384-entry range) are staged in `workspace`, then each
  * range is summed in LDS and written once -- no per-sample global atomics
- * (DESIGN.md "hash backward").  max_samples = samples the workspace holds
- * (1 KiB each; samples beyond it take the atomic path, still exact);
- * workspace = ngp_hash_backward_binned_workspace(max_samples) bytes,
- * 256-byte aligned device memory.  Replaces the same tcnn grid backward. */
+ * (DESIGN.md "hash backward").  Only levels [level_lo, 16) are processed
+ * (pair it with ngp_hash_backward_levels for the others).  max_samples =
+ * samples the workspace holds (1 KiB each; samples beyond it take the atomic
+ * path, still exact); workspace = ngp_hash_backward_binned_workspace(
+ * max_samples) bytes, 256-byte aligned device memory.  Replaces the same tcnn
+ * grid backward. */
 size_t ngp_hash_backward_binned_workspace(int64_t max_samples);
 int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                             int64_t max_samples, void* stream);
+                             int64_t max_samples, int level_lo, void* stream);
+/* ngp_hash_backward restricted to levels [level_lo, level_hi). */
+int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                             const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
+                             int level_hi, void* stream);
 
 /* ------------------------------------------------------ training step */
 /* Fused compositing + NeRFLoss + compositing backward for one training batch:
@@ -252,11 +258,12 @@ int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
  * grid_ema: grid = where(grid<0, grid, max(grid*decay, tmp)) in place, then
  * threshold_out[0] = min(mean(grid[grid>0]), thr_max) (NaN if none, as in
  * Python), threshold_out[1] = the mean; feed threshold_out to ngp_packbits'
- * threshold_dev.  sum_cnt_ws: 2 floats of scratch. */
+ * threshold_dev.  sum_cnt_ws: 16 bytes of scratch (two fp64 accumulators, 8-byte
+ * aligned; the mean is taken in fp64). */
 int ngp_density_scatter_max(const int64_t* indices, const float* sigmas, int64_t n, float* grid_tmp,
                             void* stream);
 int ngp_density_grid_ema(float* density_grid, const float* grid_tmp, int64_t n, float decay,
-                         float thr_max, float* sum_cnt_ws, float* threshold_out, void* stream);
+                         float thr_max, void* sum_cnt_ws, float* threshold_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -61,36 +61,59 @@ def main():
     L = HG._lib()
     cap = 8192 * 128
     ws = torch.empty((L.ngp_hash_backward_binned_workspace(cap) + 255) // 256, 64, dtype=torch.int32, device=dev)
+    side = torch.cuda.Stream()
+    desc = ctypes.byref(tr.grid.desc)
+    args = lambda: (p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), desc, p(tr.denc))  # noqa: E731
 
-    def binned():
-        st = L.ngp_hash_backward_binned(p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx),
-                                        ctypes.byref(tr.grid.desc), p(tr.denc), p(grad), p(ws), cap,
-                                        vp(s.cuda_stream))
-        assert st == 0, st
-    for _ in range(3):
-        binned()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(50):
-        binned()
-    e1.record()
-    torch.cuda.synchronize()
-    out["binned_us"] = round(e0.elapsed_time(e1) / 50 * 1e3, 1)
-    D.ngp_diag_hash_accum.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_int64, vp]
-    for mode in (0, 1, 2, 3):
-        for thr in (1024, 512):
-            def acc():
-                st = D.ngp_diag_hash_accum(mode, thr, ctypes.byref(tr.grid.desc), p(grad), p(ws), cap,
-                                           vp(s.cuda_stream))
-                assert st == 0, st
-            for _ in range(2):
-                acc()
-            e0.record()
-            for _ in range(20):
-                acc()
-            e1.record()
-            torch.cuda.synchronize()
-            out[f"accum_mode{mode}_t{thr}_us"] = round(e0.elapsed_time(e1) / 20 * 1e3, 1)
+    def atomic(lo, hi, stream):
+        assert L.ngp_hash_backward_levels(*args(), p(grad), lo, hi, vp(stream.cuda_stream)) == 0
+
+    def binned(lo, stream):
+        assert L.ngp_hash_backward_binned(*args(), p(grad), p(ws), cap, lo, vp(stream.cuda_stream)) == 0
+
+    def timed(fn, reps=30):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return round(e0.elapsed_time(e1) / reps * 1e3, 1)
+
+    def hybrid(lo, concurrent):
+        def fn():
+            if concurrent:
+                side.wait_stream(s)
+                binned(lo, side)
+                atomic(0, lo, s)
+                s.wait_stream(side)
+            else:
+                atomic(0, lo, s)
+                binned(lo, s)
+        return fn
+
+    out["atomic_all_us"] = timed(lambda: atomic(0, 16, s))
+    out["binned_all_us"] = timed(lambda: binned(0, s))
+    for lo in (4, 6, 8, 10):
+        out[f"hybrid{lo}_seq_us"] = timed(hybrid(lo, False))
+        out[f"hybrid{lo}_conc_us"] = timed(hybrid(lo, True))
+        out[f"atomic_0-{lo}_us"] = timed(lambda: atomic(0, lo, s))
+        out[f"binned_{lo}-16_us"] = timed(lambda: binned(lo, s))
+    binned(0, s)
+    D.ngp_diag_hash_write.argtypes = [ctypes.c_int, vp, ctypes.c_int64, vp, vp, vp, vp, vp, vp, ctypes.c_int64,
+                                      ctypes.c_int, vp]
+    for mode in (0, 1, 2, 3, 7):
+        out[f"write_mode{mode}_us"] = timed(lambda: D.ngp_diag_hash_write(
+            mode, p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), desc, p(tr.denc), p(grad), p(ws),
+            cap, 0, vp(s.cuda_stream)), reps=20)
+    binned(0, s)  # consistent workspace for the accum variants
+    D.ngp_diag_hash_accum.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_int64, ctypes.c_int, vp]
+    for mode in (0, 1, 3):
+        out[f"accum_mode{mode}_us"] = timed(lambda: D.ngp_diag_hash_accum(mode, 1024, desc, p(grad), p(ws), cap, 0,
+                                                                           vp(s.cuda_stream)), reps=20)
     if os.environ.get("BINNED_ONLY"):
         print(json.dumps(out))
         return

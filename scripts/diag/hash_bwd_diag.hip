@@ -24,18 +24,18 @@ extern "C" int ngp_diag_hash_bwd(int mode, int lo, int hi, int blocks_cap, const
 
 // pass 5 alone, on a workspace filled by ngp_hash_backward_binned
 extern "C" int ngp_diag_hash_accum(int mode, int threads, const ngp_hashgrid_t* grid, float* grad, void* workspace,
-                                   int64_t max_samples, void* stream) {
+                                   int64_t max_samples, int lo, void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
     const int64_t tiles_cap = (max_samples + TILE - 1) / TILE;
     BinArgs ba;
     uint32_t nbt;
-    st = bin_args(grid, tiles_cap, ba, nbt);
+    st = bin_args(grid, tiles_cap, lo, ba, nbt);
     if (st) return st;
     BinWs ws;
     bin_ws_bytes(tiles_cap, &ws, workspace);
-    const size_t lds = (size_t)BENT * 2 * sizeof(float);
+    const size_t lds = (size_t)BENT * 2 * sizeof(double);
     hipStream_t s = as_stream(stream);
     static bool attr[4] = {false, false, false, false};
     const void* fns[4] = {(const void*)hash_accum_kernel<0>, (const void*)hash_accum_kernel<1>,
@@ -94,6 +94,34 @@ extern "C" int ngp_diag_lds_atomics(int kind, int iters, float* out, void* strea
         case 2: lds_atomic_bench<2><<<256, 1024, lds, s>>>(iters, out); break;
         case 3: lds_atomic_bench<3><<<256, 1024, lds, s>>>(iters, out); break;
         case 4: lds_atomic_bench<4><<<256, 1024, lds, s>>>(iters, out); break;
+        default: return NGP_EINVAL;
+    }
+    return ngp_launch_status();
+}
+
+// pass 4 alone (after a full ngp_hash_backward_binned call filled ofs/rstart)
+extern "C" int ngp_diag_hash_write(int mode, const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sidx,
+                                   const ngp_hashgrid_t* grid, const float* denc, float* grad, void* workspace,
+                                   int64_t max_samples, int lo, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    const int64_t tiles_cap = (max_samples + TILE - 1) / TILE;
+    BinArgs ba;
+    uint32_t nbt;
+    st = bin_args(grid, tiles_cap, lo, ba, nbt);
+    if (st) return st;
+    BinWs ws;
+    bin_ws_bytes(tiles_cap, &ws, workspace);
+    hipStream_t s = as_stream(stream);
+    const unsigned g = persistent_blocks(n, TILE, 2048);
+    switch (mode) {
+        case 0: hash_write_kernel<0><<<g, 256, 0, s>>>(xyzs, n, n_dev, sidx, ga, ba, denc, grad, ws); break;
+        case 1: hash_write_kernel<1><<<g, 256, 0, s>>>(xyzs, n, n_dev, sidx, ga, ba, denc, grad, ws); break;
+        case 2: hash_write_kernel<2><<<g, 256, 0, s>>>(xyzs, n, n_dev, sidx, ga, ba, denc, grad, ws); break;
+        case 3: hash_write_kernel<3><<<g, 256, 0, s>>>(xyzs, n, n_dev, sidx, ga, ba, denc, grad, ws); break;
+        case 5: hash_write_kernel<5><<<g, 256, 0, s>>>(xyzs, n, n_dev, sidx, ga, ba, denc, grad, ws); break;
+        case 7: hash_write_kernel<7><<<g, 256, 0, s>>>(xyzs, n, n_dev, sidx, ga, ba, denc, grad, ws); break;
         default: return NGP_EINVAL;
     }
     return ngp_launch_status();

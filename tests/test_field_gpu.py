@@ -127,12 +127,13 @@ def test_field_autograd_function():
 
 
 @pytest.mark.parametrize("scale", [0.5, 16.0])
-@pytest.mark.parametrize("level_cap", [1 << 20, 3000])  # max_samples of the workspace
-def test_hash_backward_binned_matches_atomic(scale, level_cap):
+@pytest.mark.parametrize("level_cap,level_lo", [(1 << 20, 0), (3000, 0), (1 << 20, 8)])  # workspace max_samples
+def test_hash_backward_binned_matches_atomic(scale, level_cap, level_lo):
     """ngp_hash_backward_binned (records + LDS range sums) == ngp_hash_backward
     (per-sample atomics) up to fp32 summation order, through a sample_idx
     subset, onto a non-zero gradient (+= contract).  max_samples=3000 sends
-    most tiles through the overflow path (direct atomics)."""
+    most tiles through the overflow path (direct atomics); level_lo=8 bins the
+    fine levels only, the coarse ones going through ngp_hash_backward_levels."""
     x, _ = _points(40000, scale, seed=3)
     n = x.shape[0]
     grid = HG.HashGrid(scale)
@@ -154,7 +155,9 @@ def test_hash_backward_binned_matches_atomic(scale, level_cap):
     for _ in range(2):  # the workspace is reusable: counters reset per call
         out.copy_(base)
         vren._ok(L.ngp_hash_backward_binned(p(x), n, p(n_dev), p(sidx), HG.ctypes.byref(grid.desc), p(denc), p(out),
-                                            p(ws), level_cap, vren._stream()), "hash_backward_binned")
+                                            p(ws), level_cap, level_lo, vren._stream()), "hash_backward_binned")
+        vren._ok(L.ngp_hash_backward_levels(p(x), n, p(n_dev), p(sidx), HG.ctypes.byref(grid.desc), p(denc), p(out),
+                                            0, level_lo, vren._stream()), "hash_backward_levels")
     torch.cuda.synchronize()
     d_ref, d_out = (ref - base).cpu().double(), (out - base).cpu().double()
     assert float(d_ref.abs().max()) > 0
