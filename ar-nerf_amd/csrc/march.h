@@ -1,0 +1,160 @@
+// Occupancy-grid ray-marching step shared by the training / test marchers
+// (march.hip) and the device-resident test render loop (render.hip).
+// raymarching.cu:11-60,166-234,335-404 of the reference.
+#pragma once
+#pragma clang fp contract(off)
+#include "common.h"
+
+namespace ngp {
+
+// --------------------------------------------------------- marching
+struct MarchParams {
+    const uint8_t* bitfield;
+    const uint32_t* summary;  // nullable: bit w = (64-bit bitfield word w != 0), see ngp_bitfield_summary
+    int n_sum32;              // uint32 words of summary
+    int cascades, grid_size, max_samples;
+    float scale, esf, dt_scale;  // dt_scale: `scale` (train) or `cascades` (test quirk)
+};
+
+// One step of the reference's occupancy walk (raymarching.cu:205-233):
+// returns true and advances t by dt if the sample at t is occupied,
+// otherwise jumps t over the empty voxel with repeated calc_dt steps.
+// SIMPLE = (cascades == 1 && esf == 0): then mip == 0, mip_bound ==
+// min(0.5, scale) and dt == sqrt(3)/max_samples exactly (the general
+// expressions fold to these constants), so the compiler drops frexp /
+// scalbn / the division per step -- same values, bit for bit.
+// `wcache` holds the 64-bit bitfield word (a Morton-aligned 4x4x4 block of
+// cells) last loaded by this lane; consecutive samples along a ray mostly
+// stay in the same block, so most occupancy tests need no memory access.
+struct WordCache {
+    uint32_t idx = 0xffffffffu;
+    uint64_t word = 0;
+    const uint32_t* sum = nullptr;  // LDS copy of the bitfield summary (nullable)
+};
+
+// Copy the bitfield summary into LDS (whole workgroup; call before any
+// early return, followed by __syncthreads()).  Returns the LDS pointer or
+// nullptr when the launch has no summary.
+__device__ __forceinline__ const uint32_t* load_summary(const MarchParams& p, uint32_t* lds) {
+    if (!p.summary) return nullptr;
+    for (int i = threadIdx.x; i < p.n_sum32; i += blockDim.x) lds[i] = p.summary[i];
+    return lds;
+}
+
+// The occupancy test at t (raymarching.cu:205-221): position, cell, bit.
+// Returns the bit; for an empty cell also the voxel-exit target
+// t_target (:222-228) that the walk then steps past.
+template <bool SIMPLE>
+__device__ __forceinline__ bool march_probe(float t, const float o[3], const float d[3], const float dinv[3],
+                                            const MarchParams& p, float& x, float& y, float& z, float& dt,
+                                            WordCache& wc, float& t_target) {
+    const uint32_t G = (uint32_t)p.grid_size;
+    const uint32_t grid_size3 = G * G * G;
+    const float grid_size_inv = 1.0f / p.grid_size;
+    x = o[0] + t * d[0]; y = o[1] + t * d[1]; z = o[2] + t * d[2];
+    int mip;
+    float mip_bound, mip_bound_inv;
+    if constexpr (SIMPLE) {
+        dt = NGP_SQRT3 / p.max_samples;  // = clamp(t*0, sqrt3/max, 2 sqrt3 scale/G), t finite
+        mip = 0;
+        mip_bound = fminf(0.5f, p.scale);
+        mip_bound_inv = 1 / mip_bound;
+    } else {
+        dt = calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
+        mip = max(mip_from_pos(x, y, z, p.cascades), mip_from_dt(dt, p.grid_size, p.cascades));
+        mip_bound = fminf(scalbnf(1.0f, mip - 1), p.scale);
+        mip_bound_inv = 1 / mip_bound;
+    }
+    const float gm1 = p.grid_size - 1.0f;
+    const int nx = (int)clampf(0.5f * (x * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
+    const int ny = (int)clampf(0.5f * (y * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
+    const int nz = (int)clampf(0.5f * (z * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
+    const uint32_t idx = (uint32_t)mip * grid_size3 + morton3((uint32_t)nx, (uint32_t)ny, (uint32_t)nz);
+    const uint32_t wi = idx >> 6;
+    if (wi != wc.idx) {  // bitfield is (C*G^3/8) bytes, G^3 a multiple of 64 for G >= 4
+        // an all-empty word is known from the LDS summary: no global load, so
+        // a wave crossing empty space never waits on memory
+        const bool any = !wc.sum || ((wc.sum[wi >> 5] >> (wi & 31u)) & 1u);
+        wc.word = any ? reinterpret_cast<const uint64_t*>(p.bitfield)[wi] : 0ull;
+        wc.idx = wi;
+    }
+    const bool occ = (wc.word >> (idx & 63u)) & 1ull;
+    if (occ) return true;
+    const float tx = (((nx + 0.5f + 0.5f * copysignf(1.0f, d[0])) * grid_size_inv * 2 - 1) * mip_bound - x) * dinv[0];
+    const float ty = (((ny + 0.5f + 0.5f * copysignf(1.0f, d[1])) * grid_size_inv * 2 - 1) * mip_bound - y) * dinv[1];
+    const float tz = (((nz + 0.5f + 0.5f * copysignf(1.0f, d[2])) * grid_size_inv * 2 - 1) * mip_bound - z) * dinv[2];
+    t_target = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+    return false;
+}
+
+template <bool SIMPLE>
+__device__ __forceinline__ bool march_step(float& t, const float o[3], const float d[3], const float dinv[3],
+                                           const MarchParams& p, float& x, float& y, float& z, float& dt,
+                                           WordCache& wc) {
+    float t_target;
+    if (march_probe<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc, t_target)) {
+        t += dt;
+        return true;
+    }
+    if constexpr (SIMPLE) {
+        do { t += dt; } while (t < t_target);
+    } else {
+        do {
+            t += calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
+        } while (t < t_target);
+    }
+    return false;
+}
+
+__device__ __forceinline__ void load_ray(const float* rays_o, const float* rays_d, int64_t r, float o[3],
+                                         float d[3], float dinv[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        o[i] = rays_o[3 * r + i];
+        d[i] = rays_d[3 * r + i];
+        dinv[i] = 1.0f / d[i];
+    }
+}
+
+// custom_functions.py:83 noise + raymarching.cu:193-198 start perturbation
+__device__ __forceinline__ float start_t(const float* hits_t, const float* noise, int64_t r, const MarchParams& p) {
+    float t1 = hits_t[2 * r];
+    if (t1 >= 0) {
+        const float dt = calc_dt(t1, p.esf, p.max_samples, p.grid_size, p.scale);
+        t1 += dt * noise[r];
+    }
+    return t1;
+}
+
+}  // namespace ngp
+
+using ngp::MarchParams;
+
+// cascades == 1 and esf == 0 (the Lego configuration): see march_step.
+// Also requires the bitfield to be 8-byte aligned for the word loads (torch
+// allocations are).  dt_scale must be >= 0 so the constant-dt fold holds.
+static inline bool march_simple(const MarchParams& p) { return p.cascades == 1 && p.esf == 0.0f && p.dt_scale >= 0.0f; }
+
+static inline int march_params(const uint8_t* bf, int cascades, int grid_size, float scale, float esf, int max_samples,
+                        MarchParams& p) {
+    if (!bf || cascades < 1 || grid_size < 4 || grid_size > 1024 || max_samples < 1) return NGP_EINVAL;
+    if (((uintptr_t)bf & 7u) != 0) return NGP_EINVAL;  // 64-bit word loads
+    p.bitfield = bf; p.summary = nullptr; p.n_sum32 = 0; p.cascades = cascades; p.grid_size = grid_size; p.max_samples = max_samples;
+    p.scale = scale; p.esf = esf; p.dt_scale = scale;
+    return NGP_OK;
+}
+
+
+// Attach a bitfield summary (ngp_bitfield_summary output for this bitfield).
+// Requires the LDS copy to fit the launch's dynamic LDS budget.
+constexpr int MAX_SUM32 = 16384;  // 64 KB of LDS: cascades * G^3 <= 2^25 cells
+static inline int march_attach_summary(MarchParams& p, const uint32_t* summary) {
+    if (!summary) return NGP_OK;
+    const int64_t cells = (int64_t)p.cascades * p.grid_size * p.grid_size * p.grid_size;
+    if (cells % 2048 != 0) return NGP_EINVAL;  // whole summary words
+    if (cells / 2048 > MAX_SUM32) return NGP_ERANGE;
+    p.summary = summary;
+    p.n_sum32 = (int)(cells / 2048);
+    return NGP_OK;
+}
+static inline size_t march_summary_lds(const MarchParams& p) { return (size_t)p.n_sum32 * sizeof(uint32_t); }

@@ -14,7 +14,12 @@
 //    reference (raymarching.cu:302-305) is gone.
 #pragma clang fp contract(off)
 
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "common.h"
+#include "march.h"
 
 namespace ngp {
 
@@ -74,15 +79,10 @@ __global__ void __launch_bounds__(64) ray_aabb_kernel(const float* __restrict__ 
 // datasets/ray_utils.py:45-70 (rays_d = dir_cam @ R^T, rays_o = c2w[:,3]) for
 // the gathered training batch (train.py:85-87), then the single-box AABB
 // test and the near clamp of models/rendering.py:29-31.
-__global__ void __launch_bounds__(256) raygen_aabb_kernel(
-    const float* __restrict__ directions, const float* __restrict__ poses,
-    const int64_t* __restrict__ img_idx, const int64_t* __restrict__ pix_idx, int64_t n_rays,
-    const float* __restrict__ center, const float* __restrict__ half_size, float near,
-    float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ hits_t) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_rays) return;
-    const float* P = poses + img_idx[r] * 12;
-    const float* dc = directions + pix_idx[r] * 3;
+__device__ __forceinline__ void gen_ray(const float* __restrict__ P, const float* __restrict__ dc,
+                                        const float* __restrict__ center, const float* __restrict__ half_size,
+                                        float near, float* __restrict__ ro, float* __restrict__ rd,
+                                        float* __restrict__ ht) {
     const float d0 = dc[0], d1 = dc[1], d2 = dc[2];
     // einsum 'n1c,nba->n1a' of rearranged c2w: d_i = sum_c dc_c * R[i][c],
     // evaluated c-major like the batched matmul (fp32, no contraction).
@@ -99,9 +99,77 @@ __global__ void __launch_bounds__(256) raygen_aabb_kernel(
     if (t2 > 0) { h0 = fmaxf(t1, 0.0f); h1 = t2; }
     if (h0 >= 0 && h0 < near) h0 = near;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { rays_o[3 * r + i] = o[i]; rays_d[3 * r + i] = d[i]; }
-    hits_t[2 * r] = h0;
-    hits_t[2 * r + 1] = h1;
+    for (int i = 0; i < 3; ++i) { ro[i] = o[i]; rd[i] = d[i]; }
+    ht[0] = h0;
+    ht[1] = h1;
+}
+
+__global__ void __launch_bounds__(256) raygen_aabb_kernel(
+    const float* __restrict__ directions, const float* __restrict__ poses,
+    const int64_t* __restrict__ img_idx, const int64_t* __restrict__ pix_idx, int64_t n_rays,
+    const float* __restrict__ center, const float* __restrict__ half_size, float near,
+    float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ hits_t) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    gen_ray(poses + img_idx[r] * 12, directions + pix_idx[r] * 3, center, half_size, near, rays_o + 3 * r,
+            rays_d + 3 * r, hits_t + 2 * r);
+}
+
+// Counter-based Philox-4x32-10 (Salmon et al., SC'11): 4 independent
+// uniform uint32 per (key, counter), no state to carry between steps.
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+// uniform integer in [0, n) (multiply-shift; bias <= n / 2^32)
+__device__ __forceinline__ int64_t uniform_index(uint32_t u, int64_t n) {
+    return (int64_t)(((uint64_t)u * (uint64_t)n) >> 32);
+}
+
+// One training batch entirely on device: BaseDataset.__getitem__
+// (datasets/base.py:22-35: img_idxs ~ U{0..n_img-1}, pix_idxs ~ U{0..HW-1},
+// rgb = rays[img, pix, :3]), get_rays + AABB + near clamp (as
+// raygen_aabb_kernel) and the marcher's start perturbation noise ~ U[0,1)
+// (models/custom_functions.py:83), from Philox keyed by (seed, step).
+// gt_u8 (n_img, HW, 3) u8 -> rgb_gt = u8 / 255 (f32).
+__global__ void __launch_bounds__(256) sample_batch_kernel(
+    uint64_t seed, uint64_t step, const uint8_t* __restrict__ gt_u8, int64_t n_img, int64_t hw,
+    const float* __restrict__ directions, const float* __restrict__ poses, int64_t n_rays,
+    const float* __restrict__ center, const float* __restrict__ half_size, float near, int64_t* __restrict__ img_idx,
+    int64_t* __restrict__ pix_idx, float* __restrict__ rgb_gt, float* __restrict__ noise,
+    float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ hits_t) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    const uint4 u = philox4x32(make_uint4((uint32_t)r, (uint32_t)(r >> 32), (uint32_t)step, (uint32_t)(step >> 32)),
+                               make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    const int64_t img = uniform_index(u.x, n_img), pix = uniform_index(u.y, hw);
+    img_idx[r] = img;
+    pix_idx[r] = pix;
+    noise[r] = (float)(u.z >> 8) * (1.0f / 16777216.0f);
+    const uint8_t* g = gt_u8 + (img * hw + pix) * 3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) rgb_gt[3 * r + i] = (float)g[i] / 255.0f;
+    gen_ray(poses + img * 12, directions + pix * 3, center, half_size, near, rays_o + 3 * r, rays_d + 3 * r,
+            hits_t + 2 * r);
+}
+
+// Bitfield summary: bit w of the output = (64-bit bitfield word w != 0),
+// i.e. whether the Morton-aligned 4x4x4 cell block w holds any occupied
+// cell.  One lane per 32 words (256 B).
+__global__ void __launch_bounds__(256) bitfield_summary_kernel(const uint64_t* __restrict__ words, int64_t n_words,
+                                                               uint32_t* __restrict__ summary) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i * 32 >= n_words) return;
+    uint32_t m = 0;
+    for (int k = 0; k < 32 && i * 32 + k < n_words; ++k) m |= (words[i * 32 + k] != 0ull ? 1u : 0u) << k;
+    summary[i] = m;
 }
 
 // --------------------------------------------------- morton / packbits
@@ -132,95 +200,6 @@ __global__ void __launch_bounds__(256) packbits_kernel(const float* __restrict__
     uint32_t bits = (a.x > t) | ((a.y > t) << 1) | ((a.z > t) << 2) | ((a.w > t) << 3) |
                     ((b.x > t) << 4) | ((b.y > t) << 5) | ((b.z > t) << 6) | ((b.w > t) << 7);
     bitfield[n] = (uint8_t)bits;
-}
-
-// --------------------------------------------------------- marching
-struct MarchParams {
-    const uint8_t* bitfield;
-    int cascades, grid_size, max_samples;
-    float scale, esf, dt_scale;  // dt_scale: `scale` (train) or `cascades` (test quirk)
-};
-
-// One step of the reference's occupancy walk (raymarching.cu:205-233):
-// returns true and advances t by dt if the sample at t is occupied,
-// otherwise jumps t over the empty voxel with repeated calc_dt steps.
-// SIMPLE = (cascades == 1 && esf == 0): then mip == 0, mip_bound ==
-// min(0.5, scale) and dt == sqrt(3)/max_samples exactly (the general
-// expressions fold to these constants), so the compiler drops frexp /
-// scalbn / the division per step -- same values, bit for bit.
-// `wcache` holds the 64-bit bitfield word (a Morton-aligned 4x4x4 block of
-// cells) last loaded by this lane; consecutive samples along a ray mostly
-// stay in the same block, so most occupancy tests need no memory access.
-struct WordCache {
-    uint32_t idx = 0xffffffffu;
-    uint64_t word = 0;
-};
-
-template <bool SIMPLE>
-__device__ __forceinline__ bool march_step(float& t, const float o[3], const float d[3], const float dinv[3],
-                                           const MarchParams& p, float& x, float& y, float& z, float& dt,
-                                           WordCache& wc) {
-    const uint32_t G = (uint32_t)p.grid_size;
-    const uint32_t grid_size3 = G * G * G;
-    const float grid_size_inv = 1.0f / p.grid_size;
-    x = o[0] + t * d[0]; y = o[1] + t * d[1]; z = o[2] + t * d[2];
-    int mip;
-    float mip_bound, mip_bound_inv;
-    if constexpr (SIMPLE) {
-        dt = NGP_SQRT3 / p.max_samples;  // = clamp(t*0, sqrt3/max, 2 sqrt3 scale/G), t finite
-        mip = 0;
-        mip_bound = fminf(0.5f, p.scale);
-        mip_bound_inv = 1 / mip_bound;
-    } else {
-        dt = calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
-        mip = max(mip_from_pos(x, y, z, p.cascades), mip_from_dt(dt, p.grid_size, p.cascades));
-        mip_bound = fminf(scalbnf(1.0f, mip - 1), p.scale);
-        mip_bound_inv = 1 / mip_bound;
-    }
-    const float gm1 = p.grid_size - 1.0f;
-    const int nx = (int)clampf(0.5f * (x * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
-    const int ny = (int)clampf(0.5f * (y * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
-    const int nz = (int)clampf(0.5f * (z * mip_bound_inv + 1) * p.grid_size, 0.0f, gm1);
-    const uint32_t idx = (uint32_t)mip * grid_size3 + morton3((uint32_t)nx, (uint32_t)ny, (uint32_t)nz);
-    const uint32_t wi = idx >> 6;
-    if (wi != wc.idx) {  // bitfield is (C*G^3/8) bytes, G^3 a multiple of 64 for G >= 4
-        wc.word = reinterpret_cast<const uint64_t*>(p.bitfield)[wi];
-        wc.idx = wi;
-    }
-    const bool occ = (wc.word >> (idx & 63u)) & 1ull;
-    if (occ) { t += dt; return true; }
-    const float tx = (((nx + 0.5f + 0.5f * copysignf(1.0f, d[0])) * grid_size_inv * 2 - 1) * mip_bound - x) * dinv[0];
-    const float ty = (((ny + 0.5f + 0.5f * copysignf(1.0f, d[1])) * grid_size_inv * 2 - 1) * mip_bound - y) * dinv[1];
-    const float tz = (((nz + 0.5f + 0.5f * copysignf(1.0f, d[2])) * grid_size_inv * 2 - 1) * mip_bound - z) * dinv[2];
-    const float t_target = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
-    if constexpr (SIMPLE) {
-        do { t += dt; } while (t < t_target);
-    } else {
-        do {
-            t += calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
-        } while (t < t_target);
-    }
-    return false;
-}
-
-__device__ __forceinline__ void load_ray(const float* rays_o, const float* rays_d, int64_t r, float o[3],
-                                         float d[3], float dinv[3]) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        o[i] = rays_o[3 * r + i];
-        d[i] = rays_d[3 * r + i];
-        dinv[i] = 1.0f / d[i];
-    }
-}
-
-// custom_functions.py:83 noise + raymarching.cu:193-198 start perturbation
-__device__ __forceinline__ float start_t(const float* hits_t, const float* noise, int64_t r, const MarchParams& p) {
-    float t1 = hits_t[2 * r];
-    if (t1 >= 0) {
-        const float dt = calc_dt(t1, p.esf, p.max_samples, p.grid_size, p.scale);
-        t1 += dt * noise[r];
-    }
-    return t1;
 }
 
 // Pass 1 (raymarching.cu:200-234)
@@ -339,33 +318,257 @@ __global__ void __launch_bounds__(64) march_write_kernel(const float* __restrict
 // [r*max_samples, r*max_samples + n_r).  The reference's second walk
 // (:243-279) re-derives exactly these first n_r samples, so storing them is
 // equivalent and halves the latency-bound marching.
-template <bool SIMPLE>
-__global__ void __launch_bounds__(64) march_slots_kernel(const float* __restrict__ rays_o,
-                                                         const float* __restrict__ rays_d,
-                                                         const float* __restrict__ hits_t, int64_t n_rays,
-                                                         const float* __restrict__ noise, MarchParams p,
-                                                         int32_t* __restrict__ counts, float* __restrict__ slot_t,
-                                                         float* __restrict__ slot_dt) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// The samples are staged in LDS (SB per lane, lane-minor: conflict-free) and
+// written out SB at a time with 16-byte stores: a global store inside the
+// walk would sit in vmcnt in front of the next bitfield-word load, and the
+// s_waitcnt for that load would then wait for the (scattered, slow) store too
+// -- one store round trip per occupied sample.
+constexpr int SB = 32;
+constexpr int MARCH_RPW = 16;  // default rays per wave (NGP_MARCH_RPW overrides)
+template <bool SIMPLE, bool STAGE>
+__global__ void __launch_bounds__(256) march_slots_kernel(const float* __restrict__ rays_o,
+                                                          const float* __restrict__ rays_d,
+                                                          const float* __restrict__ hits_t, int64_t n_rays,
+                                                          const float* __restrict__ noise, MarchParams p,
+                                                          int32_t* __restrict__ counts, float* __restrict__ slot_t,
+                                                          float* __restrict__ slot_dt, int rpw) {
+    extern __shared__ uint32_t ssum[];
+    __shared__ float bt[STAGE ? SB : 1][256], bd[STAGE ? SB : 1][256];
+    WordCache wc;
+    wc.sum = load_summary(p, ssum);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, tid = threadIdx.x;
+    if (lane >= rpw) return;
+    const int64_t r = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * rpw + lane;
     if (r >= n_rays) return;
     float o[3], d[3], dinv[3];
     load_ray(rays_o, rays_d, r, o, d, dinv);
     const float t2 = hits_t[2 * r + 1];
     float t = start_t(hits_t, noise, r, p);
-    int N = 0;
+    int N = 0, nb = 0;
     float x, y, z, dt;
     float* st = slot_t + r * (int64_t)p.max_samples;
     float* sd = slot_dt + r * (int64_t)p.max_samples;
-    WordCache wc;
+    // 16-byte stores need 16-byte aligned ray slot ranges
+    const bool vec = (p.max_samples & 3) == 0 && ((uintptr_t)slot_t & 15) == 0 && ((uintptr_t)slot_dt & 15) == 0;
     while (0 <= t && t < t2 && N < p.max_samples) {
         const float tc = t;
         if (march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc)) {
-            st[N] = tc;
-            sd[N] = dt;
-            N++;
+            if constexpr (!STAGE) {
+                st[N] = tc;
+                sd[N] = dt;
+                N++;
+            } else {
+                bt[nb][tid] = tc;
+                bd[nb][tid] = dt;
+                N++;
+                if (++nb == SB) {
+                    const int b0 = N - SB;
+                    if (vec) {
+#pragma unroll
+                        for (int k = 0; k < SB; k += 4) {
+                            *reinterpret_cast<float4*>(st + b0 + k) =
+                                make_float4(bt[k][tid], bt[k + 1][tid], bt[k + 2][tid], bt[k + 3][tid]);
+                            *reinterpret_cast<float4*>(sd + b0 + k) =
+                                make_float4(bd[k][tid], bd[k + 1][tid], bd[k + 2][tid], bd[k + 3][tid]);
+                        }
+                    } else {
+                        for (int k = 0; k < SB; ++k) { st[b0 + k] = bt[k][tid]; sd[b0 + k] = bd[k][tid]; }
+                    }
+                    nb = 0;
+                }
+            }
+        }
+    }
+    if constexpr (STAGE) {
+        for (int k = 0; k < nb; ++k) {
+            st[N - nb + k] = bt[k][tid];
+            sd[N - nb + k] = bd[k][tid];
         }
     }
     counts[r] = N;
+}
+
+// ---------------------------------------------- wave-per-ray lattice march
+// For SIMPLE launches (one cascade, esf = 0) every t the walk ever holds is a
+// point of the lattice t_0, t_{k+1} = fl(t_k + dt) with a constant dt, and
+// that lattice has a closed form: inside one binade [2^e, 2^(e+1)) adding dt
+// moves a multiple of the binade's ulp u by the SAME multiple of u every time
+// (dt/u has no exact .5 fraction; with one, the increment is constant from
+// the second step on), so t_k = t_s + (k - s) * inc_s exactly (fmaf of an
+// exact product).  The walk (march_step) from point k goes to k + 1 when the
+// cell at t_k is occupied, else to the first j > k with t_j >= t_target(k).
+// So one wave takes one ray: lane i evaluates lattice point c + i of a
+// 64-point window (occupancy + jump target, in parallel), then the wave
+// follows the walk's chain through the window with scalar readlanes and
+// writes the visited occupied points with one coalesced store.  Bit-identical
+// to the serial walk; ~8192 waves per batch instead of 128 latency-bound ones.
+//
+// Segment table (per ray, in LDS): segment q starts at lattice index K[q]
+// with value T[q] and advances by I[q] per index until K[q + 1].
+constexpr int LSEG = 32;
+struct LatSeg {
+    int K[LSEG + 1];
+    float T[LSEG], I[LSEG];
+};
+
+__device__ __forceinline__ float lat_t(const LatSeg& sg, int q, int k) {
+    return fmaf((float)(k - sg.K[q]), sg.I[q], sg.T[q]);
+}
+
+// Builds the segments from t0 (>= 0) until the lattice passes t2 and returns
+// k_end = first index with t >= t2 (the walk's stop), or -1 if the table
+// overflows (caller falls back to the serial walk).  Wave-uniform.
+__device__ __forceinline__ int lat_build(float t0, float t2, float dt, LatSeg& sg, int& nseg, bool write) {
+    int k = 0, q = 0;
+    float ts = t0;
+    while (true) {
+        if (!(ts < t2)) {  // this point already stops the walk
+            if (write) sg.K[q] = k;
+            nseg = q;
+            return k;
+        }
+        if (q == LSEG) return -1;
+        int e;
+        frexpf(ts, &e);
+        const float upper = ldexpf(1.0f, e);  // binade [upper/2, upper)
+        const float a = ts + dt, b = a + dt;
+        int n_max;  // last index offset of this segment
+        float inc;
+        if (!(a > ts)) return -1;  // dt below half an ulp: no progress, leave it to the serial walk
+        if (!(b < upper) || (b - a) != (a - ts)) {
+            n_max = 0;  // single-point segment (binade end or a tie step)
+            inc = a - ts;
+        } else {
+            inc = a - ts;
+            n_max = (int)ceilf((upper - ts) / inc) - 1;
+            while (fmaf((float)(n_max + 1), inc, ts) < upper) ++n_max;
+            while (n_max > 0 && !(fmaf((float)n_max, inc, ts) < upper)) --n_max;
+        }
+        if (write) { sg.K[q] = k; sg.T[q] = ts; sg.I[q] = inc; }
+        // the stop may fall inside this segment
+        const float last = fmaf((float)n_max, inc, ts);
+        if (!(last < t2)) {
+            int n = (int)ceilf((t2 - ts) / inc);
+            n = max(0, min(n, n_max));
+            while (n > 0 && !(fmaf((float)(n - 1), inc, ts) < t2)) --n;
+            while (fmaf((float)n, inc, ts) < t2) ++n;
+            if (write) sg.K[q + 1] = k + n_max + 1;
+            nseg = q + 1;
+            return k + n;
+        }
+        ts = last + dt;  // the step that leaves the binade, as the walk rounds it
+        k += n_max + 1;
+        ++q;
+    }
+}
+
+// first j > k with t_j >= T (capped at k_end), k in segment q
+__device__ __forceinline__ int lat_jump(const LatSeg& sg, int nseg, int q, int k, float T, int k_end) {
+    int j = k + 1;
+    while (q + 1 < nseg && j >= sg.K[q + 1]) ++q;
+    while (j < k_end) {
+        const float tj = lat_t(sg, q, j);
+        if (tj >= T) return j;
+        const int send = q + 1 < nseg ? sg.K[q + 1] : k_end;
+        const float need = (T - tj) / sg.I[q];
+        // jump close to the answer, then fix up with exact lattice values
+        int m = need < 4096.f ? max(1, (int)need) : 4096;
+        int jj = min(j + m, send);
+        while (jj > j + 1 && lat_t(sg, q, jj - 1) >= T) --jj;
+        if (jj >= send) {  // target lies beyond this segment
+            if (send >= k_end) return k_end;
+            j = send;
+            ++q;
+            continue;
+        }
+        while (jj < send && lat_t(sg, q, jj) < T) ++jj;
+        if (jj < send) return jj;
+        if (send >= k_end) return k_end;
+        j = send;
+        ++q;
+    }
+    return k_end;
+}
+
+__global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __restrict__ rays_o,
+                                                               const float* __restrict__ rays_d,
+                                                               const float* __restrict__ hits_t, int64_t n_rays,
+                                                               const float* __restrict__ noise, MarchParams p,
+                                                               int32_t* __restrict__ counts,
+                                                               float* __restrict__ slot_t,
+                                                               float* __restrict__ slot_dt) {
+    extern __shared__ uint32_t ssum[];
+    __shared__ LatSeg segs[4];
+    WordCache wc;
+    wc.sum = load_summary(p, ssum);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t r = (int64_t)blockIdx.x * 4 + w;
+    if (r >= n_rays) return;
+    float o[3], d[3], dinv[3];
+    load_ray(rays_o, rays_d, r, o, d, dinv);
+    const float t2 = hits_t[2 * r + 1];
+    const float t0 = start_t(hits_t, noise, r, p);
+    const float dt = NGP_SQRT3 / p.max_samples;
+    float* st = slot_t + r * (int64_t)p.max_samples;
+    float* sd = slot_dt + r * (int64_t)p.max_samples;
+    if (!(0 <= t0) || !(t0 < t2)) {
+        if (lane == 0) counts[r] = 0;
+        return;
+    }
+    LatSeg& sg = segs[w];
+    int nseg = 0;
+    const int k_end = lat_build(t0, t2, dt, sg, nseg, lane == 0);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (k_end < 0) {  // segment table overflow: the serial walk on lane 0
+        if (lane == 0) {
+            float t = t0, x, y, z, dts;
+            int N = 0;
+            while (0 <= t && t < t2 && N < p.max_samples)
+            {
+                const float tc = t;
+                if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) { st[N] = tc; sd[N] = dts; N++; }
+            }
+            counts[r] = N;
+        }
+        return;
+    }
+    int c = 0, N = 0, q0 = 0;  // window start (a visited point), samples, its segment
+    while (c < k_end && N < p.max_samples) {
+        while (q0 + 1 < nseg && c >= sg.K[q0 + 1]) ++q0;
+        const int k = c + lane;
+        int q = q0;
+        while (q + 1 < nseg && k >= sg.K[q + 1]) ++q;
+        const bool live = k < k_end;
+        const float tk = live ? lat_t(sg, q, k) : 0.f;
+        bool occ = false;
+        int nxt = k_end;
+        if (live) {
+            float x, y, z, dts, T;
+            occ = march_probe<true>(tk, o, d, dinv, p, x, y, z, dts, wc, T);
+            nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
+        }
+        const uint64_t occm = __ballot(occ);
+        // follow the walk through the window (scalar)
+        uint64_t vis = 0;
+        int pnt = c, n = N;
+        while (pnt < c + 64 && pnt < k_end && n < p.max_samples) {
+            const int i = pnt - c;
+            if ((occm >> i) & 1ull) { vis |= 1ull << i; ++n; }
+            pnt = __builtin_amdgcn_readlane(nxt, i);
+        }
+        if ((vis >> lane) & 1ull) {
+            const int rank = N + __builtin_popcountll(vis & ((1ull << lane) - 1ull));
+            st[rank] = tk;
+            sd[rank] = dt;
+        }
+        N = n;
+        c = pnt;
+    }
+    if (lane == 0) counts[r] = N;
 }
 
 // Dense ray-ordered outputs from the slots: one wave per ray, lanes over the
@@ -406,6 +609,10 @@ __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict_
                                                         MarchParams p, int N_samples, float* __restrict__ xyzs,
                                                         float* __restrict__ dirs, float* __restrict__ deltas,
                                                         float* __restrict__ ts, int32_t* __restrict__ n_eff) {
+    extern __shared__ uint32_t ssum[];
+    WordCache wc;
+    wc.sum = load_summary(p, ssum);
+    __syncthreads();
     const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= n_alive) return;
     const int64_t r = alive[n];
@@ -416,7 +623,6 @@ __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict_
     int s = 0;
     float x, y, z, dt;
     const int64_t base = n * (int64_t)N_samples;
-    WordCache wc;
     while (t < t2 && s < N_samples) {
         const float tc = t;
         if (march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc)) {
@@ -470,6 +676,30 @@ int ngp_raygen_aabb(const float* directions, const float* poses, const int64_t* 
     return ngp_launch_status();
 }
 
+int ngp_sample_batch(uint64_t seed, uint64_t step, const uint8_t* gt_u8, int64_t n_img, int64_t hw,
+                     const float* directions, const float* poses, int64_t n_rays, const float* center,
+                     const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
+                     float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && n_img >= 1 && hw >= 1);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(gt_u8 && directions && poses && center && half_size && img_idx && pix_idx && rgb_gt && noise &&
+                  rays_o && rays_d && hits_t);
+    sample_batch_kernel<<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
+        seed, step, gt_u8, n_img, hw, directions, poses, n_rays, center, half_size, near_distance, img_idx, pix_idx,
+        rgb_gt, noise, rays_o, rays_d, hits_t);
+    return ngp_launch_status();
+}
+
+int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, uint32_t* summary, void* stream) {
+    NGP_CHECK_ARG(n_bytes >= 0);
+    if (n_bytes == 0) return NGP_OK;
+    NGP_CHECK_ARG(bitfield && summary && n_bytes % 8 == 0 && ((uintptr_t)bitfield & 7u) == 0);
+    const int64_t n_words = n_bytes / 8;
+    bitfield_summary_kernel<<<nblk((n_words + 31) / 32, 256), 256, 0, as_stream(stream)>>>(
+        reinterpret_cast<const uint64_t*>(bitfield), n_words, summary);
+    return ngp_launch_status();
+}
+
 int ngp_morton3d(const int32_t* coords, int64_t n, int32_t* indices, void* stream) {
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
@@ -495,20 +725,6 @@ int ngp_packbits(const float* density_grid, int64_t n_bytes, float threshold, co
     packbits_kernel<<<nblk(n_bytes, 256), 256, 0, as_stream(stream)>>>(density_grid, n_bytes, threshold,
                                                                       threshold_dev, bitfield);
     return ngp_launch_status();
-}
-
-// cascades == 1 and esf == 0 (the Lego configuration): see march_step.
-// Also requires the bitfield to be 8-byte aligned for the word loads (torch
-// allocations are).  dt_scale must be >= 0 so the constant-dt fold holds.
-static bool march_simple(const MarchParams& p) { return p.cascades == 1 && p.esf == 0.0f && p.dt_scale >= 0.0f; }
-
-static int march_params(const uint8_t* bf, int cascades, int grid_size, float scale, float esf, int max_samples,
-                        MarchParams& p) {
-    if (!bf || cascades < 1 || grid_size < 4 || grid_size > 1024 || max_samples < 1) return NGP_EINVAL;
-    if (((uintptr_t)bf & 7u) != 0) return NGP_EINVAL;  // 64-bit word loads
-    p.bitfield = bf; p.cascades = cascades; p.grid_size = grid_size; p.max_samples = max_samples;
-    p.scale = scale; p.esf = esf; p.dt_scale = scale;
-    return NGP_OK;
 }
 
 int ngp_march_train_count(const float* rays_o, const float* rays_d, const float* hits_t, int64_t n_rays,
@@ -551,20 +767,37 @@ int ngp_march_train_write(const float* rays_o, const float* rays_d, const float*
 int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float* hits_t, int64_t n_rays,
                           const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
                           const float* noise, int max_samples, int32_t* counts, int64_t* rays_a, int64_t* total,
-                          float* slot_t, float* slot_dt, void* stream) {
+                          float* slot_t, float* slot_dt, const uint32_t* occ_summary, void* stream) {
     MarchParams p;
     int st = march_params(bitfield, cascades, grid_size, scale, exp_step_factor, max_samples, p);
+    if (st) return st;
+    st = march_attach_summary(p, occ_summary);
     if (st) return st;
     NGP_CHECK_ARG(n_rays >= 0 && total && rays_a && counts);
     hipStream_t s = as_stream(stream);
     if (n_rays > 0) {
         NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && slot_t && slot_dt);
-        if (march_simple(p))
-            march_slots_kernel<true><<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts,
-                                                                     slot_t, slot_dt);
-        else
-            march_slots_kernel<false><<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts,
+        // Rays per 64-lane wave: the walk is a serial, latency-bound chain
+        // per ray, so fewer rays per wave (more waves on more SIMDs) can
+        // finish sooner (NGP_MARCH_RPW / NGP_MARCH_STAGE: diagnostics).
+        const char* env = getenv("NGP_MARCH_RPW");
+        const int rpw = env ? std::max(1, std::min(64, atoi(env))) : MARCH_RPW;
+        const char* es = getenv("NGP_MARCH_STAGE");
+        const bool stage = es ? atoi(es) != 0 : false;
+        const unsigned blocks = nblk(n_rays, 4 * rpw);
+        const size_t lds = march_summary_lds(p);
+        const char* eser = getenv("NGP_MARCH_SERIAL");
+        const bool serial = eser ? atoi(eser) != 0 : false;
+        if (march_simple(p) && !serial) {
+            march_slots_wave_kernel<<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts,
                                                                       slot_t, slot_dt);
+        } else if (march_simple(p)) {
+            if (stage) march_slots_kernel<true, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
+            else march_slots_kernel<true, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
+        } else {
+            if (stage) march_slots_kernel<false, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
+            else march_slots_kernel<false, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
+        }
     }
     scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total);
     return ngp_launch_status();
@@ -584,9 +817,11 @@ int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int6
 int ngp_march_test(const float* rays_o, const float* rays_d, float* hits_t, const int64_t* alive, int64_t n_alive,
                    const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
                    int N_samples, int max_samples, float* xyzs, float* dirs, float* deltas, float* ts,
-                   int32_t* n_eff, void* stream) {
+                   int32_t* n_eff, const uint32_t* occ_summary, void* stream) {
     MarchParams p;
     int st = march_params(bitfield, cascades, grid_size, scale, exp_step_factor, max_samples, p);
+    if (st) return st;
+    st = march_attach_summary(p, occ_summary);
     if (st) return st;
     p.dt_scale = (float)cascades;  // raymarching.cu:370,399 quirk
     NGP_CHECK_ARG(n_alive >= 0 && N_samples >= 1);
@@ -595,10 +830,10 @@ int ngp_march_test(const float* rays_o, const float* rays_d, float* hits_t, cons
     // test-time dt uses `cascades` as its scale: SIMPLE only needs esf == 0 and
     // cascades == 1, where calc_dt is the constant minimum either way.
     if (march_simple(p))
-        march_test_kernel<true><<<nblk(n_alive, 64), 64, 0, as_stream(stream)>>>(
+        march_test_kernel<true><<<nblk(n_alive, 64), 64, march_summary_lds(p), as_stream(stream)>>>(
             rays_o, rays_d, hits_t, alive, n_alive, p, N_samples, xyzs, dirs, deltas, ts, n_eff);
     else
-        march_test_kernel<false><<<nblk(n_alive, 64), 64, 0, as_stream(stream)>>>(
+        march_test_kernel<false><<<nblk(n_alive, 64), 64, march_summary_lds(p), as_stream(stream)>>>(
             rays_o, rays_d, hits_t, alive, n_alive, p, N_samples, xyzs, dirs, deltas, ts, n_eff);
     return ngp_launch_status();
 }

@@ -85,7 +85,7 @@ class NGPTrainer:
         f = dict(device=dev, dtype=torch.float32)
         # Two sets of ray / march buffers: the next batch is marched on a side
         # stream while the current batch's field, loss, backward and Adam run.
-        self.msets = [self._march_buffers(R, cap, f) for _ in range(2)]
+        self.msets = [self._march_buffers(R, cap, f, self.density_bitfield.numel()) for _ in range(2)]
         self.cur = 0
         self.march_stream = torch.cuda.Stream(device=dev)
         self._pending = None  # (set index, event) of a batch marched ahead
@@ -120,16 +120,21 @@ class NGPTrainer:
         self.bg = torch.ones(3, **f) if self.esf == 0 else torch.zeros(3, **f)  # models/rendering.py:287-296
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(1000 + seed + self.rank)
+        self.sample_seed = (1000003 * (seed + 1) + 7919 * self.rank) & 0xFFFFFFFFFFFFFFFF  # ngp_sample_batch key
+        self.sample_counter = 0
         self.L = vren.lib()
         HG._lib()
         # {"field_fwd"|"mlp_bwd"|"hash_bwd": (start, end) torch.cuda.Event} around those launches (bench)
         self.kernel_events = None
 
     @staticmethod
-    def _march_buffers(R, cap, f):
+    def _march_buffers(R, cap, f, cap_bits):
         dev = f["device"]
         return dict(rays_o=torch.empty(R, 3, **f), rays_d=torch.empty(R, 3, **f), hits_t=torch.empty(R, 2, **f),
                     noise=torch.empty(R, **f), counts=torch.empty(R, dtype=torch.int32, device=dev),
+                    img_idxs=torch.empty(R, dtype=torch.int64, device=dev),
+                    pix_idxs=torch.empty(R, dtype=torch.int64, device=dev), rgb_gt=torch.empty(R, 3, **f),
+                    occ_summary=torch.empty((cap_bits + 255) // 256, dtype=torch.int32, device=dev),
                     rays_a=torch.empty(R, 3, dtype=torch.int64, device=dev),
                     n_samples=torch.zeros(1, dtype=torch.int64, device=dev),
                     xyzs=torch.empty(cap, 3, **f), dirs=torch.empty(cap, 3, **f), deltas=torch.empty(cap, **f),
@@ -211,35 +216,53 @@ class NGPTrainer:
         ddp.sync_threshold_(self.threshold, self.pg)  # identical threshold on every rank
         vren.packbits(self.density_grid, self.threshold[:1], self.density_bitfield)
 
-    def _march(self, k, img_idxs, pix_idxs, directions, poses, noise, stream):
-        """Ray generation + AABB + single-pass march of one batch into buffer set k."""
+    def _march(self, k, src, directions, poses, stream):
+        """Ray generation + AABB + single-pass march of one batch into buffer
+        set k.  src = ("idx", img_idxs, pix_idxs, noise | None): rays of the
+        given pixels (noise drawn from self.gen when None); or ("sample",
+        counter, gt_u8): the whole batch drawn on device (ngp_sample_batch:
+        pixels, ground truth, noise from Philox keyed by (seed, counter))."""
         m = self.msets[k]
-        L, R = self.L, img_idxs.shape[0]
+        L, R = self.L, self.batch_size
         evs = self.kernel_events.get("march_side") if self.kernel_events is not None else None
         side = stream is self.march_stream
         with torch.cuda.stream(stream):
             if evs is not None and side:
                 evs[0].record(stream)
             s = HG.c_void_p(stream.cuda_stream)
-            vren._ok(L.ngp_raygen_aabb(_p(directions), _p(poses), _p(img_idxs), _p(pix_idxs), R, _p(self.center),
-                                       _p(self.half_size), ctypes_float(NEAR_DISTANCE), _p(m["rays_o"]),
-                                       _p(m["rays_d"]), _p(m["hits_t"]), s), "raygen")
-            if noise is None:
-                torch.rand(R, out=m["noise"], generator=self.gen)  # custom_functions.py:83
+            if src[0] == "sample":
+                _, counter, gt = src
+                n_img, hw = gt.shape[0], gt.shape[1]
+                vren._ok(L.ngp_sample_batch(self.sample_seed, counter, _p(gt), n_img, hw, _p(directions), _p(poses), R,
+                                            _p(self.center), _p(self.half_size), ctypes_float(NEAR_DISTANCE),
+                                            _p(m["img_idxs"]), _p(m["pix_idxs"]), _p(m["rgb_gt"]), _p(m["noise"]),
+                                            _p(m["rays_o"]), _p(m["rays_d"]), _p(m["hits_t"]), s), "sample_batch")
             else:
-                m["noise"].copy_(noise)
+                _, img_idxs, pix_idxs, noise = src
+                assert img_idxs.shape[0] == R
+                vren._ok(L.ngp_raygen_aabb(_p(directions), _p(poses), _p(img_idxs), _p(pix_idxs), R, _p(self.center),
+                                           _p(self.half_size), ctypes_float(NEAR_DISTANCE), _p(m["rays_o"]),
+                                           _p(m["rays_d"]), _p(m["hits_t"]), s), "raygen")
+                if noise is None:
+                    torch.rand(R, out=m["noise"], generator=self.gen)  # custom_functions.py:83
+                else:
+                    m["noise"].copy_(noise)
+            # the bitfield's block summary, rebuilt per march: any writer of
+            # density_bitfield (update_density_grid, tests, tools) stays valid
+            vren.bitfield_summary(self.density_bitfield, out=m["occ_summary"])
             vren._ok(L.ngp_march_train_slots(_p(m["rays_o"]), _p(m["rays_d"]), _p(m["hits_t"]), R,
                                              _p(self.density_bitfield), self.cascades, self.G,
                                              ctypes_float(self.scale), ctypes_float(self.esf), _p(m["noise"]),
                                              self.max_samples, _p(m["counts"]), _p(m["rays_a"]),
-                                             _p(m["n_samples"]), _p(m["slot_t"]), _p(m["slot_dt"]), s), "march_slots")
+                                             _p(m["n_samples"]), _p(m["slot_t"]), _p(m["slot_dt"]),
+                                             _p(m["occ_summary"]), s), "march_slots")
             vren._ok(L.ngp_march_train_compact(_p(m["rays_o"]), _p(m["rays_d"]), _p(m["rays_a"]), R,
                                                _p(m["slot_t"]), _p(m["slot_dt"]), self.max_samples, _p(m["xyzs"]),
                                                _p(m["dirs"]), _p(m["deltas"]), _p(m["ts"]), s), "march_compact")
             if evs is not None and side:
                 evs[1].record(stream)
 
-    def prefetch(self, img_idxs, pix_idxs, directions, poses, noise=None):
+    def prefetch(self, src, directions, poses):
         """March the NEXT batch into the idle buffer set on the side stream so
         it overlaps the current step's field / loss / backward / Adam.  Called
         by step() once the current set is bound: everything the side stream
@@ -255,12 +278,18 @@ class NGPTrainer:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream())
         self.march_stream.wait_event(ready)
-        self._march(k, img_idxs, pix_idxs, directions, poses, noise, self.march_stream)
+        self._march(k, src, directions, poses, self.march_stream)
         ev = torch.cuda.Event()
         ev.record(self.march_stream)
         self._pending = (k, ev)
         self.n_prefetched += 1
         return True
+
+    def drain(self):
+        """Order the current stream after a batch marched ahead on the side
+        stream (the batch stays pending for the next train_step)."""
+        if self._pending is not None:
+            torch.cuda.current_stream().wait_event(self._pending[1])
 
     def _ev(self, name, i):
         ev = self.kernel_events
@@ -270,26 +299,42 @@ class NGPTrainer:
     # ---------------------------------------------------------------- step
     def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True, next_batch=None):
         """One training step on a batch (train.py:174-200).  img/pix (R) i64,
-        rgb_gt (R,3) f32, directions (HW,3), poses (n_img,3,4), all on device."""
+        rgb_gt (R,3) f32, directions (HW,3), poses (n_img,3,4), all on device.
+        next_batch = (img, pix) of the following step: marched ahead on the
+        side stream."""
+        nxt = None if next_batch is None else ("idx", next_batch[0], next_batch[1], None)
+        return self._step(("idx", img_idxs, pix_idxs, noise), rgb_gt, directions, poses, apply_adam, nxt)
+
+    def train_step(self, gt_u8, directions, poses):
+        """One training step on a batch drawn on device from the training set
+        (gt_u8 (n_img, HW, 3) u8 images, directions (HW,3), poses (n_img,3,4)):
+        the reference's DataLoader + training_step with nothing on the host.
+        The next step's batch is drawn and marched ahead on the side stream."""
+        src = ("sample", self.sample_counter, gt_u8)
+        self.sample_counter += 1
+        return self._step(src, None, directions, poses, True, ("sample", self.sample_counter, gt_u8))
+
+    def _step(self, src, rgb_gt, directions, poses, apply_adam, next_src):
         L, s = self.L, vren._stream()
         self._ev("occupancy_update", 0)
         if self.global_step % self.update_interval == 0:
             self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=self.global_step < self.warmup_steps)
         self._ev("occupancy_update", 1)
         self._ev("raygen_march", 0)
-        R = img_idxs.shape[0]
-        assert R == self.batch_size
+        R = self.batch_size
         if self._pending is not None:  # this batch was marched ahead on the side stream
             k, ev = self._pending
             self._pending = None
             self.cur = k
             torch.cuda.current_stream().wait_event(ev)
         else:
-            self._march(self.cur, img_idxs, pix_idxs, directions, poses, noise, torch.cuda.current_stream())
+            self._march(self.cur, src, directions, poses, torch.cuda.current_stream())
         self._bind(self.msets[self.cur])
+        if rgb_gt is None:
+            rgb_gt = self.rgb_gt
         self._ev("raygen_march", 1)
-        if next_batch is not None and apply_adam:
-            self.prefetch(*next_batch, directions, poses)
+        if next_src is not None and apply_adam:
+            self.prefetch(next_src, directions, poses)
         s = vren._stream()
         HGL = HG._lib()
         if self.kernel_events is not None:

@@ -39,6 +39,8 @@ def _declare(L):
     sig = {
         "ngp_ray_aabb_intersect": [vp, vp, c_int64, vp, vp, c_int, c_int, vp, vp, vp, vp],
         "ngp_raygen_aabb": [vp, vp, vp, vp, c_int64, vp, vp, c_float, vp, vp, vp, vp],
+        "ngp_sample_batch": [ctypes.c_uint64, ctypes.c_uint64, vp, c_int64, c_int64, vp, vp, c_int64, vp, vp,
+                             c_float, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_morton3d": [vp, c_int64, vp, vp],
         "ngp_morton3d_invert": [vp, c_int64, vp, vp],
         "ngp_packbits": [vp, c_int64, c_float, vp, vp, vp],
@@ -46,10 +48,11 @@ def _declare(L):
         "ngp_march_train_write": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, vp, c_int, vp, vp, vp, vp,
                                   vp, vp],
         "ngp_march_train_slots": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, vp, c_int, vp, vp, vp, vp,
-                                  vp, vp],
+                                  vp, vp, vp],
+        "ngp_bitfield_summary": [vp, c_int64, vp, vp],
         "ngp_march_train_compact": [vp, vp, vp, c_int64, vp, vp, c_int, vp, vp, vp, vp, vp],
         "ngp_march_test": [vp, vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, c_int, c_int, vp, vp, vp, vp,
-                           vp, vp],
+                           vp, vp, vp],
         "ngp_composite_train_fw": [vp, vp, vp, vp, vp, c_int64, c_float, vp, vp, vp, vp, vp, vp],
         "ngp_composite_train_bw": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, c_int64, vp, vp, vp, c_float, vp, vp, vp],
         "ngp_composite_test_fw": [vp, vp, vp, vp, c_int64, c_int, vp, c_float, vp, vp, vp, vp, vp],
@@ -165,6 +168,26 @@ def packbits(density_grid, density_threshold, density_bitfield):
     _ok(lib().ngp_packbits(pg, density_bitfield.numel(), thr, thr_dev, pb, _stream()), "packbits")
 
 
+def bitfield_summary(density_bitfield, out=None):
+    """ngp_bitfield_summary: (n_bytes/256) i32 words, bit w = (64-bit word w of
+    the bitfield != 0).  The marchers keep it in LDS to skip empty blocks
+    without a global load (same results with or without it)."""
+    pb = _check("density_bitfield", density_bitfield, torch.uint8)
+    n = density_bitfield.numel()
+    if out is None:
+        out = torch.empty((n + 255) // 256, dtype=torch.int32, device=density_bitfield.device)
+    _ok(lib().ngp_bitfield_summary(pb, n, c_void_p(out.data_ptr()), _stream()), "bitfield_summary")
+    return out
+
+
+def _summary_arg(density_bitfield, cascades, grid_size):
+    """Summary for a marcher launch, or None when the grid is not whole
+    2048-cell words (the marcher then reads the bitfield directly)."""
+    if (int(cascades) * int(grid_size) ** 3) % 2048 != 0 or density_bitfield.numel() % 8 != 0:
+        return None
+    return bitfield_summary(density_bitfield)
+
+
 # ----------------------------------------------------------- marching
 def march_train_count(rays_o, rays_d, hits_t, density_bitfield, cascades, scale, exp_step_factor, noise,
                       grid_size, max_samples):
@@ -211,13 +234,15 @@ def raymarching_train(rays_o, rays_d, hits_t, density_bitfield, cascades, scale,
     slot_t = torch.empty(n * int(max_samples), device=dev)
     slot_dt = torch.empty(n * int(max_samples), device=dev)
     po, pd = _check("rays_o", rays_o, torch.float32), _check("rays_d", rays_d, torch.float32)
+    summ = _summary_arg(density_bitfield, cascades, grid_size)
     _ok(lib().ngp_march_train_slots(po, pd, _check("hits_t", hits_t, torch.float32), n,
                                     _check("density_bitfield", density_bitfield, torch.uint8), int(cascades),
                                     int(grid_size), float(scale), float(exp_step_factor),
                                     _check("noise", noise, torch.float32), int(max_samples),
                                     c_void_p(counts.data_ptr()), c_void_p(rays_a.data_ptr()),
                                     c_void_p(total.data_ptr()), c_void_p(slot_t.data_ptr()),
-                                    c_void_p(slot_dt.data_ptr()), _stream()), "march_train_slots")
+                                    c_void_p(slot_dt.data_ptr()), c_void_p(summ.data_ptr()) if summ is not None else None,
+                                    _stream()), "march_train_slots")
     N = int(total.item())
     xyzs = torch.empty(N, 3, device=dev)
     dirs = torch.empty(N, 3, device=dev)
@@ -242,12 +267,14 @@ def raymarching_test(rays_o, rays_d, hits_t, alive_indices, density_bitfield, ca
     deltas = torch.empty(n, N_samples, device=dev)
     ts = torch.empty(n, N_samples, device=dev)
     neff = torch.empty(n, dtype=torch.int32, device=dev)
+    summ = _summary_arg(density_bitfield, cascades, grid_size)
     _ok(lib().ngp_march_test(_check("rays_o", rays_o, torch.float32), _check("rays_d", rays_d, torch.float32),
                              _check("hits_t", hits_t, torch.float32), _check("alive_indices", alive_indices, torch.int64),
                              n, _check("density_bitfield", density_bitfield, torch.uint8), int(cascades),
                              int(grid_size), float(scale), float(exp_step_factor), int(N_samples), int(max_samples),
                              c_void_p(xyzs.data_ptr()), c_void_p(dirs.data_ptr()), c_void_p(deltas.data_ptr()),
-                             c_void_p(ts.data_ptr()), c_void_p(neff.data_ptr()), _stream()), "raymarching_test")
+                             c_void_p(ts.data_ptr()), c_void_p(neff.data_ptr()),
+                             c_void_p(summ.data_ptr()) if summ is not None else None, _stream()), "raymarching_test")
     return [xyzs, dirs, deltas, ts, neff]
 
 

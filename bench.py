@@ -162,31 +162,20 @@ def main():
     poses = scene.poses.to(dev).contiguous()
     trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward)
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1 + rank)
-    HW, n_img = scene.W * scene.H, scene.poses.shape[0]
     R = args.batch
 
-    def batch():
-        img = torch.randint(0, n_img, (R,), device=dev, generator=gen)
-        pix = torch.randint(0, HW, (R,), device=dev, generator=gen)
-        rgb = gt_images[img, pix].float().div_(255)
-        return img, pix, rgb
-
     def run(n, events=None):
-        """n training steps; batch i+1 is marched on the side stream during
-        step i (trainer.prefetch).  The last step does not prefetch, so every
-        march of the n batches happens inside this call."""
-        cur = batch()
+        """n training steps, each on a batch drawn on device (trainer.train_step:
+        pixels, ground truth and noise from a counter-based RNG); batch i+1 is
+        drawn and marched on the side stream during step i."""
         for i in range(n):
-            nxt = batch() if i + 1 < n else None
             if events is not None:
                 trainer.kernel_events = events[i]
-            trainer.step(*cur, directions, poses, next_batch=None if nxt is None else nxt[:2])
+            trainer.train_step(gt_images, directions, poses)
             if events is not None:
                 n_samples_acc.add_(trainer.n_samples)
                 n_active_acc.add_(trainer.n_active_total)
-            cur = nxt
+        trainer.drain()
 
     n_samples_acc = torch.zeros(1, dtype=torch.int64, device=dev)
     n_active_acc = torch.zeros(1, dtype=torch.int64, device=dev)

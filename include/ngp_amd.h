@@ -54,6 +54,18 @@ int ngp_raygen_aabb(const float* directions, const float* poses, const int64_t* 
                     const float* half_size, float near_distance, float* rays_o, float* rays_d,
                     float* hits_t, void* stream);
 
+/* One training batch generated on device (replaces the DataLoader path
+ * BaseDataset.__getitem__, datasets/base.py:22-35, the batch gathers of
+ * train.py:85-97 and the marcher's torch.rand noise, custom_functions.py:83):
+ * img_idx ~ U{0..n_img-1}, pix_idx ~ U{0..hw-1}, noise ~ U[0,1) from
+ * Philox-4x32-10 keyed by (seed, step) -- a pure function of (seed, step, ray);
+ * rgb_gt (n_rays,3) = gt_u8[img, pix, :] / 255 with gt_u8 (n_img,hw,3) u8;
+ * rays and hits_t as ngp_raygen_aabb. */
+int ngp_sample_batch(uint64_t seed, uint64_t step, const uint8_t* gt_u8, int64_t n_img, int64_t hw,
+                     const float* directions, const float* poses, int64_t n_rays, const float* center,
+                     const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
+                     float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream);
+
 /* ------------------------------------------------- occupancy grid utils */
 /* Replaces vren.morton3D (binding.cpp:36-40 -> raymarching.cu:62-88). */
 int ngp_morton3d(const int32_t* coords, int64_t n, int32_t* indices, void* stream);
@@ -93,7 +105,7 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
                           int64_t n_rays, const uint8_t* bitfield, int cascades, int grid_size,
                           float scale, float exp_step_factor, const float* noise, int max_samples,
                           int32_t* counts, int64_t* rays_a, int64_t* total, float* slot_t,
-                          float* slot_dt, void* stream);
+                          float* slot_dt, const uint32_t* occ_summary, void* stream);
 int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int64_t* rays_a,
                             int64_t n_rays, const float* slot_t, const float* slot_dt, int max_samples,
                             float* xyzs, float* dirs, float* deltas, float* ts, void* stream);
@@ -108,7 +120,15 @@ int ngp_march_test(const float* rays_o, const float* rays_d, float* hits_t, cons
                    int64_t n_alive, const uint8_t* bitfield, int cascades, int grid_size,
                    float scale, float exp_step_factor, int N_samples, int max_samples,
                    float* xyzs, float* dirs, float* deltas, float* ts, int32_t* n_eff,
-                   void* stream);
+                   const uint32_t* occ_summary, void* stream);
+
+/* Occupancy summary of a bitfield, for the marchers above (occ_summary,
+ * nullable there): bit w of summary = (64-bit bitfield word w != 0), i.e.
+ * whether the Morton-aligned 4x4x4 cell block w holds any occupied cell;
+ * n_bytes/256 uint32 words (rounded up).  The marchers keep it in LDS, so a
+ * ray crossing empty blocks never waits on a global load; results are
+ * identical with or without it.  Recompute after every ngp_packbits. */
+int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, uint32_t* summary, void* stream);
 
 /* -------------------------------------------------------- compositing */
 /* Replaces vren.composite_train_fw (binding.cpp:91-101 -> volumerendering.cu:5-83).

@@ -35,6 +35,14 @@ def _setup(R=2048, table_init=0.2, seed=3):
     return sc, tr, img, pix, noise
 
 
+def _true_div255(u8):
+    """u8 / 255 correctly rounded (numpy's astype(float32) / 255.0, the
+    reference's read_image); torch turns division by a scalar into a
+    multiplication by its reciprocal."""
+    x = u8.float()
+    return x / torch.full_like(x, 255.0)
+
+
 def test_training_step_matches_oracle():
     sc, tr, img, pix, noise = _setup()
     R = img.numel()
@@ -117,3 +125,22 @@ def test_prefetched_march_matches_inline():
     assert all(torch.equal(x, y) for x, y in zip(a0[:upd], a1[:upd]))
     for x, y in zip(l0, l1):
         assert abs(x - y) <= 2e-2 * abs(x)
+
+
+def test_train_step_on_device_batches():
+    """trainer.train_step (batches drawn on device, marched ahead on the side
+    stream): the step consumes the batch that ngp_sample_batch drew for its
+    counter, and training converges like the host-batch path."""
+    sc = S.AnalyticScene(W=200, H=200, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3)
+    losses = []
+    for it in range(300):
+        losses.append(float(tr.train_step(gt_img, dirs, poses).sum()))
+        if it == 5:  # the bound batch is the drawn one: its ground truth is the gather
+            assert torch.equal(tr.rgb_gt, _true_div255(gt_img[tr.img_idxs, tr.pix_idxs]))
+    tr.drain()
+    assert tr.n_prefetched >= 250
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert sum(losses[-20:]) / 20 < 0.5 * sum(losses[:20]) / 20

@@ -33,6 +33,14 @@ def _hits(o, d, scale):
     return ht[:, 0].contiguous()
 
 
+def _true_div255(u8):
+    """u8 / 255 correctly rounded (numpy's astype(float32) / 255.0, the
+    reference's read_image); torch turns division by a scalar into a
+    multiplication by its reciprocal."""
+    x = u8.float()
+    return x / torch.full_like(x, 255.0)
+
+
 def test_library_loads_on_gpu():
     assert torch.cuda.is_available()
     assert vren.lib().ngp_version().startswith(b"ngp_amd")
@@ -62,6 +70,44 @@ def test_raygen_aabb_matches_host_rays():
     assert torch.allclose(rd.cpu(), d, atol=1e-6, rtol=1e-6)
     ref = _hits(ro.cpu(), rd.cpu(), 0.5)  # same rays -> bit-exact AABB + clamp
     assert torch.equal(ht.cpu(), ref)
+
+
+def test_sample_batch_on_device():
+    """ngp_sample_batch (datasets/base.py:22-35 + get_rays + AABB + noise on
+    device): the rays equal raygen_aabb on the drawn pixels bit for bit, the
+    ground truth is the u8 gather / 255, indices and noise are in range and
+    roughly uniform, and the draw is a pure function of (seed, step)."""
+    import ctypes
+    sc = S.SyntheticScene(W=200, H=200, n_images=20, scale=0.5)
+    gt = torch.randint(0, 256, (20, 200 * 200, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(0)).to(DEV)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    center = torch.zeros(1, 3, device=DEV); half = torch.ones(1, 3, device=DEV) * 0.5
+    R = 1 << 16
+
+    def draw(seed, step):
+        out = dict(img=torch.empty(R, dtype=torch.int64, device=DEV), pix=torch.empty(R, dtype=torch.int64, device=DEV),
+                   rgb=torch.empty(R, 3, device=DEV), noise=torch.empty(R, device=DEV),
+                   o=torch.empty(R, 3, device=DEV), d=torch.empty(R, 3, device=DEV), ht=torch.empty(R, 2, device=DEV))
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        vren._ok(vren.lib().ngp_sample_batch(seed, step, p(gt), 20, 200 * 200, p(dirs), p(poses), R, p(center),
+                                             p(half), 0.01, p(out["img"]), p(out["pix"]), p(out["rgb"]),
+                                             p(out["noise"]), p(out["o"]), p(out["d"]), p(out["ht"]), vren._stream()),
+                 "sample_batch")
+        return out
+
+    a, b, c = draw(5, 1), draw(5, 1), draw(5, 2)
+    for k in a:
+        assert torch.equal(a[k], b[k])
+    assert not torch.equal(a["pix"], c["pix"])
+    assert int(a["img"].min()) >= 0 and int(a["img"].max()) < 20
+    assert int(a["pix"].min()) >= 0 and int(a["pix"].max()) < 200 * 200
+    assert float(a["noise"].min()) >= 0 and float(a["noise"].max()) < 1
+    hist = torch.bincount(a["img"], minlength=20).float()
+    assert float(hist.min()) > 0.9 * R / 20 and float(hist.max()) < 1.1 * R / 20
+    assert abs(float(a["noise"].mean()) - 0.5) < 0.01
+    ro, rd, ht = vren.raygen_aabb(dirs, poses, a["img"], a["pix"], center, half, 0.01)
+    assert torch.equal(ro, a["o"]) and torch.equal(rd, a["d"]) and torch.equal(ht, a["ht"])
+    assert torch.equal(a["rgb"], _true_div255(gt[a["img"], a["pix"]]))
 
 
 def test_morton_packbits():
