@@ -19,6 +19,8 @@
 // fp32 MFMA accumulation, fp16 layer outputs, fp32 TruncExp / sigmoid.
 #pragma clang fp contract(off)
 
+#include <algorithm>
+
 #include "common.h"
 #include "grid.h"
 
@@ -54,60 +56,68 @@ struct __attribute__((aligned(4))) u2a4 {
     __device__ operator uint2() const { return make_uint2(x, y); }
 };
 
+// Hash-encode level l of one sample: the two features (fp32 accumulation,
+// rounded once to fp16 by the caller).
+__device__ __forceinline__ void encode_level(const float in[3], int l, const LevelLds& lv,
+                                             const uint32_t* __restrict__ table, float& a0, float& a1) {
+    const float sc = lv.scale[l];
+    const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
+    const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
+    float pos[3];
+    uint32_t pg[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float p = fmaf(sc, in[d], 0.5f);
+        const float fl = floorf(p);
+        pg[d] = (uint32_t)(int)fl;
+        pos[d] = p - fl;
+    }
+    uint32_t v[8];
+    float w[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float wt = 1.0f;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) wt *= (c & (1 << d)) ? pos[d] : 1 - pos[d];
+        w[c] = wt;
+    }
+    // x-adjacent corner pairs: one 8-byte load when the two entries are
+    // neighbours (always on dense levels; on hashed levels when px is
+    // even, the x term of the hash being px*1), else two 4-byte loads.
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const uint32_t qy = pg[1] + (yz & 1), qz = pg[2] + (yz >> 1);
+        const uint32_t i0 = corner_index(pg[0], qy, qz, res, size, dense, pow2);
+        const uint32_t i1 = corner_index(pg[0] + 1, qy, qz, res, size, dense, pow2);
+        const uint32_t lo = min(i0, i1), hi = max(i0, i1);
+        const bool adj = hi - lo == 1u;
+        // adjacent: the (4-byte aligned) pair at lo; else the aligned pair
+        // holding lo (level sizes are even, so it stays inside the level)
+        const uint2 pr = *reinterpret_cast<const u2a4*>(table + off + (adj ? lo : (lo & ~1u)));
+        const uint32_t vlo = adj ? pr.x : ((lo & 1u) ? pr.y : pr.x);
+        uint32_t vhi = pr.y;
+        if (!adj) vhi = table[off + hi];
+        v[2 * yz] = i0 < i1 ? vlo : vhi;
+        v[2 * yz + 1] = i0 < i1 ? vhi : vlo;
+    }
+    a0 = 0.f;
+    a1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const _Float16 f0 = __builtin_bit_cast(_Float16, (uint16_t)(v[c] & 0xffffu));
+        const _Float16 f1 = __builtin_bit_cast(_Float16, (uint16_t)(v[c] >> 16));
+        a0 = fmaf(w[c], (float)f0, a0);
+        a1 = fmaf(w[c], (float)f1, a1);
+    }
+}
+
 // Hash-encode levels 4g..4g+3 of one sample -> 8 fp16 values (enc[8g..8g+7]).
 __device__ __forceinline__ h8 encode4(const float in[3], int g, const LevelLds& lv, const uint32_t* __restrict__ table) {
     h8 e;
 #pragma unroll
     for (int jl = 0; jl < 4; ++jl) {
-        const int l = 4 * g + jl;
-        const float sc = lv.scale[l];
-        const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
-        const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
-        float pos[3];
-        uint32_t pg[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const float p = fmaf(sc, in[d], 0.5f);
-            const float fl = floorf(p);
-            pg[d] = (uint32_t)(int)fl;
-            pos[d] = p - fl;
-        }
-        uint32_t v[8];
-        float w[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            float wt = 1.0f;
-#pragma unroll
-            for (int d = 0; d < 3; ++d) wt *= (c & (1 << d)) ? pos[d] : 1 - pos[d];
-            w[c] = wt;
-        }
-        // x-adjacent corner pairs: one 8-byte load when the two entries are
-        // neighbours (always on dense levels; on hashed levels when px is
-        // even, the x term of the hash being px*1), else two 4-byte loads.
-#pragma unroll
-        for (int yz = 0; yz < 4; ++yz) {
-            const uint32_t qy = pg[1] + (yz & 1), qz = pg[2] + (yz >> 1);
-            const uint32_t i0 = corner_index(pg[0], qy, qz, res, size, dense, pow2);
-            const uint32_t i1 = corner_index(pg[0] + 1, qy, qz, res, size, dense, pow2);
-            const uint32_t lo = min(i0, i1), hi = max(i0, i1);
-            const bool adj = hi - lo == 1u;
-            // adjacent: the (4-byte aligned) pair at lo; else the aligned pair
-            // holding lo (level sizes are even, so it stays inside the level)
-            const uint2 pr = *reinterpret_cast<const u2a4*>(table + off + (adj ? lo : (lo & ~1u)));
-            const uint32_t vlo = adj ? pr.x : ((lo & 1u) ? pr.y : pr.x);
-            uint32_t vhi = pr.y;
-            if (!adj) vhi = table[off + hi];
-            v[2 * yz] = i0 < i1 ? vlo : vhi;
-            v[2 * yz + 1] = i0 < i1 ? vhi : vlo;
-        }
-        float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const _Float16 f0 = __builtin_bit_cast(_Float16, (uint16_t)(v[c] & 0xffffu));
-            const _Float16 f1 = __builtin_bit_cast(_Float16, (uint16_t)(v[c] >> 16));
-            a0 = fmaf(w[c], (float)f0, a0);
-            a1 = fmaf(w[c], (float)f1, a1);
-        }
+        float a0, a1;
+        encode_level(in, 4 * g + jl, lv, table, a0, a1);
         e[2 * jl] = (_Float16)a0;
         e[2 * jl + 1] = (_Float16)a1;
     }
@@ -207,18 +217,23 @@ __device__ __forceinline__ float sigmoid_h(_Float16 o) {
     return (float)(_Float16)(1.0f / (1.0f + expf(-(float)o)));
 }
 
-template <bool COLOR>
+// ENC_IN: the encoding comes from ngp_hash_encode (pair-major enc_in with
+// row stride enc_stride) instead of being gathered here.
+template <bool COLOR, bool ENC_IN = false>
 __global__ void __launch_bounds__(256) field_fwd_kernel(const float* __restrict__ xyzs, const float* __restrict__ dirs,
                                                         int64_t n, const int64_t* __restrict__ n_dev, GridArgs ga,
                                                         const uint32_t* __restrict__ table,
                                                         const _Float16* __restrict__ mlp, float* __restrict__ sigmas,
                                                         float* __restrict__ rgbs, _Float16* __restrict__ enc_out,
-                                                        _Float16* __restrict__ h_out) {
+                                                        _Float16* __restrict__ h_out,
+                                                        const _Float16* __restrict__ enc_in = nullptr,
+                                                        int64_t enc_stride = 0,
+                                                        const int32_t* __restrict__ sidx = nullptr) {
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ __attribute__((aligned(16))) _Float16 raw[NGP_MLP_PARAMS];
     __shared__ LevelLds lv;
     stage_raw_weights(mlp, raw);
-    load_levels(ga, lv);
+    if constexpr (!ENC_IN) load_levels(ga, lv);
     __syncthreads();
     load_fwd_weights(raw, sw, COLOR);
     __syncthreads();
@@ -226,11 +241,20 @@ __global__ void __launch_bounds__(256) field_fwd_kernel(const float* __restrict_
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16; base < N; base += nw * 16) {
-        const int64_t i = base + s;
-        const bool valid = i < N;
-        float in[3];
-        load_x01(xyzs, i, valid, ga, in);
-        const h8 e = encode4(in, g, lv, table);
+        const int64_t j = base + s;  // row of the launch; sample i (sidx: only the listed samples)
+        const bool valid = j < N;
+        const int64_t i = valid && sidx ? (int64_t)sidx[j] : j;
+        h8 e;
+        if constexpr (ENC_IN) {
+            const h4 z4 = {0, 0, 0, 0};
+            const h4 ea = valid ? *reinterpret_cast<const h4*>(enc_in + ((2 * g) * enc_stride + i) * 4) : z4;
+            const h4 eb = valid ? *reinterpret_cast<const h4*>(enc_in + ((2 * g + 1) * enc_stride + i) * 4) : z4;
+            e = pack(ea, eb);
+        } else {
+            float in[3];
+            load_x01(xyzs, i, valid, ga, in);
+            e = encode4(in, g, lv, table);
+        }
         h4 h1[4];
         const h4 hh = density_net(e, sw, s, g, h1);
         if (valid) {
@@ -252,6 +276,128 @@ __global__ void __launch_bounds__(256) field_fwd_kernel(const float* __restrict_
                 rgbs[3 * i + 2] = sigmoid_h(o[2]);
             }
         }
+    }
+}
+
+// ------------------------------------------------ level-pair-per-XCD encode
+// Multires hash encoding alone (the gathers of field_fwd_kernel, same
+// arithmetic, bit-identical values), written pair-major:
+//   enc_pm[p][i][0..3] = enc[i][4p .. 4p+3]  (levels 2p, 2p+1; p = 0..7).
+// Block b encodes level pair b % 8 for its share of the samples.  Blocks b
+// and b + 8 land on the same XCD (round-robin dealing; a placement-only
+// assumption: any placement gives the same result), so each XCD's L2 serves
+// ONE level pair (<= 2 x 2 MB of fp16 table) instead of all 23 MB --
+// the fused kernel's gathers mostly missed L2 and queued on the Infinity
+// Cache.  One lane per sample: 8 independent pair-gathers in flight, ~40
+// VGPRs, full occupancy (the fused kernel ran 2 waves per SIMD).
+// One level's parameters as wave-uniform (scalar) values, so the per-level
+// index variant is chosen by scalar branches, not computed for every lane.
+struct LevelU {
+    float sc;
+    uint32_t res, res2, size, off;
+    bool dense, pow2;
+};
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ LevelU level_u(const LevelLds& lv, int l) {
+    LevelU u;
+    u.sc = __uint_as_float(rfl(__float_as_uint(lv.scale[l])));
+    u.res = rfl(lv.res[l]);
+    u.res2 = u.res * u.res;
+    u.size = rfl(lv.size[l]);
+    u.off = rfl(lv.off[l]);
+    u.dense = (rfl(lv.dense) >> l) & 1u;
+    u.pow2 = (rfl(lv.pow2) >> l) & 1u;
+    return u;
+}
+
+// encode_level with the same values (tcnn grid_index, fmaf corner order), but
+// the index reduction specialised per level: hashed levels have a power-of-two
+// size (mask); on dense levels the corner index is below 2 * size (corner
+// coordinates <= res, size >= res^3), so `% size` is one conditional
+// subtract; the generic modulo remains for any other table.
+__device__ __forceinline__ uint32_t reduce_idx(uint32_t idx, const LevelU& u) {
+    if (u.pow2) return idx & (u.size - 1u);
+    if (u.dense) return idx >= u.size ? idx - u.size : idx;
+    return idx % u.size;
+}
+
+__device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& u, const uint32_t* __restrict__ table,
+                                               float& a0, float& a1) {
+    float pos[3];
+    uint32_t pg[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float p = fmaf(u.sc, in[d], 0.5f);
+        const float fl = floorf(p);
+        pg[d] = (uint32_t)(int)fl;
+        pos[d] = p - fl;
+    }
+    float w[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float wt = 1.0f;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) wt *= (c & (1 << d)) ? pos[d] : 1 - pos[d];
+        w[c] = wt;
+    }
+    uint32_t i0[4], i1[4];
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const uint32_t qy = pg[1] + (yz & 1), qz = pg[2] + (yz >> 1);
+        uint32_t r0, r1;
+        if (u.dense) {
+            r0 = pg[0] + qy * u.res + qz * u.res2;
+            r1 = r0 + 1u;
+        } else {
+            const uint32_t h = (qy * 2654435761u) ^ (qz * 805459861u);
+            r0 = (pg[0] * 1u) ^ h;
+            r1 = ((pg[0] + 1u) * 1u) ^ h;
+        }
+        i0[yz] = reduce_idx(r0, u);
+        i1[yz] = reduce_idx(r1, u);
+    }
+    uint32_t v[8];
+    const uint32_t* tl = table + u.off;
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const uint32_t lo = min(i0[yz], i1[yz]), hi = max(i0[yz], i1[yz]);
+        const bool adj = hi - lo == 1u;
+        const uint2 pr = *reinterpret_cast<const u2a4*>(tl + (adj ? lo : (lo & ~1u)));
+        const uint32_t vlo = adj ? pr.x : ((lo & 1u) ? pr.y : pr.x);
+        uint32_t vhi = pr.y;
+        if (!adj) vhi = tl[hi];
+        v[2 * yz] = i0[yz] < i1[yz] ? vlo : vhi;
+        v[2 * yz + 1] = i0[yz] < i1[yz] ? vhi : vlo;
+    }
+    a0 = 0.f;
+    a1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const _Float16 f0 = __builtin_bit_cast(_Float16, (uint16_t)(v[c] & 0xffffu));
+        const _Float16 f1 = __builtin_bit_cast(_Float16, (uint16_t)(v[c] >> 16));
+        a0 = fmaf(w[c], (float)f0, a0);
+        a1 = fmaf(w[c], (float)f1, a1);
+    }
+}
+
+__global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restrict__ xyzs, int64_t n,
+                                                          const int64_t* __restrict__ n_dev, GridArgs ga,
+                                                          const uint32_t* __restrict__ table,
+                                                          _Float16* __restrict__ enc_pm) {
+    __shared__ LevelLds lv;
+    load_levels(ga, lv);
+    __syncthreads();
+    const int64_t N = n_dev ? *n_dev : n;
+    const int pr = blockIdx.x & 7;
+    const LevelU u0 = level_u(lv, 2 * pr), u1 = level_u(lv, 2 * pr + 1);
+    const int64_t nb = gridDim.x >> 3;
+    for (int64_t i = (int64_t)(blockIdx.x >> 3) * blockDim.x + threadIdx.x; i < N; i += nb * blockDim.x) {
+        float in[3];
+        load_x01(xyzs, i, true, ga, in);
+        float a0, a1, b0, b1;
+        encode_level_u(in, u0, table, a0, a1);
+        encode_level_u(in, u1, table, b0, b1);
+        *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) = h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
     }
 }
 
@@ -359,7 +505,7 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
     const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
     const _Float16* __restrict__ enc,
     const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
-    float* __restrict__ denc, float* __restrict__ grad_mlp) {
+    float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride) {
     extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
     _Float16* sw = smem;
     _Float16* raw = smem + SCR;  // the per-wave scratch is free until the loop
@@ -388,7 +534,11 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
         x.dx = 0.f; x.dy = 0.f; x.dz = 1.f; x.dsig = 0.f; x.gr[0] = x.gr[1] = x.gr[2] = 0.f;
         if (jj < N) {
             const int64_t ii = sidx ? (int64_t)sidx[jj] : jj;
-            x.e = *reinterpret_cast<const h8*>(enc + ii * 32 + 8 * g);
+            if (enc_pm_stride > 0)  // pair-major (ngp_hash_encode): pairs 2g, 2g+1
+                x.e = pack(*reinterpret_cast<const h4*>(enc + ((2 * g) * enc_pm_stride + ii) * 4),
+                           *reinterpret_cast<const h4*>(enc + ((2 * g + 1) * enc_pm_stride + ii) * 4));
+            else
+                x.e = *reinterpret_cast<const h8*>(enc + ii * 32 + 8 * g);
             x.dx = dirs[3 * ii]; x.dy = dirs[3 * ii + 1]; x.dz = dirs[3 * ii + 2];
             x.dsig = dL_dsig[ii];
             x.gr[0] = dL_drgb[3 * ii]; x.gr[1] = dL_drgb[3 * ii + 1]; x.gr[2] = dL_drgb[3 * ii + 2];
@@ -652,6 +802,23 @@ int ngp_field_forward(const float* xyzs, const float* dirs, int64_t n, const int
     return ngp_launch_status();
 }
 
+int ngp_field_forward_indexed(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
+                              const int32_t* sample_idx, const ngp_hashgrid_t* grid, const void* table_f16,
+                              const void* mlp_f16, float* sigmas, float* rgbs, void* enc_f16, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && dirs && sample_idx && table_f16 && mlp_f16 && sigmas && rgbs);
+    NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
+    static const unsigned cap = resident_blocks(field_fwd_kernel<true>, 256, 0);
+    field_fwd_kernel<true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
+        xyzs, dirs, n, n_dev, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16, sigmas, rgbs,
+        (_Float16*)enc_f16, nullptr, nullptr, 0, sample_idx);
+    return ngp_launch_status();
+}
+
 int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
                         const void* table_f16, const void* mlp_f16, float* sigmas, void* h_f16, void* stream) {
     GridArgs ga;
@@ -668,8 +835,37 @@ int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, cons
     return ngp_launch_status();
 }
 
+int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
+                    const void* table_f16, void* enc_pm, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && table_f16 && enc_pm && ((uintptr_t)enc_pm & 7) == 0);
+    static const unsigned cap = resident_blocks(hash_encode_kernel, 256, 0);
+    const unsigned per_pair = std::max(1u, std::min(cap / 8, (unsigned)((n + 255) / 256)));
+    hash_encode_kernel<<<8 * per_pair, 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, ga, (const uint32_t*)table_f16,
+                                                                    (_Float16*)enc_pm);
+    return ngp_launch_status();
+}
+
+int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev, const void* mlp_f16,
+                          float* sigmas, float* rgbs, void* h_f16, void* stream) {
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(enc_pm && dirs && mlp_f16 && sigmas && rgbs);
+    NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0);
+    GridArgs ga{};
+    static const unsigned cap = resident_blocks(field_fwd_kernel<true, true>, 256, 0);
+    field_fwd_kernel<true, true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
+        nullptr, dirs, n, n_dev, ga, nullptr, (const _Float16*)mlp_f16, sigmas, rgbs, nullptr, (_Float16*)h_f16,
+        (const _Float16*)enc_pm, n);
+    return ngp_launch_status();
+}
+
 int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
-                           const void* enc_f16,
+                           const void* enc_f16, int64_t enc_pm_stride,
                            const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws,
                            float* grad_mlp, void* stream) {
     NGP_CHECK_ARG(n >= 0);
@@ -686,7 +882,7 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
     }
     field_bwd_mlp_kernel<<<persistent_blocks(n, 64, 256), 256, lds, as_stream(stream)>>>(
         dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
-        grad_mlp);
+        grad_mlp, enc_pm_stride);
     return ngp_launch_status();
 }
 
@@ -724,7 +920,7 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
-    st = ngp_field_backward_mlp(dirs, n, n_dev, nullptr, enc_f16, mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp,
+    st = ngp_field_backward_mlp(dirs, n, n_dev, nullptr, enc_f16, 0, mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, grad_mlp,
                                 stream);
     if (st) return st;
     return ngp_hash_backward(xyzs, n, n_dev, nullptr, grid, denc_ws, grad_table, stream);

@@ -34,8 +34,14 @@ __device__ __forceinline__ void load_levels(const GridArgs& ga, LevelLds& lv) {
 __device__ __forceinline__ uint32_t corner_index(uint32_t px, uint32_t py, uint32_t pz, uint32_t res, uint32_t size,
                                                  bool dense, bool pow2) {
     uint32_t idx = dense ? (px + py * res + pz * (res * res)) : ((px * 1u) ^ (py * 2654435761u) ^ (pz * 805459861u));
-    if (pow2) idx &= size - 1u;
-    else if (idx >= size) idx %= size;
+    // idx % size: hashed levels have a power-of-two size; a dense level's
+    // corner index is below 2 * size (coordinates <= res, size >= res^3), so
+    // one conditional subtract; a real division only for other tables.
+    if (pow2) return idx & (size - 1u);
+    if (idx >= size) {
+        if (dense) return idx - size;
+        if (__builtin_expect(idx >= size, 0)) idx %= size;
+    }
     return idx;
 }
 

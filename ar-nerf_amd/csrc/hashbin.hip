@@ -142,6 +142,9 @@ __global__ void __launch_bounds__(256) hash_count_kernel(const float* __restrict
     const int64_t ntiles = min((N + TILE - 1) / TILE, ba.tiles_cap);
     const int t = threadIdx.x, yz = t & 3, cy = yz & 1, cz = yz >> 1;
     const float2 g0 = make_float2(0.f, 0.f);
+    // the bucket flags are set by hash_write_kernel (a later launch): clear them here
+    if (blockIdx.x == 0)
+        for (int i = t; i <= MAXB; i += blockDim.x) ws.fb[i] = 0u;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         for (int i = t; i < NSLOT; i += 256) cnt[i] = 0;
         __syncthreads();
@@ -476,7 +479,6 @@ int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev,
     BinWs ws;
     bin_ws_bytes(tiles_cap, &ws, workspace);
     hipStream_t s = as_stream(stream);
-    if (hipMemsetAsync(ws.fb, 0, (MAXB + 1) * sizeof(uint32_t), s) != hipSuccess) return ngp_launch_status();
     static const unsigned capC = resident_blocks(hash_count_kernel, 256, 0);
     static const unsigned capW = resident_blocks(hash_write_kernel<2>, 256, 0);
     hash_count_kernel<<<persistent_blocks(n, TILE, capC), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, ws);

@@ -140,13 +140,15 @@ __device__ __forceinline__ int64_t uniform_index(uint32_t u, int64_t n) {
 // (models/custom_functions.py:83), from Philox keyed by (seed, step).
 // gt_u8 (n_img, HW, 3) u8 -> rgb_gt = u8 / 255 (f32).
 __global__ void __launch_bounds__(256) sample_batch_kernel(
-    uint64_t seed, uint64_t step, const uint8_t* __restrict__ gt_u8, int64_t n_img, int64_t hw,
+    uint64_t seed, uint64_t step, const int64_t* __restrict__ step_dev, const uint8_t* __restrict__ gt_u8, int64_t n_img,
+    int64_t hw,
     const float* __restrict__ directions, const float* __restrict__ poses, int64_t n_rays,
     const float* __restrict__ center, const float* __restrict__ half_size, float near, int64_t* __restrict__ img_idx,
     int64_t* __restrict__ pix_idx, float* __restrict__ rgb_gt, float* __restrict__ noise,
     float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ hits_t) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_rays) return;
+    if (step_dev) step += (uint64_t)*step_dev;  // device counter + offset (graph replays)
     const uint4 u = philox4x32(make_uint4((uint32_t)r, (uint32_t)(r >> 32), (uint32_t)step, (uint32_t)(step >> 32)),
                                make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
     const int64_t img = uniform_index(u.x, n_img), pix = uniform_index(u.y, hw);
@@ -685,8 +687,22 @@ int ngp_sample_batch(uint64_t seed, uint64_t step, const uint8_t* gt_u8, int64_t
     NGP_CHECK_ARG(gt_u8 && directions && poses && center && half_size && img_idx && pix_idx && rgb_gt && noise &&
                   rays_o && rays_d && hits_t);
     sample_batch_kernel<<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
-        seed, step, gt_u8, n_img, hw, directions, poses, n_rays, center, half_size, near_distance, img_idx, pix_idx,
-        rgb_gt, noise, rays_o, rays_d, hits_t);
+        seed, step, nullptr, gt_u8, n_img, hw, directions, poses, n_rays, center, half_size, near_distance, img_idx,
+        pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t);
+    return ngp_launch_status();
+}
+
+int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_add, const uint8_t* gt_u8, int64_t n_img,
+                         int64_t hw, const float* directions, const float* poses, int64_t n_rays, const float* center,
+                         const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
+                         float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && n_img >= 1 && hw >= 1 && step_dev);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(gt_u8 && directions && poses && center && half_size && img_idx && pix_idx && rgb_gt && noise &&
+                  rays_o && rays_d && hits_t);
+    sample_batch_kernel<<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
+        seed, (uint64_t)step_add, step_dev, gt_u8, n_img, hw, directions, poses, n_rays, center, half_size,
+        near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t);
     return ngp_launch_status();
 }
 

@@ -59,13 +59,14 @@ __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
 }
 
 // One row of rays_a on one wave; returns the composited sample count
-// (vr_samples' share of this ray).
+// (vr_samples' share of this ray) and, in na_out, the samples that carry
+// gradient (up to and including the terminating one).
 __device__ __forceinline__ int64_t composite_loss_ray(
     int64_t n, const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, const float* __restrict__ gt,
     const float* __restrict__ bg, const LossArgs& la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
     float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
-    float* __restrict__ out_loss, int32_t* __restrict__ n_active) {
+    float* __restrict__ out_loss, int32_t* __restrict__ n_active, int64_t& na_out) {
     const int lane = threadIdx.x & 63;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
     // ---- forward
@@ -128,6 +129,7 @@ __device__ __forceinline__ int64_t composite_loss_ray(
         out_loss[ray] = loss;
         if (n_active) n_active[n] = (int32_t)na;
     }
+    na_out = na;
     // ---- backward over the na composited samples (dL/dws = 0)
     const float gs = gop * (1 - O);
     float rc = 0.f, gc = 0.f, bc = 0.f, dc = 0.f;
@@ -153,26 +155,75 @@ __device__ __forceinline__ int64_t composite_loss_ray(
     return samples;
 }
 
-// Waves stride over the rows; vr_samples is summed per block in LDS and added
-// with ONE global atomic per block (a per-ray atomic on one address
-// serialises at the memory side).
+// Each block takes 4 rows per round (one per wave).  Per round the block
+// sums its rows' gradient-carrying sample counts and reserves that many
+// entries of sample_idx with ONE atomic on alloc[0]; each wave then writes
+// its row's entries (start + k, k < na) -- a row's samples stay contiguous,
+// which the hash backward's run merging relies on.  The last block to finish
+// (alloc[1] ticket) publishes the total to *n_active_total and resets both
+// counters, so the kernel needs no memset and no scan launch.  stats
+// (nullable): [0] += marched samples, [1] += composited samples (vr_samples),
+// [2] += gradient-carrying samples, summed per block in LDS.
 __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
     const float* __restrict__ bg, LossArgs la, float* __restrict__ dL_dsig, float* __restrict__ dL_drgbs,
     float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
-    float* __restrict__ out_loss, int64_t* __restrict__ vr_samples, int32_t* __restrict__ n_active) {
-    __shared__ unsigned long long blk;
-    if (threadIdx.x == 0) blk = 0;
+    float* __restrict__ out_loss, int32_t* __restrict__ n_active, int32_t* __restrict__ sample_idx,
+    unsigned long long* __restrict__ alloc, int64_t* __restrict__ n_active_total, int64_t* __restrict__ stats) {
+    __shared__ unsigned long long blk[3];
+    __shared__ int64_t s_na[4];
+    __shared__ unsigned long long s_base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x < 3) blk[threadIdx.x] = 0;
     __syncthreads();
-    int64_t mine = 0;
-    const int64_t waves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); n < n_rays; n += waves)
-        mine += composite_loss_ray(n, sigmas, rgbs, deltas, ts, rays_a, gt, bg, la, dL_dsig, dL_drgbs, out_rgb, out_op,
-                                   out_depth, out_loss, n_active);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&blk, (unsigned long long)mine);
+    int64_t rm = 0, vr = 0, act = 0;
+    for (int64_t r0 = (int64_t)blockIdx.x * 4; r0 < n_rays; r0 += (int64_t)gridDim.x * 4) {
+        const int64_t n = r0 + wid;
+        int64_t na = 0, start = 0;
+        if (n < n_rays) {
+            vr += composite_loss_ray(n, sigmas, rgbs, deltas, ts, rays_a, gt, bg, la, dL_dsig, dL_drgbs, out_rgb,
+                                     out_op, out_depth, out_loss, n_active, na);
+            start = rays_a[3 * n + 1];
+            rm += rays_a[3 * n + 2];
+            act += na;
+        }
+        if (sample_idx) {
+            if (lane == 0) s_na[wid] = na;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int64_t tot = s_na[0] + s_na[1] + s_na[2] + s_na[3];
+                s_base = tot ? atomicAdd(alloc, (unsigned long long)tot) : 0ull;
+            }
+            __syncthreads();
+            int64_t off = (int64_t)s_base;
+            for (int w = 0; w < wid; ++w) off += s_na[w];
+            for (int64_t k = lane; k < na; k += 64) sample_idx[off + k] = (int32_t)(start + k);
+            __syncthreads();  // s_na / s_base are rewritten next round
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(&blk[0], (unsigned long long)rm);
+        atomicAdd(&blk[1], (unsigned long long)vr);
+        atomicAdd(&blk[2], (unsigned long long)act);
+    }
     __syncthreads();
-    if (threadIdx.x == 0 && vr_samples && blk) atomicAdd((unsigned long long*)vr_samples, blk);
+    if (threadIdx.x == 0) {
+        if (stats) {
+            if (blk[0]) atomicAdd((unsigned long long*)stats, blk[0]);
+            if (blk[1]) atomicAdd((unsigned long long*)stats + 1, blk[1]);
+            if (blk[2]) atomicAdd((unsigned long long*)stats + 2, blk[2]);
+        }
+        if (sample_idx) {
+            __threadfence();
+            const unsigned long long ticket = atomicAdd(alloc + 1, 1ull);
+            if (ticket == gridDim.x - 1) {  // last block: every reservation is done
+                const unsigned long long total = atomicExch(alloc, 0ull);
+                atomicExch(alloc + 1, 0ull);
+                *n_active_total = (int64_t)total;
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------ Adam
@@ -182,10 +233,20 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
 // g = grad * grad_scale (1/world_size after an all-reduce SUM).  Writes the
 // fp16 shadow the kernels read and zeroes the gradient for the next step.
 // 4 params per lane, 16-B loads/stores.
+// lr_dev / step_dev (nullable): learning rate and the 0-based count of steps
+// already taken read from device memory (graph replays), bias corrections
+// for step *step_dev + 1 computed here (same fp32 powf as the host path).
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ grad, float* __restrict__ m,
                                                    float* __restrict__ v, _Float16* __restrict__ p16, int64_t n4,
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2,
-                                                   float grad_scale, int zero_grad) {
+                                                   float grad_scale, int zero_grad, const float* __restrict__ lr_dev,
+                                                   const int64_t* __restrict__ step_dev) {
+    if (lr_dev) lr = *lr_dev;
+    if (step_dev) {
+        const float st = (float)(*step_dev + 1);
+        bc1 = 1.0f - powf(b1, st);
+        bc2 = 1.0f - powf(b2, st);
+    }
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         float4 P = reinterpret_cast<float4*>(p)[i], Gd = reinterpret_cast<float4*>(grad)[i];
@@ -264,7 +325,8 @@ __global__ void grid_threshold_kernel(const double* __restrict__ sum_cnt, float 
 // first n_active[row] samples of every row (one wave per row).
 __global__ void __launch_bounds__(1024) active_scan_kernel(const int32_t* __restrict__ n_active, int64_t n_rows,
                                                            int64_t* __restrict__ act_start,
-                                                           int64_t* __restrict__ total) {
+                                                           int64_t* __restrict__ total,
+                                                           int64_t* __restrict__ total_acc = nullptr) {
     __shared__ int64_t wave_sums[16];
     __shared__ int64_t carry_s;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -308,19 +370,64 @@ __global__ void __launch_bounds__(1024) active_scan_kernel(const int32_t* __rest
         if (tid == 1023) carry_s = run;
         __syncthreads();
     }
-    if (tid == 0) *total = carry_s;
+    if (tid == 0) {
+        *total = carry_s;
+        if (total_acc) *total_acc += carry_s;
+    }
 }
 
 __global__ void __launch_bounds__(256) active_map_kernel(const int32_t* __restrict__ n_active,
                                                          const int64_t* __restrict__ rays_a,
                                                          const int64_t* __restrict__ act_start, int64_t n_rows,
-                                                         int32_t* __restrict__ sample_idx) {
+                                                         int32_t* __restrict__ sample_idx, int first) {
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (r >= n_rows) return;
     const int lane = threadIdx.x & 63;
     const int na = n_active[r];
-    const int64_t src = rays_a[3 * r + 1], dst = act_start[r];
+    const int64_t src = rays_a[3 * r + 1] + first, dst = act_start[r];
     for (int k = lane; k < na; k += 64) sample_idx[dst + k] = (int32_t)(src + k);
+}
+
+// ------------------------------------------- chunked forward (training)
+// The training step only ever reads a row's samples up to its termination
+// (composite_train_fw breaks there, the backward stops there), so the field
+// is evaluated in two rounds: the first `first` samples of every row, then --
+// only for rows still not terminated after them -- the rest.  Same outputs as
+// evaluating every marched sample.
+// Round-1 counts: min(N_r, first).
+__global__ void __launch_bounds__(256) chunk_first_kernel(const int64_t* __restrict__ rays_a, int64_t n_rows, int first,
+                                                          int32_t* __restrict__ counts) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    counts[r] = (int32_t)min(rays_a[3 * r + 2], (int64_t)first);
+}
+
+// Round-2 counts: one wave per row walks the transmittance of its first
+// min(N_r, first) samples exactly as composite_loss_ray's forward does
+// (same expressions, same serial order); a row that has not terminated there
+// and has more samples needs N_r - first more.
+__global__ void __launch_bounds__(256) chunk_rest_kernel(const float* __restrict__ sigmas,
+                                                         const float* __restrict__ deltas,
+                                                         const int64_t* __restrict__ rays_a, int64_t n_rows, int first,
+                                                         float T_thr, int32_t* __restrict__ counts) {
+    const int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (n >= n_rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+    const int64_t M = min(N, (int64_t)first);
+    float T = 1.0f;
+    bool done = false;
+    for (int64_t k0 = 0; k0 < M && !done; k0 += 64) {
+        const int cnt = (int)(M - k0 < 64 ? M - k0 : 64);
+        float sg = 0.f, dl = 0.f;
+        if (lane < cnt) { sg = sigmas[start + k0 + lane]; dl = deltas[start + k0 + lane]; }
+        const float om = 1.0f - (1.0f - __expf(-sg * dl));
+        for (int j = 0; j < cnt; ++j) {
+            T *= __int_as_float(__builtin_amdgcn_readlane(__float_as_int(om), j));
+            if (T <= T_thr) { done = true; break; }
+        }
+    }
+    if (lane == 0) counts[n] = (!done && N > first) ? (int32_t)(N - first) : 0;
 }
 
 }  // namespace ngp
@@ -333,14 +440,45 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
                        const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg, int loss_type,
                        float lambda_opacity, float lambda_depth, float depth_scale, float T_threshold,
                        float* dL_dsigmas, float* dL_drgbs, float* out_rgb, float* out_opacity, float* out_depth,
-                       float* out_loss, int64_t* vr_samples, int32_t* n_active, void* stream) {
+                       float* out_loss, int32_t* n_active, int32_t* sample_idx, void* alloc_ws,
+                       int64_t* n_active_total, int64_t* stats, void* stream) {
     NGP_CHECK_ARG(n_rays >= 0 && loss_type >= 0 && loss_type <= 3 && depth_scale > 0);
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_a && rgb_gt && bg && out_rgb && out_opacity && out_depth && out_loss);
+    NGP_CHECK_ARG(!sample_idx || (alloc_ws && n_active_total && ((uintptr_t)alloc_ws & 7) == 0));
     LossArgs la{loss_type, lambda_opacity, lambda_depth, depth_scale, 1.0f / (float)n_rays, T_threshold};
-    composite_loss_wave_kernel<<<(unsigned)std::min<int64_t>((n_rays + 3) / 4, 512), 256, 0, as_stream(stream)>>>(
+    // one row per wave: every row's dependent load chain in flight at once
+    // (a few rows per wave serialised their memory latencies)
+    composite_loss_wave_kernel<<<(unsigned)std::min<int64_t>((n_rays + 3) / 4, 1 << 20), 256, 0, as_stream(stream)>>>(
         sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
-        out_depth, out_loss, vr_samples, n_active);
+        out_depth, out_loss, n_active, sample_idx, (unsigned long long*)alloc_ws, n_active_total, stats);
+    return ngp_launch_status();
+}
+
+int ngp_chunk_counts(const int64_t* rays_a, int64_t n_rows, int first, const float* sigmas, const float* deltas,
+                     float T_threshold, int32_t* counts, void* stream) {
+    NGP_CHECK_ARG(n_rows >= 0 && first >= 1 && counts && rays_a);
+    if (n_rows == 0) return NGP_OK;
+    if (!sigmas) {
+        chunk_first_kernel<<<(unsigned)((n_rows + 255) / 256), 256, 0, as_stream(stream)>>>(rays_a, n_rows, first,
+                                                                                           counts);
+    } else {
+        NGP_CHECK_ARG(deltas != nullptr);
+        chunk_rest_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, as_stream(stream)>>>(sigmas, deltas, rays_a, n_rows,
+                                                                                      first, T_threshold, counts);
+    }
+    return ngp_launch_status();
+}
+
+int ngp_ray_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_rows, int first, int64_t* start_ws,
+                     int64_t* total, int64_t* total_acc, int32_t* sample_idx, void* stream) {
+    NGP_CHECK_ARG(n_rows >= 0 && total && first >= 0);
+    hipStream_t s = as_stream(stream);
+    if (n_rows > 0) NGP_CHECK_ARG(counts && rays_a && start_ws && sample_idx);
+    active_scan_kernel<<<1, 1024, 0, s>>>(counts, n_rows, start_ws, total, total_acc);
+    if (n_rows > 0)
+        active_map_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, s>>>(counts, rays_a, start_ws, n_rows, sample_idx,
+                                                                      first);
     return ngp_launch_status();
 }
 
@@ -357,7 +495,35 @@ int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     if (blocks > 8192) blocks = 8192;
     adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, lr, beta1, beta2, eps, bc1,
-                                                                 bc2, grad_scale, zero_grad);
+                                                                 bc2, grad_scale, zero_grad, nullptr, nullptr);
+    return ngp_launch_status();
+}
+
+int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16, int64_t n,
+                      const float* lr_dev, float beta1, float beta2, float eps, const int64_t* step_dev,
+                      float grad_scale, int zero_grad, void* stream) {
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && params_f16 && lr_dev && step_dev);
+    if (n % 4 != 0) return NGP_ERANGE;
+    const int64_t n4 = n / 4;
+    int64_t blocks = (n4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
+                                                                 (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
+                                                                 1.f, grad_scale, zero_grad, lr_dev, step_dev);
+    return ngp_launch_status();
+}
+
+// counters[i] += 1 for i < n (the per-step device counters a replayed graph
+// advances at its end: Adam's step count, the batch RNG counter)
+__global__ void counters_inc_kernel(int64_t* __restrict__ c, int n) {
+    if ((int)threadIdx.x < n) c[threadIdx.x] += 1;
+}
+
+int ngp_counters_inc(int64_t* counters, int n, void* stream) {
+    NGP_CHECK_ARG(counters && n >= 1 && n <= 64);
+    counters_inc_kernel<<<1, 64, 0, as_stream(stream)>>>(counters, n);
     return ngp_launch_status();
 }
 
@@ -391,7 +557,7 @@ int ngp_active_samples(const int32_t* n_active, const int64_t* rays_a, int64_t n
     active_scan_kernel<<<1, 1024, 0, s>>>(n_active, n_rows, act_start_ws, n_active_total);
     if (n_rows > 0)
         active_map_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, s>>>(n_active, rays_a, act_start_ws, n_rows,
-                                                                      sample_idx);
+                                                                      sample_idx, 0);
     return ngp_launch_status();
 }
 

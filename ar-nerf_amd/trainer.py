@@ -41,7 +41,8 @@ class NGPTrainer:
     def __init__(self, scale=0.5, batch_size=8192, lr=1e-2, num_epochs=30, steps_per_epoch=1000, loss="raw",
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
-                 device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=128, bin_level_lo=8):
+                 device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=128, bin_level_lo=8,
+                 chunk_first=64):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
@@ -88,19 +89,35 @@ class NGPTrainer:
         self.msets = [self._march_buffers(R, cap, f, self.density_bitfield.numel()) for _ in range(2)]
         self.cur = 0
         self.march_stream = torch.cuda.Stream(device=dev)
+        # NGP_EXEC_PRIORITY=1: steps run on a high-priority stream (measured: no gain)
+        self.exec_stream = (torch.cuda.Stream(device=dev, priority=-1)
+                            if os.environ.get("NGP_EXEC_PRIORITY", "0") == "1" else None)
         self._pending = None  # (set index, event) of a batch marched ahead
         self.n_prefetched = 0
+        self.no_prefetch = os.environ.get("NGP_NO_PREFETCH", "0") == "1"  # march every batch inline (diagnostics)
+        # where in the step the next batch's march is launched on the side stream
+        self.prefetch_at = os.environ.get("NGP_PREFETCH_AT", "after_composite")
         self._bind(self.msets[0])
         self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
-        self.enc = torch.empty(cap, 32, dtype=torch.float16, device=dev)
+        # saved encoding: pair-major (8, cap, 4) for the split forward, else row-major (cap, 32)
+        self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "0") == "1"
+        self.enc = torch.empty(8 * cap * 4, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         self.denc = torch.empty(cap, 32, **f)
         self.out_rgb, self.out_op = torch.empty(R, 3, **f), torch.empty(R, **f)
         self.out_depth, self.out_loss = torch.empty(R, **f), torch.empty(R, **f)
-        self.vr_samples = torch.zeros(1, dtype=torch.int64, device=dev)
+        # running totals: [0] marched, [1] composited (vr_samples), [2] gradient-carrying,
+        # [3] field-evaluated samples
+        self.stats = torch.zeros(4, dtype=torch.int64, device=dev)
+        # chunked field evaluation (ngp_chunk_counts): first `chunk_first` samples of
+        # every row, then the rest of the rows not yet terminated (0 = every sample)
+        self.chunk_first = int(os.environ.get("NGP_CHUNK_FIRST", chunk_first))
+        self.eval_counts = torch.empty(R, dtype=torch.int32, device=dev)
+        self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
+        self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
         # gradient-carrying samples (up to each ray's termination): index map
         self.n_active = torch.empty(R, dtype=torch.int32, device=dev)
-        self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
         self.n_active_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.sample_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         # binned hash backward: workspace for bin_samples_per_ray gradient-
@@ -121,10 +138,16 @@ class NGPTrainer:
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(1000 + seed + self.rank)
         self.sample_seed = (1000003 * (seed + 1) + 7919 * self.rank) & 0xFFFFFFFFFFFFFFFF  # ngp_sample_batch key
-        self.sample_counter = 0
+        # device step counters: [0] Adam steps taken, [1] batches drawn (RNG counter)
+        self.dctr = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.lr_dev = torch.full((1,), float(lr), device=dev)
+        self._lr_set = float(lr)
+        # HIP graphs of the steady-state step, one per buffer set (see train_step)
+        self.use_graphs = os.environ.get("NGP_GRAPHS", "1") == "1"
+        self._graphs = {}
         self.L = vren.lib()
         HG._lib()
-        # {"field_fwd"|"mlp_bwd"|"hash_bwd": (start, end) torch.cuda.Event} around those launches (bench)
+        # {"field_fwd"|"mlp_bwd"|"hash_bwd"|stage: (start, end) torch.cuda.Event} (bench)
         self.kernel_events = None
 
     @staticmethod
@@ -219,9 +242,10 @@ class NGPTrainer:
     def _march(self, k, src, directions, poses, stream):
         """Ray generation + AABB + single-pass march of one batch into buffer
         set k.  src = ("idx", img_idxs, pix_idxs, noise | None): rays of the
-        given pixels (noise drawn from self.gen when None); or ("sample",
-        counter, gt_u8): the whole batch drawn on device (ngp_sample_batch:
-        pixels, ground truth, noise from Philox keyed by (seed, counter))."""
+        given pixels (noise drawn from self.gen when None); or ("sample", add,
+        gt_u8): the whole batch drawn on device (ngp_sample_batch_dev: pixels,
+        ground truth, noise from Philox keyed by (seed, batch counter + add),
+        the counter in device memory so a replayed graph draws fresh batches)."""
         m = self.msets[k]
         L, R = self.L, self.batch_size
         evs = self.kernel_events.get("march_side") if self.kernel_events is not None else None
@@ -231,12 +255,13 @@ class NGPTrainer:
                 evs[0].record(stream)
             s = HG.c_void_p(stream.cuda_stream)
             if src[0] == "sample":
-                _, counter, gt = src
+                _, add, gt = src
                 n_img, hw = gt.shape[0], gt.shape[1]
-                vren._ok(L.ngp_sample_batch(self.sample_seed, counter, _p(gt), n_img, hw, _p(directions), _p(poses), R,
-                                            _p(self.center), _p(self.half_size), ctypes_float(NEAR_DISTANCE),
-                                            _p(m["img_idxs"]), _p(m["pix_idxs"]), _p(m["rgb_gt"]), _p(m["noise"]),
-                                            _p(m["rays_o"]), _p(m["rays_d"]), _p(m["hits_t"]), s), "sample_batch")
+                vren._ok(L.ngp_sample_batch_dev(self.sample_seed, _p(self.dctr[1:]), add, _p(gt), n_img, hw,
+                                                _p(directions), _p(poses), R, _p(self.center), _p(self.half_size),
+                                                ctypes_float(NEAR_DISTANCE), _p(m["img_idxs"]), _p(m["pix_idxs"]),
+                                                _p(m["rgb_gt"]), _p(m["noise"]), _p(m["rays_o"]), _p(m["rays_d"]),
+                                                _p(m["hits_t"]), s), "sample_batch")
             else:
                 _, img_idxs, pix_idxs, noise = src
                 assert img_idxs.shape[0] == R
@@ -262,17 +287,21 @@ class NGPTrainer:
             if evs is not None and side:
                 evs[1].record(stream)
 
+    def _can_prefetch(self):
+        """The next batch may be marched ahead unless the next step begins with
+        an occupancy update (that batch must see the new bitfield)."""
+        return (self._pending is None and (self.global_step + 1) % self.update_interval != 0
+                and not self.no_prefetch)
+
     def prefetch(self, src, directions, poses):
         """March the NEXT batch into the idle buffer set on the side stream so
         it overlaps the current step's field / loss / backward / Adam.  Called
         by step() once the current set is bound: everything the side stream
         needs (the next batch's indices, the bitfield, the idle set's last
         readers = the previous step's backward) is already enqueued on the
-        main stream, which one event captures.  Skipped when the next step
-        begins with an occupancy update: that batch must see the new bitfield.
-        (Callers that edit density_bitfield between steps must not pass
-        next_batch.)"""
-        if self._pending is not None or (self.global_step + 1) % self.update_interval == 0:
+        main stream, which one event captures.  (Callers that edit
+        density_bitfield between steps must not pass next_batch.)"""
+        if not self._can_prefetch():
             return False
         k = 1 - self.cur
         ready = torch.cuda.Event()
@@ -288,7 +317,7 @@ class NGPTrainer:
     def drain(self):
         """Order the current stream after a batch marched ahead on the side
         stream (the batch stays pending for the next train_step)."""
-        if self._pending is not None:
+        if self._pending is not None and self._pending[1] is not None:
             torch.cuda.current_stream().wait_event(self._pending[1])
 
     def _ev(self, name, i):
@@ -297,75 +326,178 @@ class NGPTrainer:
             ev[name][i].record()
 
     # ---------------------------------------------------------------- step
+    def _on_exec_stream(self, fn, *args):
+        """Run one step on the trainer's high-priority stream (ordered after
+        and before the caller's current stream): the batch marched ahead on
+        the normal-priority side stream then only takes CU slots the step's
+        kernels leave free."""
+        if self.exec_stream is None:
+            return fn(*args)
+        caller = torch.cuda.current_stream()
+        self.exec_stream.wait_stream(caller)
+        with torch.cuda.stream(self.exec_stream):
+            out = fn(*args)
+        caller.wait_stream(self.exec_stream)
+        return out
+
     def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True, next_batch=None):
         """One training step on a batch (train.py:174-200).  img/pix (R) i64,
         rgb_gt (R,3) f32, directions (HW,3), poses (n_img,3,4), all on device.
         next_batch = (img, pix) of the following step: marched ahead on the
         side stream."""
         nxt = None if next_batch is None else ("idx", next_batch[0], next_batch[1], None)
-        return self._step(("idx", img_idxs, pix_idxs, noise), rgb_gt, directions, poses, apply_adam, nxt)
+        return self._on_exec_stream(self._step, ("idx", img_idxs, pix_idxs, noise), rgb_gt, directions, poses,
+                                    apply_adam, nxt)
 
     def train_step(self, gt_u8, directions, poses):
         """One training step on a batch drawn on device from the training set
         (gt_u8 (n_img, HW, 3) u8 images, directions (HW,3), poses (n_img,3,4)):
         the reference's DataLoader + training_step with nothing on the host.
-        The next step's batch is drawn and marched ahead on the side stream."""
-        src = ("sample", self.sample_counter, gt_u8)
-        self.sample_counter += 1
-        return self._step(src, None, directions, poses, True, ("sample", self.sample_counter, gt_u8))
+        The next step's batch is drawn and marched ahead on the side stream.
+        Steady-state steps (batch already marched ahead, no occupancy update
+        now or next step) replay a captured HIP graph of the whole step
+        (NGP_GRAPHS=0: always eager)."""
+        gs, ui = self.global_step, self.update_interval
+        if (self.use_graphs and self._pending is not None and gs % ui != 0 and (gs + 1) % ui != 0
+                and self.kernel_events is None and not self.random_bg and not self.no_prefetch):
+            return self._replay(gt_u8, directions, poses)
+        return self._on_exec_stream(self._step, ("sample", 0, gt_u8), None, directions, poses, True,
+                                    ("sample", 1, gt_u8))
+
+    def _set_lr(self):
+        lr = self.lr()
+        if lr != self._lr_set:
+            self.lr_dev.fill_(lr)
+            self._lr_set = lr
+
+    def _replay(self, gt_u8, directions, poses):
+        """Graph-replayed steady-state step for the batch pending in set k: the
+        step's kernels on the capture stream, the next batch's march forked
+        onto the side stream and joined before the end, the device counters
+        advanced last."""
+        k, ev = self._pending
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+        self._set_lr()
+        key = (k, gt_u8.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt_u8.shape)
+        g = self._graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            # capture on a side stream, ordered after everything enqueued so far
+            torch.cuda.current_stream().synchronize()
+            with torch.cuda.graph(g):
+                self._graph_body(k, gt_u8, directions, poses)
+            self._graphs[key] = g
+        g.replay()
+        self.cur = k
+        self._bind(self.msets[k])
+        self._pending = (1 - k, None)  # marched and joined inside the graph
+        self.n_prefetched += 1
+        self.global_step += 1
+        return self.out_loss
+
+    def _graph_body(self, k, gt_u8, directions, poses):
+        self.cur = k
+        self._bind(self.msets[k])
+        cs = torch.cuda.current_stream()
+
+        def fork():
+            self.march_stream.wait_stream(cs)
+            self._march(1 - k, ("sample", 1, gt_u8), directions, poses, self.march_stream)
+
+        self._compute(self.rgb_gt, True, fork)
+        cs.wait_stream(self.march_stream)
+        vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
 
     def _step(self, src, rgb_gt, directions, poses, apply_adam, next_src):
-        L, s = self.L, vren._stream()
         self._ev("occupancy_update", 0)
         if self.global_step % self.update_interval == 0:
             self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=self.global_step < self.warmup_steps)
         self._ev("occupancy_update", 1)
         self._ev("raygen_march", 0)
-        R = self.batch_size
         if self._pending is not None:  # this batch was marched ahead on the side stream
             k, ev = self._pending
             self._pending = None
             self.cur = k
-            torch.cuda.current_stream().wait_event(ev)
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
         else:
             self._march(self.cur, src, directions, poses, torch.cuda.current_stream())
         self._bind(self.msets[self.cur])
         if rgb_gt is None:
             rgb_gt = self.rgb_gt
         self._ev("raygen_march", 1)
+        fork = None
         if next_src is not None and apply_adam:
-            self.prefetch(next_src, directions, poses)
-        s = vren._stream()
-        HGL = HG._lib()
-        if self.kernel_events is not None:
-            self.kernel_events["field_fwd"][0].record()
-        vren._ok(HGL.ngp_field_forward(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples),
-                                       HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
-                                       _p(self.params16), _p(self.sigmas), _p(self.rgbs), _p(self.enc), None, s),
-                 "field_forward")
-        if self.kernel_events is not None:
-            self.kernel_events["field_fwd"][1].record()
+            fork = lambda: self.prefetch(next_src, directions, poses)  # noqa: E731
+        if apply_adam:
+            self._set_lr()
+        out = self._compute(rgb_gt, apply_adam, fork)
+        if apply_adam:
+            vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
+            self.global_step += 1
+        return out
+
+    def _compute(self, rgb_gt, apply_adam, fork):
+        """Field forward (chunked), compositing + loss + its backward, field
+        backward, [all-reduce], Adam -- on the current stream, no host sync.
+        fork() (nullable) launches the next batch's march on the side stream at
+        the step point self.prefetch_at."""
+        L, s, HGL, R = self.L, vren._stream(), HG._lib(), self.batch_size
+
+        def at(point):
+            if fork is not None and self.prefetch_at == point:
+                fork()
+
+        at("start")
+        self._ev("field_fwd", 0)
+        if self.split_forward:  # level pair per XCD encode (pair-major self.enc), then the MLPs
+            vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.n_samples), HG.ctypes.byref(self.grid.desc),
+                                         _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc), s), "hash_encode")
+            vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), _p(self.dirs), self.cap, _p(self.n_samples),
+                                               _p(self.params16), _p(self.sigmas), _p(self.rgbs), None, s),
+                     "field_mlp_forward")
+        elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
+            K = self.chunk_first
+            vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, None, None, ctypes_float(1e-4), _p(self.eval_counts),
+                                        s), "chunk_counts")
+            vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, 0, _p(self.act_start),
+                                        _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
+            self._field_indexed(s)
+            vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, _p(self.sigmas), _p(self.deltas), ctypes_float(1e-4),
+                                        _p(self.eval_counts), s), "chunk_counts")
+            vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, K, _p(self.act_start),
+                                        _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
+            self._field_indexed(s)
+        else:  # fused gathers + MLPs over every marched sample (row-major self.enc)
+            vren._ok(HGL.ngp_field_forward(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples),
+                                           HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
+                                           _p(self.params16), _p(self.sigmas), _p(self.rgbs), _p(self.enc), None, s),
+                     "field_forward")
+        self._ev("field_fwd", 1)
+        at("after_fwd")
         bg = torch.rand(3, device=self.dev, generator=self.gen) if self.random_bg else self.bg
         self._ev("composite_loss", 0)
         vren._ok(L.ngp_composite_loss(_p(self.sigmas), _p(self.rgbs), _p(self.deltas), _p(self.ts), _p(self.rays_a), R,
                                       _p(rgb_gt), _p(bg), self.loss_type, ctypes_float(self.lambda_opacity),
                                       ctypes_float(self.lambda_depth), ctypes_float(self.scale), ctypes_float(1e-4),
                                       _p(self.dsig), _p(self.drgb), _p(self.out_rgb), _p(self.out_op),
-                                      _p(self.out_depth), _p(self.out_loss), _p(self.vr_samples), _p(self.n_active),
-                                      s), "composite_loss")
+                                      _p(self.out_depth), _p(self.out_loss), _p(self.n_active), None, None, None,
+                                      _p(self.stats), s), "composite_loss")
+        # compacted gradient-carrying samples: scan + map (a per-block atomic
+        # reservation inside composite_loss serialises on one address and was slower)
         vren._ok(L.ngp_active_samples(_p(self.n_active), _p(self.rays_a), R, _p(self.act_start),
                                       _p(self.n_active_total), _p(self.sample_idx), s), "active_samples")
         self._ev("composite_loss", 1)
-        ev = self.kernel_events
-        if ev is not None:
-            ev["mlp_bwd"][0].record()
+        at("after_composite")
+        self._ev("mlp_bwd", 0)
         vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                                            _p(self.enc),
+                                            _p(self.enc), self.cap if self.split_forward else 0,
                                             _p(self.params16), _p(self.dsig), _p(self.drgb), _p(self.denc),
                                             _p(self.grad), s), "field_backward_mlp")
-        if ev is not None:
-            ev["mlp_bwd"][1].record()
-            ev["hash_bwd"][0].record()
+        self._ev("mlp_bwd", 1)
+        at("after_mlp_bwd")
+        self._ev("hash_bwd", 0)
         if self.hash_backward != "atomic":
             vren._ok(HGL.ngp_hash_backward_binned(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
@@ -379,21 +511,28 @@ class NGPTrainer:
             vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
                                            HG.ctypes.byref(self.grid.desc),
                                            _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
-        if ev is not None:
-            ev["hash_bwd"][1].record()
+        self._ev("hash_bwd", 1)
         self._ev("allreduce", 0)
         ddp.allreduce_grad_(self.grad, self.pg)  # DDP gradient all-reduce (RCCL over xGMI)
         self._ev("allreduce", 1)
         if not apply_adam:  # (tests) leave the summed gradient in self.grad
             return self.out_loss
-        self.global_step += 1
         self._ev("adam", 0)
-        vren._ok(L.ngp_adam_step(_p(self.params), _p(self.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
-                                 _p(self.params16), self.params.numel(), ctypes_float(self.lr()), ctypes_float(0.9),
-                                 ctypes_float(0.999), ctypes_float(1e-15), self.global_step,
-                                 ctypes_float(1.0 / self.world), 1, s), "adam")
+        # lr and the step count from device memory (graph replays); dctr[0] =
+        # steps taken so far, advanced after the step by ngp_counters_inc
+        vren._ok(L.ngp_adam_step_dev(_p(self.params), _p(self.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
+                                     _p(self.params16), self.params.numel(), _p(self.lr_dev), ctypes_float(0.9),
+                                     ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                                     ctypes_float(1.0 / self.world), 1, s), "adam")
         self._ev("adam", 1)
         return self.out_loss
+
+    def _field_indexed(self, s):
+        HGL = HG._lib()
+        vren._ok(HGL.ngp_field_forward_indexed(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.eval_total),
+                                               _p(self.eval_idx), HG.ctypes.byref(self.grid.desc),
+                                               _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.sigmas),
+                                               _p(self.rgbs), _p(self.enc), s), "field_forward_indexed")
 
     # ---------------------------------------------------- test-time render
     @torch.no_grad()

@@ -41,6 +41,10 @@ def _declare(L):
         "ngp_raygen_aabb": [vp, vp, vp, vp, c_int64, vp, vp, c_float, vp, vp, vp, vp],
         "ngp_sample_batch": [ctypes.c_uint64, ctypes.c_uint64, vp, c_int64, c_int64, vp, vp, c_int64, vp, vp,
                              c_float, vp, vp, vp, vp, vp, vp, vp, vp],
+        "ngp_sample_batch_dev": [ctypes.c_uint64, vp, c_int64, vp, c_int64, c_int64, vp, vp, c_int64, vp, vp,
+                                 c_float, vp, vp, vp, vp, vp, vp, vp, vp],
+        "ngp_adam_step_dev": [vp, vp, vp, vp, vp, c_int64, vp, c_float, c_float, c_float, vp, c_float, c_int, vp],
+        "ngp_counters_inc": [vp, c_int, vp],
         "ngp_morton3d": [vp, c_int64, vp, vp],
         "ngp_morton3d_invert": [vp, c_int64, vp, vp],
         "ngp_packbits": [vp, c_int64, c_float, vp, vp, vp],
@@ -57,8 +61,10 @@ def _declare(L):
         "ngp_composite_train_bw": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, c_int64, vp, vp, vp, c_float, vp, vp, vp],
         "ngp_composite_test_fw": [vp, vp, vp, vp, c_int64, c_int, vp, c_float, vp, vp, vp, vp, vp],
         "ngp_composite_loss": [vp, vp, vp, vp, vp, c_int64, vp, vp, c_int, c_float, c_float, c_float, c_float, vp,
-                               vp, vp, vp, vp, vp, vp, vp, vp],
+                               vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_active_samples": [vp, vp, c_int64, vp, vp, vp, vp],
+        "ngp_chunk_counts": [vp, c_int64, c_int, vp, vp, c_float, vp, vp],
+        "ngp_ray_segments": [vp, vp, c_int64, c_int, vp, vp, vp, vp, vp],
         "ngp_adam_step": [vp, vp, vp, vp, vp, c_int64, c_float, c_float, c_float, c_float, c_int64, c_float, c_int,
                           vp],
         "ngp_density_scatter_max": [vp, vp, c_int64, vp, vp],

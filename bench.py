@@ -40,14 +40,14 @@ from trainer import NGPTrainer  # noqa: E402
 with open(os.path.join(ROOT, "BASELINE.json")) as f:
     BASELINE = json.load(f)
 
-# Algorithmic work per marched sample of the three per-sample kernels
-# (DESIGN.md "Measurement"):
-#  field_fwd: 16 levels x 8 corners x fp16x2 gathered + xyz + dir read,
-#             fp16 encoding (64 B), sigma + rgb (16 B) written      -> bytes
+# Algorithmic work per marched (field_fwd) or gradient-carrying (mlp_bwd,
+# hash_bwd) sample of the per-sample kernels (DESIGN.md "Measurement"):
+#  field_fwd: 16 levels x 8 corners x fp16x2 gathered (512 B) + xyz, dir read
+#             (24 B), fp16 encoding (64 B) + sigma, rgb (16 B) written -> bytes
 #  hash_bwd : xyz (12 B) + dL/denc fp32 (128 B) read + read-modify-write of
-#             16 x 8 x 2 fp32 table gradients (2 x 1024 B)           -> bytes
-#  mlp_bwd  : forward recompute + dX + dW of the 32-64-16 / 32-64-64-16 MLPs
-#             (16-row output layer as computed)                      -> FLOPs
+#             16 x 8 x 2 fp32 table gradients (2 x 1024 B)         -> bytes
+#  mlp_bwd  : forward recompute + dX + dW of the two MLPs (16-row output
+#             layers as computed)                                 -> FLOPs
 KERNEL_WORK = {
     "field_fwd": ("hbm", 16 * 8 * 4 + 12 + 12 + 64 + 4 + 12, "GB/s"),
     "hash_bwd": ("hbm", 12 + 128 + 2 * 16 * 8 * 2 * 4, "GB/s"),
@@ -55,6 +55,7 @@ KERNEL_WORK = {
                 + 2 * (16 * 64 + 64 * 64 + 64 * 16 + 16 * 64 + 64 * 32)
                 + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32), "TFLOP/s"),
 }
+FWD_KERNELS = ("field_fwd",)  # run over every marched sample
 PEAK = {"hbm": 8000.0, "mfma": 2500.0}  # MI355X: HBM3E GB/s; dense fp16 MFMA TFLOP/s
 
 
@@ -73,6 +74,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--breakdown-steps", type=int, default=50, help="eager steps with per-kernel HIP events")
     ap.add_argument("--hash-backward", default="hybrid", choices=["hybrid", "binned", "atomic"])
     return ap.parse_args()
 
@@ -172,64 +174,77 @@ def main():
             if events is not None:
                 trainer.kernel_events = events[i]
             trainer.train_step(gt_images, directions, poses)
-            if events is not None:
-                n_samples_acc.add_(trainer.n_samples)
-                n_active_acc.add_(trainer.n_active_total)
         trainer.drain()
 
-    n_samples_acc = torch.zeros(1, dtype=torch.int64, device=dev)
-    n_active_acc = torch.zeros(1, dtype=torch.int64, device=dev)
     t0 = time.time()
     run(args.pretrain)
     torch.cuda.synchronize()
     log(rank, f"[bench] pretrain {args.pretrain} steps in {time.time() - t0:.1f}s, "
               f"samples last batch {int(trainer.n_samples.item())}")
     run(args.warmup)
-    # ---- timed region
-    trainer.vr_samples.zero_()
-    names = list(KERNEL_WORK)
-    # raygen_march = inline march on the main stream (steps after an occupancy
-    # update); march_side = the next batch's march on the side stream, which
-    # overlaps the step's compute (averaged over the steps that launched one)
-    stages = ["occupancy_update", "raygen_march", "march_side", "composite_loss", "allreduce", "adam"]
-    ev = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in names + stages}
-          for _ in range(args.steps)]
+    # ---- timed region: steady-state steps replay captured HIP graphs
+    # (trainer.train_step); no per-kernel instrumentation inside
+    trainer.stats.zero_()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    run(args.steps, ev)
+    run(args.steps)
+    t_enq = time.perf_counter() - t_start  # host time to enqueue the steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t_el = time.perf_counter() - t_start
-    trainer.kernel_events = None
     t_max = torch.tensor([t_el], device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     t_el = float(t_max.item())
     total_rays = R * args.steps * world
     value = total_rays / t_el
-    samples = int(n_samples_acc.item())
-    samples_per_step = samples / args.steps
-    active_per_step = int(n_active_acc.item()) / args.steps
+    marched, composited, active, evaluated = (int(v) for v in trainer.stats.tolist())
+    if trainer.chunk_first <= 0:
+        evaluated = marched
+    rm_s = marched / (R * args.steps)
+    vr_s = composited / (R * args.steps)
+    ev_s = evaluated / (R * args.steps)
+    # ---- breakdown region: the same steps run eagerly with HIP events around
+    # each kernel / stage (events cannot sit between the nodes of a replayed
+    # graph); per-kernel durations and the roofline come from here
+    n_bd = max(1, min(args.steps, args.breakdown_steps))
+    names = list(KERNEL_WORK)
+    # raygen_march = inline march on the main stream (steps after an occupancy
+    # update); march_side = the next batch's march on the side stream, which
+    # overlaps the step's compute (averaged over the steps that launched one)
+    stages = ["occupancy_update", "raygen_march", "march_side", "composite_loss", "allreduce", "adam"]
+    ev = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in names + stages}
+          for _ in range(n_bd)]
+    trainer.stats.zero_()
+    torch.cuda.synchronize()
+    t_bd = time.perf_counter()
+    run(n_bd, ev)
+    torch.cuda.synchronize()
+    t_bd = time.perf_counter() - t_bd
+    trainer.kernel_events = None
+    marched_bd, _, active_bd, evaluated_bd = (int(v) for v in trainer.stats.tolist())
+    if trainer.chunk_first <= 0:
+        evaluated_bd = marched_bd
+    samples_per_step = evaluated_bd / n_bd  # field_fwd runs over the evaluated samples
+    active_per_step = active_bd / n_bd
     kernels = {}
     for k in names:
-        ms = sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / args.steps
+        ms = sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / n_bd
         bound, per_sample, unit = KERNEL_WORK[k]
         # the backward kernels run over the gradient-carrying samples only
-        units = samples_per_step if k == "field_fwd" else active_per_step
+        units = samples_per_step if k in FWD_KERNELS else active_per_step
         achieved = units * per_sample / (ms * 1e-3) / (1e9 if bound == "hbm" else 1e12)
         kernels[k] = {"bound": bound, "achieved": round(achieved, 2), "peak": PEAK[bound], "unit": unit,
                       "frac": round(achieved / PEAK[bound], 4), "avg_launch_ms": round(ms, 4),
                       "work_per_sample": per_sample, "samples_per_launch": round(units, 1)}
     dominant = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
-    stage_ms = {k: round(sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / args.steps, 4)
+    stage_ms = {k: round(sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / n_bd, 4)
                 for k in stages if k != "march_side"}
     side = [e["march_side"][0].elapsed_time(e["march_side"][1]) for e in ev if _recorded(e["march_side"][1])]
     stage_ms["march_side"] = round(sum(side) / max(len(side), 1), 4)
-    rm_s = samples / (R * args.steps)
-    vr_s = int(trainer.vr_samples.item()) / (R * args.steps)
     loss = float(trainer.out_loss.sum().item())
     psnr = psnr_eval(trainer, scene, args.psnr_views, args.psnr_res) if (rank == 0 and args.psnr_views > 0) else None
     cpu = None
@@ -246,13 +261,19 @@ def main():
                                    "T=2^19 hash, 64-wide MLPs, raw loss, Adam lr 1e-2",
                        "batch_rays_per_gpu": R, "global_batch_rays": R * world, "pretrain_steps": args.pretrain,
                        "rm_samples_per_ray": round(rm_s, 2), "vr_samples_per_ray": round(vr_s, 2),
+                       "field_evaluated_per_ray": round(ev_s, 2),
+                       "graphs": trainer.use_graphs,
+                       "chunk_first": trainer.chunk_first,
                        "parallelism": f"dp{world}", "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
             "roofline": dict(kernel=dominant, traffic=None, **kernels[dominant]),
             "kernels": kernels,
             "stage_ms": stage_ms,
-            "ms_per_step_breakdown_note": "kernels = HIP-event averages over the timed steps",
+            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
+            "breakdown_note": (f"kernels / stage_ms / roofline: HIP-event averages over {n_bd} eagerly run steps after "
+                               f"the timed region ({t_bd / n_bd * 1e3:.3f} ms/step eager); the timed steps replay "
+                               "captured HIP graphs"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

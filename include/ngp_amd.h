@@ -66,6 +66,14 @@ int ngp_sample_batch(uint64_t seed, uint64_t step, const uint8_t* gt_u8, int64_t
                      const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
                      float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream);
 
+/* ngp_sample_batch with the RNG counter in device memory: step = *step_dev +
+ * step_add (a captured graph replays with the counter advanced on device). */
+int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_add, const uint8_t* gt_u8,
+                         int64_t n_img, int64_t hw, const float* directions, const float* poses,
+                         int64_t n_rays, const float* center, const float* half_size,
+                         float near_distance, int64_t* img_idx, int64_t* pix_idx, float* rgb_gt,
+                         float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream);
+
 /* ------------------------------------------------- occupancy grid utils */
 /* Replaces vren.morton3D (binding.cpp:36-40 -> raymarching.cu:62-88). */
 int ngp_morton3d(const int32_t* coords, int64_t n, int32_t* indices, void* stream);
@@ -209,14 +217,36 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
                        const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
                        float* grad_table, void* stream);
 
+/* ngp_field_forward split in two launches (the training path):
+ * ngp_hash_encode writes the encoding PAIR-MAJOR, enc_pm (8, n, 4) fp16 with
+ * enc_pm[p][i][k] = enc[i][4p + k] (levels 2p, 2p+1 of sample i; the row
+ * stride of the pair planes is n, the capacity, also with n_dev); its
+ * workgroups take one level pair each so every XCD's L2 holds one pair's
+ * table slice.  ngp_field_mlp_forward runs the density net, SH4 and colour
+ * net on it.  Same values as ngp_field_forward, bit for bit. */
+int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
+                    const void* table_f16, void* enc_pm, void* stream);
+int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev,
+                          const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16, void* stream);
+
+/* ngp_field_forward over the listed samples only: rows j < n (or *n_dev) of
+ * sample_idx; sample i = sample_idx[j] reads xyzs/dirs row i and writes
+ * sigmas/rgbs/enc_f16 row i (other rows untouched). */
+int ngp_field_forward_indexed(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
+                              const int32_t* sample_idx, const ngp_hashgrid_t* grid, const void* table_f16,
+                              const void* mlp_f16, float* sigmas, float* rgbs, void* enc_f16, void* stream);
+
 /* The two halves of ngp_field_backward as separate launches (so each can be
  * timed / overlapped): the MLP backward (writes dL/denc to denc_ws, += grad_mlp)
  * and the hash-table scatter (+= grad_table from denc).  sample_idx (nullable):
  * process only the samples sample_idx[0..n) (compact row j of denc_ws <->
- * sample sample_idx[j]); see ngp_active_samples. */
+ * sample sample_idx[j]); see ngp_active_samples.  enc_pm_stride: 0 = enc_f16
+ * is row-major (n,32) (ngp_field_forward), > 0 = pair-major (ngp_hash_encode)
+ * with that plane stride. */
 int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
-                           const void* enc_f16, const void* mlp_f16, const float* dL_dsigmas,
-                           const float* dL_drgbs, float* denc_ws, float* grad_mlp, void* stream);
+                           const void* enc_f16, int64_t enc_pm_stride, const void* mlp_f16,
+                           const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
+                           void* stream);
 int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                       const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* stream);
 
@@ -247,17 +277,23 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
  * and composite_train_bw with dL/dws = 0.  rgb_gt (n_rays,3).
  * Out: dL_dsigmas (N), dL_drgbs (N,3) for each row's first n_active samples
  * (later entries are left unwritten: their gradient is exactly zero); per
- * ray out_rgb (n_rays,3) (after bg),
- * out_opacity, out_depth, out_loss (n_rays; sum = the batch loss);
- * vr_samples (1) i64 += composited samples (nullable); n_active (n_rays) i32
- * (nullable) = samples of each row that can carry gradient (up to and
- * including the terminating one; all later ones get exactly 0). */
+ * ray out_rgb (n_rays,3) (after bg), out_opacity, out_depth, out_loss
+ * (n_rays; sum = the batch loss); n_active (n_rays) i32 (nullable) = samples
+ * of each row that can carry gradient (up to and including the terminating
+ * one; all later ones get exactly 0).
+ * sample_idx (nullable; capacity >= total samples) receives the compacted
+ * list of those samples, each row's entries contiguous (row order not
+ * fixed), and *n_active_total its length; alloc_ws = 16 bytes of zeroed,
+ * 8-byte aligned scratch that the kernel leaves zeroed again.  stats
+ * (nullable, 3 x i64) accumulates [0] marched, [1] composited (vr_samples),
+ * [2] gradient-carrying samples. */
 int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
                        const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg,
                        int loss_type, float lambda_opacity, float lambda_depth, float depth_scale,
                        float T_threshold, float* dL_dsigmas, float* dL_drgbs, float* out_rgb,
-                       float* out_opacity, float* out_depth, float* out_loss, int64_t* vr_samples,
-                       int32_t* n_active, void* stream);
+                       float* out_opacity, float* out_depth, float* out_loss, int32_t* n_active,
+                       int32_t* sample_idx, void* alloc_ws, int64_t* n_active_total, int64_t* stats,
+                       void* stream);
 
 /* Compacted list of the gradient-carrying samples: act_start_ws (n_rows) i64
  * scratch, n_active_total (1) i64, sample_idx (>= total) i32 with
@@ -266,12 +302,37 @@ int ngp_active_samples(const int32_t* n_active, const int64_t* rays_a, int64_t n
                        int64_t* act_start_ws, int64_t* n_active_total, int32_t* sample_idx,
                        void* stream);
 
+/* Chunked field evaluation of a training batch (exact: the step reads a row's
+ * samples only up to its termination).  sigmas == NULL: counts[r] =
+ * min(N_r, first) (round 1).  Else (after round 1 evaluated them): counts[r] =
+ * N_r - first if row r's transmittance over its first min(N_r, first) samples
+ * (composite_train_fw's serial product, volumerendering.cu:27-41) stays above
+ * T_threshold and N_r > first, else 0 (round 2). */
+int ngp_chunk_counts(const int64_t* rays_a, int64_t n_rows, int first, const float* sigmas,
+                     const float* deltas, float T_threshold, int32_t* counts, void* stream);
+/* Sample list of per-row segments: sample_idx[start_r + k] = rays_a[r].start +
+ * first + k for k < counts[r] (start = exclusive prefix of counts, in
+ * start_ws (n_rows) i64); *total = the list length, *total_acc += it
+ * (nullable). */
+int ngp_ray_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_rows, int first,
+                     int64_t* start_ws, int64_t* total, int64_t* total_acc, int32_t* sample_idx,
+                     void* stream);
+
 /* apex FusedAdam step (train.py:146; weight decay 0) over n (multiple of 4)
  * fp32 params with grad *= grad_scale, bias corrections for `step` (1-based);
  * writes the fp16 shadow params_f16 and, if zero_grad, zeroes grads. */
 int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16,
                   int64_t n, float lr, float beta1, float beta2, float eps, int64_t step,
                   float grad_scale, int zero_grad, void* stream);
+
+/* ngp_adam_step with the learning rate and the step count in device memory
+ * (lr_dev f32; step_dev = steps already taken, this is step *step_dev + 1;
+ * not advanced here -- see ngp_counters_inc). */
+int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16,
+                      int64_t n, const float* lr_dev, float beta1, float beta2, float eps,
+                      const int64_t* step_dev, float grad_scale, int zero_grad, void* stream);
+/* counters[i] += 1, i < n (n <= 64): advances the device step counters. */
+int ngp_counters_inc(int64_t* counters, int n, void* stream);
 
 /* Occupancy update (models/networks.py:252-281).  scatter_max: grid_tmp[idx[i]]
  * = max(grid_tmp[idx[i]], sigmas[i]) (flat cascade*G^3 indices, sigmas >= 0).

@@ -50,7 +50,7 @@ def main():
     for n in (4096, 16384, 65536, 131072, 262144, 524288):
         fwd = lambda: L.ngp_field_forward(p(xyz), p(d), n, None, ctypes.byref(grid.desc), p(p16[HG.MLP_PARAMS:]),  # noqa
                                           p(p16), p(sig), p(rgb), p(enc), None, s)
-        mlp = lambda: L.ngp_field_backward_mlp(p(d), n, None, None, p(enc), p(p16), p(dsig), p(drgb), p(denc),  # noqa
+        mlp = lambda: L.ngp_field_backward_mlp(p(d), n, None, None, p(enc), 0, p(p16), p(dsig), p(drgb), p(denc),  # noqa
                                                p(grad), s)
         hsh = lambda: L.ngp_hash_backward(p(xyz), n, None, None, ctypes.byref(grid.desc), p(denc),  # noqa
                                           p(grad[HG.MLP_PARAMS:]), s)

@@ -57,6 +57,32 @@ def test_hashgrid_levels_match_oracle(scale):
 
 
 @pytest.mark.parametrize("scale", [0.5, 16.0])
+def test_split_encode_mlp_equals_fused(scale):
+    """ngp_hash_encode (level pair per XCD, pair-major) + ngp_field_mlp_forward
+    (the training path) give the fused ngp_field_forward's encoding, sigma
+    and rgb bit for bit."""
+    import ctypes
+    _, flat = _oracle_and_params(scale=scale)
+    x, d = _points(20000, scale)
+    n = x.shape[0]
+    grid = HG.HashGrid(scale)
+    p16 = flat.to(DEV).half()
+    x, d = x.to(DEV), d.to(DEV)
+    sig, rgb, enc, _ = HG.field_forward(x, d, grid, p16)
+    enc_pm = torch.empty(8, n, 4, dtype=torch.float16, device=DEV)
+    sig2, rgb2 = torch.empty(n, device=DEV), torch.empty(n, 3, device=DEV)
+    L = HG._lib()
+    vp = ctypes.c_void_p
+    vren._ok(L.ngp_hash_encode(vp(x.data_ptr()), n, None, ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:].data_ptr()),
+                               vp(enc_pm.data_ptr()), vren._stream()), "hash_encode")
+    vren._ok(L.ngp_field_mlp_forward(vp(enc_pm.data_ptr()), vp(d.data_ptr()), n, None, vp(p16.data_ptr()),
+                                     vp(sig2.data_ptr()), vp(rgb2.data_ptr()), None, vren._stream()), "mlp_forward")
+    assert torch.equal(enc_pm.permute(1, 0, 2).reshape(n, 32).view(torch.int16), enc.view(torch.int16))
+    assert torch.equal(sig2, sig)
+    assert torch.equal(rgb2, rgb)
+
+
+@pytest.mark.parametrize("scale", [0.5, 16.0])
 def test_field_forward_parity(scale):
     f, flat = _oracle_and_params(scale)
     x, d = _points(20000, scale)
