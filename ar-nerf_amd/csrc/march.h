@@ -30,6 +30,7 @@ struct WordCache {
     uint32_t idx = 0xffffffffu;
     uint64_t word = 0;
     const uint32_t* sum = nullptr;  // LDS copy of the bitfield summary (nullable)
+    const uint32_t* dil = nullptr;  // its one-block dilation (nullable; mip-0 blocks of cascade 0)
 };
 
 // Copy the bitfield summary into LDS (whole workgroup; call before any
@@ -37,7 +38,7 @@ struct WordCache {
 // nullptr when the launch has no summary.
 __device__ __forceinline__ const uint32_t* load_summary(const MarchParams& p, uint32_t* lds) {
     if (!p.summary) return nullptr;
-    for (int i = threadIdx.x; i < p.n_sum32; i += blockDim.x) lds[i] = p.summary[i];
+    for (int i = threadIdx.x; i < 2 * p.n_sum32; i += blockDim.x) lds[i] = p.summary[i];
     return lds;
 }
 
@@ -147,7 +148,7 @@ static inline int march_params(const uint8_t* bf, int cascades, int grid_size, f
 
 // Attach a bitfield summary (ngp_bitfield_summary output for this bitfield).
 // Requires the LDS copy to fit the launch's dynamic LDS budget.
-constexpr int MAX_SUM32 = 16384;  // 64 KB of LDS: cascades * G^3 <= 2^25 cells
+constexpr int MAX_SUM32 = 8192;  // 2 x 32 KB of LDS: cascades * G^3 <= 2^24 cells
 static inline int march_attach_summary(MarchParams& p, const uint32_t* summary) {
     if (!summary) return NGP_OK;
     const int64_t cells = (int64_t)p.cascades * p.grid_size * p.grid_size * p.grid_size;
@@ -157,4 +158,5 @@ static inline int march_attach_summary(MarchParams& p, const uint32_t* summary) 
     p.n_sum32 = (int)(cells / 2048);
     return NGP_OK;
 }
-static inline size_t march_summary_lds(const MarchParams& p) { return (size_t)p.n_sum32 * sizeof(uint32_t); }
+// LDS for the summary and its dilation (both n_sum32 words)
+static inline size_t march_summary_lds(const MarchParams& p) { return (size_t)2 * p.n_sum32 * sizeof(uint32_t); }

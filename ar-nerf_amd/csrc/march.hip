@@ -162,16 +162,46 @@ __global__ void __launch_bounds__(256) sample_batch_kernel(
             hits_t + 2 * r);
 }
 
-// Bitfield summary: bit w of the output = (64-bit bitfield word w != 0),
-// i.e. whether the Morton-aligned 4x4x4 cell block w holds any occupied
-// cell.  One lane per 32 words (256 B).
+// Bitfield summary: bit w of summary = (64-bit bitfield word w != 0), i.e.
+// whether the Morton-aligned 4x4x4 cell block w holds any occupied cell;
+// bit w of dilated = OR of that over block w and its 26 neighbours (same
+// cascade).  One lane per block: the block index IS the cell Morton code
+// without its low 6 bits, so its (bx, by, bz) are compact3 of it.
 __global__ void __launch_bounds__(256) bitfield_summary_kernel(const uint64_t* __restrict__ words, int64_t n_words,
-                                                               uint32_t* __restrict__ summary) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i * 32 >= n_words) return;
-    uint32_t m = 0;
-    for (int k = 0; k < 32 && i * 32 + k < n_words; ++k) m |= (words[i * 32 + k] != 0ull ? 1u : 0u) << k;
-    summary[i] = m;
+                                                               int64_t blocks_per_cascade, int bside,
+                                                               uint32_t* __restrict__ summary,
+                                                               uint32_t* __restrict__ dilated) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = w < n_words;
+    bool s = false, dl = false;
+    if (in) {
+        s = words[w] != 0ull;
+        if (bside <= 0) {
+            dl = true;  // no block geometry: every block counts as near (disables the early out)
+        } else {
+            const int64_t c0 = (w / blocks_per_cascade) * blocks_per_cascade;
+            const uint32_t local = (uint32_t)(w - c0);
+            const int bx = (int)compact3(local), by = (int)compact3(local >> 1), bz = (int)compact3(local >> 2);
+            for (int dz = -1; dz <= 1 && !dl; ++dz)
+                for (int dy = -1; dy <= 1 && !dl; ++dy)
+                    for (int dx = -1; dx <= 1 && !dl; ++dx) {
+                        const int x = bx + dx, y = by + dy, z = bz + dz;
+                        if (x < 0 || y < 0 || z < 0 || x >= bside || y >= bside || z >= bside) continue;
+                        dl = words[c0 + morton3((uint32_t)x, (uint32_t)y, (uint32_t)z)] != 0ull;
+                    }
+        }
+    }
+    const uint64_t bs = __ballot(s), bd = __ballot(dl);
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = w - lane;  // 64 consecutive blocks per wave = two summary words
+    if (lane == 0 && w0 < n_words) {
+        summary[w0 >> 5] = (uint32_t)bs;
+        dilated[w0 >> 5] = (uint32_t)bd;
+    }
+    if (lane == 32 && w0 + 32 < n_words) {
+        summary[(w0 >> 5) + 1] = (uint32_t)(bs >> 32);
+        dilated[(w0 >> 5) + 1] = (uint32_t)(bd >> 32);
+    }
 }
 
 // --------------------------------------------------- morton / packbits
@@ -493,6 +523,7 @@ __device__ __forceinline__ int lat_jump(const LatSeg& sg, int nseg, int q, int k
     return k_end;
 }
 
+template <int DIAG = 0>  // DIAG != 0: timing-only variants for scripts/diag (1: no chase, 2: no jump targets)
 __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __restrict__ rays_o,
                                                                const float* __restrict__ rays_d,
                                                                const float* __restrict__ hits_t, int64_t n_rays,
@@ -504,6 +535,7 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
     __shared__ LatSeg segs[4];
     WordCache wc;
     wc.sum = load_summary(p, ssum);
+    wc.dil = wc.sum ? wc.sum + p.n_sum32 : nullptr;
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t r = (int64_t)blockIdx.x * 4 + w;
@@ -518,6 +550,37 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
     if (!(0 <= t0) || !(t0 < t2)) {
         if (lane == 0) counts[r] = 0;
         return;
+    }
+    // Conservative early out (exact): points every half 4^3-block along
+    // [t0, t2]; the walk's every probe lies within one block of one of them,
+    // so if no point's block has an occupied cell within one block
+    // (dilated summary), the walk emits nothing.  Most rays crossing the box
+    // miss the object and cost this instead of a full lattice walk.
+    if (wc.dil) {
+        const float mb = fminf(0.5f, p.scale);
+        const float dn = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+        const float step = 0.45f * (4.0f * 2.0f * mb / p.grid_size) / dn;
+        const int npts = (int)ceilf((t2 - t0) / step) + 1;
+        const float gm1 = p.grid_size - 1.0f, mbi = 1 / mb;
+        bool near = false;
+        for (int j0 = 0; j0 < npts && !near; j0 += 64) {
+            const int j = j0 + lane;
+            bool b = false;
+            if (j < npts) {
+                const float t = fminf(t0 + (float)j * step, t2);
+                const float x = o[0] + t * d[0], y = o[1] + t * d[1], z = o[2] + t * d[2];
+                const int nx = (int)clampf(0.5f * (x * mbi + 1) * p.grid_size, 0.0f, gm1);
+                const int ny = (int)clampf(0.5f * (y * mbi + 1) * p.grid_size, 0.0f, gm1);
+                const int nz = (int)clampf(0.5f * (z * mbi + 1) * p.grid_size, 0.0f, gm1);
+                const uint32_t wi = morton3((uint32_t)nx >> 2, (uint32_t)ny >> 2, (uint32_t)nz >> 2);
+                b = (wc.dil[wi >> 5] >> (wi & 31u)) & 1u;
+            }
+            near = __ballot(b) != 0ull;
+        }
+        if (!near) {
+            if (lane == 0) counts[r] = 0;
+            return;
+        }
     }
     LatSeg& sg = segs[w];
     int nseg = 0;
@@ -551,23 +614,52 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
         if (live) {
             float x, y, z, dts, T;
             occ = march_probe<true>(tk, o, d, dinv, p, x, y, z, dts, wc, T);
-            nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
+            if constexpr (DIAG == 2) nxt = k + 1 + (T > 1e30f);
+            else nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
         }
-        const uint64_t occm = __ballot(occ);
-        // follow the walk through the window (scalar)
-        uint64_t vis = 0;
-        int pnt = c, n = N;
-        while (pnt < c + 64 && pnt < k_end && n < p.max_samples) {
-            const int i = pnt - c;
-            if ((occm >> i) & 1ull) { vis |= 1ull << i; ++n; }
-            pnt = __builtin_amdgcn_readlane(nxt, i);
+        const uint64_t occm = __ballot(occ && live);
+        uint64_t vis;
+        int pnt;
+        if constexpr (DIAG == 1) {
+            pnt = c + 64 + (__builtin_amdgcn_readlane(nxt, 63) > 1 << 30);
+            vis = occm;
+        } else {
+            // The walk's chain through the window, in parallel: J_b(i) = the
+            // 2^b-th successor of window point i (64 = out of the window),
+            // built by pointer doubling; every lane then climbs from point 0
+            // with binary lifting to the last chain point <= itself -- it is
+            // on the chain iff that is itself.  (Successors only move forward.)
+            int J[6];
+            J[0] = live ? min(nxt - c, 64) : 64;
+#pragma unroll
+            for (int b = 1; b < 6; ++b) {
+                const int prev = J[b - 1];
+                const int v = __builtin_amdgcn_ds_bpermute(min(prev, 63) << 2, prev);
+                J[b] = prev >= 64 ? 64 : v;
+            }
+            int cur = 0;
+#pragma unroll
+            for (int b = 5; b >= 0; --b) {
+                const int v = __builtin_amdgcn_ds_bpermute(min(cur, 63) << 2, J[b]);
+                const int to = cur >= 64 ? 64 : v;
+                if (to <= lane) cur = to;
+            }
+            vis = __ballot(cur == lane);
+            const int last = 63 - __builtin_clzll(vis);  // the chain's last point in the window
+            pnt = __builtin_amdgcn_readlane(nxt, last);   // k_end if it ends the walk
+            vis &= occm;
         }
+        // emit the chain's occupied points, at most up to max_samples
+        const int room = p.max_samples - N;
+        const int nv = __builtin_popcountll(vis);
         if ((vis >> lane) & 1ull) {
-            const int rank = N + __builtin_popcountll(vis & ((1ull << lane) - 1ull));
-            st[rank] = tk;
-            sd[rank] = dt;
+            const int rank = __builtin_popcountll(vis & ((1ull << lane) - 1ull));
+            if (rank < room) {
+                st[N + rank] = tk;
+                sd[N + rank] = dt;
+            }
         }
-        N = n;
+        N += min(nv, room);
         c = pnt;
     }
     if (lane == 0) counts[r] = N;
@@ -706,13 +798,18 @@ int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_ad
     return ngp_launch_status();
 }
 
-int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, uint32_t* summary, void* stream) {
+int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, int grid_size, uint32_t* summary, void* stream) {
     NGP_CHECK_ARG(n_bytes >= 0);
     if (n_bytes == 0) return NGP_OK;
     NGP_CHECK_ARG(bitfield && summary && n_bytes % 8 == 0 && ((uintptr_t)bitfield & 7u) == 0);
     const int64_t n_words = n_bytes / 8;
-    bitfield_summary_kernel<<<nblk((n_words + 31) / 32, 256), 256, 0, as_stream(stream)>>>(
-        reinterpret_cast<const uint64_t*>(bitfield), n_words, summary);
+    // the dilated half needs whole cascades of a power-of-two grid (Morton blocks)
+    const int64_t bpc = (int64_t)grid_size * grid_size * grid_size / 64;
+    const bool dil = grid_size >= 4 && (grid_size & (grid_size - 1)) == 0 && bpc > 0 && n_words % bpc == 0 &&
+                     n_words % 64 == 0;
+    bitfield_summary_kernel<<<nblk(n_words, 256), 256, 0, as_stream(stream)>>>(
+        reinterpret_cast<const uint64_t*>(bitfield), n_words, dil ? bpc : 1, dil ? grid_size / 4 : 0, summary,
+        summary + (n_words + 31) / 32);
     return ngp_launch_status();
 }
 
@@ -805,8 +902,17 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
         const char* eser = getenv("NGP_MARCH_SERIAL");
         const bool serial = eser ? atoi(eser) != 0 : false;
         if (march_simple(p) && !serial) {
-            march_slots_wave_kernel<<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts,
-                                                                      slot_t, slot_dt);
+            const char* edg = getenv("NGP_MARCH_DIAG");
+            const int dg = edg ? atoi(edg) : 0;
+            if (dg == 1)
+                march_slots_wave_kernel<1><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
+                                                                            counts, slot_t, slot_dt);
+            else if (dg == 2)
+                march_slots_wave_kernel<2><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
+                                                                            counts, slot_t, slot_dt);
+            else
+                march_slots_wave_kernel<0><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
+                                                                            counts, slot_t, slot_dt);
         } else if (march_simple(p)) {
             if (stage) march_slots_kernel<true, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
             else march_slots_kernel<true, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);

@@ -157,7 +157,7 @@ class NGPTrainer:
                     noise=torch.empty(R, **f), counts=torch.empty(R, dtype=torch.int32, device=dev),
                     img_idxs=torch.empty(R, dtype=torch.int64, device=dev),
                     pix_idxs=torch.empty(R, dtype=torch.int64, device=dev), rgb_gt=torch.empty(R, 3, **f),
-                    occ_summary=torch.empty((cap_bits + 255) // 256, dtype=torch.int32, device=dev),
+                    occ_summary=torch.empty(2 * ((cap_bits + 255) // 256), dtype=torch.int32, device=dev),
                     rays_a=torch.empty(R, 3, dtype=torch.int64, device=dev),
                     n_samples=torch.zeros(1, dtype=torch.int64, device=dev),
                     xyzs=torch.empty(cap, 3, **f), dirs=torch.empty(cap, 3, **f), deltas=torch.empty(cap, **f),
@@ -274,7 +274,7 @@ class NGPTrainer:
                     m["noise"].copy_(noise)
             # the bitfield's block summary, rebuilt per march: any writer of
             # density_bitfield (update_density_grid, tests, tools) stays valid
-            vren.bitfield_summary(self.density_bitfield, out=m["occ_summary"])
+            vren.bitfield_summary(self.density_bitfield, self.G, out=m["occ_summary"])
             vren._ok(L.ngp_march_train_slots(_p(m["rays_o"]), _p(m["rays_d"]), _p(m["hits_t"]), R,
                                              _p(self.density_bitfield), self.cascades, self.G,
                                              ctypes_float(self.scale), ctypes_float(self.esf), _p(m["noise"]),

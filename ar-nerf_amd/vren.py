@@ -53,7 +53,7 @@ def _declare(L):
                                   vp, vp],
         "ngp_march_train_slots": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, vp, c_int, vp, vp, vp, vp,
                                   vp, vp, vp],
-        "ngp_bitfield_summary": [vp, c_int64, vp, vp],
+        "ngp_bitfield_summary": [vp, c_int64, c_int, vp, vp],
         "ngp_march_train_compact": [vp, vp, vp, c_int64, vp, vp, c_int, vp, vp, vp, vp, vp],
         "ngp_march_test": [vp, vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, c_int, c_int, vp, vp, vp, vp,
                            vp, vp, vp],
@@ -174,15 +174,16 @@ def packbits(density_grid, density_threshold, density_bitfield):
     _ok(lib().ngp_packbits(pg, density_bitfield.numel(), thr, thr_dev, pb, _stream()), "packbits")
 
 
-def bitfield_summary(density_bitfield, out=None):
-    """ngp_bitfield_summary: (n_bytes/256) i32 words, bit w = (64-bit word w of
-    the bitfield != 0).  The marchers keep it in LDS to skip empty blocks
-    without a global load (same results with or without it)."""
+def bitfield_summary(density_bitfield, grid_size=128, out=None):
+    """ngp_bitfield_summary: 2 x (n_bytes/256) i32 words: bit w = (64-bit word w
+    of the bitfield != 0), then the same dilated by one 4^3 block.  The
+    marchers keep it in LDS to skip empty blocks without a global load and
+    rays that pass no occupied block (same results with or without it)."""
     pb = _check("density_bitfield", density_bitfield, torch.uint8)
     n = density_bitfield.numel()
     if out is None:
-        out = torch.empty((n + 255) // 256, dtype=torch.int32, device=density_bitfield.device)
-    _ok(lib().ngp_bitfield_summary(pb, n, c_void_p(out.data_ptr()), _stream()), "bitfield_summary")
+        out = torch.empty(2 * ((n + 255) // 256), dtype=torch.int32, device=density_bitfield.device)
+    _ok(lib().ngp_bitfield_summary(pb, n, int(grid_size), c_void_p(out.data_ptr()), _stream()), "bitfield_summary")
     return out
 
 
@@ -191,7 +192,7 @@ def _summary_arg(density_bitfield, cascades, grid_size):
     2048-cell words (the marcher then reads the bitfield directly)."""
     if (int(cascades) * int(grid_size) ** 3) % 2048 != 0 or density_bitfield.numel() % 8 != 0:
         return None
-    return bitfield_summary(density_bitfield)
+    return bitfield_summary(density_bitfield, grid_size)
 
 
 # ----------------------------------------------------------- marching

@@ -131,12 +131,16 @@ int ngp_march_test(const float* rays_o, const float* rays_d, float* hits_t, cons
                    const uint32_t* occ_summary, void* stream);
 
 /* Occupancy summary of a bitfield, for the marchers above (occ_summary,
- * nullable there): bit w of summary = (64-bit bitfield word w != 0), i.e.
- * whether the Morton-aligned 4x4x4 cell block w holds any occupied cell;
- * n_bytes/256 uint32 words (rounded up).  The marchers keep it in LDS, so a
- * ray crossing empty blocks never waits on a global load; results are
- * identical with or without it.  Recompute after every ngp_packbits. */
-int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, uint32_t* summary, void* stream);
+ * nullable there): 2 x ceil(n_bytes/256) uint32 words.  First half: bit w =
+ * (64-bit bitfield word w != 0), i.e. whether the Morton-aligned 4x4x4 cell
+ * block w holds any occupied cell; second half: the same dilated by one
+ * block in each direction (grid_size a power of two; else all ones).  The
+ * marchers keep both in LDS: a ray crossing empty blocks never waits on a
+ * global load, and the training marcher skips rays that pass no occupied
+ * block exactly; results are identical with or without it.  Recompute
+ * after every change of the bitfield. */
+int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, int grid_size, uint32_t* summary,
+                         void* stream);
 
 /* -------------------------------------------------------- compositing */
 /* Replaces vren.composite_train_fw (binding.cpp:91-101 -> volumerendering.cu:5-83).

@@ -29,8 +29,9 @@ def main():
     out = {"samples": int(tr.n_samples.item())}
     src = ("sample", 12345, gt)
     cur = torch.cuda.current_stream()
-    for ser, stage, rpw in [(1, 0, 16), (1, 0, 4), (1, 1, 4), (0, 0, 16)]:
+    for ser, stage, rpw in [(1, 0, 4), (0, 0, 16), (0, 1, 16), (0, 2, 16)]:
         os.environ["NGP_MARCH_SERIAL"] = str(ser)
+        os.environ["NGP_MARCH_DIAG"] = str(stage)
         os.environ["NGP_MARCH_RPW"] = str(rpw)
         os.environ["NGP_MARCH_STAGE"] = str(stage)
         for _ in range(3):
@@ -45,6 +46,7 @@ def main():
     os.environ["NGP_MARCH_RPW"] = "16"
     os.environ["NGP_MARCH_STAGE"] = "0"
     os.environ["NGP_MARCH_SERIAL"] = "0"
+    os.environ["NGP_MARCH_DIAG"] = "0"
     saved = tr.density_bitfield.clone()
     for name, val in (("empty", 0), ("full", 255)):
         tr.density_bitfield.fill_(val)

@@ -59,6 +59,6 @@ def test_bad_arguments_return_einval():
     assert L.ngp_composite_train_fw(None, None, None, None, None, 5, 1e-4, None, None, None, None, None, None) == -1
     assert L.ngp_march_test(None, None, None, None, 1, None, 1, 128, 0.5, 0.0, 1, 1024, None, None, None, None, None,
                             None, None) == -1
-    assert L.ngp_bitfield_summary(None, 256, None, None) == -1
+    assert L.ngp_bitfield_summary(None, 256, 128, None, None) == -1
     # zero-size calls are no-ops
     assert L.ngp_morton3d(None, 0, None, None) == 0
