@@ -80,4 +80,22 @@ __device__ __forceinline__ uint32_t compact3(uint32_t x) {
     return x;
 }
 
+// Counter-based Philox-4x32-10 (Salmon et al., SC'11): 4 independent
+// uniform uint32 per (key, counter), no state to carry between steps.
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+// uniform integer in [0, n) (multiply-shift; bias <= n / 2^32)
+__device__ __forceinline__ int64_t uniform_index(uint32_t u, int64_t n) {
+    return (int64_t)(((uint64_t)u * (uint64_t)n) >> 32);
+}
+
 }  // namespace ngp

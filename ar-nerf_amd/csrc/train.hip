@@ -69,20 +69,30 @@ __device__ __forceinline__ int64_t composite_loss_ray(
     float* __restrict__ out_loss, int32_t* __restrict__ n_active, int64_t& na_out) {
     const int lane = threadIdx.x & 63;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+    // The first two 64-sample chunks (most rows terminate within them) are
+    // loaded together up front and kept in registers for the backward: two
+    // memory round trips per row instead of one per chunk and pass.
+    struct Chunk {
+        float sg, dl, cr, cg, cb, tt, w, Ta;
+    };
+    auto load = [&](int64_t k0, Chunk& c) {
+        const int64_t s = start + k0 + lane;
+        c.sg = c.dl = c.cr = c.cg = c.cb = c.tt = 0.f;
+        if (k0 + lane < N) {
+            c.sg = sigmas[s]; c.dl = deltas[s]; c.tt = ts[s];
+            c.cr = rgbs[3 * s]; c.cg = rgbs[3 * s + 1]; c.cb = rgbs[3 * s + 2];
+        }
+    };
+    Chunk c0, c1;
+    load(0, c0);
+    if (N > 64) load(64, c1);
     // ---- forward
     float T = 1.0f, R = 0.f, G = 0.f, B = 0.f, D = 0.f, O = 0.f;
     int64_t samples = 0, na = 0;
     bool done = false;
-    for (int64_t k0 = 0; k0 < N && !done; k0 += 64) {
+    auto fw_chunk = [&](int64_t k0, Chunk& c) {
         const int cnt = (int)(N - k0 < 64 ? N - k0 : 64);
-        const bool in = lane < cnt;
-        const int64_t s = start + k0 + lane;
-        float sg = 0.f, dl = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, tt = 0.f;
-        if (in) {
-            sg = sigmas[s]; dl = deltas[s]; tt = ts[s];
-            cr = rgbs[3 * s]; cg = rgbs[3 * s + 1]; cb = rgbs[3 * s + 2];
-        }
-        const float a = 1.0f - __expf(-sg * dl);
+        const float a = 1.0f - __expf(-c.sg * c.dl);
         const float om = 1.0f - a;
         float Tk = 0.f;
         int stop = cnt;
@@ -93,12 +103,21 @@ __device__ __forceinline__ int64_t composite_loss_ray(
             if (T <= la.T_thr) { stop = j + 1; done = true; break; }
         }
         const bool act = lane < stop;
-        const float w = act ? a * Tk : 0.f;
-        if (act) { dL_drgbs[3 * s] = w; dL_drgbs[3 * s + 1] = Tk * om; }
-        R += wave_sum(w * cr); G += wave_sum(w * cg); B += wave_sum(w * cb);
-        D += wave_sum(w * tt); O += wave_sum(w);
+        c.w = act ? a * Tk : 0.f;
+        c.Ta = Tk * om;
+        R += wave_sum(c.w * c.cr); G += wave_sum(c.w * c.cg); B += wave_sum(c.w * c.cb);
+        D += wave_sum(c.w * c.tt); O += wave_sum(c.w);
         samples += done ? stop - 1 : stop;
         na += stop;
+    };
+    fw_chunk(0, c0);
+    if (!done && N > 64) fw_chunk(64, c1);
+    for (int64_t k0 = 128; k0 < N && !done; k0 += 64) {  // long rows: spill w / T to memory
+        Chunk c;
+        load(k0, c);
+        fw_chunk(k0, c);
+        const int64_t s = start + k0 + lane;
+        if (k0 + lane < N) { dL_drgbs[3 * s] = c.w; dL_drgbs[3 * s + 1] = c.Ta; }
     }
     // ---- background + loss (wave-uniform)
     const float bgc[3] = {bg[0], bg[1], bg[2]};
@@ -133,24 +152,29 @@ __device__ __forceinline__ int64_t composite_loss_ray(
     // ---- backward over the na composited samples (dL/dws = 0)
     const float gs = gop * (1 - O);
     float rc = 0.f, gc = 0.f, bc = 0.f, dc = 0.f;
-    for (int64_t k0 = 0; k0 < na; k0 += 64) {
+    auto bw_chunk = [&](int64_t k0, const Chunk& c) {
         const int cnt = (int)(na - k0 < 64 ? na - k0 : 64);
         const bool in = lane < cnt;
         const int64_t s = start + k0 + lane;
-        float dl = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, tt = 0.f, w = 0.f, Ta = 0.f;
-        if (in) {
-            dl = deltas[s]; tt = ts[s];
-            cr = rgbs[3 * s]; cg = rgbs[3 * s + 1]; cb = rgbs[3 * s + 2];
-            w = dL_drgbs[3 * s]; Ta = dL_drgbs[3 * s + 1];
-        }
-        const float pr = rc + wave_incl_scan(w * cr, lane), pg = gc + wave_incl_scan(w * cg, lane);
-        const float pb = bc + wave_incl_scan(w * cb, lane), pd = dc + wave_incl_scan(w * tt, lane);
+        const float w = in ? c.w : 0.f, Ta = c.Ta;
+        const float pr = rc + wave_incl_scan(w * c.cr, lane), pg = gc + wave_incl_scan(w * c.cg, lane);
+        const float pb = bc + wave_incl_scan(w * c.cb, lane), pd = dc + wave_incl_scan(w * c.tt, lane);
         if (in) {
             dL_drgbs[3 * s] = g[0] * w; dL_drgbs[3 * s + 1] = g[1] * w; dL_drgbs[3 * s + 2] = g[2] * w;
-            dL_dsig[s] = dl * (g[0] * (cr * Ta - (R - pr)) + g[1] * (cg * Ta - (G - pg)) +
-                               g[2] * (cb * Ta - (B - pb)) + gs + gdep * (tt * Ta - (D - pd)));
+            dL_dsig[s] = c.dl * (g[0] * (c.cr * Ta - (R - pr)) + g[1] * (c.cg * Ta - (G - pg)) +
+                                 g[2] * (c.cb * Ta - (B - pb)) + gs + gdep * (c.tt * Ta - (D - pd)));
         }
         rc = __shfl(pr, 63, 64); gc = __shfl(pg, 63, 64); bc = __shfl(pb, 63, 64); dc = __shfl(pd, 63, 64);
+    };
+    if (na > 0) bw_chunk(0, c0);
+    if (na > 64) bw_chunk(64, c1);
+    for (int64_t k0 = 128; k0 < na; k0 += 64) {
+        Chunk c;
+        load(k0, c);
+        const int64_t s = start + k0 + lane;
+        c.w = 0.f; c.Ta = 0.f;
+        if (k0 + lane < na) { c.w = dL_drgbs[3 * s]; c.Ta = dL_drgbs[3 * s + 1]; }
+        bw_chunk(k0, c);
     }
     return samples;
 }
@@ -275,11 +299,95 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
 // density_grid_tmp[c, idx] = sigma (models/networks.py:268); duplicates keep
 // the max (the reference's last-writer-wins is order-undefined on a GPU).
 // sigma >= 0, so an unsigned-int max on the fp32 bits is a float max.
+// Negative indices are skipped (occupancy samples that do not exist: no
+// occupied cell to resample, see occ_sample_kernel).
 __global__ void scatter_max_kernel(const int64_t* __restrict__ idx, const float* __restrict__ sig, int64_t n,
                                    float* __restrict__ tmp) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    atomicMax(reinterpret_cast<unsigned int*>(tmp) + idx[i], __float_as_uint(fmaxf(sig[i], 0.f)));
+    const int64_t j = idx[i];
+    if (j < 0) return;
+    atomicMax(reinterpret_cast<unsigned int*>(tmp) + j, __float_as_uint(fmaxf(sig[i], 0.f)));
+}
+
+// ---------------------------------------- occupancy cell sampling on device
+// sample_uniform_and_occupied_cells (models/networks.py:181-207) without the
+// host sync of torch.nonzero: occ_list_kernel lists the cells of one cascade
+// with density > threshold (order unspecified; one atomic per workgroup),
+// occ_sample_kernel draws M uniform cells and M cells uniformly from that
+// list (none if it is empty, as the reference's empty nonzero gives none)
+// and their jittered world positions (networks.py:262-266).
+__global__ void __launch_bounds__(1024) occ_list_kernel(const float* __restrict__ grid_c, int64_t n_cells, float thr,
+                                                        int32_t* __restrict__ list,
+                                                        unsigned long long* __restrict__ count) {
+    __shared__ uint32_t wcnt[16];
+    __shared__ unsigned long long base;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int PER = 8;
+    const int64_t c0 = ((int64_t)blockIdx.x * 1024 + tid) * PER;
+    bool hit[PER];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        hit[k] = c0 + k < n_cells && grid_c[c0 + k] > thr;
+        mine += hit[k];
+    }
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wcnt[wid] = incl;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < 16; ++w) { const uint32_t v = wcnt[w]; wcnt[w] = tot; tot += v; }
+        base = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    int64_t pos = (int64_t)base + wcnt[wid] + incl - mine;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+        if (hit[k]) list[pos++] = (int32_t)(c0 + k);
+}
+
+__global__ void __launch_bounds__(256) occ_sample_kernel(uint64_t seed, const int64_t* __restrict__ ctr, int cascade,
+                                                         int G, int64_t M, float s_minus_hgs, float hgs,
+                                                         const int32_t* __restrict__ list,
+                                                         const unsigned long long* __restrict__ count, int64_t lo,
+                                                         int64_t hi, float* __restrict__ xyzs,
+                                                         int64_t* __restrict__ flat) {
+    const int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= hi) return;
+    const int64_t o = i - lo;
+    const uint64_t step = (uint64_t)*ctr;
+    const uint4 u = philox4x32(make_uint4((uint32_t)i, (uint32_t)(i >> 32), (uint32_t)step, (uint32_t)cascade),
+                               make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    int32_t idx;
+    if (i < M) {  // uniform cell: torch.randint(G, (M, 3)) then morton3D
+        const uint4 v = philox4x32(make_uint4((uint32_t)i, (uint32_t)(i >> 32), (uint32_t)step, 0x9E3779B9u ^ cascade),
+                                   make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+        idx = (int32_t)morton3((uint32_t)uniform_index(v.x, G), (uint32_t)uniform_index(v.y, G),
+                               (uint32_t)uniform_index(v.z, G));
+    } else {  // a cell drawn from the occupied list
+        const unsigned long long cnt = *count;
+        if (cnt == 0) {
+            flat[o] = -1;
+            xyzs[3 * o] = 0.f; xyzs[3 * o + 1] = 0.f; xyzs[3 * o + 2] = 0.f;
+            return;
+        }
+        idx = list[uniform_index(u.w, (int64_t)cnt)];
+    }
+    const uint32_t cx = compact3((uint32_t)idx), cy = compact3((uint32_t)idx >> 1), cz = compact3((uint32_t)idx >> 2);
+    // xyzs_w = (coords / (G-1) * 2 - 1) * (s - hgs) + (rand * 2 - 1) * hgs, fp32 as torch evaluates it
+    const float gm1 = (float)(G - 1);
+    const float jr[3] = {(float)(u.x >> 8) * (1.0f / 16777216.0f), (float)(u.y >> 8) * (1.0f / 16777216.0f),
+                         (float)(u.z >> 8) * (1.0f / 16777216.0f)};
+    const uint32_t cc[3] = {cx, cy, cz};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) xyzs[3 * o + d] = ((float)cc[d] / gm1 * 2.0f - 1.0f) * s_minus_hgs + (jr[d] * 2.0f - 1.0f) * hgs;
+    flat[o] = (int64_t)cascade * G * G * G + idx;
 }
 
 // models/networks.py:273-278: grid = where(grid<0, grid, max(grid*decay, tmp));
@@ -288,7 +396,7 @@ __global__ void scatter_max_kernel(const int64_t* __restrict__ idx, const float*
 // every cell holds sigma ~= 1 and the threshold (= that mean) splits them, so
 // a last-digit difference in an fp32 sum flips thousands of cells and sends
 // training down a different trajectory.
-__global__ void __launch_bounds__(256) grid_ema_kernel(float* __restrict__ grid, const float* __restrict__ tmp, int64_t n,
+__global__ void __launch_bounds__(256) grid_ema_kernel(float* __restrict__ grid, float* __restrict__ tmp, int64_t n,
                                                        float decay, double* __restrict__ sum_cnt) {
     double s = 0.0, c = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -296,6 +404,7 @@ __global__ void __launch_bounds__(256) grid_ema_kernel(float* __restrict__ grid,
         const float gv = grid[i];
         const float nv = gv < 0 ? gv : fmaxf(gv * decay, tmp[i]);
         grid[i] = nv;
+        tmp[i] = 0.f;  // consumed: left zeroed for the next update
         if (nv > 0) { s += (double)nv; c += 1.0; }
     }
 #pragma unroll
@@ -535,7 +644,30 @@ int ngp_density_scatter_max(const int64_t* indices, const float* sigmas, int64_t
     return ngp_launch_status();
 }
 
-int ngp_density_grid_ema(float* density_grid, const float* grid_tmp, int64_t n, float decay, float thr_max,
+int ngp_occupied_cells(const float* grid_cascade, int64_t n_cells, float threshold, int32_t* list, int64_t* count,
+                       void* stream) {
+    NGP_CHECK_ARG(n_cells > 0 && grid_cascade && list && count && ((uintptr_t)count & 7) == 0);
+    hipStream_t s = as_stream(stream);
+    hipError_t e = hipMemsetAsync(count, 0, sizeof(int64_t), s);
+    if (e != hipSuccess) return (int)e;
+    occ_list_kernel<<<(unsigned)((n_cells + 8191) / 8192), 1024, 0, s>>>(grid_cascade, n_cells, threshold, list,
+                                                                        (unsigned long long*)count);
+    return ngp_launch_status();
+}
+
+int ngp_occupancy_samples(uint64_t seed, const int64_t* counter_dev, int cascade, int grid_size, int64_t M,
+                          float s_minus_hgs, float hgs, const int32_t* occ_list, const int64_t* occ_count, int64_t lo,
+                          int64_t hi, float* xyzs, int64_t* flat_idx, void* stream) {
+    NGP_CHECK_ARG(counter_dev && occ_list && occ_count && xyzs && flat_idx && grid_size >= 2 && M >= 0 && lo >= 0 &&
+                  lo <= hi && hi <= 2 * M && cascade >= 0);
+    if (hi == lo) return NGP_OK;
+    occ_sample_kernel<<<(unsigned)((hi - lo + 255) / 256), 256, 0, as_stream(stream)>>>(
+        seed, counter_dev, cascade, grid_size, M, s_minus_hgs, hgs, occ_list, (const unsigned long long*)occ_count, lo,
+        hi, xyzs, flat_idx);
+    return ngp_launch_status();
+}
+
+int ngp_density_grid_ema(float* density_grid, float* grid_tmp, int64_t n, float decay, float thr_max,
                          void* sum_cnt_ws, float* threshold_out, void* stream) {
     NGP_CHECK_ARG(n > 0 && density_grid && grid_tmp && sum_cnt_ws && threshold_out);
     NGP_CHECK_ARG(((uintptr_t)sum_cnt_ws & 7) == 0);

@@ -76,6 +76,14 @@ class NGPTrainer:
         self.grid_coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3).contiguous()
         self.all_indices = vren.morton3D(self.grid_coords).long()
         self._sum_cnt = torch.zeros(2, dtype=torch.float64, device=dev)
+        # device-side occupancy sampling buffers (update_density_grid)
+        M2 = 2 * (self.G ** 3 // 4)
+        self._occ_tmp = torch.zeros_like(self.density_grid)
+        self._occ_list = torch.empty(self.G ** 3, dtype=torch.int32, device=dev)
+        self._occ_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._occ_xyz = torch.empty(M2, 3, device=dev)
+        self._occ_flat = torch.empty(M2, dtype=torch.int64, device=dev)
+        self._occ_sig = torch.empty(M2, device=dev)
         self.threshold = torch.zeros(2, device=dev)
         # ---- per-step buffers
         R = batch_size
@@ -138,8 +146,10 @@ class NGPTrainer:
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(1000 + seed + self.rank)
         self.sample_seed = (1000003 * (seed + 1) + 7919 * self.rank) & 0xFFFFFFFFFFFFFFFF  # ngp_sample_batch key
-        # device step counters: [0] Adam steps taken, [1] batches drawn (RNG counter)
-        self.dctr = torch.zeros(2, dtype=torch.int64, device=dev)
+        # device step counters: [0] Adam steps taken, [1] batches drawn (RNG
+        # counter), [2] device-sampled occupancy updates (their RNG counter)
+        self.dctr = torch.zeros(3, dtype=torch.int64, device=dev)
+        self._updated_for = -1  # global step whose occupancy update already ran (end of the previous graph)
         self.lr_dev = torch.full((1,), float(lr), device=dev)
         self._lr_set = float(lr)
         # HIP graphs of the steady-state step, one per buffer set (see train_step)
@@ -202,39 +212,47 @@ class NGPTrainer:
 
     @torch.no_grad()
     def update_density_grid(self, density_threshold, warmup=False, decay=0.95):
-        """models/networks.py:252-281.  Multi-GPU: each rank evaluates its 1/world
-        share of the cells and the cell maxima are combined with one MAX
-        all-reduce, so every rank packs an identical bitfield."""
+        """models/networks.py:252-281.  Past warmup the cells are drawn on device
+        (ngp_occupied_cells + ngp_occupancy_samples: no host sync, so the update
+        can sit inside a captured graph).  Multi-GPU: each rank evaluates its
+        1/world share of the (identically drawn) cells and the cell maxima are
+        combined with one MAX all-reduce, so every rank packs an identical
+        bitfield."""
         C, G = self.cascades, self.G
-        tmp = torch.zeros_like(self.density_grid)
+        L, s = self.L, vren._stream()
+        tmp = self._occ_tmp  # zero on entry; the EMA consumes (re-zeroes) it
         for c in range(C):
+            sc = min(2 ** (c - 1), self.scale)
+            half_grid_size = sc / G
             if warmup:  # get_all_cells (networks.py:167-179)
                 indices, coords = self.all_indices, self.grid_coords
-            else:  # sample_uniform_and_occupied_cells (networks.py:181-207)
+                if self.world > 1:  # each rank evaluates its share of the cells
+                    indices, coords = ddp.shard_cells(indices, coords, self.rank, self.world)
+                xyzs_w = (coords / (G - 1) * 2 - 1) * (sc - half_grid_size)
+                xyzs_w += (torch.rand(xyzs_w.shape, device=self.dev, generator=self.gen) * 2 - 1) * half_grid_size
+                sig, _ = HG.density_forward(xyzs_w.float().contiguous(), self.grid, self.params16)
+                flat = (indices + c * G ** 3).contiguous()
+                n = flat.shape[0]
+            else:  # sample_uniform_and_occupied_cells (networks.py:181-207), on device
                 M = G ** 3 // 4
-                coords1 = torch.randint(G, (M, 3), dtype=torch.int32, device=self.dev, generator=self.gen)
-                indices1 = vren.morton3D(coords1).long()
-                indices2 = torch.nonzero(self.density_grid[c] > density_threshold)[:, 0]
-                if len(indices2) > 0:
-                    rand_idx = torch.randint(len(indices2), (M,), device=self.dev, generator=self.gen)
-                    indices2 = indices2[rand_idx]
-                coords2 = vren.morton3D_invert(indices2.int().contiguous())
-                indices = torch.cat([indices1, indices2])
-                coords = torch.cat([coords1, coords2])
-            if self.world > 1:  # each rank evaluates its share of the cells
-                indices, coords = ddp.shard_cells(indices, coords, self.rank, self.world)
-            s = min(2 ** (c - 1), self.scale)
-            half_grid_size = s / G
-            xyzs_w = (coords / (G - 1) * 2 - 1) * (s - half_grid_size)
-            xyzs_w += (torch.rand(xyzs_w.shape, device=self.dev, generator=self.gen) * 2 - 1) * half_grid_size
-            sig, _ = HG.density_forward(xyzs_w.float().contiguous(), self.grid, self.params16)
-            flat = (indices + c * G ** 3).contiguous()
-            vren._ok(self.L.ngp_density_scatter_max(_p(flat), _p(sig), flat.shape[0], _p(tmp), vren._stream()),
-                     "density_scatter_max")
+                vren._ok(L.ngp_occupied_cells(_p(self.density_grid[c]), G ** 3, ctypes_float(density_threshold),
+                                              _p(self._occ_list), _p(self._occ_count), s), "occupied_cells")
+                lo, hi = ddp.shard_range(2 * M, self.rank, self.world)
+                n = hi - lo
+                vren._ok(L.ngp_occupancy_samples(self.sample_seed ^ 0x5DEECE66D, _p(self.dctr[2:]), c, G, M,
+                                                 ctypes_float(sc - half_grid_size), ctypes_float(half_grid_size),
+                                                 _p(self._occ_list), _p(self._occ_count), lo, hi,
+                                                 _p(self._occ_xyz), _p(self._occ_flat), s), "occupancy_samples")
+                vren._ok(HG._lib().ngp_density_forward(_p(self._occ_xyz), n, None, HG.ctypes.byref(self.grid.desc),
+                                                       _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16),
+                                                       _p(self._occ_sig), None, s), "density_forward")
+                sig, flat = self._occ_sig, self._occ_flat
+            vren._ok(L.ngp_density_scatter_max(_p(flat), _p(sig), n, _p(tmp), s), "density_scatter_max")
+        if not warmup:
+            vren._ok(L.ngp_counters_inc(_p(self.dctr[2:]), 1, s), "counters_inc")
         ddp.combine_density_tmp_(tmp, self.pg)
-        st = self.L.ngp_density_grid_ema(_p(self.density_grid), _p(tmp), self.density_grid.numel(),
-                                         ctypes_float(decay), ctypes_float(density_threshold), _p(self._sum_cnt),
-                                         _p(self.threshold), vren._stream())
+        st = L.ngp_density_grid_ema(_p(self.density_grid), _p(tmp), self.density_grid.numel(), ctypes_float(decay),
+                                    ctypes_float(density_threshold), _p(self._sum_cnt), _p(self.threshold), s)
         vren._ok(st, "density_grid_ema")
         ddp.sync_threshold_(self.threshold, self.pg)  # identical threshold on every rank
         vren.packbits(self.density_grid, self.threshold[:1], self.density_bitfield)
@@ -358,9 +376,10 @@ class NGPTrainer:
         now or next step) replay a captured HIP graph of the whole step
         (NGP_GRAPHS=0: always eager)."""
         gs, ui = self.global_step, self.update_interval
-        if (self.use_graphs and self._pending is not None and gs % ui != 0 and (gs + 1) % ui != 0
-                and self.kernel_events is None and not self.random_bg and not self.no_prefetch):
-            return self._replay(gt_u8, directions, poses)
+        if (self.use_graphs and self._pending is not None and (gs % ui != 0 or self._updated_for == gs)
+                and gs >= self.warmup_steps and self.kernel_events is None and not self.random_bg
+                and not self.no_prefetch):
+            return self._replay(gt_u8, directions, poses, (gs + 1) % ui == 0)
         return self._on_exec_stream(self._step, ("sample", 0, gt_u8), None, directions, poses, True,
                                     ("sample", 1, gt_u8))
 
@@ -370,48 +389,58 @@ class NGPTrainer:
             self.lr_dev.fill_(lr)
             self._lr_set = lr
 
-    def _replay(self, gt_u8, directions, poses):
-        """Graph-replayed steady-state step for the batch pending in set k: the
-        step's kernels on the capture stream, the next batch's march forked
-        onto the side stream and joined before the end, the device counters
-        advanced last."""
+    def _replay(self, gt_u8, directions, poses, update_after):
+        """Graph-replayed steady-state step for the batch pending in set k.
+        Plain variant: the step's kernels on the capture stream, the next
+        batch's march forked onto the side stream and joined before the end,
+        the device counters advanced last.  update_after (the next step opens
+        with an occupancy update): no fork; after the step the update
+        (networks.py:252-281, cells drawn on device) and then the next batch's
+        march against the new bitfield, all inside the graph."""
         k, ev = self._pending
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
         self._set_lr()
-        key = (k, gt_u8.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt_u8.shape)
+        key = (k, bool(update_after), gt_u8.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt_u8.shape)
         g = self._graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
             # capture on a side stream, ordered after everything enqueued so far
             torch.cuda.current_stream().synchronize()
             with torch.cuda.graph(g):
-                self._graph_body(k, gt_u8, directions, poses)
+                self._graph_body(k, gt_u8, directions, poses, update_after)
             self._graphs[key] = g
         g.replay()
         self.cur = k
         self._bind(self.msets[k])
-        self._pending = (1 - k, None)  # marched and joined inside the graph
+        self._pending = (1 - k, None)  # marched (and joined) inside the graph
         self.n_prefetched += 1
         self.global_step += 1
+        if update_after:
+            self._updated_for = self.global_step
         return self.out_loss
 
-    def _graph_body(self, k, gt_u8, directions, poses):
+    def _graph_body(self, k, gt_u8, directions, poses, update_after=False):
         self.cur = k
         self._bind(self.msets[k])
         cs = torch.cuda.current_stream()
+        if not update_after:
+            def fork():
+                self.march_stream.wait_stream(cs)
+                self._march(1 - k, ("sample", 1, gt_u8), directions, poses, self.march_stream)
 
-        def fork():
-            self.march_stream.wait_stream(cs)
-            self._march(1 - k, ("sample", 1, gt_u8), directions, poses, self.march_stream)
-
-        self._compute(self.rgb_gt, True, fork)
-        cs.wait_stream(self.march_stream)
-        vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
+            self._compute(self.rgb_gt, True, fork)
+            cs.wait_stream(self.march_stream)
+            vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
+        else:
+            self._compute(self.rgb_gt, True, None)
+            vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
+            self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=False)
+            self._march(1 - k, ("sample", 0, gt_u8), directions, poses, cs)
 
     def _step(self, src, rgb_gt, directions, poses, apply_adam, next_src):
         self._ev("occupancy_update", 0)
-        if self.global_step % self.update_interval == 0:
+        if self.global_step % self.update_interval == 0 and self._updated_for != self.global_step:
             self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=self.global_step < self.warmup_steps)
         self._ev("occupancy_update", 1)
         self._ev("raygen_march", 0)

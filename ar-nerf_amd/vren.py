@@ -45,6 +45,9 @@ def _declare(L):
                                  c_float, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_adam_step_dev": [vp, vp, vp, vp, vp, c_int64, vp, c_float, c_float, c_float, vp, c_float, c_int, vp],
         "ngp_counters_inc": [vp, c_int, vp],
+        "ngp_occupied_cells": [vp, c_int64, c_float, vp, vp, vp],
+        "ngp_occupancy_samples": [ctypes.c_uint64, vp, c_int, c_int, c_int64, c_float, c_float, vp, vp, c_int64,
+                                  c_int64, vp, vp, vp],
         "ngp_morton3d": [vp, c_int64, vp, vp],
         "ngp_morton3d_invert": [vp, c_int64, vp, vp],
         "ngp_packbits": [vp, c_int64, c_float, vp, vp, vp],

@@ -340,15 +340,33 @@ int ngp_counters_inc(int64_t* counters, int n, void* stream);
 
 /* Occupancy update (models/networks.py:252-281).  scatter_max: grid_tmp[idx[i]]
  * = max(grid_tmp[idx[i]], sigmas[i]) (flat cascade*G^3 indices, sigmas >= 0).
- * grid_ema: grid = where(grid<0, grid, max(grid*decay, tmp)) in place, then
+ * (negative indices skipped).  grid_ema: grid = where(grid<0, grid,
+ * max(grid*decay, tmp)) in place (tmp is consumed: left zeroed), then
  * threshold_out[0] = min(mean(grid[grid>0]), thr_max) (NaN if none, as in
  * Python), threshold_out[1] = the mean; feed threshold_out to ngp_packbits'
  * threshold_dev.  sum_cnt_ws: 16 bytes of scratch (two fp64 accumulators, 8-byte
  * aligned; the mean is taken in fp64). */
 int ngp_density_scatter_max(const int64_t* indices, const float* sigmas, int64_t n, float* grid_tmp,
                             void* stream);
-int ngp_density_grid_ema(float* density_grid, const float* grid_tmp, int64_t n, float decay,
+int ngp_density_grid_ema(float* density_grid, float* grid_tmp, int64_t n, float decay,
                          float thr_max, void* sum_cnt_ws, float* threshold_out, void* stream);
+/* sample_uniform_and_occupied_cells (models/networks.py:181-207) on device,
+ * no host sync: ngp_occupied_cells lists the cells of one cascade (n_cells
+ * f32, Morton order) with density > threshold into list (capacity n_cells,
+ * order unspecified), *count = their number (8-byte aligned).
+ * ngp_occupancy_samples writes samples [lo, hi) of the 2*M list: sample i <
+ * M a uniform cell, i >= M a cell drawn uniformly from the occupied list
+ * (flat_idx = -1, skipped by ngp_density_scatter_max, when it is empty);
+ * xyzs (hi-lo, 3) = (coords/(G-1)*2-1)*(s-hgs) + (U*2-1)*hgs (networks.py:
+ * 262-266; s_minus_hgs, hgs as fp32), flat_idx (hi-lo) = cascade*G^3 +
+ * Morton index.  Randoms from Philox keyed by (seed, *counter_dev, cascade,
+ * i): every rank of a data-parallel job draws the same list and can
+ * evaluate a disjoint [lo, hi). */
+int ngp_occupied_cells(const float* grid_cascade, int64_t n_cells, float threshold, int32_t* list,
+                       int64_t* count, void* stream);
+int ngp_occupancy_samples(uint64_t seed, const int64_t* counter_dev, int cascade, int grid_size, int64_t M,
+                          float s_minus_hgs, float hgs, const int32_t* occ_list, const int64_t* occ_count,
+                          int64_t lo, int64_t hi, float* xyzs, int64_t* flat_idx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -80,6 +80,14 @@ def main():
     st["hash_bwd_atomic_coarse"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_levels(
         p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
         p(tr.grad[HG.MLP_PARAMS:]), 0, tr.bin_level_lo, s), "ha"))
+    for lo, hi in ((0, 2), (2, 4), (4, 6), (6, 8), (8, 10), (10, 12), (12, 14), (14, 16)):
+        st[f"hash_atomic_L{lo}_{hi}"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_levels(
+            p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
+            p(tr.grad[HG.MLP_PARAMS:]), lo, hi, s), "hl"))
+    for lo in (4, 6, 10, 12):
+        st[f"hash_binned_from_L{lo}"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_binned(
+            p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
+            p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, lo, s), "hb"))
     st["hash_bwd_atomic_all"] = timed(lambda: vren._ok(HGL.ngp_hash_backward(
         p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
         p(tr.grad[HG.MLP_PARAMS:]), s), "hall"))
@@ -88,6 +96,7 @@ def main():
         ctypes_float(1e-2), ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), 100, ctypes_float(1.0), 0,
         s), "adam"))
     st["occupancy_update"] = timed(lambda: tr.update_density_grid(0.01 * 1024 / 3 ** 0.5), reps=5)
+    st["density_fwd_1M"] = timed(lambda: HG.density_forward(tr.xyzs[:1 << 20].contiguous(), tr.grid, tr.params16), reps=5)
     import time
     torch.cuda.synchronize()
     c0 = time.perf_counter()

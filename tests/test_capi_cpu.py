@@ -36,6 +36,15 @@ def test_library_exports_every_declared_symbol():
     assert L.ngp_version().startswith(b"ngp_amd")
 
 
+def test_every_declared_function_has_a_ctypes_signature():
+    """An undeclared argtypes list lets ctypes pass Python ints as 32-bit C ints
+    and floats not at all: every C-ABI entry point must be declared."""
+    import hashgrid as HG
+    L = HG._lib()
+    missing = [n for n in _declared() if n != "ngp_version" and getattr(L, n).argtypes is None]
+    assert not missing, missing
+
+
 def test_library_levels_equal_oracle_levels():
     for scale in (0.5, 16.0):
         g = HG.HashGrid(scale)

@@ -213,3 +213,53 @@ def test_check_input_errors_like_reference():
     y = torch.zeros(4, 6, dtype=torch.int32, device=DEV)[:, ::2]
     with pytest.raises(RuntimeError, match="must be contiguous"):
         vren.morton3D(y)
+
+
+def test_device_occupancy_sampling():
+    """ngp_occupied_cells lists exactly the cells above the threshold;
+    ngp_occupancy_samples draws M uniform + M occupied cells (none when the
+    list is empty) with positions inside the jittered cell (networks.py:
+    181-207, 262-266), a pure function of the device counter."""
+    import ctypes
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    L = vren.lib()
+    G, s = 128, 0.5
+    hgs = s / G
+    g = torch.Generator(device=DEV).manual_seed(0)
+    grid = torch.rand(G ** 3, device=DEV, generator=g) * 10
+    grid[torch.rand(G ** 3, device=DEV, generator=g) < 0.3] = -1
+    thr = 5.9
+    lst = torch.empty(G ** 3, dtype=torch.int32, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    vren._ok(L.ngp_occupied_cells(p(grid), G ** 3, thr, p(lst), p(cnt), vren._stream()), "occ")
+    ref = torch.nonzero(grid > thr)[:, 0]
+    n = int(cnt.item())
+    assert n == ref.numel()
+    assert torch.equal(torch.sort(lst[:n].long())[0], ref)
+    M = G ** 3 // 4
+    ctr = torch.tensor([7], dtype=torch.int64, device=DEV)
+    xyz = torch.empty(2 * M, 3, device=DEV)
+    flat = torch.empty(2 * M, dtype=torch.int64, device=DEV)
+
+    def draw(c_lst, c_cnt, lo=0, hi=2 * M):
+        vren._ok(L.ngp_occupancy_samples(99, p(ctr), 0, G, M, s - hgs, hgs, p(c_lst), p(c_cnt), lo, hi, p(xyz),
+                                         p(flat), vren._stream()), "samples")
+        return xyz[:hi - lo].clone(), flat[:hi - lo].clone()
+
+    x, f = draw(lst, cnt)
+    assert int(f.min()) >= 0 and int(f.max()) < G ** 3
+    occ = torch.zeros(G ** 3, dtype=torch.bool, device=DEV)
+    occ[ref] = True
+    assert bool(occ[f[M:]].all())  # second half drawn from the occupied list
+    coords = vren.morton3D_invert(f.int().contiguous()).float()
+    centre = (coords / (G - 1) * 2 - 1) * (s - hgs)
+    assert float((x - centre).abs().max()) <= hgs * (1 + 1e-5)
+    # uniform half: roughly uniform over cells
+    assert abs(float(occ[f[:M]].float().mean()) - n / G ** 3) < 0.01
+    # shards of the same draw are slices of it
+    x2, f2 = draw(lst, cnt, lo=1000, hi=5000)
+    assert torch.equal(f2, f[1000:5000]) and torch.equal(x2, x[1000:5000])
+    # empty occupied list: the second half is skipped (-1)
+    cnt.zero_()
+    _, f3 = draw(lst, cnt)
+    assert bool((f3[M:] == -1).all()) and torch.equal(f3[:M], f[:M])
