@@ -253,7 +253,7 @@ def test_device_occupancy_sampling():
     assert bool(occ[f[M:]].all())  # second half drawn from the occupied list
     coords = vren.morton3D_invert(f.int().contiguous()).float()
     centre = (coords / (G - 1) * 2 - 1) * (s - hgs)
-    assert float((x - centre).abs().max()) <= hgs * (1 + 1e-5)
+    assert float((x - centre).abs().max()) <= hgs + 4e-7  # a few fp32 ulps at |x| <= 0.5
     # uniform half: roughly uniform over cells
     assert abs(float(occ[f[:M]].float().mean()) - n / G ** 3) < 0.01
     # shards of the same draw are slices of it
