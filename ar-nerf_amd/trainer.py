@@ -37,6 +37,9 @@ def _p(t):
     return HG._ptr(t)
 
 
+STAT_STRIPES, STAT_STRIDE = 32, 16  # include/ngp_amd.h NGP_STAT_*
+
+
 class NGPTrainer:
     def __init__(self, scale=0.5, batch_size=8192, lr=1e-2, num_epochs=30, steps_per_epoch=1000, loss="raw",
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
@@ -116,7 +119,9 @@ class NGPTrainer:
         self.out_depth, self.out_loss = torch.empty(R, **f), torch.empty(R, **f)
         # running totals: [0] marched, [1] composited (vr_samples), [2] gradient-carrying,
         # [3] field-evaluated samples
-        self.stats = torch.zeros(4, dtype=torch.int64, device=dev)
+        # striped counters (ngp_composite_loss: NGP_STAT_STRIPES x NGP_STAT_STRIDE);
+        # [0, 3] = field-evaluated samples (ngp_ray_segments total_acc)
+        self.stats = torch.zeros(STAT_STRIPES * STAT_STRIDE, dtype=torch.int64, device=dev)
         # chunked field evaluation (ngp_chunk_counts): first `chunk_first` samples of
         # every row, then the rest of the rows not yet terminated (0 = every sample)
         self.chunk_first = int(os.environ.get("NGP_CHUNK_FIRST", chunk_first))
@@ -357,6 +362,11 @@ class NGPTrainer:
             out = fn(*args)
         caller.wait_stream(self.exec_stream)
         return out
+
+    def stat_totals(self):
+        """(marched, composited, active, evaluated) samples accumulated since
+        stats was last zeroed (sum over the stripes)."""
+        return [int(v) for v in self.stats.view(STAT_STRIPES, STAT_STRIDE)[:, :4].sum(0).tolist()]
 
     def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True, next_batch=None):
         """One training step on a batch (train.py:174-200).  img/pix (R) i64,

@@ -201,7 +201,7 @@ def main():
     t_el = float(t_max.item())
     total_rays = R * args.steps * world
     value = total_rays / t_el
-    marched, composited, active, evaluated = (int(v) for v in trainer.stats.tolist())
+    marched, composited, active, evaluated = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         evaluated = marched
     rm_s = marched / (R * args.steps)
@@ -225,7 +225,7 @@ def main():
     torch.cuda.synchronize()
     t_bd = time.perf_counter() - t_bd
     trainer.kernel_events = None
-    marched_bd, _, active_bd, evaluated_bd = (int(v) for v in trainer.stats.tolist())
+    marched_bd, _, active_bd, evaluated_bd = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         evaluated_bd = marched_bd
     samples_per_step = evaluated_bd / n_bd  # field_fwd runs over the evaluated samples

@@ -289,8 +289,13 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
  * list of those samples, each row's entries contiguous (row order not
  * fixed), and *n_active_total its length; alloc_ws = 16 bytes of zeroed,
  * 8-byte aligned scratch that the kernel leaves zeroed again.  stats
- * (nullable, 3 x i64) accumulates [0] marched, [1] composited (vr_samples),
- * [2] gradient-carrying samples. */
+ * (nullable, NGP_STAT_STRIPES x NGP_STAT_STRIDE i64) accumulates, striped
+ * over blocks so that no single address takes every block's atomic,
+ * counter k of stripe s at stats[s * NGP_STAT_STRIDE + k]: k = 0 marched,
+ * 1 composited (vr_samples), 2 gradient-carrying samples; a counter's value
+ * is the sum over stripes. */
+#define NGP_STAT_STRIPES 32
+#define NGP_STAT_STRIDE 16
 int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
                        const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg,
                        int loss_type, float lambda_opacity, float lambda_depth, float depth_scale,
