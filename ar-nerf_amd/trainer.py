@@ -111,6 +111,11 @@ class NGPTrainer:
         self._bind(self.msets[0])
         self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         # saved encoding: pair-major (8, cap, 4) for the split forward, else row-major (cap, 32)
+        # hybrid hash backward: the atomic coarse levels run on their own
+        # stream beside the binned fine levels (disjoint gradient ranges;
+        # memory-side atomics vs LDS-bound passes overlap)
+        self.bwd_stream = torch.cuda.Stream(device=dev)
+        self.overlap_hash_bwd = os.environ.get("NGP_BWD_OVERLAP", "1") == "1"
         self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "0") == "1"
         self.enc = torch.empty(8 * cap * 4, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
@@ -538,14 +543,19 @@ class NGPTrainer:
         at("after_mlp_bwd")
         self._ev("hash_bwd", 0)
         if self.hash_backward != "atomic":
+            cs = torch.cuda.current_stream()
+            bs = self.bwd_stream if self.overlap_hash_bwd else cs
+            bs.wait_stream(cs)
+            with torch.cuda.stream(bs):
+                vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                      _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
+                                                      _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), 0,
+                                                      self.bin_level_lo, vren._stream()), "hash_backward_levels")
             vren._ok(HGL.ngp_hash_backward_binned(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
                                                   _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
                                                   self.bin_level_lo, s), "hash_backward_binned")
-            vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                  _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
-                                                  _p(self.grad[HG.MLP_PARAMS:]), 0, self.bin_level_lo, s),
-                     "hash_backward_levels")
+            cs.wait_stream(bs)
         else:
             vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
                                            HG.ctypes.byref(self.grid.desc),
