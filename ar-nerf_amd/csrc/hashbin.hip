@@ -230,7 +230,9 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
                                                          BinWs ws) {
     __shared__ LevelLds lv;
     __shared__ uint32_t base[NSLOT];          // this tile's first slot in each bucket region
-    __shared__ uint32_t hist[NBL], loff[NBL + 1];
+    // hist is double-buffered by level parity: the MODE-2 path has no barrier
+    // between a level's rank atomics and the next level's reset
+    __shared__ uint32_t hist2[2][NBL], loff[NBL + 1];
     __shared__ uint4 stage[TILE * 4];         // one level's records, sorted by bucket
     __shared__ uint8_t sbk[TILE * 4];
     load_levels(ga, lv);
@@ -259,6 +261,7 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
                              : float2{0.f, 0.f};
 #pragma unroll 1
         for (int l = ba.lo; l < L; ++l) {
+            uint32_t* hist = hist2[l & 1];
             if (t < NBL) hist[t] = 0;
             __syncthreads();  // also: base[] ready; previous level's stage[] reads done
 #pragma unroll
@@ -458,17 +461,19 @@ size_t ngp_hash_backward_binned_workspace(int64_t max_samples) {
     return bin_ws_bytes((max_samples + TILE - 1) / TILE, nullptr, nullptr);
 }
 
-int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
-                             const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                             int64_t max_samples, int level_lo, void* stream) {
+// phase bit 1: count + scan + plan (xyzs / sample_idx only); bit 2: write +
+// accumulate (needs denc and the plan of the same inputs).
+static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                       const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                       int64_t max_samples, int level_lo, int phase, void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
     NGP_CHECK_ARG(n >= 0 && max_samples > 0);
     if (n == 0) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && denc && grad_table && workspace);
-    NGP_CHECK_ARG(((uintptr_t)workspace & 255) == 0 && ((uintptr_t)denc & 7) == 0 &&
-                  ((uintptr_t)grad_table & 15) == 0);
+    NGP_CHECK_ARG(xyzs && workspace && ((uintptr_t)workspace & 255) == 0);
+    if (phase & 2)
+        NGP_CHECK_ARG(denc && grad_table && ((uintptr_t)denc & 7) == 0 && ((uintptr_t)grad_table & 15) == 0);
     const int64_t tiles_cap = (max_samples + TILE - 1) / TILE;
     // record slots are uint32-indexed
     NGP_CHECK_ARG(tiles_cap * TILE * 4 * L < (int64_t)0xffffffffLL);
@@ -479,24 +484,49 @@ int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev,
     BinWs ws;
     bin_ws_bytes(tiles_cap, &ws, workspace);
     hipStream_t s = as_stream(stream);
-    static const unsigned capC = resident_blocks(hash_count_kernel, 256, 0);
-    static const unsigned capW = resident_blocks(hash_write_kernel<2>, 256, 0);
-    hash_count_kernel<<<persistent_blocks(n, TILE, capC), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, ws);
-    hash_scan_kernel<<<NSLOT, 256, 0, s>>>(n_dev, n, ba, ws);
-    hash_plan_kernel<<<1, MAXB, 0, s>>>(nbt, ws);
-    hash_write_kernel<2><<<persistent_blocks(n, TILE, capW), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, denc,
-                                                                       grad_table, ws);
-    static bool attr = false;
-    const size_t lds = (size_t)BENT * 2 * sizeof(double);
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)hash_accum_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds) != hipSuccess)
-            return NGP_ERANGE;
-        attr = true;
+    if (phase & 1) {
+        static const unsigned capC = resident_blocks(hash_count_kernel, 256, 0);
+        hash_count_kernel<<<persistent_blocks(n, TILE, capC), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, ws);
+        hash_scan_kernel<<<NSLOT, 256, 0, s>>>(n_dev, n, ba, ws);
+        hash_plan_kernel<<<1, MAXB, 0, s>>>(nbt, ws);
     }
-    static const unsigned capB = resident_blocks(hash_accum_kernel<0>, 1024, lds);
-    hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws);
+    if (phase & 2) {
+        static const unsigned capW = resident_blocks(hash_write_kernel<2>, 256, 0);
+        hash_write_kernel<2><<<persistent_blocks(n, TILE, capW), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba,
+                                                                           denc, grad_table, ws);
+        static bool attr = false;
+        const size_t lds = (size_t)BENT * 2 * sizeof(double);
+        if (!attr) {
+            if (hipFuncSetAttribute((const void*)hash_accum_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds) != hipSuccess)
+                return NGP_ERANGE;
+            attr = true;
+        }
+        static const unsigned capB = resident_blocks(hash_accum_kernel<0>, 1024, lds);
+        hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws);
+    }
     return ngp_launch_status();
+}
+
+int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                             const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                             int64_t max_samples, int level_lo, void* stream) {
+    return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo, 3,
+                       stream);
+}
+
+int ngp_hash_binned_plan(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                         const ngp_hashgrid_t* grid, void* workspace, int64_t max_samples, int level_lo,
+                         void* stream) {
+    return hash_binned(xyzs, n, n_dev, sample_idx, grid, nullptr, nullptr, workspace, max_samples, level_lo, 1,
+                       stream);
+}
+
+int ngp_hash_binned_apply(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                          const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                          int64_t max_samples, int level_lo, void* stream) {
+    return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo, 2,
+                       stream);
 }
 
 }  // extern "C"

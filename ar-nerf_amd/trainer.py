@@ -534,6 +534,18 @@ class NGPTrainer:
                                       _p(self.n_active_total), _p(self.sample_idx), s), "active_samples")
         self._ev("composite_loss", 1)
         at("after_composite")
+        cs = torch.cuda.current_stream()
+        hybrid = self.hash_backward != "atomic"
+        bs = self.bwd_stream if self.overlap_hash_bwd else cs
+        if hybrid:  # bucket plan of the binned fine levels (xyzs / sample_idx only) beside the MLP backward
+            bs.wait_stream(cs)
+            with torch.cuda.stream(bs):
+                vren._ok(HGL.ngp_hash_binned_plan(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                  _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
+                                                  _p(self.bin_ws), self.bin_max_samples, self.bin_level_lo,
+                                                  vren._stream()), "hash_binned_plan")
+                planned = torch.cuda.Event()
+                planned.record(bs)
         self._ev("mlp_bwd", 0)
         vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
                                             _p(self.enc), self.cap if self.split_forward else 0,
@@ -542,19 +554,20 @@ class NGPTrainer:
         self._ev("mlp_bwd", 1)
         at("after_mlp_bwd")
         self._ev("hash_bwd", 0)
-        if self.hash_backward != "atomic":
-            cs = torch.cuda.current_stream()
-            bs = self.bwd_stream if self.overlap_hash_bwd else cs
+        if hybrid:
+            # atomic coarse levels on the side stream (after the MLP backward),
+            # binned fine levels here (after the plan): disjoint gradient ranges
             bs.wait_stream(cs)
             with torch.cuda.stream(bs):
                 vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                       _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
                                                       _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), 0,
                                                       self.bin_level_lo, vren._stream()), "hash_backward_levels")
-            vren._ok(HGL.ngp_hash_backward_binned(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                  _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
-                                                  _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
-                                                  self.bin_level_lo, s), "hash_backward_binned")
+            cs.wait_event(planned)
+            vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                               _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
+                                               _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
+                                               self.bin_level_lo, s), "hash_binned_apply")
             cs.wait_stream(bs)
         else:
             vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),

@@ -267,6 +267,16 @@ size_t ngp_hash_backward_binned_workspace(int64_t max_samples);
 int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
                              int64_t max_samples, int level_lo, void* stream);
+/* ngp_hash_backward_binned in two phases on the same workspace and inputs:
+ * _plan (record counts, bucket regions: reads xyzs / sample_idx only, so it
+ * can run beside the MLP backward that produces denc) then _apply (records,
+ * LDS range sums, gradient). */
+int ngp_hash_binned_plan(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                         const ngp_hashgrid_t* grid, void* workspace, int64_t max_samples, int level_lo,
+                         void* stream);
+int ngp_hash_binned_apply(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                          const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                          int64_t max_samples, int level_lo, void* stream);
 /* ngp_hash_backward restricted to levels [level_lo, level_hi). */
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,

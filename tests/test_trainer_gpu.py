@@ -172,3 +172,25 @@ def test_chunked_forward_matches_full(first, table_init):
     assert ev1 <= n1
     if term and first == 8:  # some row stops early: its tail is never evaluated
         assert ev1 < n1
+
+
+def test_repeated_step_gradients_agree_per_level():
+    """The same step from the same state, repeated: every parameter group and
+    hash level agrees to fp32 atomic-order noise (a lost or duplicated
+    contribution -- e.g. an LDS race in the binned backward that shows only
+    when another kernel shares the CUs -- moves a level by percents)."""
+    import hashgrid as HG
+    grads = []
+    for _ in range(4):
+        sc, tr, img, pix, noise = _setup(table_init=2.0)
+        tr.chunk_first = 0
+        o, d = sc.rays(img, pix)
+        tr.step(img.to(DEV), pix.to(DEV), sc.gt_rgb_rays(o, d).to(DEV), sc.directions.to(DEV), sc.poses.to(DEV),
+                noise=noise.to(DEV), apply_adam=False)
+        torch.cuda.synchronize()
+        grads.append(tr.grad.clone())
+    off = [0, HG.MLP_PARAMS] + [HG.MLP_PARAMS + 2 * o for o in tr.grid.offsets[1:]]
+    for g in grads[1:]:
+        for a, b in zip(off[:-1], off[1:]):
+            ref = grads[0][a:b]
+            assert float((g[a:b] - ref).norm()) <= 1e-5 * float(ref.norm()) + 1e-12, (a, b)
