@@ -500,6 +500,85 @@ __global__ void __launch_bounds__(256) active_map_kernel(const int32_t* __restri
     for (int k = lane; k < na; k += 64) sample_idx[dst + k] = (int32_t)(src + k);
 }
 
+// Fused scan + map for batch-sized row counts (one launch instead of a
+// one-block scan and a map launch, both latency-bound on the step's critical
+// path).  Block b owns rows [b*SEG_ROWS, (b+1)*SEG_ROWS): it first sums the
+// counts of every row before its range itself (a redundant reduction over
+// L2-resident counts, so no block waits on another), then scans its own rows
+// in LDS and writes their sample indices.  CAP > 0: counts[r] = min(N_r, CAP)
+// read from rays_a (counts unused).  The last block publishes the total.
+constexpr int SEG_ROWS = 64, SEG_THREADS = 512;
+constexpr int64_t SEG_MAX_ROWS = 65536;  // beyond: scan + map launches (O(rows^2 / SEG_ROWS) reads here)
+
+template <bool CAPPED>
+__global__ void __launch_bounds__(SEG_THREADS) segments_kernel(const int32_t* __restrict__ counts,
+                                                               const int64_t* __restrict__ rays_a, int64_t n_rows,
+                                                               int cap, int first, int64_t* __restrict__ start_ws,
+                                                               int64_t* __restrict__ total,
+                                                               int64_t* __restrict__ total_acc,
+                                                               int32_t* __restrict__ sample_idx) {
+    __shared__ int64_t red[SEG_THREADS / 64];
+    __shared__ int32_t lofs[SEG_ROWS + 1];
+    __shared__ int64_t src[SEG_ROWS];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t r0 = (int64_t)blockIdx.x * SEG_ROWS, r1 = min(r0 + SEG_ROWS, n_rows);
+    auto count = [&](int64_t r) -> int64_t {
+        return CAPPED ? min(rays_a[3 * r + 2], (int64_t)cap) : (int64_t)counts[r];
+    };
+    // 1) prefix of the rows before this block
+    int64_t acc = 0;
+    for (int64_t r = t; r < r0; r += SEG_THREADS) acc += count(r);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) red[w] = acc;
+    // 2) own rows: exclusive scan in wave 0 (SEG_ROWS = 64 = one wave)
+    if (w == 0) {
+        const int64_t r = r0 + lane;
+        const int32_t c = r < r1 ? (int32_t)count(r) : 0;
+        int32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        lofs[lane] = x - c;
+        if (lane == 63) lofs[SEG_ROWS] = x;
+        src[lane] = r < r1 ? rays_a[3 * r + 1] + first : 0;
+    }
+    __syncthreads();
+    int64_t prefix = 0;
+#pragma unroll
+    for (int i = 0; i < SEG_THREADS / 64; ++i) prefix += red[i];
+    if (t < r1 - r0) start_ws[r0 + t] = prefix + lofs[t];
+    const int32_t nb = lofs[SEG_ROWS];
+    if (blockIdx.x == gridDim.x - 1 && t == 0) {
+        *total = prefix + nb;
+        if (total_acc) *total_acc += prefix + nb;
+    }
+    // 3) map: entry q of this block belongs to the row whose [lofs, lofs+c) holds it
+    for (int32_t q = t; q < nb; q += SEG_THREADS) {
+        int lo = 0, hi = SEG_ROWS;  // lofs[lo] <= q < lofs[hi]
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int mid = (lo + hi) >> 1;
+            if (lofs[mid] <= q) lo = mid; else hi = mid;
+        }
+        sample_idx[prefix + q] = (int32_t)(src[lo] + (q - lofs[lo]));
+    }
+}
+
+static void launch_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_rows, int cap, int first,
+                            int64_t* start_ws, int64_t* total, int64_t* total_acc, int32_t* sample_idx,
+                            hipStream_t s) {
+    const unsigned blocks = (unsigned)((n_rows + SEG_ROWS - 1) / SEG_ROWS);
+    if (cap > 0)
+        segments_kernel<true><<<blocks, SEG_THREADS, 0, s>>>(nullptr, rays_a, n_rows, cap, first, start_ws, total,
+                                                             total_acc, sample_idx);
+    else
+        segments_kernel<false><<<blocks, SEG_THREADS, 0, s>>>(counts, rays_a, n_rows, 0, first, start_ws, total,
+                                                              total_acc, sample_idx);
+}
+
 // ------------------------------------------- chunked forward (training)
 // The training step only ever reads a row's samples up to its termination
 // (composite_train_fw breaks there, the backward stops there), so the field
@@ -587,11 +666,31 @@ int ngp_ray_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_row
     NGP_CHECK_ARG(n_rows >= 0 && total && first >= 0);
     hipStream_t s = as_stream(stream);
     if (n_rows > 0) NGP_CHECK_ARG(counts && rays_a && start_ws && sample_idx);
+    if (n_rows > 0 && n_rows <= SEG_MAX_ROWS) {
+        launch_segments(counts, rays_a, n_rows, 0, first, start_ws, total, total_acc, sample_idx, s);
+        return ngp_launch_status();
+    }
     active_scan_kernel<<<1, 1024, 0, s>>>(counts, n_rows, start_ws, total, total_acc);
     if (n_rows > 0)
         active_map_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, s>>>(counts, rays_a, start_ws, n_rows, sample_idx,
                                                                       first);
     return ngp_launch_status();
+}
+
+int ngp_ray_segments_capped(const int64_t* rays_a, int64_t n_rows, int cap, int64_t* start_ws, int64_t* total,
+                            int64_t* total_acc, int32_t* sample_idx, void* stream) {
+    NGP_CHECK_ARG(n_rows >= 0 && total && cap >= 1);
+    hipStream_t s = as_stream(stream);
+    if (n_rows == 0) {
+        active_scan_kernel<<<1, 1024, 0, s>>>(nullptr, 0, start_ws, total, total_acc);  // total = 0
+        return ngp_launch_status();
+    }
+    NGP_CHECK_ARG(rays_a && start_ws && sample_idx);
+    if (n_rows <= SEG_MAX_ROWS) {
+        launch_segments(nullptr, rays_a, n_rows, cap, 0, start_ws, total, total_acc, sample_idx, s);
+        return ngp_launch_status();
+    }
+    return NGP_ERANGE;
 }
 
 int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16, int64_t n,
@@ -689,6 +788,11 @@ int ngp_active_samples(const int32_t* n_active, const int64_t* rays_a, int64_t n
     NGP_CHECK_ARG(n_rows >= 0 && n_active_total);
     hipStream_t s = as_stream(stream);
     if (n_rows > 0) NGP_CHECK_ARG(n_active && rays_a && act_start_ws && sample_idx);
+    if (n_rows > 0 && n_rows <= SEG_MAX_ROWS) {
+        NGP_CHECK_ARG(n_active && rays_a && act_start_ws && sample_idx);
+        launch_segments(n_active, rays_a, n_rows, 0, 0, act_start_ws, n_active_total, nullptr, sample_idx, s);
+        return ngp_launch_status();
+    }
     active_scan_kernel<<<1, 1024, 0, s>>>(n_active, n_rows, act_start_ws, n_active_total);
     if (n_rows > 0)
         active_map_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, s>>>(n_active, rays_a, act_start_ws, n_rows,

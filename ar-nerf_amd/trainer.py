@@ -503,10 +503,14 @@ class NGPTrainer:
                      "field_mlp_forward")
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
-            vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, None, None, ctypes_float(1e-4), _p(self.eval_counts),
-                                        s), "chunk_counts")
-            vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, 0, _p(self.act_start),
-                                        _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
+            if R <= 65536:  # counts min(N_r, K) + scan + list in one launch
+                vren._ok(L.ngp_ray_segments_capped(_p(self.rays_a), R, K, _p(self.act_start), _p(self.eval_total),
+                                                   _p(self.stats[3:]), _p(self.eval_idx), s), "segments_capped")
+            else:
+                vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, None, None, ctypes_float(1e-4),
+                                            _p(self.eval_counts), s), "chunk_counts")
+                vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, 0, _p(self.act_start),
+                                            _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
             self._field_indexed(s)
             vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, _p(self.sigmas), _p(self.deltas), ctypes_float(1e-4),
                                         _p(self.eval_counts), s), "chunk_counts")

@@ -336,6 +336,11 @@ int ngp_chunk_counts(const int64_t* rays_a, int64_t n_rows, int first, const flo
 int ngp_ray_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_rows, int first,
                      int64_t* start_ws, int64_t* total, int64_t* total_acc, int32_t* sample_idx,
                      void* stream);
+/* ngp_ray_segments of each row's first min(N_r, cap) samples (counts read
+ * from rays_a: chunked evaluation round 1 in one launch).  NGP_ERANGE above
+ * 65536 rows (use ngp_chunk_counts + ngp_ray_segments there). */
+int ngp_ray_segments_capped(const int64_t* rays_a, int64_t n_rows, int cap, int64_t* start_ws, int64_t* total,
+                            int64_t* total_acc, int32_t* sample_idx, void* stream);
 
 /* apex FusedAdam step (train.py:146; weight decay 0) over n (multiple of 4)
  * fp32 params with grad *= grad_scale, bias corrections for `step` (1-based);

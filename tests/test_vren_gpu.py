@@ -263,3 +263,53 @@ def test_device_occupancy_sampling():
     cnt.zero_()
     _, f3 = draw(lst, cnt)
     assert bool((f3[M:] == -1).all()) and torch.equal(f3[:M], f[:M])
+
+
+@pytest.mark.parametrize("n_rows", [1, 63, 64, 8192, 8193, 70000])
+def test_ray_segments_lists(n_rows):
+    """ngp_ray_segments / ngp_active_samples / ngp_ray_segments_capped (fused
+    scan + map up to 65536 rows, scan + map launches above): start offsets,
+    totals and index lists equal a torch cumsum / repeat_interleave, incl.
+    empty rows."""
+    import ctypes
+    L = vren.lib()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    g = torch.Generator().manual_seed(n_rows)
+    N = torch.randint(0, 200, (n_rows,), generator=g)
+    N[torch.rand(n_rows, generator=g) < 0.2] = 0
+    start = torch.cumsum(N, 0) - N
+    rays_a = torch.stack([torch.arange(n_rows), start, N], 1).to(DEV)
+    first = 5
+    counts = torch.clamp(N - first, min=0).to(torch.int32)
+
+    def expect(c, off):
+        c64 = c.long()
+        st = torch.cumsum(c64, 0) - c64
+        idx = torch.repeat_interleave(start + off, c64) + (torch.arange(int(c64.sum())) -
+                                                            torch.repeat_interleave(st, c64))
+        return st, int(c64.sum()), idx
+
+    st_ws = torch.empty(n_rows, dtype=torch.int64, device=DEV)
+    tot = torch.zeros(1, dtype=torch.int64, device=DEV)
+    acc = torch.full((1,), 7, dtype=torch.int64, device=DEV)
+    sidx = torch.full((int(N.sum()) + 1,), -1, dtype=torch.int32, device=DEV)
+    cd = counts.to(DEV)
+    vren._ok(L.ngp_ray_segments(p(cd), p(rays_a), n_rows, first, p(st_ws), p(tot), p(acc), p(sidx), vren._stream()),
+             "segments")
+    st, total, idx = expect(counts, first)
+    assert torch.equal(st_ws.cpu(), st) and int(tot) == total and int(acc) == 7 + total
+    assert torch.equal(sidx[:total].cpu().long(), idx)
+    # active samples: offset 0, no accumulator
+    vren._ok(L.ngp_active_samples(p(cd), p(rays_a), n_rows, p(st_ws), p(tot), p(sidx), vren._stream()), "active")
+    st, total, idx = expect(counts, 0)
+    assert int(tot) == total and torch.equal(sidx[:total].cpu().long(), idx)
+    # capped (round 1 of the chunked forward)
+    K = 64
+    rc = L.ngp_ray_segments_capped(p(rays_a), n_rows, K, p(st_ws), p(tot), None, p(sidx), vren._stream())
+    if n_rows > 65536:
+        assert rc != 0
+        return
+    vren._ok(rc, "capped")
+    st, total, idx = expect(torch.clamp(N, max=K), 0)
+    assert torch.equal(st_ws.cpu(), st) and int(tot) == total
+    assert torch.equal(sidx[:total].cpu().long(), idx)
