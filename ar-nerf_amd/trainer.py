@@ -116,6 +116,9 @@ class NGPTrainer:
         # memory-side atomics vs LDS-bound passes overlap)
         self.bwd_stream = torch.cuda.Stream(device=dev)
         self.overlap_hash_bwd = os.environ.get("NGP_BWD_OVERLAP", "1") == "1"
+        # NGP_ADAM_SPLIT=1: Adam of the MLP + coarse levels beside the binned
+        # levels (measured slower: it takes HBM bandwidth from the apply)
+        self.adam_split = os.environ.get("NGP_ADAM_SPLIT", "0") == "1"
         self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "0") == "1"
         self.enc = torch.empty(8 * cap * 4, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
@@ -567,12 +570,27 @@ class NGPTrainer:
                                                       _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
                                                       _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), 0,
                                                       self.bin_level_lo, vren._stream()), "hash_backward_levels")
+                # single process: Adam of the MLP + coarse levels here too, beside
+                # the binned levels (no all-reduce orders it after the whole grad)
+                split = HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
+                adam_split = self.adam_split and apply_adam and self.world == 1 and bs is not cs
+                if adam_split:
+                    self._adam(0, split, vren._stream())
             cs.wait_event(planned)
             vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
                                                _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
                                                self.bin_level_lo, s), "hash_binned_apply")
+            if adam_split:
+                self._ev("adam", 0)
+                self._adam(split, self.params.numel(), s)
+                self._ev("adam", 1)
             cs.wait_stream(bs)
+            if adam_split:
+                self._ev("hash_bwd", 1)
+                self._ev("allreduce", 0)  # (no all-reduce: one process)
+                self._ev("allreduce", 1)
+                return self.out_loss
         else:
             vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
                                            HG.ctypes.byref(self.grid.desc),
@@ -584,14 +602,19 @@ class NGPTrainer:
         if not apply_adam:  # (tests) leave the summed gradient in self.grad
             return self.out_loss
         self._ev("adam", 0)
-        # lr and the step count from device memory (graph replays); dctr[0] =
-        # steps taken so far, advanced after the step by ngp_counters_inc
-        vren._ok(L.ngp_adam_step_dev(_p(self.params), _p(self.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
-                                     _p(self.params16), self.params.numel(), _p(self.lr_dev), ctypes_float(0.9),
-                                     ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
-                                     ctypes_float(1.0 / self.world), 1, s), "adam")
+        self._adam(0, self.params.numel(), s)
         self._ev("adam", 1)
         return self.out_loss
+
+    def _adam(self, lo, hi, s):
+        """FusedAdam over params[lo:hi] (16-byte aligned bounds).  lr and the
+        step count from device memory (graph replays); dctr[0] = steps taken
+        so far, advanced after the step by ngp_counters_inc."""
+        q = lambda t: _p(t[lo:hi])  # noqa: E731
+        vren._ok(self.L.ngp_adam_step_dev(q(self.params), q(self.grad), q(self.exp_avg), q(self.exp_avg_sq),
+                                          q(self.params16), hi - lo, _p(self.lr_dev), ctypes_float(0.9),
+                                          ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                                          ctypes_float(1.0 / self.world), 1, s), "adam")
 
     def _field_indexed(self, s):
         HGL = HG._lib()
