@@ -393,6 +393,145 @@ __global__ void __launch_bounds__(256) occ_sample_kernel(uint64_t seed, const in
     flat[o] = (int64_t)cascade * G * G * G + idx;
 }
 
+// Sorted variant: the same two multisets of cells (M i.i.d. uniform cells, M
+// i.i.d. uniform picks from the occupied list) emitted in ascending order, so
+// that a wave's points share cache lines on the coarse hash levels (the
+// density forward of the 1M points runs ~1.8x faster Morton-sorted than in
+// draw order: scripts/diag/density_order.py).  Ascending i.i.d. uniforms are
+// drawn directly as order statistics, U_(k) = S_k / S_M with S the running
+// sum of M+1 i.i.d. Exp(1) variates (fp64), so no sort is needed: three
+// launches -- block sums, one scan of the block sums, then each block
+// regenerates its exponentials, scans them and writes its samples.
+constexpr int OSC_T = 256, OSC_PER = 16, OSC_CH = OSC_T * OSC_PER;  // exponentials per block
+
+__device__ __forceinline__ double occ_exp(uint64_t seed, uint64_t step, int cascade, int half, int64_t k) {
+    const uint4 v = philox4x32(make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)step,
+                                          0x7F4A7C15u ^ (uint32_t)(cascade << 1) ^ (uint32_t)half),
+                               make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    const double u = ((double)(v.x >> 11) + 1.0) * (1.0 / 2097152.0);  // (0, 1], 21 bits
+    const double u2 = u + (double)(v.y >> 11) * (1.0 / 2097152.0 / 2097152.0);  // 42-bit uniform
+    return -log(fmin(u2, 1.0));
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(OSC_T) occ_exp_sums_kernel(uint64_t seed, const int64_t* __restrict__ ctr,
+                                                             int cascade, int64_t M, int64_t nb,
+                                                             double* __restrict__ sums) {
+    __shared__ double red[OSC_T / 64];
+    const int half = (int)(blockIdx.x / nb);
+    const int64_t c = blockIdx.x % nb;
+    const uint64_t step = (uint64_t)*ctr;
+    double v = 0.0;
+#pragma unroll 4
+    for (int j = 0; j < OSC_PER; ++j) {
+        const int64_t k = c * OSC_CH + (int64_t)j * OSC_T + threadIdx.x;
+        if (k <= M) v += occ_exp(seed, step, cascade, half, k);
+    }
+    v = block_sum_d(v, red);
+    if (threadIdx.x == 0) sums[blockIdx.x] = v;
+}
+
+// exclusive prefix of the block sums within each half (in place), totals
+// after; one workgroup per half, 1024 sums per round
+__global__ void __launch_bounds__(1024) occ_exp_scan_kernel(int64_t nb, double* __restrict__ sums) {
+    __shared__ double wsum[16];
+    __shared__ double carry_s;
+    double* p = sums + blockIdx.x * nb;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) carry_s = 0.0;
+    __syncthreads();
+    for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
+        const int64_t b = b0 + t;
+        const double v = b < nb ? p[b] : 0.0;
+        double incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        double before = carry_s;
+        for (int q = 0; q < w; ++q) before += wsum[q];
+        if (b < nb) p[b] = before + incl - v;
+        __syncthreads();
+        if (t == 1023) carry_s = before + incl;
+        __syncthreads();
+    }
+    if (t == 0) sums[2 * nb + blockIdx.x] = carry_s;
+}
+
+__global__ void __launch_bounds__(OSC_T) occ_sample_sorted_kernel(
+    uint64_t seed, const int64_t* __restrict__ ctr, int cascade, int G, int64_t M, int64_t nb, float s_minus_hgs,
+    float hgs, const int32_t* __restrict__ list, const unsigned long long* __restrict__ count,
+    const double* __restrict__ sums, int64_t lo, int64_t hi, float* __restrict__ xyzs, int64_t* __restrict__ flat) {
+    __shared__ double wsum[OSC_T / 64];
+    const int half = (int)(blockIdx.x / nb);
+    const int64_t c = blockIdx.x % nb;
+    const int64_t i0 = half * M + c * OSC_CH;  // sample index of this block's first exponential
+    if (i0 >= hi || i0 + OSC_CH <= lo) return;  // (block-uniform)
+    const uint64_t step = (uint64_t)*ctr;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // thread t takes the OSC_PER consecutive exponentials k0 + t*OSC_PER + j
+    const int64_t k0 = c * OSC_CH + (int64_t)t * OSC_PER;
+    double e[OSC_PER], loc = 0.0;
+#pragma unroll
+    for (int j = 0; j < OSC_PER; ++j) {
+        e[j] = k0 + j <= M ? occ_exp(seed, step, cascade, half, k0 + j) : 0.0;
+        loc += e[j];
+    }
+    double incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    double run = sums[blockIdx.x];
+    for (int q = 0; q < w; ++q) run += wsum[q];
+    run += incl - loc;
+    const double inv_tot = 1.0 / sums[2 * nb + half];
+    const unsigned long long cnt = half ? *count : 0ull;
+    const float gm1 = (float)(G - 1);
+    const int64_t n_cells = (int64_t)G * G * G;
+#pragma unroll 1
+    for (int j = 0; j < OSC_PER; ++j) {
+        run += e[j];
+        const int64_t k = k0 + j, i = half * M + k;
+        if (k >= M || i < lo || i >= hi) continue;
+        const int64_t o = i - lo;
+        const double u = run * inv_tot;  // U_(k), ascending in k
+        int32_t idx;
+        if (!half) {
+            idx = (int32_t)min((int64_t)(u * (double)n_cells), n_cells - 1);
+        } else {
+            if (cnt == 0) {
+                flat[o] = -1;
+                xyzs[3 * o] = 0.f; xyzs[3 * o + 1] = 0.f; xyzs[3 * o + 2] = 0.f;
+                continue;
+            }
+            idx = list[min((int64_t)(u * (double)cnt), (int64_t)cnt - 1)];
+        }
+        const uint4 r = philox4x32(make_uint4((uint32_t)i, (uint32_t)(i >> 32), (uint32_t)step, (uint32_t)cascade),
+                                   make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+        const uint32_t cc[3] = {compact3((uint32_t)idx), compact3((uint32_t)idx >> 1), compact3((uint32_t)idx >> 2)};
+        const float jr[3] = {(float)(r.x >> 8) * (1.0f / 16777216.0f), (float)(r.y >> 8) * (1.0f / 16777216.0f),
+                             (float)(r.z >> 8) * (1.0f / 16777216.0f)};
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            xyzs[3 * o + d] = ((float)cc[d] / gm1 * 2.0f - 1.0f) * s_minus_hgs + (jr[d] * 2.0f - 1.0f) * hgs;
+        flat[o] = (int64_t)cascade * n_cells + idx;
+    }
+}
+
 // models/networks.py:273-278: grid = where(grid<0, grid, max(grid*decay, tmp));
 // accumulates sum and count of grid > 0 for the mean, in fp64 so the mean is
 // the correctly rounded one whatever the summation order: at initialisation
@@ -766,6 +905,31 @@ int ngp_occupancy_samples(uint64_t seed, const int64_t* counter_dev, int cascade
     occ_sample_kernel<<<(unsigned)((hi - lo + 255) / 256), 256, 0, as_stream(stream)>>>(
         seed, counter_dev, cascade, grid_size, M, s_minus_hgs, hgs, occ_list, (const unsigned long long*)occ_count, lo,
         hi, xyzs, flat_idx);
+    return ngp_launch_status();
+}
+
+size_t ngp_occupancy_sorted_workspace(int64_t M) {
+    const int64_t nb = (M + 1 + OSC_CH - 1) / OSC_CH;
+    return (size_t)(2 * nb + 2) * sizeof(double);
+}
+
+int ngp_occupancy_samples_sorted(uint64_t seed, const int64_t* counter_dev, int cascade, int grid_size, int64_t M,
+                                 float s_minus_hgs, float hgs, const int32_t* occ_list, const int64_t* occ_count,
+                                 int64_t lo, int64_t hi, void* workspace, float* xyzs, int64_t* flat_idx,
+                                 void* stream) {
+    NGP_CHECK_ARG(counter_dev && occ_list && occ_count && xyzs && flat_idx && workspace && grid_size >= 2 &&
+                  M >= 0 && lo >= 0 && lo <= hi && hi <= 2 * M && cascade >= 0 && ((uintptr_t)workspace & 7) == 0);
+    if (hi == lo) return NGP_OK;
+    NGP_CHECK_ARG((int64_t)grid_size * grid_size * grid_size <= (1ll << 31));
+    hipStream_t s = as_stream(stream);
+    const int64_t nb = (M + 1 + OSC_CH - 1) / OSC_CH;
+    double* sums = reinterpret_cast<double*>(workspace);
+    occ_exp_sums_kernel<<<(unsigned)(2 * nb), OSC_T, 0, s>>>(seed, counter_dev, cascade, M, nb, sums);
+    occ_exp_scan_kernel<<<2, 1024, 0, s>>>(nb, sums);
+    occ_sample_sorted_kernel<<<(unsigned)(2 * nb), OSC_T, 0, s>>>(seed, counter_dev, cascade, grid_size, M, nb,
+                                                                 s_minus_hgs, hgs, occ_list,
+                                                                 (const unsigned long long*)occ_count, sums, lo, hi,
+                                                                 xyzs, flat_idx);
     return ngp_launch_status();
 }
 

@@ -87,6 +87,10 @@ class NGPTrainer:
         self._occ_xyz = torch.empty(M2, 3, device=dev)
         self._occ_flat = torch.empty(M2, dtype=torch.int64, device=dev)
         self._occ_sig = torch.empty(M2, device=dev)
+        # NGP_OCC_SORTED=0: cells in draw order (ngp_occupancy_samples)
+        self.occ_sorted = os.environ.get("NGP_OCC_SORTED", "1") == "1"
+        self._occ_ws = torch.empty((vren.lib().ngp_occupancy_sorted_workspace(M2 // 2) + 7) // 8, dtype=torch.float64,
+                                   device=dev)
         self.threshold = torch.zeros(2, device=dev)
         # ---- per-step buffers
         R = batch_size
@@ -252,10 +256,14 @@ class NGPTrainer:
                                               _p(self._occ_list), _p(self._occ_count), s), "occupied_cells")
                 lo, hi = ddp.shard_range(2 * M, self.rank, self.world)
                 n = hi - lo
-                vren._ok(L.ngp_occupancy_samples(self.sample_seed ^ 0x5DEECE66D, _p(self.dctr[2:]), c, G, M,
-                                                 ctypes_float(sc - half_grid_size), ctypes_float(half_grid_size),
-                                                 _p(self._occ_list), _p(self._occ_count), lo, hi,
-                                                 _p(self._occ_xyz), _p(self._occ_flat), s), "occupancy_samples")
+                args = (self.sample_seed ^ 0x5DEECE66D, _p(self.dctr[2:]), c, G, M, ctypes_float(sc - half_grid_size),
+                        ctypes_float(half_grid_size), _p(self._occ_list), _p(self._occ_count), lo, hi)
+                if self.occ_sorted:  # ascending cells: the density forward's waves stay cache-local
+                    vren._ok(L.ngp_occupancy_samples_sorted(*args, _p(self._occ_ws), _p(self._occ_xyz),
+                                                            _p(self._occ_flat), s), "occupancy_samples_sorted")
+                else:
+                    vren._ok(L.ngp_occupancy_samples(*args, _p(self._occ_xyz), _p(self._occ_flat), s),
+                             "occupancy_samples")
                 vren._ok(HG._lib().ngp_density_forward(_p(self._occ_xyz), n, None, HG.ctypes.byref(self.grid.desc),
                                                        _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16),
                                                        _p(self._occ_sig), None, s), "density_forward")

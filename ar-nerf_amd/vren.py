@@ -48,6 +48,8 @@ def _declare(L):
         "ngp_occupied_cells": [vp, c_int64, c_float, vp, vp, vp],
         "ngp_occupancy_samples": [ctypes.c_uint64, vp, c_int, c_int, c_int64, c_float, c_float, vp, vp, c_int64,
                                   c_int64, vp, vp, vp],
+        "ngp_occupancy_samples_sorted": [ctypes.c_uint64, vp, c_int, c_int, c_int64, c_float, c_float, vp, vp,
+                                         c_int64, c_int64, vp, vp, vp, vp],
         "ngp_morton3d": [vp, c_int64, vp, vp],
         "ngp_morton3d_invert": [vp, c_int64, vp, vp],
         "ngp_packbits": [vp, c_int64, c_float, vp, vp, vp],
@@ -81,6 +83,8 @@ def _declare(L):
     L.ngp_version.restype = ctypes.c_char_p
     L.ngp_hashgrid_levels.argtypes = [c_int, c_int, c_int, c_float, vp, vp, vp, vp]
     L.ngp_hashgrid_levels.restype = ctypes.c_uint32
+    L.ngp_occupancy_sorted_workspace.argtypes = [c_int64]
+    L.ngp_occupancy_sorted_workspace.restype = ctypes.c_size_t
 
 
 def lib():

@@ -62,7 +62,7 @@ PEAK = {"hbm": 8000.0, "mfma": 2500.0}  # MI355X: HBM3E GB/s; dense fp16 MFMA TF
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=800)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--pretrain", type=int, default=2000, help="untimed setup training steps (steady-state occupancy)")
     ap.add_argument("--batch", type=int, default=8192)

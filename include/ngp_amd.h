@@ -387,6 +387,17 @@ int ngp_occupied_cells(const float* grid_cascade, int64_t n_cells, float thresho
 int ngp_occupancy_samples(uint64_t seed, const int64_t* counter_dev, int cascade, int grid_size, int64_t M,
                           float s_minus_hgs, float hgs, const int32_t* occ_list, const int64_t* occ_count,
                           int64_t lo, int64_t hi, float* xyzs, int64_t* flat_idx, void* stream);
+/* ngp_occupancy_samples with each half's cells in ascending order (uniform
+ * half: Morton order; occupied half: list order), so the density forward's
+ * waves stay local: the same two multisets in distribution (M i.i.d. uniform
+ * cells, M i.i.d. picks from the list), drawn as order statistics (running
+ * sums of Exp(1) variates); other randoms as ngp_occupancy_samples.
+ * workspace: ngp_occupancy_sorted_workspace(M) bytes, 8-byte aligned. */
+size_t ngp_occupancy_sorted_workspace(int64_t M);
+int ngp_occupancy_samples_sorted(uint64_t seed, const int64_t* counter_dev, int cascade, int grid_size, int64_t M,
+                                 float s_minus_hgs, float hgs, const int32_t* occ_list, const int64_t* occ_count,
+                                 int64_t lo, int64_t hi, void* workspace, float* xyzs, int64_t* flat_idx,
+                                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -215,11 +215,14 @@ def test_check_input_errors_like_reference():
         vren.morton3D(y)
 
 
-def test_device_occupancy_sampling():
+@pytest.mark.parametrize("sorted_", [False, True])
+def test_device_occupancy_sampling(sorted_):
     """ngp_occupied_cells lists exactly the cells above the threshold;
     ngp_occupancy_samples draws M uniform + M occupied cells (none when the
     list is empty) with positions inside the jittered cell (networks.py:
-    181-207, 262-266), a pure function of the device counter."""
+    181-207, 262-266), a pure function of the device counter.  The sorted
+    variant emits each half in ascending order with the same distribution:
+    the empirical CDFs stay within a DKW band of the uniform ones."""
     import ctypes
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     L = vren.lib()
@@ -241,9 +244,15 @@ def test_device_occupancy_sampling():
     xyz = torch.empty(2 * M, 3, device=DEV)
     flat = torch.empty(2 * M, dtype=torch.int64, device=DEV)
 
+    ws = torch.empty((L.ngp_occupancy_sorted_workspace(M) + 7) // 8, dtype=torch.float64, device=DEV)
+
     def draw(c_lst, c_cnt, lo=0, hi=2 * M):
-        vren._ok(L.ngp_occupancy_samples(99, p(ctr), 0, G, M, s - hgs, hgs, p(c_lst), p(c_cnt), lo, hi, p(xyz),
-                                         p(flat), vren._stream()), "samples")
+        if sorted_:
+            vren._ok(L.ngp_occupancy_samples_sorted(99, p(ctr), 0, G, M, s - hgs, hgs, p(c_lst), p(c_cnt), lo, hi,
+                                                    p(ws), p(xyz), p(flat), vren._stream()), "samples_sorted")
+        else:
+            vren._ok(L.ngp_occupancy_samples(99, p(ctr), 0, G, M, s - hgs, hgs, p(c_lst), p(c_cnt), lo, hi, p(xyz),
+                                             p(flat), vren._stream()), "samples")
         return xyz[:hi - lo].clone(), flat[:hi - lo].clone()
 
     x, f = draw(lst, cnt)
@@ -256,6 +265,15 @@ def test_device_occupancy_sampling():
     assert float((x - centre).abs().max()) <= hgs + 4e-7  # a few fp32 ulps at |x| <= 0.5
     # uniform half: roughly uniform over cells
     assert abs(float(occ[f[:M]].float().mean()) - n / G ** 3) < 0.01
+    if sorted_:
+        pos = torch.empty(G ** 3, dtype=torch.int64, device=DEV)
+        pos[lst[:n].long()] = torch.arange(n, device=DEV)
+        lp = pos[f[M:]]  # list positions of the occupied half
+        assert bool((f[1:M] >= f[:M - 1]).all()) and bool((lp[1:] >= lp[:-1]).all())
+        k = (torch.arange(M, device=DEV, dtype=torch.float64) + 0.5) / M
+        band = 2.0 / M ** 0.5  # DKW: P(sup|F_M - F| > 2/sqrt(M)) = 2 exp(-8) ~ 7e-4
+        assert float((f[:M].double() / G ** 3 - k).abs().max()) < band + 1.0 / G ** 3
+        assert float((lp.double() / n - k).abs().max()) < band + 1.0 / n
     # shards of the same draw are slices of it
     x2, f2 = draw(lst, cnt, lo=1000, hi=5000)
     assert torch.equal(f2, f[1000:5000]) and torch.equal(x2, x[1000:5000])
