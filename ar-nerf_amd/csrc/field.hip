@@ -56,6 +56,38 @@ struct __attribute__((aligned(4))) u2a4 {
     __device__ operator uint2() const { return make_uint2(x, y); }
 };
 
+__device__ __forceinline__ uint32_t pick4(uint4 q, uint32_t k) {
+    return k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
+}
+
+// The two entries i0 (corner x) and i1 (corner x+1) of one y/z pair of a
+// level's table tl.  Dense levels: always neighbours, one 8-byte load.
+// Hashed levels (x term of the hash is px*1, size a power of two): i1 =
+// i0 ^ (px ^ (px+1)), so both sit in one aligned 4-entry group unless px = 3
+// mod 4 -- one 16-byte load for 3 of 4 pairs, plus a 4-byte load otherwise
+// (the gather cost is per lane request, not per byte).
+__device__ __forceinline__ void fetch_pair(const uint32_t* __restrict__ tl, uint32_t i0, uint32_t i1, bool dense,
+                                           uint32_t& v0, uint32_t& v1) {
+    const uint32_t lo = min(i0, i1), hi = max(i0, i1);
+    uint32_t vlo, vhi;
+    if (dense) {
+        const bool adj = hi - lo == 1u;
+        const uint2 pr = *reinterpret_cast<const u2a4*>(tl + (adj ? lo : (lo & ~1u)));
+        vlo = adj ? pr.x : ((lo & 1u) ? pr.y : pr.x);
+        vhi = pr.y;
+        if (!adj) vhi = tl[hi];
+    } else {
+        const uint4 q = *reinterpret_cast<const uint4*>(tl + (lo & ~3u));
+        const bool near = (hi ^ lo) < 4u;
+        uint32_t vfar = 0u;
+        if (!near) vfar = tl[hi];  // (the branch only issues the load: no wait inside it)
+        vlo = pick4(q, lo & 3u);
+        vhi = near ? pick4(q, hi & 3u) : vfar;
+    }
+    v0 = i0 < i1 ? vlo : vhi;
+    v1 = i0 < i1 ? vhi : vlo;
+}
+
 // Hash-encode level l of one sample: the two features (fp32 accumulation,
 // rounded once to fp16 by the caller).
 __device__ __forceinline__ void encode_level(const float in[3], int l, const LevelLds& lv,
@@ -89,16 +121,9 @@ __device__ __forceinline__ void encode_level(const float in[3], int l, const Lev
         const uint32_t qy = pg[1] + (yz & 1), qz = pg[2] + (yz >> 1);
         const uint32_t i0 = corner_index(pg[0], qy, qz, res, size, dense, pow2);
         const uint32_t i1 = corner_index(pg[0] + 1, qy, qz, res, size, dense, pow2);
-        const uint32_t lo = min(i0, i1), hi = max(i0, i1);
-        const bool adj = hi - lo == 1u;
-        // adjacent: the (4-byte aligned) pair at lo; else the aligned pair
-        // holding lo (level sizes are even, so it stays inside the level)
-        const uint2 pr = *reinterpret_cast<const u2a4*>(table + off + (adj ? lo : (lo & ~1u)));
-        const uint32_t vlo = adj ? pr.x : ((lo & 1u) ? pr.y : pr.x);
-        uint32_t vhi = pr.y;
-        if (!adj) vhi = table[off + hi];
-        v[2 * yz] = i0 < i1 ? vlo : vhi;
-        v[2 * yz + 1] = i0 < i1 ? vhi : vlo;
+        // (level sizes are multiples of 4 and offsets of 8 entries: the
+        // aligned groups stay inside the level)
+        fetch_pair(table + off, i0, i1, dense || !pow2, v[2 * yz], v[2 * yz + 1]);
     }
     a0 = 0.f;
     a1 = 0.f;
@@ -359,16 +384,7 @@ __device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& 
     uint32_t v[8];
     const uint32_t* tl = table + u.off;
 #pragma unroll
-    for (int yz = 0; yz < 4; ++yz) {
-        const uint32_t lo = min(i0[yz], i1[yz]), hi = max(i0[yz], i1[yz]);
-        const bool adj = hi - lo == 1u;
-        const uint2 pr = *reinterpret_cast<const u2a4*>(tl + (adj ? lo : (lo & ~1u)));
-        const uint32_t vlo = adj ? pr.x : ((lo & 1u) ? pr.y : pr.x);
-        uint32_t vhi = pr.y;
-        if (!adj) vhi = tl[hi];
-        v[2 * yz] = i0[yz] < i1[yz] ? vlo : vhi;
-        v[2 * yz + 1] = i0[yz] < i1[yz] ? vhi : vlo;
-    }
+    for (int yz = 0; yz < 4; ++yz) fetch_pair(tl, i0[yz], i1[yz], u.dense || !u.pow2, v[2 * yz], v[2 * yz + 1]);
     a0 = 0.f;
     a1 = 0.f;
 #pragma unroll
@@ -380,24 +396,39 @@ __device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& 
     }
 }
 
+// ALL = true (the product path): each lane encodes every level of one
+// sample, so a wave instruction gathers ONE level for 64 consecutive samples
+// (a ray's neighbours: shared lines on the coarse levels) -- measured 1.55x
+// the rate of one level pair per XCD (ALL = false, kept for diagnostics:
+// NGP_ENCODE_XCD=1) and 1.8x the fused kernel's lane (sample, level group)
+// layout (scripts/diag/encode_split.py).  sidx (nullable): rows j < N encode
+// sample sidx[j] (rows of enc_pm are samples).
+template <bool ALL>
 __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restrict__ xyzs, int64_t n,
-                                                          const int64_t* __restrict__ n_dev, GridArgs ga,
+                                                          const int64_t* __restrict__ n_dev,
+                                                          const int32_t* __restrict__ sidx, GridArgs ga,
                                                           const uint32_t* __restrict__ table,
                                                           _Float16* __restrict__ enc_pm) {
     __shared__ LevelLds lv;
     load_levels(ga, lv);
     __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
-    const int pr = blockIdx.x & 7;
-    const LevelU u0 = level_u(lv, 2 * pr), u1 = level_u(lv, 2 * pr + 1);
-    const int64_t nb = gridDim.x >> 3;
-    for (int64_t i = (int64_t)(blockIdx.x >> 3) * blockDim.x + threadIdx.x; i < N; i += nb * blockDim.x) {
+    const int p0 = ALL ? 0 : blockIdx.x & 7;
+    const int64_t nb = ALL ? gridDim.x : gridDim.x >> 3;
+    const int64_t b = ALL ? blockIdx.x : blockIdx.x >> 3;
+    for (int64_t j = b * blockDim.x + threadIdx.x; j < N; j += nb * blockDim.x) {
+        const int64_t i = sidx ? (int64_t)sidx[j] : j;
         float in[3];
         load_x01(xyzs, i, true, ga, in);
-        float a0, a1, b0, b1;
-        encode_level_u(in, u0, table, a0, a1);
-        encode_level_u(in, u1, table, b0, b1);
-        *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) = h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
+#pragma unroll 1
+        for (int pr = p0; pr < (ALL ? 8 : p0 + 1); ++pr) {
+            const LevelU u0 = level_u(lv, 2 * pr), u1 = level_u(lv, 2 * pr + 1);
+            float a0, a1, b0, b1;
+            encode_level_u(in, u0, table, a0, a1);
+            encode_level_u(in, u1, table, b0, b1);
+            *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) =
+                h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
+        }
     }
 }
 
@@ -794,6 +825,7 @@ int ngp_field_forward(const float* xyzs, const float* dirs, int64_t n, const int
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && dirs && table_f16 && mlp_f16 && sigmas && rgbs);
+    NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0);  // 16-byte group gathers
     NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
     static const unsigned cap = resident_blocks(field_fwd_kernel<true>, 256, 0);
     field_fwd_kernel<true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
@@ -811,6 +843,7 @@ int ngp_field_forward_indexed(const float* xyzs, const float* dirs, int64_t n, c
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && dirs && sample_idx && table_f16 && mlp_f16 && sigmas && rgbs);
+    NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0);  // 16-byte group gathers
     NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
     static const unsigned cap = resident_blocks(field_fwd_kernel<true>, 256, 0);
     field_fwd_kernel<true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
@@ -827,6 +860,7 @@ int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, cons
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && table_f16 && mlp_f16 && sigmas);
+    NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0);  // 16-byte group gathers
     NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
     static const unsigned cap = resident_blocks(field_fwd_kernel<false>, 256, 0);
     field_fwd_kernel<false><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
@@ -835,23 +869,34 @@ int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, cons
     return ngp_launch_status();
 }
 
-int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
-                    const void* table_f16, void* enc_pm, void* stream) {
+int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                    const ngp_hashgrid_t* grid, const void* table_f16, void* enc_pm, void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && table_f16 && enc_pm && ((uintptr_t)enc_pm & 7) == 0);
-    static const unsigned cap = resident_blocks(hash_encode_kernel, 256, 0);
+    NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0);  // 16-byte group gathers
+    static const bool xcd = getenv("NGP_ENCODE_XCD") && getenv("NGP_ENCODE_XCD")[0] == '1';  // diagnostic
+    if (!xcd) {
+        static const unsigned cap = resident_blocks(hash_encode_kernel<true>, 256, 0);
+        hash_encode_kernel<true><<<std::max(1u, std::min(cap, (unsigned)((n + 255) / 256))), 256, 0,
+                                   as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16,
+                                                        (_Float16*)enc_pm);
+        return ngp_launch_status();
+    }
+    static const unsigned cap = resident_blocks(hash_encode_kernel<false>, 256, 0);
     const unsigned per_pair = std::max(1u, std::min(cap / 8, (unsigned)((n + 255) / 256)));
-    hash_encode_kernel<<<8 * per_pair, 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, ga, (const uint32_t*)table_f16,
-                                                                    (_Float16*)enc_pm);
+    hash_encode_kernel<false><<<8 * per_pair, 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga,
+                                                                           (const uint32_t*)table_f16,
+                                                                           (_Float16*)enc_pm);
     return ngp_launch_status();
 }
 
-int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev, const void* mlp_f16,
-                          float* sigmas, float* rgbs, void* h_f16, void* stream) {
+int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev,
+                          const int32_t* sample_idx, const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16,
+                          void* stream) {
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(enc_pm && dirs && mlp_f16 && sigmas && rgbs);
@@ -860,7 +905,7 @@ int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, cons
     static const unsigned cap = resident_blocks(field_fwd_kernel<true, true>, 256, 0);
     field_fwd_kernel<true, true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
         nullptr, dirs, n, n_dev, ga, nullptr, (const _Float16*)mlp_f16, sigmas, rgbs, nullptr, (_Float16*)h_f16,
-        (const _Float16*)enc_pm, n);
+        (const _Float16*)enc_pm, n, sample_idx);
     return ngp_launch_status();
 }
 

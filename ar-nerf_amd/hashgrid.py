@@ -44,9 +44,9 @@ def _lib():
         L.ngp_density_forward.argtypes = [vp, c_int64, vp, P, vp, vp, vp, vp, vp]
         L.ngp_field_backward.argtypes = [vp, vp, c_int64, vp, P, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_backward_mlp.argtypes = [vp, c_int64, vp, vp, vp, c_int64, vp, vp, vp, vp, vp, vp]
-        L.ngp_hash_encode.argtypes = [vp, c_int64, vp, P, vp, vp, vp]
+        L.ngp_hash_encode.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
         L.ngp_field_forward_indexed.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp]
-        L.ngp_field_mlp_forward.argtypes = [vp, vp, c_int64, vp, vp, vp, vp, vp, vp]
+        L.ngp_field_mlp_forward.argtypes = [vp, vp, c_int64, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_hash_backward.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
         L.ngp_hash_backward_binned.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, vp]
         L.ngp_hash_backward_levels.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp]

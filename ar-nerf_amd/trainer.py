@@ -123,7 +123,7 @@ class NGPTrainer:
         # NGP_ADAM_SPLIT=1: Adam of the MLP + coarse levels beside the binned
         # levels (measured slower: it takes HBM bandwidth from the apply)
         self.adam_split = os.environ.get("NGP_ADAM_SPLIT", "0") == "1"
-        self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "0") == "1"
+        self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "1") == "1"
         self.enc = torch.empty(8 * cap * 4, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         self.denc = torch.empty(cap, 32, **f)
@@ -506,13 +506,7 @@ class NGPTrainer:
 
         at("start")
         self._ev("field_fwd", 0)
-        if self.split_forward:  # level pair per XCD encode (pair-major self.enc), then the MLPs
-            vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.n_samples), HG.ctypes.byref(self.grid.desc),
-                                         _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc), s), "hash_encode")
-            vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), _p(self.dirs), self.cap, _p(self.n_samples),
-                                               _p(self.params16), _p(self.sigmas), _p(self.rgbs), None, s),
-                     "field_mlp_forward")
-        elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
+        if self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
             if R <= 65536:  # counts min(N_r, K) + scan + list in one launch
                 vren._ok(L.ngp_ray_segments_capped(_p(self.rays_a), R, K, _p(self.act_start), _p(self.eval_total),
@@ -528,6 +522,13 @@ class NGPTrainer:
             vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, K, _p(self.act_start),
                                         _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
             self._field_indexed(s)
+        elif self.split_forward:  # encode (pair-major self.enc), then the MLPs, over every marched sample
+            vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.n_samples), None,
+                                         HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
+                                         _p(self.enc), s), "hash_encode")
+            vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), _p(self.dirs), self.cap, _p(self.n_samples), None,
+                                               _p(self.params16), _p(self.sigmas), _p(self.rgbs), None, s),
+                     "field_mlp_forward")
         else:  # fused gathers + MLPs over every marched sample (row-major self.enc)
             vren._ok(HGL.ngp_field_forward(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples),
                                            HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
@@ -625,7 +626,16 @@ class NGPTrainer:
                                           ctypes_float(1.0 / self.world), 1, s), "adam")
 
     def _field_indexed(self, s):
+        """Field forward over the listed samples eval_idx[:eval_total]."""
         HGL = HG._lib()
+        if self.split_forward:
+            vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.eval_total), _p(self.eval_idx),
+                                         HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
+                                         _p(self.enc), s), "hash_encode")
+            vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), _p(self.dirs), self.cap, _p(self.eval_total),
+                                               _p(self.eval_idx), _p(self.params16), _p(self.sigmas), _p(self.rgbs),
+                                               None, s), "field_mlp_forward")
+            return
         vren._ok(HGL.ngp_field_forward_indexed(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.eval_total),
                                                _p(self.eval_idx), HG.ctypes.byref(self.grid.desc),
                                                _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.sigmas),

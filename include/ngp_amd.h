@@ -197,7 +197,7 @@ typedef struct {
  *   x01 = (x - xyz_min)/(xyz_max - xyz_min); enc = hash(x01) (32, fp16)
  *   h = W2 relu(W1 enc) (16, fp16); sigma = exp(h[0]) (TruncExp, fp32)
  *   rgb = sigmoid(W5 relu(W4 relu(W3 [SH4(d/|d|), h])))[0:3]
- * xyzs, dirs (n,3) f32; table_f16 (entries,2) fp16; mlp_f16 as above.
+ * xyzs, dirs (n,3) f32; table_f16 (entries,2) fp16, 16-byte aligned; mlp_f16 as above.
  * Out: sigmas (n) f32, rgbs (n,3) f32 (fp16 values), optional enc_f16 (n,32)
  * (saved for the backward) and h_f16 (n,16).  If n_dev != NULL the sample
  * count is read from device memory (n = capacity, for graph capture). */
@@ -224,14 +224,17 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
 /* ngp_field_forward split in two launches (the training path):
  * ngp_hash_encode writes the encoding PAIR-MAJOR, enc_pm (8, n, 4) fp16 with
  * enc_pm[p][i][k] = enc[i][4p + k] (levels 2p, 2p+1 of sample i; the row
- * stride of the pair planes is n, the capacity, also with n_dev); its
- * workgroups take one level pair each so every XCD's L2 holds one pair's
- * table slice.  ngp_field_mlp_forward runs the density net, SH4 and colour
- * net on it.  Same values as ngp_field_forward, bit for bit. */
-int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const ngp_hashgrid_t* grid,
-                    const void* table_f16, void* enc_pm, void* stream);
+ * stride of the pair planes is n, the capacity, also with n_dev); one lane
+ * per sample encodes all 16 levels, so each gather instruction serves one
+ * level for 64 consecutive samples.  ngp_field_mlp_forward runs the density
+ * net, SH4 and colour net on it.  sample_idx (nullable): process rows j <
+ * *n_dev (or n) = samples sample_idx[j] (< n), as ngp_field_forward_indexed.
+ * Same values as ngp_field_forward, bit for bit. */
+int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                    const ngp_hashgrid_t* grid, const void* table_f16, void* enc_pm, void* stream);
 int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev,
-                          const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16, void* stream);
+                          const int32_t* sample_idx, const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16,
+                          void* stream);
 
 /* ngp_field_forward over the listed samples only: rows j < n (or *n_dev) of
  * sample_idx; sample i = sample_idx[j] reads xyzs/dirs row i and writes

@@ -61,7 +61,7 @@ def main():
     grad = torch.zeros(tr.params.numel(), device=dev)
     for name, (x, dd) in (("ray_order", (xyz, d)), ("morton_sorted", (xyz[perm].contiguous(), d[perm].contiguous()))):
         fns = {
-            "encode": lambda: L.ngp_hash_encode(p(x), n, None, ctypes.byref(grid.desc), p(p16[HG.MLP_PARAMS:]),
+            "encode": lambda: L.ngp_hash_encode(p(x), n, None, None, ctypes.byref(grid.desc), p(p16[HG.MLP_PARAMS:]),
                                                 p(enc_pm), s),
             "fused_fwd": lambda: L.ngp_field_forward(p(x), p(dd), n, None, ctypes.byref(grid.desc),
                                                      p(p16[HG.MLP_PARAMS:]), p(p16), p(sig), p(rgb), p(enc), None, s),

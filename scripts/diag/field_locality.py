@@ -35,9 +35,9 @@ def main():
     for name, half_extent in (("box", 0.5), ("cube_0.1", 0.05), ("cube_0.01", 0.005), ("point", 0.0)):
         xyz = ((torch.rand(N, 3, device=dev, generator=g) * 2 - 1) * half_extent).contiguous()
         enc_pm = torch.empty(8, N, 4, dtype=torch.float16, device=dev)
-        fe = lambda: L.ngp_hash_encode(p(xyz), N, None, ctypes.byref(grid.desc), p(p16[HG.MLP_PARAMS:]),  # noqa
+        fe = lambda: L.ngp_hash_encode(p(xyz), N, None, None, ctypes.byref(grid.desc), p(p16[HG.MLP_PARAMS:]),  # noqa
                                        p(enc_pm), s)
-        fm = lambda: L.ngp_field_mlp_forward(p(enc_pm), p(d), N, None, p(p16), p(sig), p(rgb), None, s)  # noqa
+        fm = lambda: L.ngp_field_mlp_forward(p(enc_pm), p(d), N, None, None, p(p16), p(sig), p(rgb), None, s)  # noqa
         for nm, f in (("encode", fe), ("mlp", fm)):
             for _ in range(3):
                 f()

@@ -73,13 +73,30 @@ def test_split_encode_mlp_equals_fused(scale):
     sig2, rgb2 = torch.empty(n, device=DEV), torch.empty(n, 3, device=DEV)
     L = HG._lib()
     vp = ctypes.c_void_p
-    vren._ok(L.ngp_hash_encode(vp(x.data_ptr()), n, None, ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:].data_ptr()),
+    vren._ok(L.ngp_hash_encode(vp(x.data_ptr()), n, None, None, ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:].data_ptr()),
                                vp(enc_pm.data_ptr()), vren._stream()), "hash_encode")
-    vren._ok(L.ngp_field_mlp_forward(vp(enc_pm.data_ptr()), vp(d.data_ptr()), n, None, vp(p16.data_ptr()),
+    vren._ok(L.ngp_field_mlp_forward(vp(enc_pm.data_ptr()), vp(d.data_ptr()), n, None, None, vp(p16.data_ptr()),
                                      vp(sig2.data_ptr()), vp(rgb2.data_ptr()), None, vren._stream()), "mlp_forward")
     assert torch.equal(enc_pm.permute(1, 0, 2).reshape(n, 32).view(torch.int16), enc.view(torch.int16))
     assert torch.equal(sig2, sig)
     assert torch.equal(rgb2, rgb)
+    # indexed: only the listed samples (rows = samples), the others untouched
+    g = torch.Generator().manual_seed(1)
+    sidx = torch.randperm(n, generator=g)[: n // 3].to(torch.int32).to(DEV)
+    m = torch.tensor([sidx.numel()], dtype=torch.int64, device=DEV)
+    enc_pm.fill_(7.0); sig2.fill_(-1.0); rgb2.fill_(-1.0)
+    vren._ok(L.ngp_hash_encode(vp(x.data_ptr()), n, vp(m.data_ptr()), vp(sidx.data_ptr()), ctypes.byref(grid.desc),
+                               vp(p16[HG.MLP_PARAMS:].data_ptr()), vp(enc_pm.data_ptr()), vren._stream()), "encode_ix")
+    vren._ok(L.ngp_field_mlp_forward(vp(enc_pm.data_ptr()), vp(d.data_ptr()), n, vp(m.data_ptr()),
+                                     vp(sidx.data_ptr()), vp(p16.data_ptr()), vp(sig2.data_ptr()), vp(rgb2.data_ptr()),
+                                     None, vren._stream()), "mlp_ix")
+    ix = sidx.long()
+    rows = enc_pm.permute(1, 0, 2).reshape(n, 32)
+    assert torch.equal(rows[ix].view(torch.int16), enc[ix].view(torch.int16))
+    assert torch.equal(sig2[ix], sig[ix]) and torch.equal(rgb2[ix], rgb[ix])
+    rest = torch.ones(n, dtype=torch.bool, device=DEV)
+    rest[ix] = False
+    assert bool((sig2[rest] == -1.0).all()) and bool((rows[rest] == 7.0).all())
 
 
 @pytest.mark.parametrize("scale", [0.5, 16.0])
