@@ -899,9 +899,16 @@ int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, cons
                           void* stream) {
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
-    NGP_CHECK_ARG(enc_pm && dirs && mlp_f16 && sigmas && rgbs);
+    NGP_CHECK_ARG(enc_pm && mlp_f16 && sigmas && (dirs != nullptr) == (rgbs != nullptr));
     NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0);
     GridArgs ga{};
+    if (!dirs) {  // density net only (occupancy updates)
+        static const unsigned capd = resident_blocks(field_fwd_kernel<false, true>, 256, 0);
+        field_fwd_kernel<false, true><<<persistent_blocks(n, 64, capd), 256, 0, as_stream(stream)>>>(
+            nullptr, nullptr, n, n_dev, ga, nullptr, (const _Float16*)mlp_f16, sigmas, nullptr, nullptr,
+            (_Float16*)h_f16, (const _Float16*)enc_pm, n, sample_idx);
+        return ngp_launch_status();
+    }
     static const unsigned cap = resident_blocks(field_fwd_kernel<true, true>, 256, 0);
     field_fwd_kernel<true, true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
         nullptr, dirs, n, n_dev, ga, nullptr, (const _Float16*)mlp_f16, sigmas, rgbs, nullptr, (_Float16*)h_f16,

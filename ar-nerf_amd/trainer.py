@@ -264,9 +264,16 @@ class NGPTrainer:
                 else:
                     vren._ok(L.ngp_occupancy_samples(*args, _p(self._occ_xyz), _p(self._occ_flat), s),
                              "occupancy_samples")
-                vren._ok(HG._lib().ngp_density_forward(_p(self._occ_xyz), n, None, HG.ctypes.byref(self.grid.desc),
-                                                       _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16),
-                                                       _p(self._occ_sig), None, s), "density_forward")
+                HGL = HG._lib()
+                if self.split_forward and 32 * n <= self.enc.numel():  # encode into the step's (free) enc buffer
+                    vren._ok(HGL.ngp_hash_encode(_p(self._occ_xyz), n, None, None, HG.ctypes.byref(self.grid.desc),
+                                                 _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc), s), "hash_encode")
+                    vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), None, n, None, None, _p(self.params16),
+                                                       _p(self._occ_sig), None, None, s), "density_mlp")
+                else:
+                    vren._ok(HGL.ngp_density_forward(_p(self._occ_xyz), n, None, HG.ctypes.byref(self.grid.desc),
+                                                     _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16),
+                                                     _p(self._occ_sig), None, s), "density_forward")
                 sig, flat = self._occ_sig, self._occ_flat
             vren._ok(L.ngp_density_scatter_max(_p(flat), _p(sig), n, _p(tmp), s), "density_scatter_max")
         if not warmup:

@@ -229,6 +229,7 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
  * level for 64 consecutive samples.  ngp_field_mlp_forward runs the density
  * net, SH4 and colour net on it.  sample_idx (nullable): process rows j <
  * *n_dev (or n) = samples sample_idx[j] (< n), as ngp_field_forward_indexed.
+ * dirs == rgbs == NULL: the density net only (ngp_density_forward's values).
  * Same values as ngp_field_forward, bit for bit. */
 int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                     const ngp_hashgrid_t* grid, const void* table_f16, void* enc_pm, void* stream);

@@ -80,6 +80,11 @@ def test_split_encode_mlp_equals_fused(scale):
     assert torch.equal(enc_pm.permute(1, 0, 2).reshape(n, 32).view(torch.int16), enc.view(torch.int16))
     assert torch.equal(sig2, sig)
     assert torch.equal(rgb2, rgb)
+    # density net only (occupancy updates): ngp_density_forward's sigmas
+    sig3 = torch.empty(n, device=DEV)
+    vren._ok(L.ngp_field_mlp_forward(vp(enc_pm.data_ptr()), None, n, None, None, vp(p16.data_ptr()),
+                                     vp(sig3.data_ptr()), None, None, vren._stream()), "density_mlp")
+    assert torch.equal(sig3, HG.density_forward(x, grid, p16)[0])
     # indexed: only the listed samples (rows = samples), the others untouched
     g = torch.Generator().manual_seed(1)
     sidx = torch.randperm(n, generator=g)[: n // 3].to(torch.int32).to(DEV)
