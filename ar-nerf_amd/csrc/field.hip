@@ -742,7 +742,8 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
 // so equal indices of the same (cx, f) at lane stride 4 are first summed by a
 // segmented suffix scan; only each run's head issues its fp32 atomic.
 // MODE != 0 and a level range other than [0, L) are diagnostic variants used
-// only by scripts/diag (1: no atomics, 2: plain stores, 3: no run merge).
+// only by scripts/diag (1: no atomics, 2: plain stores, 3: no run merge,
+// 4: neither run merge nor atomics).
 template <int MODE>
 __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__ xyzs, int64_t n,
                                                        const int64_t* __restrict__ n_dev,
@@ -751,20 +752,38 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
                                                        int lo, int hi) {
     float sink = 0.f;
     __shared__ LevelLds lv;
+    // the wave's 16 denc rows, staged once per iteration with coalesced 16-B
+    // loads (one global round trip instead of one per level)
+    __shared__ __attribute__((aligned(16))) float drow[4][16][36];
     load_levels(ga, lv);
     __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
-    const int lane = threadIdx.x & 63, s = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1;
+    const int lane = threadIdx.x & 63, s = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1, wv = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16; base < N; base += nw * 16) {
+    for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * 16; base < N; base += nw * 16) {
         const int64_t j = base + s;  // compact position (denc row)
         const bool valid = j < N;
         const int64_t i = valid && sidx ? (int64_t)sidx[j] : j;  // sample
+        {
+            // lane (s, q = lane & 3) copies floats [8q, 8q+8) of row j
+            const int q = lane & 3;
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+            if (valid && 8 * q + 8 > 2 * lo && 8 * q < 2 * hi) {
+                a = *reinterpret_cast<const float4*>(denc + j * 32 + 8 * q);
+                b = *reinterpret_cast<const float4*>(denc + j * 32 + 8 * q + 4);
+            }
+            __builtin_amdgcn_wave_barrier();  // previous iteration's reads of drow are done (in order per wave)
+            *reinterpret_cast<float4*>(&drow[wv][s][8 * q]) = a;
+            *reinterpret_cast<float4*>(&drow[wv][s][8 * q + 4]) = b;
+        }
         float in[3];
         load_x01(xyzs, i, valid, ga, in);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll 1
         for (int l = lo; l < hi; ++l) {
-            const float gd = valid ? denc[j * 32 + 2 * l + f] : 0.f;
+            const float gd = drow[wv][s][2 * l + f];
             const float sc = lv.scale[l];
             const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
             const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
@@ -777,7 +796,12 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
                 pg[d] = (uint32_t)(int)fl;
                 pos[d] = p - fl;
             }
-            // corner c = cx | (cy<<1) | (cz<<2); weight product in tcnn's d order
+            // corner c = cx | (cy<<1) | (cz<<2); weight product in tcnn's d order.
+            // The four y/z corners are independent: their shuffles are issued
+            // together (one LDS round trip per scan step, not four).
+            uint32_t idx[4];
+            float v[4];
+            uint64_t heads[4];
 #pragma unroll
             for (int yz = 0; yz < 4; ++yz) {
                 const int cy = yz & 1, cz = yz >> 1;
@@ -785,29 +809,39 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
                 wt *= cx ? pos[0] : 1 - pos[0];
                 wt *= cy ? pos[1] : 1 - pos[1];
                 wt *= cz ? pos[2] : 1 - pos[2];
-                const uint32_t idx = valid ? off + corner_index(pg[0] + cx, pg[1] + cy, pg[2] + cz, res, size, dense, pow2)
-                                           : 0xffffffffu;
-                float v = wt * gd;
-                const uint32_t prev = __shfl_up(idx, 4, 64);
-                const bool head = lane < 4 || prev != idx;
-                const uint64_t heads = __ballot(head);
-                if (MODE != 3 && heads != ~0ull) {  // some runs: segmented suffix sum at lane stride 4
+                idx[yz] = valid ? off + corner_index(pg[0] + cx, pg[1] + cy, pg[2] + cz, res, size, dense, pow2)
+                                : 0xffffffffu;
+                v[yz] = wt * gd;
+            }
+            uint32_t prev[4];
 #pragma unroll
-                    for (int o4 = 4; o4 < 64; o4 <<= 1) {
-                        const float ov = __shfl_down(v, o4, 64);
-                        // lanes lane+4, lane+8, ..., lane+o4 must all continue the run
-                        const uint64_t span = (0x1111111111111111ull & ((2ull << o4) - 1ull)) & ~1ull;
-                        const bool in_seg = lane + o4 < 64 && (heads & (span << lane)) == 0;
-                        if (in_seg) v += ov;
-                    }
+            for (int yz = 0; yz < 4; ++yz) prev[yz] = __shfl_up(idx[yz], 4, 64);
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz) heads[yz] = __ballot(lane < 4 || prev[yz] != idx[yz]);
+            if (MODE != 3 && MODE != 4 && (heads[0] & heads[1] & heads[2] & heads[3]) != ~0ull) {
+                // some runs: segmented suffix sums at lane stride 4
+#pragma unroll
+                for (int o4 = 4; o4 < 64; o4 <<= 1) {
+                    float ov[4];
+#pragma unroll
+                    for (int yz = 0; yz < 4; ++yz) ov[yz] = __shfl_down(v[yz], o4, 64);
+                    // lanes lane+4, lane+8, ..., lane+o4 must all continue the run
+                    const uint64_t span = ((0x1111111111111111ull & ((2ull << o4) - 1ull)) & ~1ull) << lane;
+#pragma unroll
+                    for (int yz = 0; yz < 4; ++yz)
+                        if (lane + o4 < 64 && (heads[yz] & span) == 0) v[yz] += ov[yz];
                 }
-                if (MODE == 1) sink += head && valid ? v : 0.f;
-                else if (MODE == 2) { if ((head || MODE == 3) && valid) grad[2 * (size_t)idx + f] = v; }
-                else if ((head || MODE == 3) && valid) atomicAdd(&grad[2 * (size_t)idx + f], v);
+            }
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz) {
+                const bool head = (heads[yz] >> lane) & 1ull;
+                if (MODE == 1 || MODE == 4) sink += head && valid ? v[yz] : 0.f;
+                else if (MODE == 2) { if (head && valid) grad[2 * (size_t)idx[yz] + f] = v[yz]; }
+                else if ((head || MODE == 3) && valid) atomicAdd(&grad[2 * (size_t)idx[yz] + f], v[yz]);
             }
         }
     }
-    if (MODE == 1 && sink == 1234.5f) grad[threadIdx.x] = sink;
+    if ((MODE == 1 || MODE == 4) && sink == 1234.5f) grad[threadIdx.x] = sink;
 }
 
 }  // namespace ngp
@@ -945,7 +979,7 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
     if (st) return st;
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && denc && grad_table);
+    NGP_CHECK_ARG(xyzs && denc && grad_table && ((uintptr_t)denc & 15) == 0);
     hash_bwd_kernel<0><<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx,
                                                                                      ga, denc, grad_table, 0, L);
     return ngp_launch_status();
@@ -959,9 +993,23 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
     if (st) return st;
     NGP_CHECK_ARG(n >= 0 && 0 <= level_lo && level_lo <= level_hi && level_hi <= L);
     if (n == 0 || level_lo == level_hi) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && denc && grad_table);
-    hash_bwd_kernel<0><<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(
-        xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+    NGP_CHECK_ARG(xyzs && denc && grad_table && ((uintptr_t)denc & 15) == 0);
+    static const int mode = getenv("NGP_HASH_BWD_MODE") ? atoi(getenv("NGP_HASH_BWD_MODE")) : 0;  // diagnostic
+    // (NGP_HASH_BWD_BLOCKS: diagnostic grid cap; 2048 measured slower)
+    static const unsigned cap = (unsigned)std::max(1, getenv("NGP_HASH_BWD_BLOCKS") ? atoi(getenv("NGP_HASH_BWD_BLOCKS"))
+                                                                                    : 8192);
+    const unsigned blocks = persistent_blocks(n, 64, cap);
+    hipStream_t s = as_stream(stream);
+    if (mode == 1)
+        hash_bwd_kernel<1><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+    else if (mode == 2)
+        hash_bwd_kernel<2><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+    else if (mode == 4)
+        hash_bwd_kernel<4><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+    else if (mode == 3)
+        hash_bwd_kernel<3><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+    else
+        hash_bwd_kernel<0><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
     return ngp_launch_status();
 }
 

@@ -18,13 +18,28 @@ from trainer import NGPTrainer, ctypes_float  # noqa: E402
 
 
 def timed(f, reps=20):
+    """Average GPU time of f: reps calls captured in one HIP graph and
+    replayed (no host launch overhead in the number); eager if the stage
+    cannot be captured."""
     for _ in range(3):
         f()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        f()
-    e1.record()
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                f()
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+    except RuntimeError:
+        e0.record()
+        for _ in range(reps):
+            f()
+        e1.record()
     torch.cuda.synchronize()
     return round(e0.elapsed_time(e1) / reps * 1e3, 1)
 
@@ -43,22 +58,22 @@ def main():
     p, L, HGL, s, R = HG._ptr, tr.L, HG._lib(), vren._stream(), 8192
     cur = torch.cuda.current_stream()
     st = {}
-    st["march"] = timed(lambda: tr._march(tr.cur, ("sample", 777, gt), dirs, poses, cur))
+    st["march"] = timed(lambda: tr._march(tr.cur, ("sample", 777, gt), dirs, poses, torch.cuda.current_stream()))
     st["field_fwd"] = timed(lambda: vren._ok(HGL.ngp_field_forward(
         p(tr.xyzs), p(tr.dirs), tr.cap, p(tr.n_samples), HG.ctypes.byref(tr.grid.desc), p(tr.params16[HG.MLP_PARAMS:]),
-        p(tr.params16), p(tr.sigmas), p(tr.rgbs), p(tr.enc), None, s), "ff"))
+        p(tr.params16), p(tr.sigmas), p(tr.rgbs), p(tr.enc), None, vren._stream()), "ff"))
     K = 64
     def chunk_round(first_round):
         if first_round:
-            vren._ok(L.ngp_chunk_counts(p(tr.rays_a), R, K, None, None, ctypes_float(1e-4), p(tr.eval_counts), s), "c")
+            vren._ok(L.ngp_chunk_counts(p(tr.rays_a), R, K, None, None, ctypes_float(1e-4), p(tr.eval_counts), vren._stream()), "c")
             vren._ok(L.ngp_ray_segments(p(tr.eval_counts), p(tr.rays_a), R, 0, p(tr.act_start), p(tr.eval_total), None,
-                                        p(tr.eval_idx), s), "sg")
+                                        p(tr.eval_idx), vren._stream()), "sg")
         else:
             vren._ok(L.ngp_chunk_counts(p(tr.rays_a), R, K, p(tr.sigmas), p(tr.deltas), ctypes_float(1e-4),
-                                        p(tr.eval_counts), s), "c")
+                                        p(tr.eval_counts), vren._stream()), "c")
             vren._ok(L.ngp_ray_segments(p(tr.eval_counts), p(tr.rays_a), R, K, p(tr.act_start), p(tr.eval_total), None,
-                                        p(tr.eval_idx), s), "sg")
-    field_ix = lambda: tr._field_indexed(s)  # noqa: E731
+                                        p(tr.eval_idx), vren._stream()), "sg")
+    field_ix = lambda: tr._field_indexed(vren._stream())  # noqa: E731
     st["chunk1_list"] = timed(lambda: chunk_round(True))
     st["chunk1_field"] = timed(field_ix)
     st["chunk1_n"] = int(tr.eval_total.item())
@@ -68,33 +83,33 @@ def main():
     st["composite"] = timed(lambda: vren._ok(L.ngp_composite_loss(
         p(tr.sigmas), p(tr.rgbs), p(tr.deltas), p(tr.ts), p(tr.rays_a), R, p(tr.rgb_gt), p(tr.bg), 0,
         ctypes_float(1e-3), ctypes_float(0.0), ctypes_float(0.5), ctypes_float(1e-4), p(tr.dsig), p(tr.drgb),
-        p(tr.out_rgb), p(tr.out_op), p(tr.out_depth), p(tr.out_loss), p(tr.n_active), None, None, None, None, s), "cl"))
+        p(tr.out_rgb), p(tr.out_op), p(tr.out_depth), p(tr.out_loss), p(tr.n_active), None, None, None, None, vren._stream()), "cl"))
     st["active_samples"] = timed(lambda: vren._ok(L.ngp_active_samples(
-        p(tr.n_active), p(tr.rays_a), R, p(tr.act_start), p(tr.n_active_total), p(tr.sample_idx), s), "as"))
+        p(tr.n_active), p(tr.rays_a), R, p(tr.act_start), p(tr.n_active_total), p(tr.sample_idx), vren._stream()), "as"))
     st["mlp_bwd"] = timed(lambda: vren._ok(HGL.ngp_field_backward_mlp(
         p(tr.dirs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), p(tr.enc), 0, p(tr.params16), p(tr.dsig),
-        p(tr.drgb), p(tr.denc), p(tr.grad), s), "mb"))
+        p(tr.drgb), p(tr.denc), p(tr.grad), vren._stream()), "mb"))
     st["hash_bwd_binned_fine"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_binned(
         p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
-        p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, tr.bin_level_lo, s), "hb"))
+        p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, tr.bin_level_lo, vren._stream()), "hb"))
     st["hash_bwd_atomic_coarse"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_levels(
         p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
-        p(tr.grad[HG.MLP_PARAMS:]), 0, tr.bin_level_lo, s), "ha"))
+        p(tr.grad[HG.MLP_PARAMS:]), 0, tr.bin_level_lo, vren._stream()), "ha"))
     for lo, hi in ((0, 2), (2, 4), (4, 6), (6, 8), (8, 10), (10, 12), (12, 14), (14, 16)):
         st[f"hash_atomic_L{lo}_{hi}"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_levels(
             p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
-            p(tr.grad[HG.MLP_PARAMS:]), lo, hi, s), "hl"))
+            p(tr.grad[HG.MLP_PARAMS:]), lo, hi, vren._stream()), "hl"))
     for lo in (4, 6, 10, 12):
         st[f"hash_binned_from_L{lo}"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_binned(
             p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
-            p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, lo, s), "hb"))
+            p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, lo, vren._stream()), "hb"))
     st["hash_bwd_atomic_all"] = timed(lambda: vren._ok(HGL.ngp_hash_backward(
         p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
-        p(tr.grad[HG.MLP_PARAMS:]), s), "hall"))
+        p(tr.grad[HG.MLP_PARAMS:]), vren._stream()), "hall"))
     st["adam"] = timed(lambda: vren._ok(L.ngp_adam_step(
         p(tr.params), p(tr.grad), p(tr.exp_avg), p(tr.exp_avg_sq), p(tr.params16), tr.params.numel(),
         ctypes_float(1e-2), ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), 100, ctypes_float(1.0), 0,
-        s), "adam"))
+        vren._stream()), "adam"))
     st["occupancy_update"] = timed(lambda: tr.update_density_grid(0.01 * 1024 / 3 ** 0.5), reps=5)
     st["density_fwd_1M"] = timed(lambda: HG.density_forward(tr.xyzs[:1 << 20].contiguous(), tr.grid, tr.params16), reps=5)
     import time
