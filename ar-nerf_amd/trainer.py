@@ -294,11 +294,10 @@ class NGPTrainer:
         the counter in device memory so a replayed graph draws fresh batches)."""
         m = self.msets[k]
         L, R = self.L, self.batch_size
-        evs = self.kernel_events.get("march_side") if self.kernel_events is not None else None
         side = stream is self.march_stream
         with torch.cuda.stream(stream):
-            if evs is not None and side:
-                evs[0].record(stream)
+            if side:
+                self._ev("march_side", 0, stream)
             s = HG.c_void_p(stream.cuda_stream)
             if src[0] == "sample":
                 _, add, gt = src
@@ -330,8 +329,8 @@ class NGPTrainer:
             vren._ok(L.ngp_march_train_compact(_p(m["rays_o"]), _p(m["rays_d"]), _p(m["rays_a"]), R,
                                                _p(m["slot_t"]), _p(m["slot_dt"]), self.max_samples, _p(m["xyzs"]),
                                                _p(m["dirs"]), _p(m["deltas"]), _p(m["ts"]), s), "march_compact")
-            if evs is not None and side:
-                evs[1].record(stream)
+            if side:
+                self._ev("march_side", 1, stream)
 
     def _can_prefetch(self):
         """The next batch may be marched ahead unless the next step begins with
@@ -366,10 +365,21 @@ class NGPTrainer:
         if self._pending is not None and self._pending[1] is not None:
             torch.cuda.current_stream().wait_event(self._pending[1])
 
-    def _ev(self, name, i):
+    def _ev(self, name, i, stream=None):
+        """Breakdown instrumentation (eager steps only): i = 0 opens a new
+        (start, end) HIP-event pair for `name` on `stream` (default: the
+        current one), i = 1 closes the last one.  kernel_events maps a name to
+        the list of its pairs (a kernel launched twice per step has two)."""
         ev = self.kernel_events
-        if ev is not None and name in ev:
-            ev[name][i].record()
+        if ev is None:
+            return
+        st = stream if stream is not None else torch.cuda.current_stream()
+        if i == 0:
+            pair = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            pair[0].record(st)
+            ev.setdefault(name, []).append(pair)
+        else:
+            ev[name][-1][1].record(st)
 
     # ---------------------------------------------------------------- step
     def _on_exec_stream(self, fn, *args):
@@ -545,12 +555,14 @@ class NGPTrainer:
         at("after_fwd")
         bg = torch.rand(3, device=self.dev, generator=self.gen) if self.random_bg else self.bg
         self._ev("composite_loss", 0)
+        self._ev("composite", 0)
         vren._ok(L.ngp_composite_loss(_p(self.sigmas), _p(self.rgbs), _p(self.deltas), _p(self.ts), _p(self.rays_a), R,
                                       _p(rgb_gt), _p(bg), self.loss_type, ctypes_float(self.lambda_opacity),
                                       ctypes_float(self.lambda_depth), ctypes_float(self.scale), ctypes_float(1e-4),
                                       _p(self.dsig), _p(self.drgb), _p(self.out_rgb), _p(self.out_op),
                                       _p(self.out_depth), _p(self.out_loss), _p(self.n_active), None, None, None,
                                       _p(self.stats), s), "composite_loss")
+        self._ev("composite", 1)
         # compacted gradient-carrying samples: scan + map (a per-block atomic
         # reservation inside composite_loss serialises on one address and was slower)
         vren._ok(L.ngp_active_samples(_p(self.n_active), _p(self.rays_a), R, _p(self.act_start),
@@ -582,10 +594,12 @@ class NGPTrainer:
             # binned fine levels here (after the plan): disjoint gradient ranges
             bs.wait_stream(cs)
             with torch.cuda.stream(bs):
+                self._ev("hash_bwd_coarse", 0)
                 vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                       _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
                                                       _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), 0,
                                                       self.bin_level_lo, vren._stream()), "hash_backward_levels")
+                self._ev("hash_bwd_coarse", 1)
                 # single process: Adam of the MLP + coarse levels here too, beside
                 # the binned levels (no all-reduce orders it after the whole grad)
                 split = HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
@@ -593,10 +607,12 @@ class NGPTrainer:
                 if adam_split:
                     self._adam(0, split, vren._stream())
             cs.wait_event(planned)
+            self._ev("hash_binned_apply", 0)
             vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
                                                _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
                                                self.bin_level_lo, s), "hash_binned_apply")
+            self._ev("hash_binned_apply", 1)
             if adam_split:
                 self._ev("adam", 0)
                 self._adam(split, self.params.numel(), s)
@@ -636,12 +652,16 @@ class NGPTrainer:
         """Field forward over the listed samples eval_idx[:eval_total]."""
         HGL = HG._lib()
         if self.split_forward:
+            self._ev("hash_encode", 0)
             vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.eval_total), _p(self.eval_idx),
                                          HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
                                          _p(self.enc), s), "hash_encode")
+            self._ev("hash_encode", 1)
+            self._ev("field_mlp", 0)
             vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), _p(self.dirs), self.cap, _p(self.eval_total),
                                                _p(self.eval_idx), _p(self.params16), _p(self.sigmas), _p(self.rgbs),
                                                None, s), "field_mlp_forward")
+            self._ev("field_mlp", 1)
             return
         vren._ok(HGL.ngp_field_forward_indexed(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.eval_total),
                                                _p(self.eval_idx), HG.ctypes.byref(self.grid.desc),

@@ -40,22 +40,28 @@ from trainer import NGPTrainer  # noqa: E402
 with open(os.path.join(ROOT, "BASELINE.json")) as f:
     BASELINE = json.load(f)
 
-# Algorithmic work per marched (field_fwd) or gradient-carrying (mlp_bwd,
-# hash_bwd) sample of the per-sample kernels (DESIGN.md "Measurement"):
-#  field_fwd: 16 levels x 8 corners x fp16x2 gathered (512 B) + xyz, dir read
-#             (24 B), fp16 encoding (64 B) + sigma, rgb (16 B) written -> bytes
-#  hash_bwd : xyz (12 B) + dL/denc fp32 (128 B) read + read-modify-write of
-#             16 x 8 x 2 fp32 table gradients (2 x 1024 B)         -> bytes
-#  mlp_bwd  : forward recompute + dX + dW of the two MLPs (16-row output
-#             layers as computed)                                 -> FLOPs
+# Algorithmic work per unit of the per-kernel breakdown:
+#  hash_encode (unit: field-evaluated sample): 16 levels x 8 corners x fp16x2
+#      gathered (512 B) + xyz (12 B) + list index (4 B) read + fp16 encoding
+#      (64 B) written                                              -> bytes
+#  field_mlp (evaluated sample): density 32-64-16 + colour 32-64-64-16 forward
+#      (2 x (3072 + 7168) FLOP)                                    -> FLOPs
+#  mlp_bwd (gradient-carrying sample): forward recompute + dX + dW of both
+#      MLPs (16-row output layers as computed)                     -> FLOPs
+#  hash_bwd_coarse (gradient-carrying sample, levels 0-7): xyz + index (16 B)
+#      + dL/denc (64 B) read + read-modify-write of 8 x 8 x 2 fp32 table
+#      gradients (2 x 512 B)                                       -> bytes
+#  adam (parameter): p, g, m, v read; p, m, v, fp16 p written, g zeroed (34 B)
+_MLP_FWD = 2 * (32 * 64 + 64 * 16) + 2 * (32 * 64 + 64 * 64 + 64 * 16)
 KERNEL_WORK = {
-    "field_fwd": ("hbm", 16 * 8 * 4 + 12 + 12 + 64 + 4 + 12, "GB/s"),
-    "hash_bwd": ("hbm", 12 + 128 + 2 * 16 * 8 * 2 * 4, "GB/s"),
+    "hash_encode": ("hbm", 16 * 8 * 4 + 12 + 4 + 64, "GB/s", "evaluated"),
+    "field_mlp": ("mfma", _MLP_FWD, "TFLOP/s", "evaluated"),
     "mlp_bwd": ("mfma", 2 * (32 * 64 + 64 * 16 + 32 * 64 + 64 * 64 + 64 * 16)
                 + 2 * (16 * 64 + 64 * 64 + 64 * 16 + 16 * 64 + 64 * 32)
-                + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32), "TFLOP/s"),
+                + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32), "TFLOP/s", "active"),
+    "hash_bwd_coarse": ("hbm", 16 + 64 + 2 * 8 * 8 * 2 * 4, "GB/s", "active"),
+    "adam": ("hbm", 34, "GB/s", "params"),
 }
-FWD_KERNELS = ("field_fwd",)  # run over every marched sample
 PEAK = {"hbm": 8000.0, "mfma": 2500.0}  # MI355X: HBM3E GB/s; dense fp16 MFMA TFLOP/s
 
 
@@ -145,6 +151,20 @@ def cpu_baseline(trainer, scene, gt_images, budget_s, batch):
                       f"{samples / max(1, steps) / batch:.1f} samples/ray, {t_total:.1f} s"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
+    corrected per MI355X_MICROARCH.md "HBM"), or None if not measured."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f).get(kernel)
+    except (OSError, ValueError):
+        return None
+    return None if t is None else t.get("bytes_per_launch")
+
+
 def _recorded(event):
     try:
         event.elapsed_time(event)
@@ -208,16 +228,16 @@ def main():
     vr_s = composited / (R * args.steps)
     ev_s = evaluated / (R * args.steps)
     # ---- breakdown region: the same steps run eagerly with HIP events around
-    # each kernel / stage (events cannot sit between the nodes of a replayed
-    # graph); per-kernel durations and the roofline come from here
+    # each kernel / stage, on the stream each is launched on (events cannot
+    # sit between the nodes of a replayed graph); per-kernel durations and the
+    # roofline come from here
     n_bd = max(1, min(args.steps, args.breakdown_steps))
-    names = list(KERNEL_WORK)
     # raygen_march = inline march on the main stream (steps after an occupancy
     # update); march_side = the next batch's march on the side stream, which
     # overlaps the step's compute (averaged over the steps that launched one)
-    stages = ["occupancy_update", "raygen_march", "march_side", "composite_loss", "allreduce", "adam"]
-    ev = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for k in names + stages}
-          for _ in range(n_bd)]
+    stages = ["occupancy_update", "raygen_march", "march_side", "field_fwd", "composite_loss", "mlp_bwd", "hash_bwd",
+              "hash_binned_apply", "allreduce", "adam"]
+    ev = [dict() for _ in range(n_bd)]
     trainer.stats.zero_()
     torch.cuda.synchronize()
     t_bd = time.perf_counter()
@@ -228,23 +248,30 @@ def main():
     marched_bd, _, active_bd, evaluated_bd = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         evaluated_bd = marched_bd
-    samples_per_step = evaluated_bd / n_bd  # field_fwd runs over the evaluated samples
-    active_per_step = active_bd / n_bd
+
+    def durations(name):
+        return [p[0].elapsed_time(p[1]) for e in ev for p in e.get(name, []) if _recorded(p[1])]
+
+    per_step = {"evaluated": evaluated_bd / n_bd, "active": active_bd / n_bd, "params": trainer.params.numel()}
     kernels = {}
-    for k in names:
-        ms = sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / n_bd
-        bound, per_sample, unit = KERNEL_WORK[k]
-        # the backward kernels run over the gradient-carrying samples only
-        units = samples_per_step if k in FWD_KERNELS else active_per_step
-        achieved = units * per_sample / (ms * 1e-3) / (1e9 if bound == "hbm" else 1e12)
+    for k, (bound, per_unit, unit, basis) in KERNEL_WORK.items():
+        d = durations(k)
+        if not d:
+            continue
+        ms = sum(d) / len(d)
+        launches = len(d) / n_bd
+        units = per_step[basis] / launches if basis != "params" else per_step[basis] / launches
+        achieved = units * per_unit / (ms * 1e-3) / (1e9 if bound == "hbm" else 1e12)
         kernels[k] = {"bound": bound, "achieved": round(achieved, 2), "peak": PEAK[bound], "unit": unit,
                       "frac": round(achieved / PEAK[bound], 4), "avg_launch_ms": round(ms, 4),
-                      "work_per_sample": per_sample, "samples_per_launch": round(units, 1)}
+                      "launches_per_step": round(launches, 2), "work_per_unit": per_unit,
+                      "units_per_launch": round(units, 1), "unit_basis": basis}
     dominant = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
-    stage_ms = {k: round(sum(e[k][0].elapsed_time(e[k][1]) for e in ev) / n_bd, 4)
-                for k in stages if k != "march_side"}
-    side = [e["march_side"][0].elapsed_time(e["march_side"][1]) for e in ev if _recorded(e["march_side"][1])]
-    stage_ms["march_side"] = round(sum(side) / max(len(side), 1), 4)
+    stage_ms = {}
+    for k in stages:
+        d = durations(k)
+        if d:  # per step (march_side: per launch, over the steps that launched one)
+            stage_ms[k] = round(sum(d) / (len(d) if k == "march_side" else n_bd), 4)
     loss = float(trainer.out_loss.sum().item())
     psnr = psnr_eval(trainer, scene, args.psnr_views, args.psnr_res) if (rank == 0 and args.psnr_views > 0) else None
     cpu = None
@@ -267,7 +294,7 @@ def main():
                        "parallelism": f"dp{world}", "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
-            "roofline": dict(kernel=dominant, traffic=None, **kernels[dominant]),
+            "roofline": dict(kernel=dominant, traffic=pmc_traffic(dominant), **kernels[dominant]),
             "kernels": kernels,
             "stage_ms": stage_ms,
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
