@@ -111,7 +111,7 @@ class NGPTrainer:
         self.n_prefetched = 0
         self.no_prefetch = os.environ.get("NGP_NO_PREFETCH", "0") == "1"  # march every batch inline (diagnostics)
         # where in the step the next batch's march is launched on the side stream
-        self.prefetch_at = os.environ.get("NGP_PREFETCH_AT", "after_composite")
+        self.prefetch_at = os.environ.get("NGP_PREFETCH_AT", "after_fwd")
         self._bind(self.msets[0])
         self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         # saved encoding: pair-major (8, cap, 4) for the split forward, else row-major (cap, 32)
@@ -590,33 +590,39 @@ class NGPTrainer:
         at("after_mlp_bwd")
         self._ev("hash_bwd", 0)
         if hybrid:
-            # atomic coarse levels on the side stream (after the MLP backward),
-            # binned fine levels here (after the plan): disjoint gradient ranges
-            bs.wait_stream(cs)
-            with torch.cuda.stream(bs):
+            # atomic coarse levels on the side stream and binned fine levels
+            # (after the plan) here, side by side: disjoint gradient ranges
+            split = HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
+            adam_split = self.adam_split and apply_adam and self.world == 1 and bs is not cs
+
+            def coarse():
                 self._ev("hash_bwd_coarse", 0)
                 vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                       _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
                                                       _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), 0,
                                                       self.bin_level_lo, vren._stream()), "hash_backward_levels")
                 self._ev("hash_bwd_coarse", 1)
-                # single process: Adam of the MLP + coarse levels here too, beside
-                # the binned levels (no all-reduce orders it after the whole grad)
-                split = HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
-                adam_split = self.adam_split and apply_adam and self.world == 1 and bs is not cs
+                # single process: Adam of the MLP + coarse levels right after them
+                # (no all-reduce orders it after the whole gradient)
                 if adam_split:
                     self._adam(0, split, vren._stream())
+
+            def apply():
+                self._ev("hash_binned_apply", 0)
+                vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
+                                                   _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws),
+                                                   self.bin_max_samples, self.bin_level_lo, vren._stream()),
+                         "hash_binned_apply")
+                self._ev("hash_binned_apply", 1)
+                if adam_split:
+                    self._adam(split, self.params.numel(), vren._stream())
+
+            bs.wait_stream(cs)
+            with torch.cuda.stream(bs):
+                coarse()
             cs.wait_event(planned)
-            self._ev("hash_binned_apply", 0)
-            vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                               _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
-                                               _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
-                                               self.bin_level_lo, s), "hash_binned_apply")
-            self._ev("hash_binned_apply", 1)
-            if adam_split:
-                self._ev("adam", 0)
-                self._adam(split, self.params.numel(), s)
-                self._ev("adam", 1)
+            apply()
             cs.wait_stream(bs)
             if adam_split:
                 self._ev("hash_bwd", 1)

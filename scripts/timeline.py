@@ -35,7 +35,18 @@ def main():
                 ce = max(ce, e)
         busy += ce - cs
         print(f"  queue {k}: {len(vv) / steps:.1f} kernels/step, busy {busy / 1e3 / steps:.1f} us/step")
+    # time with no kernel running on any queue (dependency / launch latency)
+    allv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in win)
+    idle, ce = 0, allv[0][1]
+    for st, en in allv[1:]:
+        if st > ce:
+            idle += st - ce
+        ce = max(ce, en)
+    print(f"  all queues idle {idle / 1e3 / steps:.1f} us/step")
     seg = rows[anch[-back - 1] + 1:anch[-back] + 1]
+    prev_end = int(rows[anch[-back - 1]]["End_Timestamp"])
+    print(f"  gap from the previous step's adam end to this step's first kernel: "
+          f"{(int(seg[0]['Start_Timestamp']) - prev_end) / 1e3:.1f} us")
     s0 = int(seg[0]["Start_Timestamp"])
     for r in seg:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
