@@ -513,6 +513,25 @@ __device__ __forceinline__ h4 get_tile(const _Float16* T, int s, int g) {
     return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
                                       (__attribute__((address_space(3))) hp4*)(const_cast<_Float16*>(a))));
 }
+// bf16 operands of the weight-gradient MFMAs (v_mfma_f32_16x16x16_bf16: the
+// same fragment layout as the f16 form).  bf16 keeps fp32's exponent, so the
+// true gradients go in unscaled and every iteration accumulates straight into
+// the MFMA C operand (no per-iteration unscale-and-add in VALU).
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 b2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
+}
+__device__ __forceinline__ h4 bf16x4(f4 v) {  // (bf16 bits carried in an h4 for the LDS tile helpers)
+    const uint2 u = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+    return __builtin_bit_cast(h4, u);
+}
+__device__ __forceinline__ h4 bf16x4(h4 v) { return bf16x4(f4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]}); }
+__device__ __forceinline__ f4 mfma16bf(h4 a, h4 b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4v, a), __builtin_bit_cast(s4v, b), c, 0, 0,
+                                                     0);
+}
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -661,48 +680,53 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
             c = c * is_1;
             if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
         }
-        // ---- weight gradients: transpose operands through LDS, K = 16 samples
+        // ---- weight gradients dW = sum_s G[o][s] H[i][s]: bf16 operands (true,
+        // unscaled gradients), transposed through LDS, K = 16 samples,
+        // accumulated in the MFMA C operand
         wave_sync_lds();  // previous iteration's reads are done
-        put_tile(scr + T_DO * TTILE, do_h, s, g);
+        put_tile(scr + T_DO * TTILE, bf16x4(dout), s, g);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            put_tile(scr + (T_DA4 + t) * TTILE, da4h[t], s, g);
-            put_tile(scr + (T_DA3 + t) * TTILE, da3h[t], s, g);
-            put_tile(scr + (T_DA1 + t) * TTILE, da1h[t], s, g);
-            put_tile(scr + (T_H4 + t) * TTILE, h4v[t], s, g);
-            put_tile(scr + (T_H3 + t) * TTILE, h3[t], s, g);
-            put_tile(scr + (T_H1 + t) * TTILE, h1[t], s, g);
+            put_tile(scr + (T_DA4 + t) * TTILE, bf16x4(da4[t]), s, g);
+            put_tile(scr + (T_DA3 + t) * TTILE, bf16x4(da3[t]), s, g);
+            put_tile(scr + (T_DA1 + t) * TTILE, bf16x4(da1[t]), s, g);
+            put_tile(scr + (T_H4 + t) * TTILE, bf16x4(h4v[t]), s, g);
+            put_tile(scr + (T_H3 + t) * TTILE, bf16x4(h3[t]), s, g);
+            put_tile(scr + (T_H1 + t) * TTILE, bf16x4(h1[t]), s, g);
         }
-        put_tile(scr + T_DH * TTILE, dhh, s, g);
-        put_tile(scr + T_C * TTILE, shh, s, g);
-        put_tile(scr + (T_C + 1) * TTILE, hh, s, g);
+        put_tile(scr + T_DH * TTILE, bf16x4(dh), s, g);
+        put_tile(scr + T_C * TTILE, bf16x4(shh), s, g);
+        put_tile(scr + (T_C + 1) * TTILE, bf16x4(hh), s, g);
         // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
-        *reinterpret_cast<h8*>(scr + (T_E + (g >> 1)) * TTILE + s * TROW + 8 * (g & 1)) = e;
+        {
+            const h4 e0 = bf16x4(h4{e[0], e[1], e[2], e[3]}), e1 = bf16x4(h4{e[4], e[5], e[6], e[7]});
+            *reinterpret_cast<h8*>(scr + (T_E + (g >> 1)) * TTILE + s * TROW + 8 * (g & 1)) = pack(e0, e1);
+        }
         wave_sync_lds();
         int k = 0;
         const h4 gdo = get_tile(scr + T_DO * TTILE, s, g);
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt, ++k) acc[k] += mfma16(gdo, get_tile(scr + (T_H4 + nt) * TTILE, s, g), z) * is_o;
+        for (int nt = 0; nt < 4; ++nt, ++k) acc[k] = mfma16bf(gdo, get_tile(scr + (T_H4 + nt) * TTILE, s, g), acc[k]);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
             const h4 ga = get_tile(scr + (T_DA4 + mt) * TTILE, s, g);
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt, ++k) acc[k] += mfma16(ga, get_tile(scr + (T_H3 + nt) * TTILE, s, g), z) * is_4;
+            for (int nt = 0; nt < 4; ++nt, ++k) acc[k] = mfma16bf(ga, get_tile(scr + (T_H3 + nt) * TTILE, s, g), acc[k]);
         }
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
             const h4 ga = get_tile(scr + (T_DA3 + mt) * TTILE, s, g);
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt, ++k) acc[k] += mfma16(ga, get_tile(scr + (T_C + nt) * TTILE, s, g), z) * is_3;
+            for (int nt = 0; nt < 2; ++nt, ++k) acc[k] = mfma16bf(ga, get_tile(scr + (T_C + nt) * TTILE, s, g), acc[k]);
         }
         const h4 gdh = get_tile(scr + T_DH * TTILE, s, g);
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt, ++k) acc[k] += mfma16(gdh, get_tile(scr + (T_H1 + nt) * TTILE, s, g), z) * is_h;
+        for (int nt = 0; nt < 4; ++nt, ++k) acc[k] = mfma16bf(gdh, get_tile(scr + (T_H1 + nt) * TTILE, s, g), acc[k]);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
             const h4 ga = get_tile(scr + (T_DA1 + mt) * TTILE, s, g);
 #pragma unroll
-            for (int nt = 0; nt < 2; ++nt, ++k) acc[k] += mfma16(ga, get_tile(scr + (T_E + nt) * TTILE, s, g), z) * is_1;
+            for (int nt = 0; nt < 2; ++nt, ++k) acc[k] = mfma16bf(ga, get_tile(scr + (T_E + nt) * TTILE, s, g), acc[k]);
         }
         cur = nxt;
     }
