@@ -58,6 +58,37 @@ __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
     return v;
 }
 
+// Transmittance over one 64-sample chunk of a row, lane j < cnt holding
+// om_j = 1 - a_j: T after sample j is T_in x (inclusive product of om, a
+// fixed Hillis-Steele order -- the reference's serial product reassociated,
+// like the wave sums), Tk the transmittance in front of sample j.  stop = 1 +
+// the first j with T after it <= thr (where composite_train_fw breaks), else
+// cnt.  chunk_rest_kernel calls the same function, so the chunked field
+// evaluation sees exactly the composite's termination.  A serial readlane
+// walk here set the kernel time by the longest rows (hundreds of samples).
+struct ChunkT {
+    float Tk, Tn;
+    int stop;
+    bool hit;
+};
+__device__ __forceinline__ ChunkT chunk_transmittance(float om, int cnt, float T_in, float thr, int lane) {
+    float p = lane < cnt ? om : 1.0f;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float y = __shfl_up(p, o, 64);
+        if (lane >= o) p *= y;
+    }
+    float pe = __shfl_up(p, 1, 64);
+    if (lane == 0) pe = 1.0f;
+    ChunkT r;
+    r.Tk = T_in * pe;
+    r.Tn = T_in * p;
+    const uint64_t h = __ballot(lane < cnt && r.Tn <= thr);
+    r.hit = h != 0ull;
+    r.stop = r.hit ? __ffsll((unsigned long long)h) : cnt;
+    return r;
+}
+
 // One row of rays_a on one wave; returns the composited sample count
 // (vr_samples' share of this ray) and, in na_out, the samples that carry
 // gradient (up to and including the terminating one).
@@ -94,17 +125,13 @@ __device__ __forceinline__ int64_t composite_loss_ray(
         const int cnt = (int)(N - k0 < 64 ? N - k0 : 64);
         const float a = 1.0f - __expf(-c.sg * c.dl);
         const float om = 1.0f - a;
-        float Tk = 0.f;
-        int stop = cnt;
-        for (int j = 0; j < cnt; ++j) {
-            const float omj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(om), j));
-            if (lane == j) Tk = T;
-            T *= omj;
-            if (T <= la.T_thr) { stop = j + 1; done = true; break; }
-        }
+        const ChunkT ct = chunk_transmittance(om, cnt, T, la.T_thr, lane);
+        const int stop = ct.stop;
+        if (ct.hit) done = true;
+        T = __shfl(ct.Tn, stop - 1, 64);
         const bool act = lane < stop;
-        c.w = act ? a * Tk : 0.f;
-        c.Ta = Tk * om;
+        c.w = act ? a * ct.Tk : 0.f;
+        c.Ta = ct.Tk * om;
         R += wave_sum(c.w * c.cr); G += wave_sum(c.w * c.cg); B += wave_sum(c.w * c.cb);
         D += wave_sum(c.w * c.tt); O += wave_sum(c.w);
         samples += done ? stop - 1 : stop;
@@ -112,12 +139,17 @@ __device__ __forceinline__ int64_t composite_loss_ray(
     };
     fw_chunk(0, c0);
     if (!done && N > 64) fw_chunk(64, c1);
-    for (int64_t k0 = 128; k0 < N && !done; k0 += 64) {  // long rows: spill w / T to memory
+    if (!done && N > 128) {  // long rows: the next chunk in flight while one is composited; w / T spilled
         Chunk c;
-        load(k0, c);
-        fw_chunk(k0, c);
-        const int64_t s = start + k0 + lane;
-        if (k0 + lane < N) { dL_drgbs[3 * s] = c.w; dL_drgbs[3 * s + 1] = c.Ta; }
+        load(128, c);
+        for (int64_t k0 = 128; k0 < N && !done; k0 += 64) {
+            Chunk nx;
+            if (k0 + 64 < N) load(k0 + 64, nx);
+            fw_chunk(k0, c);
+            const int64_t s = start + k0 + lane;
+            if (k0 + lane < N) { dL_drgbs[3 * s] = c.w; dL_drgbs[3 * s + 1] = c.Ta; }
+            c = nx;
+        }
     }
     // ---- background + loss (wave-uniform)
     const float bgc[3] = {bg[0], bg[1], bg[2]};
@@ -732,10 +764,10 @@ __global__ void __launch_bounds__(256) chunk_first_kernel(const int64_t* __restr
     counts[r] = (int32_t)min(rays_a[3 * r + 2], (int64_t)first);
 }
 
-// Round-2 counts: one wave per row walks the transmittance of its first
-// min(N_r, first) samples exactly as composite_loss_ray's forward does
-// (same expressions, same serial order); a row that has not terminated there
-// and has more samples needs N_r - first more.
+// Round-2 counts: one wave per row computes the transmittance of its first
+// min(N_r, first) samples exactly as composite_loss_ray's forward does (same
+// expressions, chunk_transmittance); a row that has not terminated there and
+// has more samples needs N_r - first more.
 __global__ void __launch_bounds__(256) chunk_rest_kernel(const float* __restrict__ sigmas,
                                                          const float* __restrict__ deltas,
                                                          const int64_t* __restrict__ rays_a, int64_t n_rows, int first,
@@ -752,10 +784,9 @@ __global__ void __launch_bounds__(256) chunk_rest_kernel(const float* __restrict
         float sg = 0.f, dl = 0.f;
         if (lane < cnt) { sg = sigmas[start + k0 + lane]; dl = deltas[start + k0 + lane]; }
         const float om = 1.0f - (1.0f - __expf(-sg * dl));
-        for (int j = 0; j < cnt; ++j) {
-            T *= __int_as_float(__builtin_amdgcn_readlane(__float_as_int(om), j));
-            if (T <= T_thr) { done = true; break; }
-        }
+        const ChunkT ct = chunk_transmittance(om, cnt, T, T_thr, lane);
+        done = ct.hit;
+        T = __shfl(ct.Tn, ct.stop - 1, 64);
     }
     if (lane == 0) counts[n] = (!done && N > first) ? (int32_t)(N - first) : 0;
 }

@@ -235,7 +235,8 @@ def main():
     # raygen_march = inline march on the main stream (steps after an occupancy
     # update); march_side = the next batch's march on the side stream, which
     # overlaps the step's compute (averaged over the steps that launched one)
-    stages = ["occupancy_update", "raygen_march", "march_side", "field_fwd", "composite_loss", "mlp_bwd", "hash_bwd",
+    stages = ["occupancy_update", "raygen_march", "march_side", "field_fwd", "composite_loss", "composite", "mlp_bwd",
+              "hash_bwd",
               "hash_binned_apply", "allreduce", "adam"]
     ev = [dict() for _ in range(n_bd)]
     trainer.stats.zero_()
