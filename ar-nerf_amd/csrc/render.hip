@@ -1,0 +1,279 @@
+// Device-resident test-time render loop for gfx950: the reference's
+// __render_rays_test (models/rendering.py:162-253) with every host decision
+// moved into device memory, so a whole frame is a few HIP-graph replays with
+// one host sync at the end instead of a sync + ~5 launches per iteration.
+//
+// Per iteration (parity p = iteration & 1 selects the alive list pair):
+//   render_iter_kernel      N_alive = state[p]; stop if 0 or samples >= budget;
+//                           N_samples = max(min(N_rays // N_alive, 64), min_samples)
+//                           (rendering.py:188-195)
+//   render_march_kernel     raymarching_test for the alive rays (raymarching.cu:335-404,
+//                           identical walk to march_test_kernel) into slots
+//                           [n*N_samples + s]; appends the valid slots to a sample
+//                           list (the reference's valid_mask, rendering.py:204)
+//   (field kernels)         ngp_hash_encode + ngp_field_mlp_forward over the list
+//   render_composite_kernel composite_test_fw (volumerendering.cu:204-284) and the
+//                           alive compaction (rendering.py:236) into list p^1
+//
+// Results are per ray and depend on the alive list only through N_alive (an
+// order-independent count), so the unordered atomic compaction gives the
+// reference's values bit for bit.
+#pragma clang fp contract(off)
+#include "march.h"
+
+namespace ngp {
+
+// state (int64[NGP_RENDER_STATE_WORDS]) word indices
+enum : int { RS_ALIVE0 = 0, RS_ALIVE1 = 1, RS_SAMPLES = 2, RS_NS = 3, RS_ACTIVE = 4, RS_VALID = 5, RS_TOTAL = 6,
+             RS_ITERS = 7 };
+
+__global__ void __launch_bounds__(256) render_begin_kernel(int64_t n_rays, int64_t* __restrict__ state,
+                                                           int32_t* __restrict__ alive0, float* __restrict__ opacity,
+                                                           float* __restrict__ depth, float* __restrict__ rgb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < NGP_RENDER_STATE_WORDS) {
+        int64_t v = 0;
+        if (i == RS_ALIVE0) v = n_rays;
+        if (i == RS_ACTIVE) v = 1;
+        state[i] = v;
+    }
+    if (i >= n_rays) return;
+    alive0[i] = (int32_t)i;  // torch.arange(N_rays) (rendering.py:183)
+    opacity[i] = 0.f;
+    depth[i] = 0.f;
+    rgb[3 * i] = 0.f; rgb[3 * i + 1] = 0.f; rgb[3 * i + 2] = 0.f;
+}
+
+__global__ void render_iter_kernel(int64_t* __restrict__ state, int parity, int64_t n_rays, int min_samples,
+                                   int64_t sample_budget) {
+    if (threadIdx.x != 0 || !state[RS_ACTIVE]) return;
+    const int64_t n_alive = state[parity];
+    if (n_alive == 0 || state[RS_SAMPLES] >= sample_budget) {  // rendering.py:187-190
+        state[RS_ACTIVE] = 0;
+        state[RS_VALID] = 0;
+        return;
+    }
+    int64_t ns = n_rays / n_alive;
+    ns = ns < 64 ? ns : 64;
+    ns = ns > min_samples ? ns : min_samples;
+    state[RS_SAMPLES] += ns;
+    state[RS_NS] = ns;
+    state[RS_VALID] = 0;
+    state[parity ^ 1] = 0;
+    state[RS_ITERS] += 1;
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+template <bool SIMPLE>
+__global__ void __launch_bounds__(256) render_march_kernel(const float* __restrict__ rays_o,
+                                                           const float* __restrict__ rays_d,
+                                                           float* __restrict__ hits_t, MarchParams p,
+                                                           int64_t* __restrict__ state, int parity,
+                                                           const int32_t* __restrict__ alive,
+                                                           float* __restrict__ xyzs, float* __restrict__ dirs,
+                                                           float* __restrict__ deltas, float* __restrict__ ts,
+                                                           int32_t* __restrict__ n_eff,
+                                                           int32_t* __restrict__ sample_idx) {
+    if (!state[RS_ACTIVE]) return;
+    const int64_t n_alive = state[parity];
+    if ((int64_t)blockIdx.x * blockDim.x >= n_alive) return;  // block-uniform, before the barrier
+    const int Ns = (int)state[RS_NS];
+    extern __shared__ uint32_t ssum[];
+    WordCache wc;
+    wc.sum = load_summary(p, ssum);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t wbase = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); wbase < n_alive; wbase += stride) {
+        const int64_t n = wbase + lane;
+        int s = 0;
+        if (n < n_alive) {
+            const int64_t r = alive[n];
+            float o[3], d[3], dinv[3];
+            load_ray(rays_o, rays_d, r, o, d, dinv);
+            float t = hits_t[2 * r];
+            const float t2 = hits_t[2 * r + 1];
+            float x, y, z, dt, t_emit = t;
+            const int64_t base = n * (int64_t)Ns;
+            while (t < t2 && s < Ns) {  // raymarching.cu:366-400
+                const float tc = t;
+                if (march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc)) {
+                    t_emit = t;
+                    const int64_t q = base + s;
+                    xyzs[3 * q] = x; xyzs[3 * q + 1] = y; xyzs[3 * q + 2] = z;
+                    dirs[3 * q] = d[0]; dirs[3 * q + 1] = d[1]; dirs[3 * q + 2] = d[2];
+                    ts[q] = tc;
+                    deltas[q] = dt;
+                    s++;
+                }
+            }
+            if (s) hits_t[2 * r] = t_emit;  // raymarching.cu:390: t after the last emitted sample
+            n_eff[n] = s;
+        }
+        // append this wave's valid slots to the sample list (one atomic per wave)
+        const int incl = wave_incl_scan(s);
+        const int total = __shfl(incl, 63, 64);
+        if (total == 0) continue;
+        int64_t off = 0;
+        if (lane == 0) off = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(&state[RS_VALID]),
+                                                (unsigned long long)total);
+        off = __shfl(off, 0, 64) + (incl - s);
+        const int64_t base = n * (int64_t)Ns;
+        for (int k = 0; k < s; ++k) sample_idx[off + k] = (int32_t)(base + k);
+    }
+}
+
+__global__ void __launch_bounds__(256) render_composite_kernel(const float* __restrict__ sigmas,
+                                                               const float* __restrict__ rgbs,
+                                                               const float* __restrict__ deltas,
+                                                               const float* __restrict__ ts,
+                                                               const int32_t* __restrict__ n_eff,
+                                                               int64_t* __restrict__ state, int parity,
+                                                               const int32_t* __restrict__ alive_in,
+                                                               int32_t* __restrict__ alive_out, float T_thr,
+                                                               float* __restrict__ opacity, float* __restrict__ depth,
+                                                               float* __restrict__ rgb) {
+    if (!state[RS_ACTIVE]) return;
+    const int64_t n_alive = state[parity];
+    const int Ns = (int)state[RS_NS];
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t wbase = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); wbase < n_alive; wbase += stride) {
+        const int64_t n = wbase + lane;
+        bool keep = false;
+        int ne = 0;
+        int32_t r = -1;
+        if (n < n_alive) {
+            ne = n_eff[n];
+            r = alive_in[n];
+            if (ne > 0) {  // volumerendering.cu:221-224: no samples -> dead
+                keep = true;
+                float op = opacity[r], dp = depth[r], cr = rgb[3 * r], cg = rgb[3 * r + 1], cb = rgb[3 * r + 2];
+                float T = 1 - op;
+                for (int s = 0; s < ne; ++s) {  // volumerendering.cu:228-256
+                    const int64_t o = n * (int64_t)Ns + s;
+                    const float a = 1.0f - __expf(-sigmas[o] * deltas[o]);
+                    const float w = a * T;
+                    cr += w * rgbs[3 * o]; cg += w * rgbs[3 * o + 1]; cb += w * rgbs[3 * o + 2];
+                    dp += w * ts[o];
+                    op += w;
+                    T *= 1.0f - a;
+                    if (T <= T_thr) { keep = false; break; }
+                }
+                rgb[3 * r] = cr; rgb[3 * r + 1] = cg; rgb[3 * r + 2] = cb;
+                depth[r] = dp;
+                opacity[r] = op;
+            }
+        }
+        // total_samples += N_eff_samples.sum() (rendering.py:199)
+        int tot = ne;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        const uint64_t live = __ballot(keep);
+        const int n_keep = __popcll(live);
+        int64_t off = 0;
+        if (lane == 0) {
+            if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&state[RS_TOTAL]), (unsigned long long)tot);
+            if (n_keep)
+                off = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(&state[parity ^ 1]),
+                                         (unsigned long long)n_keep);
+        }
+        off = __shfl(off, 0, 64);
+        if (keep) alive_out[off + __popcll(live & ((1ull << lane) - 1ull))] = r;
+    }
+}
+
+// rendering.py:240-251: rgb += bg * (1 - opacity)
+__global__ void __launch_bounds__(256) render_finish_kernel(const float* __restrict__ opacity, int64_t n_rays, float b0,
+                                                            float b1, float b2, float* __restrict__ rgb) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_rays) return;
+    const float m = 1 - opacity[i];
+    rgb[3 * i] += b0 * m; rgb[3 * i + 1] += b1 * m; rgb[3 * i + 2] += b2 * m;
+}
+
+}  // namespace ngp
+
+using namespace ngp;
+
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+extern "C" {
+
+int64_t ngp_render_test_capacity(int64_t n_rays, int min_samples) {
+    if (n_rays < 0 || min_samples < 1) return -1;
+    // N_alive * N_samples <= max(N_rays, N_alive * min_samples) <= N_rays * min_samples
+    return n_rays * (int64_t)min_samples;
+}
+
+int ngp_render_test_begin(int64_t n_rays, int64_t* state, int32_t* alive0, float* opacity, float* depth, float* rgb,
+                          void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && n_rays < INT32_MAX && state);
+    NGP_CHECK_ARG(n_rays == 0 || (alive0 && opacity && depth && rgb));
+    const int64_t n = n_rays > NGP_RENDER_STATE_WORDS ? n_rays : NGP_RENDER_STATE_WORDS;
+    render_begin_kernel<<<nblk(n, 256), 256, 0, as_stream(stream)>>>(n_rays, state, alive0, opacity, depth, rgb);
+    return ngp_launch_status();
+}
+
+int ngp_render_test_march(const float* rays_o, const float* rays_d, float* hits_t, int64_t n_rays,
+                          const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
+                          int max_samples, int min_samples, int64_t sample_budget, int parity, int64_t* state,
+                          const int32_t* alive, const uint32_t* occ_summary, float* xyzs, float* dirs, float* deltas,
+                          float* ts, int32_t* n_eff, int32_t* sample_idx, void* stream) {
+    MarchParams p;
+    int st = march_params(bitfield, cascades, grid_size, scale, exp_step_factor, max_samples, p);
+    if (st) return st;
+    st = march_attach_summary(p, occ_summary);
+    if (st) return st;
+    p.dt_scale = (float)cascades;  // raymarching.cu:370,399 quirk (test time)
+    NGP_CHECK_ARG(n_rays >= 0 && n_rays < INT32_MAX && min_samples >= 1 && (parity == 0 || parity == 1) && state);
+    NGP_CHECK_ARG(ngp_render_test_capacity(n_rays, min_samples) < INT32_MAX);
+    hipStream_t s = as_stream(stream);
+    render_iter_kernel<<<1, 64, 0, s>>>(state, parity, n_rays, min_samples, sample_budget);
+    if (n_rays == 0) return ngp_launch_status();
+    NGP_CHECK_ARG(rays_o && rays_d && hits_t && alive && xyzs && dirs && deltas && ts && n_eff && sample_idx);
+    const unsigned blocks = std::min(nblk(n_rays, 256), 2048u);
+    if (march_simple(p))
+        render_march_kernel<true><<<blocks, 256, march_summary_lds(p), s>>>(
+            rays_o, rays_d, hits_t, p, state, parity, alive, xyzs, dirs, deltas, ts, n_eff, sample_idx);
+    else
+        render_march_kernel<false><<<blocks, 256, march_summary_lds(p), s>>>(
+            rays_o, rays_d, hits_t, p, state, parity, alive, xyzs, dirs, deltas, ts, n_eff, sample_idx);
+    return ngp_launch_status();
+}
+
+int ngp_render_test_composite(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                              const int32_t* n_eff, int64_t n_rays, int parity, int64_t* state,
+                              const int32_t* alive_in, int32_t* alive_out, float T_threshold, float* opacity,
+                              float* depth, float* rgb, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && (parity == 0 || parity == 1) && state);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(sigmas && rgbs && deltas && ts && n_eff && alive_in && alive_out && alive_in != alive_out &&
+                  opacity && depth && rgb);
+    const unsigned blocks = std::min(nblk(n_rays, 256), 2048u);
+    render_composite_kernel<<<blocks, 256, 0, as_stream(stream)>>>(sigmas, rgbs, deltas, ts, n_eff, state, parity,
+                                                                  alive_in, alive_out, T_threshold, opacity, depth,
+                                                                  rgb);
+    return ngp_launch_status();
+}
+
+int ngp_render_test_finish(const float* opacity, int64_t n_rays, const float* bg_rgb, float* rgb, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && bg_rgb);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(opacity && rgb);
+    render_finish_kernel<<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(opacity, n_rays, bg_rgb[0], bg_rgb[1],
+                                                                           bg_rgb[2], rgb);
+    return ngp_launch_status();
+}
+
+}  // extern "C"

@@ -75,6 +75,11 @@ def _declare(L):
                           vp],
         "ngp_density_scatter_max": [vp, vp, c_int64, vp, vp],
         "ngp_density_grid_ema": [vp, vp, c_int64, c_float, c_float, vp, vp, vp],
+        "ngp_render_test_begin": [c_int64, vp, vp, vp, vp, vp, vp],
+        "ngp_render_test_march": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, c_int, c_int, c_int64,
+                                  c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+        "ngp_render_test_composite": [vp, vp, vp, vp, vp, c_int64, c_int, vp, vp, vp, c_float, vp, vp, vp, vp],
+        "ngp_render_test_finish": [vp, c_int64, vp, vp, vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -85,6 +90,8 @@ def _declare(L):
     L.ngp_hashgrid_levels.restype = ctypes.c_uint32
     L.ngp_occupancy_sorted_workspace.argtypes = [c_int64]
     L.ngp_occupancy_sorted_workspace.restype = ctypes.c_size_t
+    L.ngp_render_test_capacity.argtypes = [c_int64, c_int]
+    L.ngp_render_test_capacity.restype = c_int64
 
 
 def lib():

@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--breakdown-steps", type=int, default=50, help="eager steps with per-kernel HIP events")
     ap.add_argument("--hash-backward", default="hybrid", choices=["hybrid", "binned", "atomic"])
+    ap.add_argument("--infer-frames", type=int, default=20, help="timed full-frame test renders (0: skip)")
+    ap.add_argument("--infer-res", type=int, default=800)
     return ap.parse_args()
 
 
@@ -118,6 +120,52 @@ def psnr_eval(trainer, scene, n_views, res, seed=123):
         mse = torch.mean((out["rgb"].clamp(0, 1) - gt) ** 2).item()
         psnrs.append(-10 * math.log10(max(mse, 1e-12)))
     return sum(psnrs) / len(psnrs)
+
+
+def inference_bench(trainer, res, frames, world, rank):
+    """BASELINE config 5: full-frame test-time render (models/rendering.py:162-253)
+    of the trained model, graph-captured (renderer.TestRenderer), `frames` poses
+    per rank (frames are independent: replicas).  The host-driven loop
+    (trainer.render, the reference's control flow) is timed on one frame beside it."""
+    import renderer as RD
+    sc = S.AnalyticScene(W=res, H=res, n_images=max(2, frames), scale=trainer.scale, seed=321 + rank)
+    n = res * res
+    rr = RD.TestRenderer(n, trainer.grid, trainer.params16, trainer.density_bitfield, trainer.cascades,
+                         trainer.scale, trainer.G, exp_step_factor=trainer.esf)
+    rr.set_camera(sc.directions.cuda(), trainer.center, trainer.half_size)
+    poses = sc.poses.cuda()
+    for i in range(2):  # capture + warm
+        rr.render_pose(poses[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    iters = samples = 0
+    for i in range(frames):
+        out = rr.render_pose(poses[i % poses.shape[0]])
+        iters += rr.last_iterations
+        samples += int(out["total_samples"])
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([t], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    # the host-driven loop on the last pose, same rays
+    o, d = rr.rays_o.clone(), rr.rays_d.clone()
+    trainer.render(o, d)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ref = trainer.render(o, d)
+    torch.cuda.synchronize()
+    t_host = time.perf_counter() - t1
+    same = bool(torch.equal(ref["rgb"], out["rgb"]) and torch.equal(ref["opacity"], out["opacity"]))
+    return {"fps": round(world * frames / t, 2), "ms_per_frame": round(t / frames * 1e3, 3), "frames_per_rank": frames,
+            "resolution": [res, res], "n_gpus": world, "iterations_per_frame": round(iters / frames, 1),
+            "samples_per_ray": round(samples / (frames * n), 2), "graphs": True,
+            "host_loop_ms_per_frame": round(t_host * 1e3, 3), "host_loop_bit_exact": same,
+            "workload": "full-frame test render of the trained model (black bg), march+field+composite per "
+                        "iteration in HIP graphs, one host sync per 16 iterations"}
 
 
 def cpu_baseline(trainer, scene, gt_images, budget_s, batch):
@@ -275,6 +323,7 @@ def main():
             stage_ms[k] = round(sum(d) / (len(d) if k == "march_side" else n_bd), 4)
     loss = float(trainer.out_loss.sum().item())
     psnr = psnr_eval(trainer, scene, args.psnr_views, args.psnr_res) if (rank == 0 and args.psnr_views > 0) else None
+    infer = inference_bench(trainer, args.infer_res, args.infer_frames, world, rank) if args.infer_frames > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(trainer, scene, gt_images, args.cpu_budget_s, R)
@@ -303,6 +352,7 @@ def main():
                                f"the timed region ({t_bd / n_bd * 1e3:.3f} ms/step eager); the timed steps replay "
                                "captured HIP graphs"),
             "cpu_baseline": cpu,
+            "inference": infer,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -165,6 +165,45 @@ int ngp_composite_test_fw(const float* sigmas, const float* rgbs, const float* d
                           float T_threshold, const int32_t* n_eff, float* opacity, float* depth,
                           float* rgb, void* stream);
 
+/* ------------------------------------ device-resident test-time render */
+/* Replaces the host loop of __render_rays_test (models/rendering.py:162-253:
+ * per iteration vren.raymarching_test, model(), vren.composite_test_fw and the
+ * alive compaction, with a host sync on len(alive_indices)) by a loop whose
+ * every decision lives in device memory, so iterations can be captured in a
+ * HIP graph and replayed (renderer.py).  state: int64[NGP_RENDER_STATE_WORDS]
+ *   [0],[1] alive counts of list 0/1, [2] samples (loop budget, rendering.py:186),
+ *   [3] N_samples of the current iteration, [4] active (0 once finished),
+ *   [5] valid samples listed this iteration (the n_dev of the field kernels),
+ *   [6] total_samples (sum of N_eff), [7] iterations run.
+ * Iteration k uses parity p = k & 1: ngp_render_test_march reads alive list p,
+ * ngp_render_test_composite writes the survivors to list p^1.  Buffers:
+ * alive lists (n_rays) i32; slots xyzs/dirs (cap,3), deltas/ts/sigmas (cap),
+ * rgbs (cap,3) f32; n_eff (n_rays) i32; sample_idx (cap) i32, cap =
+ * ngp_render_test_capacity(n_rays, min_samples).  Per-ray results equal the
+ * host loop's bit for bit (compaction order does not enter them). */
+#define NGP_RENDER_STATE_WORDS 8
+int64_t ngp_render_test_capacity(int64_t n_rays, int min_samples);
+/* state init, alive list 0 = arange(n_rays), opacity/depth/rgb = 0 (rendering.py:177-183) */
+int ngp_render_test_begin(int64_t n_rays, int64_t* state, int32_t* alive0, float* opacity, float* depth, float* rgb,
+                          void* stream);
+/* Loop test + N_samples (rendering.py:186-195), then raymarching_test
+ * (raymarching.cu:335-404, `cascades` as calc_dt's scale) over the alive rays
+ * into slots [n*N_samples + s] (hits_t (n_rays,2) t1 advanced in place), and
+ * the valid slots appended to sample_idx (count in state[5]). */
+int ngp_render_test_march(const float* rays_o, const float* rays_d, float* hits_t, int64_t n_rays,
+                          const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
+                          int max_samples, int min_samples, int64_t sample_budget, int parity, int64_t* state,
+                          const int32_t* alive, const uint32_t* occ_summary, float* xyzs, float* dirs, float* deltas,
+                          float* ts, int32_t* n_eff, int32_t* sample_idx, void* stream);
+/* composite_test_fw (volumerendering.cu:204-284) + total_samples + survivors
+ * (n_eff > 0 and T > T_threshold) appended to alive_out. */
+int ngp_render_test_composite(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
+                              const int32_t* n_eff, int64_t n_rays, int parity, int64_t* state,
+                              const int32_t* alive_in, int32_t* alive_out, float T_threshold, float* opacity,
+                              float* depth, float* rgb, void* stream);
+/* rgb += bg_rgb (host float[3]) * (1 - opacity) (rendering.py:240-251) */
+int ngp_render_test_finish(const float* opacity, int64_t n_rays, const float* bg_rgb, float* rgb, void* stream);
+
 /* --------------------------------------------- hash grid + fused MLPs */
 /* Level table of tcnn's Grid/Hash encoding as configured at
  * models/networks.py:33-49 (host function; fp32 arithmetic like tcnn).
