@@ -120,6 +120,60 @@ __global__ void __launch_bounds__(64) composite_test_kernel(const float* __restr
     opacity[r] = op;
 }
 
+// Distortion loss (losses.cu:8-107, DVGO-v2 form): one lane per row.  The
+// reference's per-thread thrust scans / reduce are sequential left folds, so
+// the folds stay serial per ray for the reference's bits; rows are independent.
+__global__ void __launch_bounds__(256) distortion_fw_kernel(const float* __restrict__ ws,
+                                                            const float* __restrict__ deltas,
+                                                            const float* __restrict__ ts,
+                                                            const int64_t* __restrict__ rays_a, int64_t n_rays,
+                                                            float* __restrict__ loss, float* __restrict__ ws_inc,
+                                                            float* __restrict__ wts_inc) {
+    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_rays) return;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+    const float third = 1.0f / 3;
+    float a = 0.f, b = 0.f, acc = 0.f;
+    for (int64_t k = 0; k < N; ++k) {
+        const int64_t s = start + k;
+        const float w = ws[s];
+        const float wts = w * ts[s];  // losses.cu:70
+        const float ws_exc = a, wts_exc = b;
+        a = a + w;
+        b = b + wts;
+        ws_inc[s] = a;
+        wts_inc[s] = b;
+        // losses.cu:92-93, one rounding per torch op
+        acc = acc + (2 * (b * ws_exc - a * wts_exc) + ((third * w) * w) * deltas[s]);
+    }
+    loss[ray] = acc;
+}
+
+// losses.cu:110-140: every sample's gradient is independent given the scans,
+// so one wave per row, lanes over its samples (coalesced).
+__global__ void __launch_bounds__(256) distortion_bw_kernel(const float* __restrict__ dL_dloss,
+                                                            const float* __restrict__ ws_inc,
+                                                            const float* __restrict__ wts_inc,
+                                                            const float* __restrict__ ws,
+                                                            const float* __restrict__ deltas,
+                                                            const float* __restrict__ ts,
+                                                            const int64_t* __restrict__ rays_a, int64_t n_rays,
+                                                            float* __restrict__ dL_dws) {
+    const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (n >= n_rays) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+    if (N <= 0) return;
+    const int64_t end = start + N - 1;
+    const float ws_sum = ws_inc[end], wts_sum = wts_inc[end], g = dL_dloss[ray];
+    for (int64_t s = start + lane; s <= end; s += 64) {
+        const float t = ts[s];
+        const float A = s == start ? 0.0f : t * ws_inc[s - 1] - wts_inc[s - 1];
+        const float B = (wts_sum - wts_inc[s]) - t * (ws_sum - ws_inc[s]);
+        dL_dws[s] = (g * 2) * (A + B) + (((g * 2.0f) / 3.0f) * ws[s]) * deltas[s];
+    }
+}
+
 }  // namespace ngp
 
 using namespace ngp;
@@ -163,6 +217,28 @@ int ngp_composite_test_fw(const float* sigmas, const float* rgbs, const float* d
     composite_test_kernel<<<nblk(n_alive, 64), 64, 0, as_stream(stream)>>>(sigmas, rgbs, deltas, ts, n_alive,
                                                                           N_samples, alive, T_threshold, n_eff,
                                                                           opacity, depth, rgb);
+    return ngp_launch_status();
+}
+
+int ngp_distortion_loss_fw(const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                           int64_t n_rays, float* loss, float* ws_inclusive_scan, float* wts_inclusive_scan,
+                           void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(ws && deltas && ts && rays_a && loss && ws_inclusive_scan && wts_inclusive_scan);
+    distortion_fw_kernel<<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(ws, deltas, ts, rays_a, n_rays, loss,
+                                                                          ws_inclusive_scan, wts_inclusive_scan);
+    return ngp_launch_status();
+}
+
+int ngp_distortion_loss_bw(const float* dL_dloss, const float* ws_inclusive_scan, const float* wts_inclusive_scan,
+                           const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                           int64_t n_rays, float* dL_dws, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0);
+    if (n_rays == 0) return NGP_OK;
+    NGP_CHECK_ARG(dL_dloss && ws_inclusive_scan && wts_inclusive_scan && ws && deltas && ts && rays_a && dL_dws);
+    distortion_bw_kernel<<<nblk(n_rays, 4), 256, 0, as_stream(stream)>>>(
+        dL_dloss, ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a, n_rays, dL_dws);
     return ngp_launch_status();
 }
 

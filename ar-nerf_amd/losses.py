@@ -6,11 +6,21 @@ import vren
 
 
 class DistortionLoss(torch.autograd.Function):
-    """losses.py:7-38 (off by default, opt.py:25): next-row item."""
+    """losses.py:7-38: Mip-NeRF 360 distortion loss in the DVGO-v2 form, per
+    ray (off by default, opt.py:25), on the gfx950 kernels."""
 
     @staticmethod
     def forward(ctx, ws, deltas, ts, rays_a):
-        return vren.distortion_loss_fw(ws, deltas, ts, rays_a)
+        loss, ws_inclusive_scan, wts_inclusive_scan = vren.distortion_loss_fw(ws, deltas, ts, rays_a)
+        ctx.save_for_backward(ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dL_dloss):
+        ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a = ctx.saved_tensors
+        dL_dws = vren.distortion_loss_bw(dL_dloss.contiguous(), ws_inclusive_scan, wts_inclusive_scan, ws, deltas,
+                                         ts, rays_a)
+        return dL_dws, None, None, None
 
 
 class NeRFLoss(nn.Module):

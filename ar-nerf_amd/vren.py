@@ -75,6 +75,8 @@ def _declare(L):
                           vp],
         "ngp_density_scatter_max": [vp, vp, c_int64, vp, vp],
         "ngp_density_grid_ema": [vp, vp, c_int64, c_float, c_float, vp, vp, vp],
+        "ngp_distortion_loss_fw": [vp, vp, vp, vp, c_int64, vp, vp, vp, vp],
+        "ngp_distortion_loss_bw": [vp, vp, vp, vp, vp, vp, vp, c_int64, vp, vp],
         "ngp_render_test_begin": [c_int64, vp, vp, vp, vp, vp, vp],
         "ngp_render_test_march": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, c_int, c_int, c_int64,
                                   c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
@@ -355,8 +357,26 @@ def ray_sphere_intersect(*args, **kwargs):
                               "out of scope (SURVEY.md §2 row 3)")
 
 
-def distortion_loss_fw(*args, **kwargs):
-    raise NotImplementedError("distortion loss is off by default (opt.py:25); next-row item (SURVEY.md §8f)")
+def distortion_loss_fw(ws, deltas, ts, rays_a):
+    """losses.cu:62-107 -> [loss (N_rays), ws_inclusive_scan (N), wts_inclusive_scan (N)]
+    (zero-initialised like the reference's torch::zeros outputs)."""
+    pw, pd, pt = (_check("ws", ws, torch.float32), _check("deltas", deltas, torch.float32),
+                  _check("ts", ts, torch.float32))
+    pr = _check("rays_a", rays_a, torch.int64)
+    nr, N = rays_a.shape[0], ws.shape[0]
+    loss = torch.zeros(nr, device=ws.device)
+    wsi, wtsi = torch.zeros(N, device=ws.device), torch.zeros(N, device=ws.device)
+    _ok(lib().ngp_distortion_loss_fw(pw, pd, pt, pr, nr, c_void_p(loss.data_ptr()), c_void_p(wsi.data_ptr()),
+                                     c_void_p(wtsi.data_ptr()), _stream()), "distortion_loss_fw")
+    return [loss, wsi, wtsi]
 
 
-distortion_loss_bw = distortion_loss_fw
+def distortion_loss_bw(dL_dloss, ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a):
+    """losses.cu:143-173 -> dL_dws (N)"""
+    a = [_check("dL_dloss", dL_dloss, torch.float32), _check("ws_inclusive_scan", ws_inclusive_scan, torch.float32),
+         _check("wts_inclusive_scan", wts_inclusive_scan, torch.float32), _check("ws", ws, torch.float32),
+         _check("deltas", deltas, torch.float32), _check("ts", ts, torch.float32),
+         _check("rays_a", rays_a, torch.int64)]
+    dws = torch.zeros(ws.shape[0], device=ws.device)
+    _ok(lib().ngp_distortion_loss_bw(*a, rays_a.shape[0], c_void_p(dws.data_ptr()), _stream()), "distortion_loss_bw")
+    return dws

@@ -165,6 +165,20 @@ int ngp_composite_test_fw(const float* sigmas, const float* rgbs, const float* d
                           float T_threshold, const int32_t* n_eff, float* opacity, float* depth,
                           float* rgb, void* stream);
 
+/* ---------------------------------------------------- distortion loss */
+/* Replace vren.distortion_loss_fw / _bw (binding.cpp, losses.cu:62-107,143-173;
+ * autograd wrapper losses.py:7-38).  ws, deltas, ts (N) f32; rays_a (n_rays,3)
+ * i64.  fw: loss (indexed by rays_a[:,0]) and the two inclusive scans (N);
+ * samples of no row and rows not listed are left untouched (the reference
+ * zero-fills: pass zeroed buffers for its outputs).  bw: dL_dws (N) for the
+ * listed rows' samples. */
+int ngp_distortion_loss_fw(const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                           int64_t n_rays, float* loss, float* ws_inclusive_scan, float* wts_inclusive_scan,
+                           void* stream);
+int ngp_distortion_loss_bw(const float* dL_dloss, const float* ws_inclusive_scan, const float* wts_inclusive_scan,
+                           const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                           int64_t n_rays, float* dL_dws, void* stream);
+
 /* ------------------------------------ device-resident test-time render */
 /* Replaces the host loop of __render_rays_test (models/rendering.py:162-253:
  * per iteration vren.raymarching_test, model(), vren.composite_test_fw and the

@@ -58,6 +58,8 @@ def lib():
         L.or_composite_train_bw.argtypes = [c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                             c_float, vp, vp]
         L.or_composite_test_fw.argtypes = [c_int, c_int, vp, vp, vp, vp, vp, c_float, vp, vp, vp, vp]
+        L.or_distortion_loss_fw.argtypes = [c_int, vp, vp, vp, vp, vp, vp, vp]
+        L.or_distortion_loss_bw.argtypes = [c_int, vp, vp, vp, vp, vp, vp, vp, vp]
         L.or_hash_levels.argtypes = [c_int, c_int, c_int, c_float, vp, vp, vp, vp]
         L.or_hash_levels.restype = c_uint32
         L.or_hash_encode_fwd.argtypes = [c_int, vp, vp, vp, c_int, vp, vp, vp, vp, vp, vp]
@@ -189,6 +191,25 @@ def composite_test_fw(sigmas, rgbs, deltas, ts, hits_t, alive_indices, T_thresho
         assert x.is_contiguous() and x.device.type == "cpu"
     lib().or_composite_test_fw(n, Ns, _p(s), _p(c), _p(dl), _p(t), _p(alive_indices), float(T_threshold),
                                _p(ne), _p(opacity), _p(depth), _p(rgb))
+
+
+def distortion_loss_fw(ws, deltas, ts, rays_a):
+    """losses.cu:62-107 -> [loss (N_rays), ws_inclusive_scan (N), wts_inclusive_scan (N)]"""
+    w, dl, t, ra = (_c(ws, torch.float32), _c(deltas, torch.float32), _c(ts, torch.float32),
+                    _c(rays_a, torch.int64))
+    nr, N = ra.shape[0], w.shape[0]
+    loss, wsi, wtsi = torch.zeros(nr), torch.zeros(N), torch.zeros(N)
+    lib().or_distortion_loss_fw(nr, _p(w), _p(dl), _p(t), _p(ra), _p(loss), _p(wsi), _p(wtsi))
+    return [loss, wsi, wtsi]
+
+
+def distortion_loss_bw(dL_dloss, ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a):
+    """losses.cu:143-173 -> dL_dws (N)"""
+    f = lambda x: _c(x, torch.float32)
+    a = [f(dL_dloss), f(ws_inclusive_scan), f(wts_inclusive_scan), f(ws), f(deltas), f(ts), _c(rays_a, torch.int64)]
+    dws = torch.zeros(a[3].shape[0])
+    lib().or_distortion_loss_bw(a[6].shape[0], *[_p(x) for x in a], _p(dws))
+    return dws
 
 
 # ------------------------------------------------ tcnn-semantics hash grid

@@ -396,6 +396,56 @@ void or_composite_test_fw(int n_alive, int Ns, const float* sigmas, const float*
     }
 }
 
+/* ------------------------------------------------ distortion loss */
+/* losses.cu:8-107 (DVGO-v2 form of the Mip-NeRF 360 distortion loss).
+ * thrust::inclusive/exclusive_scan and reduce inside a kernel thread run
+ * sequentially (no dynamic parallelism): left folds from 0.  wts = ws*ts and
+ * the _loss expression are separate torch ops (:70, :92-93), each rounded.
+ * Outputs zeroed by the caller (torch::zeros, :72-75,95). */
+void or_distortion_loss_fw(int n_rays, const float* ws, const float* deltas, const float* ts,
+                           const int64_t* rays_a, float* loss, float* ws_inc, float* wts_inc) {
+    const float third = 1.0f / 3;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int n = 0; n < n_rays; ++n) {
+        const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+        float a = 0.f, b = 0.f, acc = 0.f;
+        for (int64_t k = 0; k < N; ++k) {
+            const int64_t s = start + k;
+            const float wts = ws[s] * ts[s];
+            const float ws_exc = a, wts_exc = b;
+            a = a + ws[s];
+            b = b + wts;
+            ws_inc[s] = a;
+            wts_inc[s] = b;
+            const float p = b * ws_exc, q = a * wts_exc;
+            const float l = 2 * (p - q) + ((third * ws[s]) * ws[s]) * deltas[s];
+            acc = acc + l;
+        }
+        loss[ray] = acc;
+    }
+}
+
+/* losses.cu:110-140 */
+void or_distortion_loss_bw(int n_rays, const float* dL_dloss, const float* ws_inc, const float* wts_inc,
+                           const float* ws, const float* deltas, const float* ts, const int64_t* rays_a,
+                           float* dL_dws) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int n = 0; n < n_rays; ++n) {
+        const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+        if (N <= 0) continue;
+        const int64_t end = start + N - 1;
+        const float ws_sum = ws_inc[end], wts_sum = wts_inc[end];
+        const float g = dL_dloss[ray];
+        for (int64_t s = start; s <= end; ++s) {
+            const float A = s == start ? 0.0f : ts[s] * ws_inc[s - 1] - wts_inc[s - 1];
+            const float B = (wts_sum - wts_inc[s]) - ts[s] * (ws_sum - ws_inc[s]);
+            const float x = (g * 2) * (A + B);
+            const float y = (((g * 2.0f) / 3.0f) * ws[s]) * deltas[s];
+            dL_dws[s] = x + y;
+        }
+    }
+}
+
 /* ------------------------------------------- multires hash grid (a4) */
 /* tiny-cuda-nn GridEncoding (Hash, Linear), restated from its published
  * algorithm as configured at models/networks.py:33-49:
