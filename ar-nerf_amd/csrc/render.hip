@@ -8,8 +8,9 @@
 //                           N_samples = max(min(N_rays // N_alive, 64), min_samples)
 //                           (rendering.py:188-195)
 //   render_march_kernel     raymarching_test for the alive rays (raymarching.cu:335-404,
-//                           identical walk to march_test_kernel) into slots
-//                           [n*N_samples + s]; appends the valid slots to a sample
+//                           identical walk to march_test_kernel) into SAMPLE-MAJOR
+//                           slots [s*N_alive + n] (lane-per-ray stores and the
+//                           composite's loads coalesce across lanes); appends the valid slots to a sample
 //                           list (the reference's valid_mask, rendering.py:204)
 //   (field kernels)         ngp_hash_encode + ngp_field_mlp_forward over the list
 //   render_composite_kernel composite_test_fw (volumerendering.cu:204-284) and the
@@ -74,6 +75,29 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
+// Block-wide append (blockDim 256, called by every thread of the block):
+// this thread's first index for `cnt` items; ONE counter atomic per block
+// (same-address atomics serialise: one per wave cost ~100 us per iteration
+// at 640K rays).
+__device__ __forceinline__ int64_t block_append(int cnt, unsigned long long* counter) {
+    __shared__ int wtot[4];
+    __shared__ int64_t boff;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int incl = wave_incl_scan(cnt);
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        boff = tot ? (int64_t)atomicAdd(counter, (unsigned long long)tot) : 0;
+    }
+    __syncthreads();
+    int before = 0;
+    for (int i = 0; i < w; ++i) before += wtot[i];
+    const int64_t off = boff + before + incl - cnt;
+    __syncthreads();  // wtot / boff are reused by the next call
+    return off;
+}
+
 template <bool SIMPLE>
 __global__ void __launch_bounds__(256) render_march_kernel(const float* __restrict__ rays_o,
                                                            const float* __restrict__ rays_d,
@@ -92,10 +116,10 @@ __global__ void __launch_bounds__(256) render_march_kernel(const float* __restri
     WordCache wc;
     wc.sum = load_summary(p, ssum);
     __syncthreads();
-    const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t wbase = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); wbase < n_alive; wbase += stride) {
-        const int64_t n = wbase + lane;
+    // block-uniform trip count (block_append synchronises the block)
+    for (int64_t bbase = (int64_t)blockIdx.x * blockDim.x; bbase < n_alive; bbase += stride) {
+        const int64_t n = bbase + threadIdx.x;
         int s = 0;
         if (n < n_alive) {
             const int64_t r = alive[n];
@@ -104,12 +128,11 @@ __global__ void __launch_bounds__(256) render_march_kernel(const float* __restri
             float t = hits_t[2 * r];
             const float t2 = hits_t[2 * r + 1];
             float x, y, z, dt, t_emit = t;
-            const int64_t base = n * (int64_t)Ns;
             while (t < t2 && s < Ns) {  // raymarching.cu:366-400
                 const float tc = t;
                 if (march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc)) {
                     t_emit = t;
-                    const int64_t q = base + s;
+                    const int64_t q = s * n_alive + n;  // sample-major: lanes' stores coalesce
                     xyzs[3 * q] = x; xyzs[3 * q + 1] = y; xyzs[3 * q + 2] = z;
                     dirs[3 * q] = d[0]; dirs[3 * q + 1] = d[1]; dirs[3 * q + 2] = d[2];
                     ts[q] = tc;
@@ -120,16 +143,9 @@ __global__ void __launch_bounds__(256) render_march_kernel(const float* __restri
             if (s) hits_t[2 * r] = t_emit;  // raymarching.cu:390: t after the last emitted sample
             n_eff[n] = s;
         }
-        // append this wave's valid slots to the sample list (one atomic per wave)
-        const int incl = wave_incl_scan(s);
-        const int total = __shfl(incl, 63, 64);
-        if (total == 0) continue;
-        int64_t off = 0;
-        if (lane == 0) off = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(&state[RS_VALID]),
-                                                (unsigned long long)total);
-        off = __shfl(off, 0, 64) + (incl - s);
-        const int64_t base = n * (int64_t)Ns;
-        for (int k = 0; k < s; ++k) sample_idx[off + k] = (int32_t)(base + k);
+        // append the valid slots to the sample list
+        const int64_t off = block_append(s, reinterpret_cast<unsigned long long*>(&state[RS_VALID]));
+        for (int k = 0; k < s; ++k) sample_idx[off + k] = (int32_t)(k * n_alive + n);
     }
 }
 
@@ -145,11 +161,11 @@ __global__ void __launch_bounds__(256) render_composite_kernel(const float* __re
                                                                float* __restrict__ rgb) {
     if (!state[RS_ACTIVE]) return;
     const int64_t n_alive = state[parity];
-    const int Ns = (int)state[RS_NS];
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t wbase = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); wbase < n_alive; wbase += stride) {
-        const int64_t n = wbase + lane;
+    int my_total = 0;
+    for (int64_t bbase = (int64_t)blockIdx.x * blockDim.x; bbase < n_alive; bbase += stride) {  // block-uniform
+        const int64_t n = bbase + threadIdx.x;
         bool keep = false;
         int ne = 0;
         int32_t r = -1;
@@ -161,7 +177,7 @@ __global__ void __launch_bounds__(256) render_composite_kernel(const float* __re
                 float op = opacity[r], dp = depth[r], cr = rgb[3 * r], cg = rgb[3 * r + 1], cb = rgb[3 * r + 2];
                 float T = 1 - op;
                 for (int s = 0; s < ne; ++s) {  // volumerendering.cu:228-256
-                    const int64_t o = n * (int64_t)Ns + s;
+                    const int64_t o = s * n_alive + n;  // sample-major slots (render_march_kernel)
                     const float a = 1.0f - __expf(-sigmas[o] * deltas[o]);
                     const float w = a * T;
                     cr += w * rgbs[3 * o]; cg += w * rgbs[3 * o + 1]; cb += w * rgbs[3 * o + 2];
@@ -175,22 +191,14 @@ __global__ void __launch_bounds__(256) render_composite_kernel(const float* __re
                 opacity[r] = op;
             }
         }
-        // total_samples += N_eff_samples.sum() (rendering.py:199)
-        int tot = ne;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-        const uint64_t live = __ballot(keep);
-        const int n_keep = __popcll(live);
-        int64_t off = 0;
-        if (lane == 0) {
-            if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&state[RS_TOTAL]), (unsigned long long)tot);
-            if (n_keep)
-                off = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(&state[parity ^ 1]),
-                                         (unsigned long long)n_keep);
-        }
-        off = __shfl(off, 0, 64);
-        if (keep) alive_out[off + __popcll(live & ((1ull << lane) - 1ull))] = r;
+        my_total += ne;  // total_samples += N_eff_samples.sum() (rendering.py:199)
+        const int64_t off = block_append(keep ? 1 : 0, reinterpret_cast<unsigned long long*>(&state[parity ^ 1]));
+        if (keep) alive_out[off] = r;
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) my_total += __shfl_xor(my_total, o, 64);
+    if (lane == 0 && my_total)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&state[RS_TOTAL]), (unsigned long long)my_total);
 }
 
 // rendering.py:240-251: rgb += bg * (1 - opacity)
@@ -260,7 +268,7 @@ int ngp_render_test_composite(const float* sigmas, const float* rgbs, const floa
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(sigmas && rgbs && deltas && ts && n_eff && alive_in && alive_out && alive_in != alive_out &&
                   opacity && depth && rgb);
-    const unsigned blocks = std::min(nblk(n_rays, 256), 2048u);
+    const unsigned blocks = std::min(nblk(n_rays, 256), 1024u);
     render_composite_kernel<<<blocks, 256, 0, as_stream(stream)>>>(sigmas, rgbs, deltas, ts, n_eff, state, parity,
                                                                   alive_in, alive_out, T_threshold, opacity, depth,
                                                                   rgb);

@@ -11,9 +11,10 @@ TestRenderer runs the same loop with every decision in device memory
   ngp_render_test_march   (loop test, N_samples, march, valid-sample list)
   ngp_hash_encode + ngp_field_mlp_forward over the list (NGP.forward)
   ngp_render_test_composite (composite_test_fw + survivor compaction)
-and `iters_per_graph` iterations are captured in one HIP graph.  A frame is
-graph A (begin + summary + K iterations), then graph B (K more) only while
-the device says the loop is still running -- one host sync per K iterations.
+and the iterations are captured in HIP graphs: a frame is graph A (begin +
+summary + `iters_per_graph` iterations), then graph B (`iters_tail` more)
+only while the device says the loop is still running -- one host sync per
+graph; iterations after the loop ends are no-ops (early exits).
 Results (opacity, depth, rgb, total_samples) equal the host loop's bit for
 bit: tests/test_renderer_gpu.py.
 """
@@ -45,9 +46,10 @@ class TestRenderer:
 
     def __init__(self, n_rays, grid: HG.HashGrid, params16, density_bitfield, cascades, scale, grid_size=128,
                  exp_step_factor=0.0, T_threshold=1e-4, max_samples=MAX_SAMPLES, iters_per_graph=16,
-                 bg_rgb=(0.0, 0.0, 0.0), use_graphs=True):
-        if iters_per_graph < 2 or iters_per_graph % 2:
-            raise ValueError("iters_per_graph must be even (alive lists alternate per iteration)")
+                 bg_rgb=(0.0, 0.0, 0.0), use_graphs=True, iters_tail=None):
+        iters_tail = iters_per_graph if iters_tail is None else iters_tail
+        if min(iters_per_graph, iters_tail) < 2 or iters_per_graph % 2 or iters_tail % 2:
+            raise ValueError("iters_per_graph / iters_tail must be even (alive lists alternate per iteration)")
         dev = params16.device
         vren._check("params16", params16, torch.float16)
         vren._check("density_bitfield", density_bitfield, torch.uint8)
@@ -56,7 +58,8 @@ class TestRenderer:
         self.esf, self.T_threshold, self.max_samples = float(exp_step_factor), float(T_threshold), int(max_samples)
         # rendering.py:185: min_samples = 1 if exp_step_factor == 0 else 4
         self.min_samples = 1 if self.esf == 0 else 4
-        self.K, self.use_graphs = int(iters_per_graph), bool(use_graphs)
+        # graph A: frame opening + K iterations; graph B (replayed while the loop runs): K_tail
+        self.K, self.K_tail, self.use_graphs = int(iters_per_graph), int(iters_tail), bool(use_graphs)
         self.bg = (ctypes.c_float * 3)(*[float(b) for b in bg_rgb])
         L = HG._lib()
         self.cap = int(L.ngp_render_test_capacity(self.n_rays, self.min_samples))
@@ -115,10 +118,10 @@ class TestRenderer:
         vren.bitfield_summary(self.bitfield, self.grid_size, out=self.summary)
 
     def _run(self, first):
-        """K iterations (graph A also opens the frame)."""
+        """K iterations (graph A, which also opens the frame) or K_tail (graph B)."""
         if first:
             self._begin()
-        for k in range(self.K):
+        for k in range(self.K if first else self.K_tail):
             self._iteration(k)
 
     def _launch(self, first):

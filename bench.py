@@ -131,7 +131,7 @@ def inference_bench(trainer, res, frames, world, rank):
     sc = S.AnalyticScene(W=res, H=res, n_images=max(2, frames), scale=trainer.scale, seed=321 + rank)
     n = res * res
     rr = RD.TestRenderer(n, trainer.grid, trainer.params16, trainer.density_bitfield, trainer.cascades,
-                         trainer.scale, trainer.G, exp_step_factor=trainer.esf)
+                         trainer.scale, trainer.G, exp_step_factor=trainer.esf, iters_per_graph=16, iters_tail=8)
     rr.set_camera(sc.directions.cuda(), trainer.center, trainer.half_size)
     poses = sc.poses.cuda()
     for i in range(2):  # capture + warm
@@ -165,7 +165,7 @@ def inference_bench(trainer, res, frames, world, rank):
             "samples_per_ray": round(samples / (frames * n), 2), "graphs": True,
             "host_loop_ms_per_frame": round(t_host * 1e3, 3), "host_loop_bit_exact": same,
             "workload": "full-frame test render of the trained model (black bg), march+field+composite per "
-                        "iteration in HIP graphs, one host sync per 16 iterations"}
+                        "iteration in HIP graphs (16 iterations, then 8 per replay while rays remain), one host sync per graph"}
 
 
 def cpu_baseline(trainer, scene, gt_images, budget_s, batch):

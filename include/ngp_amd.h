@@ -202,7 +202,7 @@ int ngp_render_test_begin(int64_t n_rays, int64_t* state, int32_t* alive0, float
                           void* stream);
 /* Loop test + N_samples (rendering.py:186-195), then raymarching_test
  * (raymarching.cu:335-404, `cascades` as calc_dt's scale) over the alive rays
- * into slots [n*N_samples + s] (hits_t (n_rays,2) t1 advanced in place), and
+ * into slots [s*N_alive + n] (sample-major) (hits_t (n_rays,2) t1 advanced in place), and
  * the valid slots appended to sample_idx (count in state[5]). */
 int ngp_render_test_march(const float* rays_o, const float* rays_d, float* hits_t, int64_t n_rays,
                           const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
