@@ -127,6 +127,108 @@ __device__ __forceinline__ float start_t(const float* hits_t, const float* noise
     return t1;
 }
 
+// ---------------------------------------------- wave-per-ray lattice march
+// For SIMPLE launches (one cascade, esf = 0) every t the walk ever holds is a
+// point of the lattice t_0, t_{k+1} = fl(t_k + dt) with a constant dt, and
+// that lattice has a closed form: inside one binade [2^e, 2^(e+1)) adding dt
+// moves a multiple of the binade's ulp u by the SAME multiple of u every time
+// (dt/u has no exact .5 fraction; with one, the increment is constant from
+// the second step on), so t_k = t_s + (k - s) * inc_s exactly (fmaf of an
+// exact product).  The walk (march_step) from point k goes to k + 1 when the
+// cell at t_k is occupied, else to the first j > k with t_j >= t_target(k).
+// So one wave takes one ray: lane i evaluates lattice point c + i of a
+// 64-point window (occupancy + jump target, in parallel), then the wave
+// follows the walk's chain through the window with scalar readlanes and
+// writes the visited occupied points with one coalesced store.  Bit-identical
+// to the serial walk; ~8192 waves per batch instead of 128 latency-bound ones.
+//
+// Segment table (per ray, in LDS): segment q starts at lattice index K[q]
+// with value T[q] and advances by I[q] per index until K[q + 1].
+constexpr int LSEG = 32;
+struct LatSeg {
+    int K[LSEG + 1];
+    float T[LSEG], I[LSEG];
+};
+
+__device__ __forceinline__ float lat_t(const LatSeg& sg, int q, int k) {
+    return fmaf((float)(k - sg.K[q]), sg.I[q], sg.T[q]);
+}
+
+// Builds the segments from t0 (>= 0) until the lattice passes t2 and returns
+// k_end = first index with t >= t2 (the walk's stop), or -1 if the table
+// overflows (caller falls back to the serial walk).  Wave-uniform.
+__device__ __forceinline__ int lat_build(float t0, float t2, float dt, LatSeg& sg, int& nseg, bool write) {
+    int k = 0, q = 0;
+    float ts = t0;
+    while (true) {
+        if (!(ts < t2)) {  // this point already stops the walk
+            if (write) sg.K[q] = k;
+            nseg = q;
+            return k;
+        }
+        if (q == LSEG) return -1;
+        int e;
+        frexpf(ts, &e);
+        const float upper = ldexpf(1.0f, e);  // binade [upper/2, upper)
+        const float a = ts + dt, b = a + dt;
+        int n_max;  // last index offset of this segment
+        float inc;
+        if (!(a > ts)) return -1;  // dt below half an ulp: no progress, leave it to the serial walk
+        if (!(b < upper) || (b - a) != (a - ts)) {
+            n_max = 0;  // single-point segment (binade end or a tie step)
+            inc = a - ts;
+        } else {
+            inc = a - ts;
+            n_max = (int)ceilf((upper - ts) / inc) - 1;
+            while (fmaf((float)(n_max + 1), inc, ts) < upper) ++n_max;
+            while (n_max > 0 && !(fmaf((float)n_max, inc, ts) < upper)) --n_max;
+        }
+        if (write) { sg.K[q] = k; sg.T[q] = ts; sg.I[q] = inc; }
+        // the stop may fall inside this segment
+        const float last = fmaf((float)n_max, inc, ts);
+        if (!(last < t2)) {
+            int n = (int)ceilf((t2 - ts) / inc);
+            n = max(0, min(n, n_max));
+            while (n > 0 && !(fmaf((float)(n - 1), inc, ts) < t2)) --n;
+            while (fmaf((float)n, inc, ts) < t2) ++n;
+            if (write) sg.K[q + 1] = k + n_max + 1;
+            nseg = q + 1;
+            return k + n;
+        }
+        ts = last + dt;  // the step that leaves the binade, as the walk rounds it
+        k += n_max + 1;
+        ++q;
+    }
+}
+
+// first j > k with t_j >= T (capped at k_end), k in segment q
+__device__ __forceinline__ int lat_jump(const LatSeg& sg, int nseg, int q, int k, float T, int k_end) {
+    int j = k + 1;
+    while (q + 1 < nseg && j >= sg.K[q + 1]) ++q;
+    while (j < k_end) {
+        const float tj = lat_t(sg, q, j);
+        if (tj >= T) return j;
+        const int send = q + 1 < nseg ? sg.K[q + 1] : k_end;
+        const float need = (T - tj) / sg.I[q];
+        // jump close to the answer, then fix up with exact lattice values
+        int m = need < 4096.f ? max(1, (int)need) : 4096;
+        int jj = min(j + m, send);
+        while (jj > j + 1 && lat_t(sg, q, jj - 1) >= T) --jj;
+        if (jj >= send) {  // target lies beyond this segment
+            if (send >= k_end) return k_end;
+            j = send;
+            ++q;
+            continue;
+        }
+        while (jj < send && lat_t(sg, q, jj) < T) ++jj;
+        if (jj < send) return jj;
+        if (send >= k_end) return k_end;
+        j = send;
+        ++q;
+    }
+    return k_end;
+}
+
 }  // namespace ngp
 
 using ngp::MarchParams;

@@ -98,6 +98,176 @@ __device__ __forceinline__ int64_t block_append(int cnt, unsigned long long* cou
     return off;
 }
 
+// ---- wave-per-ray mode (SIMPLE launches, N_samples >= WAVE_NS) ----------
+// Late iterations have few alive rays with many samples each: one lane per
+// ray leaves most of the chip idle while each lane walks ~N_samples occupied
+// points serially.  Here one wave takes one ray and walks it with the
+// lattice machinery of march_slots_wave_kernel (march.hip: the fp32 t-lattice
+// in closed form per binade, a 64-point window evaluated in parallel, the
+// walk's chain resolved by pointer doubling) -- the same points as the serial
+// walk, bit for bit.  Sample indices are staged in LDS and appended with one
+// global atomic per block flush.
+constexpr int WAVE_NS = 16;  // default threshold (NGP_RENDER_WAVE_NS overrides, for A/B runs)
+constexpr int STAGE = 2048;
+
+struct WaveLds {
+    LatSeg segs[4];
+    int32_t stage[STAGE];
+    int nst;
+    int64_t goff;
+};
+
+__device__ __forceinline__ void stage_flush(WaveLds& L, int64_t* state, int32_t* sample_idx) {
+    if (threadIdx.x == 0)
+        L.goff = L.nst ? (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(&state[RS_VALID]),
+                                            (unsigned long long)L.nst)
+                       : 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < L.nst; i += blockDim.x) sample_idx[L.goff + i] = L.stage[i];
+    __syncthreads();
+    if (threadIdx.x == 0) L.nst = 0;
+    __syncthreads();
+}
+
+__device__ void render_march_waves(const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+                                   float* __restrict__ hits_t, const MarchParams& p, WordCache& wc,
+                                   int64_t* __restrict__ state, int64_t n_alive, int Ns,
+                                   const int32_t* __restrict__ alive, float* __restrict__ xyzs,
+                                   float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts,
+                                   int32_t* __restrict__ n_eff, int32_t* __restrict__ sample_idx, WaveLds& L) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float dt = NGP_SQRT3 / p.max_samples;
+    if (threadIdx.x == 0) L.nst = 0;
+    __syncthreads();
+    for (int64_t b0 = (int64_t)blockIdx.x * 4; b0 < n_alive; b0 += (int64_t)gridDim.x * 4) {  // block-uniform
+        const int64_t n = b0 + w;
+        if (n < n_alive) {
+            const int64_t r = alive[n];
+            float o[3], d[3], dinv[3];
+            load_ray(rays_o, rays_d, r, o, d, dinv);
+            const float t0 = hits_t[2 * r], t2 = hits_t[2 * r + 1];
+            int N = 0;
+            bool near = t0 < t2;  // raymarching.cu:366 loop condition at entry
+            if (near && wc.dil) {
+                // exact early out (march_slots_wave_kernel): no occupied block
+                // within one block of the segment -> the walk emits nothing
+                const float mb = fminf(0.5f, p.scale);
+                const float dn = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+                const float step = 0.45f * (4.0f * 2.0f * mb / p.grid_size) / dn;
+                const int npts = (int)ceilf((t2 - t0) / step) + 1;
+                const float gm1 = p.grid_size - 1.0f, mbi = 1 / mb;
+                bool any = false;
+                for (int j0 = 0; j0 < npts && !any; j0 += 64) {
+                    const int j = j0 + lane;
+                    bool b = false;
+                    if (j < npts) {
+                        const float t = fminf(t0 + (float)j * step, t2);
+                        const float x = o[0] + t * d[0], y = o[1] + t * d[1], z = o[2] + t * d[2];
+                        const int nx = (int)clampf(0.5f * (x * mbi + 1) * p.grid_size, 0.0f, gm1);
+                        const int ny = (int)clampf(0.5f * (y * mbi + 1) * p.grid_size, 0.0f, gm1);
+                        const int nz = (int)clampf(0.5f * (z * mbi + 1) * p.grid_size, 0.0f, gm1);
+                        const uint32_t wi = morton3((uint32_t)nx >> 2, (uint32_t)ny >> 2, (uint32_t)nz >> 2);
+                        b = (wc.dil[wi >> 5] >> (wi & 31u)) & 1u;
+                    }
+                    any = __ballot(b) != 0ull;
+                }
+                near = any;
+            }
+            if (near) {
+                LatSeg& sg = L.segs[w];
+                int nseg = 0;
+                const int k_end = t0 >= 0 ? lat_build(t0, t2, dt, sg, nseg, lane == 0) : -1;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (k_end < 0) {  // table overflow: the serial walk on lane 0
+                    if (lane == 0) {
+                        float t = t0, x, y, z, dts, t_emit = t0;
+                        while (t < t2 && N < Ns) {
+                            const float tc = t;
+                            if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) {
+                                t_emit = t;
+                                const int64_t q = N * n_alive + n;
+                                xyzs[3 * q] = x; xyzs[3 * q + 1] = y; xyzs[3 * q + 2] = z;
+                                dirs[3 * q] = d[0]; dirs[3 * q + 1] = d[1]; dirs[3 * q + 2] = d[2];
+                                ts[q] = tc;
+                                deltas[q] = dts;
+                                N++;
+                            }
+                        }
+                        if (N) hits_t[2 * r] = t_emit;
+                    }
+                    N = __builtin_amdgcn_readfirstlane(N);
+                } else {
+                    int c = 0, q0 = 0;
+                    while (c < k_end && N < Ns) {
+                        while (q0 + 1 < nseg && c >= sg.K[q0 + 1]) ++q0;
+                        const int k = c + lane;
+                        int q = q0;
+                        while (q + 1 < nseg && k >= sg.K[q + 1]) ++q;
+                        const bool live = k < k_end;
+                        const float tk = live ? lat_t(sg, q, k) : 0.f;
+                        bool occ = false;
+                        int nxt = k_end;
+                        float x = 0.f, y = 0.f, z = 0.f;
+                        if (live) {
+                            float dts, T;
+                            occ = march_probe<true>(tk, o, d, dinv, p, x, y, z, dts, wc, T);
+                            nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
+                        }
+                        const uint64_t occm = __ballot(occ && live);
+                        int J[6];
+                        J[0] = live ? min(nxt - c, 64) : 64;
+#pragma unroll
+                        for (int b = 1; b < 6; ++b) {
+                            const int prev = J[b - 1];
+                            const int v = __builtin_amdgcn_ds_bpermute(min(prev, 63) << 2, prev);
+                            J[b] = prev >= 64 ? 64 : v;
+                        }
+                        int cur = 0;
+#pragma unroll
+                        for (int b = 5; b >= 0; --b) {
+                            const int v = __builtin_amdgcn_ds_bpermute(min(cur, 63) << 2, J[b]);
+                            const int to = cur >= 64 ? 64 : v;
+                            if (to <= lane) cur = to;
+                        }
+                        uint64_t vis = __ballot(cur == lane);
+                        const int last = 63 - __builtin_clzll(vis);
+                        const int pnt = __builtin_amdgcn_readlane(nxt, last);
+                        vis &= occm;
+                        const int room = Ns - N;
+                        const int nv = __builtin_popcountll(vis);
+                        const int ne = min(nv, room);
+                        if ((vis >> lane) & 1ull) {
+                            const int rank = __builtin_popcountll(vis & ((1ull << lane) - 1ull));
+                            if (rank < room) {
+                                const int64_t qq = (N + rank) * n_alive + n;
+                                xyzs[3 * qq] = x; xyzs[3 * qq + 1] = y; xyzs[3 * qq + 2] = z;
+                                dirs[3 * qq] = d[0]; dirs[3 * qq + 1] = d[1]; dirs[3 * qq + 2] = d[2];
+                                ts[qq] = tk;
+                                deltas[qq] = dt;
+                                if (rank == ne - 1) hits_t[2 * r] = tk + dt;  // raymarching.cu:390
+                            }
+                        }
+                        N += ne;
+                        c = pnt;
+                    }
+                }
+            }
+            int base = 0;
+            if (lane == 0) {
+                n_eff[n] = N;
+                base = N ? atomicAdd(&L.nst, N) : 0;  // LDS
+            }
+            base = __builtin_amdgcn_readfirstlane(base);
+            for (int k = lane; k < N; k += 64) L.stage[base + k] = (int32_t)(k * n_alive + n);
+        }
+        __syncthreads();
+        if (L.nst > STAGE - 4 * 64) stage_flush(L, state, sample_idx);  // block-uniform (read after the barrier)
+    }
+    stage_flush(L, state, sample_idx);
+}
+
 template <bool SIMPLE>
 __global__ void __launch_bounds__(256) render_march_kernel(const float* __restrict__ rays_o,
                                                            const float* __restrict__ rays_d,
@@ -107,15 +277,26 @@ __global__ void __launch_bounds__(256) render_march_kernel(const float* __restri
                                                            float* __restrict__ xyzs, float* __restrict__ dirs,
                                                            float* __restrict__ deltas, float* __restrict__ ts,
                                                            int32_t* __restrict__ n_eff,
-                                                           int32_t* __restrict__ sample_idx) {
+                                                           int32_t* __restrict__ sample_idx, int wave_ns) {
     if (!state[RS_ACTIVE]) return;
     const int64_t n_alive = state[parity];
-    if ((int64_t)blockIdx.x * blockDim.x >= n_alive) return;  // block-uniform, before the barrier
     const int Ns = (int)state[RS_NS];
+    const bool waves = SIMPLE && Ns >= wave_ns;
+    // block-uniform, before the barrier
+    if ((int64_t)blockIdx.x * (waves ? 4 : blockDim.x) >= n_alive) return;
     extern __shared__ uint32_t ssum[];
     WordCache wc;
     wc.sum = load_summary(p, ssum);
+    wc.dil = wc.sum ? wc.sum + p.n_sum32 : nullptr;
     __syncthreads();
+    if constexpr (SIMPLE) {
+        if (waves) {
+            __shared__ WaveLds L;
+            render_march_waves(rays_o, rays_d, hits_t, p, wc, state, n_alive, Ns, alive, xyzs, dirs, deltas, ts,
+                               n_eff, sample_idx, L);
+            return;
+        }
+    }
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     // block-uniform trip count (block_append synchronises the block)
     for (int64_t bbase = (int64_t)blockIdx.x * blockDim.x; bbase < n_alive; bbase += stride) {
@@ -251,12 +432,13 @@ int ngp_render_test_march(const float* rays_o, const float* rays_d, float* hits_
     if (n_rays == 0) return ngp_launch_status();
     NGP_CHECK_ARG(rays_o && rays_d && hits_t && alive && xyzs && dirs && deltas && ts && n_eff && sample_idx);
     const unsigned blocks = std::min(nblk(n_rays, 256), 2048u);
+    static const int wave_ns = getenv("NGP_RENDER_WAVE_NS") ? atoi(getenv("NGP_RENDER_WAVE_NS")) : WAVE_NS;
     if (march_simple(p))
         render_march_kernel<true><<<blocks, 256, march_summary_lds(p), s>>>(
-            rays_o, rays_d, hits_t, p, state, parity, alive, xyzs, dirs, deltas, ts, n_eff, sample_idx);
+            rays_o, rays_d, hits_t, p, state, parity, alive, xyzs, dirs, deltas, ts, n_eff, sample_idx, wave_ns);
     else
         render_march_kernel<false><<<blocks, 256, march_summary_lds(p), s>>>(
-            rays_o, rays_d, hits_t, p, state, parity, alive, xyzs, dirs, deltas, ts, n_eff, sample_idx);
+            rays_o, rays_d, hits_t, p, state, parity, alive, xyzs, dirs, deltas, ts, n_eff, sample_idx, wave_ns);
     return ngp_launch_status();
 }
 
