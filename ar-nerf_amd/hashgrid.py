@@ -42,6 +42,7 @@ def _lib():
         P = ctypes.POINTER(ngp_hashgrid_t)
         L.ngp_field_forward.argtypes = [vp, vp, c_int64, vp, P, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_density_forward.argtypes = [vp, c_int64, vp, P, vp, vp, vp, vp, vp]
+        L.ngp_density_input_grad.argtypes = [vp, c_int64, P, vp, vp, vp, vp, vp]
         L.ngp_field_backward.argtypes = [vp, vp, c_int64, vp, P, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_backward_mlp.argtypes = [vp, c_int64, vp, vp, vp, c_int64, vp, vp, vp, vp, vp, vp]
         L.ngp_hash_encode.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
@@ -54,7 +55,7 @@ def _lib():
         L.ngp_hash_binned_apply.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, vp]
         L.ngp_hash_backward_binned_workspace.argtypes = [c_int64]
         L.ngp_hash_backward_binned_workspace.restype = ctypes.c_size_t
-        for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_field_backward, L.ngp_field_backward_mlp,
+        for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_density_input_grad, L.ngp_field_backward, L.ngp_field_backward_mlp,
                   L.ngp_hash_encode, L.ngp_field_mlp_forward, L.ngp_field_forward_indexed,
                   L.ngp_hash_backward, L.ngp_hash_backward_binned, L.ngp_hash_backward_levels,
                   L.ngp_hash_binned_plan, L.ngp_hash_binned_apply):
@@ -146,6 +147,21 @@ def density_forward(xyzs, grid: HashGrid, params16, want_h=False, n_dev=None):
                                     _ptr(params16), _ptr(sig), _ptr(h), vren._stream())
     vren._ok(st, "ngp_density_forward")
     return sig, h
+
+
+def density_input_grad(xyzs, grid: HashGrid, params16, dL_dsigma=None):
+    """dL/dx (n,3) of NGP.density through hash grid + density MLP + TruncExp
+    (dL_dsigma None = ones: d sigma / d x, render_surface_normal)."""
+    n = xyzs.shape[0]
+    _check(xyzs, "xyzs", torch.float32)
+    _check(params16, "params16", torch.float16, grid.n_params)
+    if dL_dsigma is not None:
+        _check(dL_dsigma, "dL_dsigma", torch.float32)
+    out = torch.empty(n, 3, device=xyzs.device)
+    st = _lib().ngp_density_input_grad(_ptr(xyzs), n, ctypes.byref(grid.desc), _ptr(params16[MLP_PARAMS:]),
+                                       _ptr(params16), _ptr(dL_dsigma), _ptr(out), vren._stream())
+    vren._ok(st, "ngp_density_input_grad")
+    return out
 
 
 def field_backward(xyzs, dirs, grid: HashGrid, params16, enc, dL_dsig, dL_drgb, grad, n_dev=None, denc_ws=None):

@@ -34,10 +34,14 @@ class _DensityFn(torch.autograd.Function):
         xyzs, dirs, enc = ctx.saved_tensors
         n = xyzs.shape[0]
         dsig = torch.zeros(n, device=xyzs.device) if dsig is None else dsig.float().contiguous()
-        grad = torch.zeros(ctx.grid.n_params, device=xyzs.device)
-        HG.field_backward(xyzs.contiguous(), dirs, ctx.grid, ctx.p16, enc, dsig,
-                          torch.zeros(n, 3, device=xyzs.device), grad)
-        return None, grad, None, None
+        grad = dx = None
+        if ctx.needs_input_grad[1]:
+            grad = torch.zeros(ctx.grid.n_params, device=xyzs.device)
+            HG.field_backward(xyzs.contiguous(), dirs, ctx.grid, ctx.p16, enc, dsig,
+                              torch.zeros(n, 3, device=xyzs.device), grad)
+        if ctx.needs_input_grad[0]:  # d sigma / d x through the hash grid (render_surface_normal)
+            dx = HG.density_input_grad(xyzs.float().contiguous(), ctx.grid, ctx.p16, dsig)
+        return dx, grad, None, None
 
 
 class NGP(nn.Module):
@@ -82,7 +86,7 @@ class NGP(nn.Module):
     def density(self, x, return_feat=False):
         """networks.py:95-108 -> sigmas (N) [, h (N,16) fp16]"""
         x = x.float().contiguous()
-        if torch.is_grad_enabled() and self.params.requires_grad:
+        if torch.is_grad_enabled() and (self.params.requires_grad or x.requires_grad):
             sig, h = _DensityFn.apply(x, self.params, self.grid, self._shadow)
         else:
             sig, h = HG.density_forward(x, self.grid, self._shadow.get(), want_h=return_feat)

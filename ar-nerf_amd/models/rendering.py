@@ -133,7 +133,19 @@ def render_surface_rgb(model, pts, rays_d, **kwargs):
     return rgbs.reshape(H, W, 3)
 
 
+def normalize_eps(vec, eps=1e-6):
+    """insert/insert_utils.py:18-19"""
+    return vec / (torch.norm(vec, dim=-1, keepdim=True) + eps)
+
+
+@torch.enable_grad()
 def render_surface_normal(model, pts, **kwargs):
-    """models/rendering.py:300-312 needs dsigma/dx through the hash grid
-    (input gradient); a 'next' item."""
-    raise NotImplementedError("hash-grid input gradient (render_surface_normal) is not implemented yet")
+    """models/rendering.py:300-313: normals = -normalize(d sigma / d x) at the
+    surface points, the input gradient taken through the hash grid by
+    autograd (NGP.density -> ngp_density_input_grad)."""
+    H, W, _ = pts.shape
+    pts_grad = pts.reshape(-1, 3).detach().clone().requires_grad_(True)
+    sigmas = model.density(pts_grad)
+    normals = torch.autograd.grad(sigmas, pts_grad, torch.ones_like(sigmas))[0]
+    normals = normals.reshape(H, W, 3).nan_to_num(0.0, 1.0, -1.0).detach()
+    return -normalize_eps(normals)

@@ -264,6 +264,13 @@ int ngp_density_forward(const float* xyzs, int64_t n, const int64_t* n_dev, cons
                         const void* table_f16, const void* mlp_f16, float* sigmas, void* h_f16,
                         void* stream);
 
+/* Input gradient of NGP.density (models/networks.py:95-108) through the hash
+ * grid, density MLP and TruncExp (custom_functions.py:162-173): dL_dx (n,3) =
+ * dL_dsigma (n, nullable = ones) * dsigma/dx -- what render_surface_normal
+ * (models/rendering.py:300-313) takes from torch.autograd.grad. */
+int ngp_density_input_grad(const float* xyzs, int64_t n, const ngp_hashgrid_t* grid, const void* table_f16,
+                           const void* mlp_f16, const float* dL_dsigma, float* dL_dx, void* stream);
+
 /* Backward of ngp_field_forward (tcnn's backward for the three modules +
  * TruncExp.backward, custom_functions.py:169-173).  enc_f16 is the forward's
  * saved encoding; dL_dsigmas (n) f32, dL_drgbs (n,3) f32.  denc_ws (n,32) f32

@@ -385,6 +385,42 @@ class OracleNGPField(torch.nn.Module):
         return sig, rgb
 
 
+def density_input_grad(xyz_params, n_dens, spec: "HashGridSpec", x, xyz_min, xyz_max):
+    """d sigma / d x of NGP.density (models/networks.py:95-108) for
+    render_surface_normal (models/rendering.py:300-313), by fp32 autograd:
+    trilinear weights of tcnn's grid encoding as functions of x (corner
+    indices from or_hash_corners), fp16 table / weights, the encoding's VALUE
+    taken bit-exact from or_hash_encode_fwd (straight-through), fp16 storage
+    points in the MLP, TruncExp.backward's clamp.  tcnn's own input-gradient
+    arithmetic is not available here: parity unpinned."""
+    x = _c(x, torch.float32)
+    mn, mx = xyz_min.reshape(1, 3).float(), xyz_max.reshape(1, 3).float()
+    idx, _ = hash_corners(spec, x, mn, mx)
+    table = xyz_params[n_dens:].detach().half().float().view(-1, 2)
+    enc_exact = hash_encode_fwd(spec, x, mn, mx, xyz_params[n_dens:].detach()).float()
+    xg = x.clone().requires_grad_(True)
+    x01 = (xg - mn) / (mx - mn)
+    feats = []
+    for l in range(spec.L):
+        p = x01 * float(spec.scales[l]) + 0.5
+        f = p - torch.floor(p).detach()
+        w = []
+        for c in range(8):
+            wc = 1.0
+            for d in range(3):
+                wc = wc * (f[:, d] if (c >> d) & 1 else 1 - f[:, d])
+            w.append(wc)
+        w = torch.stack(w, 1)  # (n, 8)
+        vals = table[idx[:, l, :].long()]  # (n, 8, 2); or_hash_corners returns global entries
+        feats.append((w[:, :, None] * vals).sum(1))
+    enc = torch.cat(feats, 1)
+    enc = enc_exact + (enc - enc.detach())
+    Ws, _ = mlp_layers(xyz_params[:n_dens].detach(), (2 * spec.L, 64, 16))
+    h = mlp_forward(enc, Ws)
+    sig = TruncExpCPU.apply(h[:, 0])
+    return torch.autograd.grad(sig.sum(), xg)[0]
+
+
 class TruncExpCPU(torch.autograd.Function):
     """custom_functions.py:162-173"""
 
