@@ -1,0 +1,18 @@
+"""datasets/__init__.py of the reference.  Implemented: 'nerf' (NeRF-synthetic
+/ Blender).  The other loaders of the reference (nsvf, colmap, colmap_exr,
+colmap_real_exr, myblender, nerfpp, rtmv) are SURVEY.md §8f rank-2 work not
+done yet; asking for one raises."""
+from .nerf import NeRFDataset
+
+
+class _Missing:
+    def __init__(self, name):
+        self.name = name
+
+    def __call__(self, *a, **k):
+        raise NotImplementedError(f"dataset '{self.name}' is not implemented in this build (only 'nerf')")
+
+
+dataset_dict = {'nerf': NeRFDataset}
+for _n in ('nsvf', 'colmap', 'colmap_exr', 'colmap_real_exr', 'myblender', 'nerfpp', 'rtmv'):
+    dataset_dict[_n] = _Missing(_n)

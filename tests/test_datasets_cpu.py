@@ -1,0 +1,103 @@
+"""NeRF-synthetic ingest (datasets/nerf.py, color_utils.py, ray_utils.py of the
+reference): PNG decoding (all five scanline filters),
+alpha blending onto white, cv2-style linear resize, pose conversion to
+[right down front] at radius 1.5, intrinsics from camera_angle_x."""
+import json
+import math
+import struct
+import zlib
+
+import numpy as np
+import torch
+
+import synthetic as S
+from datasets import NeRFDataset, dataset_dict
+from datasets.png import read_png, write_png
+from datasets.ray_utils import get_ray_directions, get_rays
+
+
+def _png_with_filters(path, img):
+    """Encoder using filter type (row % 5) so the decoder sees every filter."""
+    H, W, C = img.shape
+    rows, prev = [], np.zeros(W * C, np.int32)
+    for y in range(H):
+        cur = img[y].reshape(-1).astype(np.int32)
+        ft = y % 5
+        left = np.concatenate([np.zeros(C, np.int32), cur[:-C]])
+        ul = np.concatenate([np.zeros(C, np.int32), prev[:-C]])
+        if ft == 0:
+            f = cur
+        elif ft == 1:
+            f = cur - left
+        elif ft == 2:
+            f = cur - prev
+        elif ft == 3:
+            f = cur - (left + prev) // 2
+        else:
+            p = left + prev - ul
+            pa, pb, pc = abs(p - left), abs(p - prev), abs(p - ul)
+            f = cur - np.where((pa <= pb) & (pa <= pc), left, np.where(pb <= pc, prev, ul))
+        rows.append(bytes([ft]) + (f & 255).astype(np.uint8).tobytes())
+        prev = cur
+
+    def chunk(kind, body):
+        return struct.pack(">I", len(body)) + kind + body + struct.pack(">I", zlib.crc32(kind + body) & 0xffffffff)
+
+    ctype = {3: 2, 4: 6}[C]
+    with open(path, "wb") as fh:
+        fh.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, 8, ctype, 0, 0, 0)) +
+                 chunk(b"IDAT", zlib.compress(b"".join(rows))) + chunk(b"IEND", b""))
+
+
+def test_png_decoder_all_filters(tmp_path):
+    rng = np.random.default_rng(0)
+    for C in (3, 4):
+        img = rng.integers(0, 256, (13, 11, C), dtype=np.uint8)
+        _png_with_filters(str(tmp_path / "f.png"), img)
+        assert np.array_equal(read_png(str(tmp_path / "f.png")), img)
+        write_png(str(tmp_path / "p.png"), img)
+        assert np.array_equal(read_png(str(tmp_path / "p.png")), img)
+
+
+def test_ray_directions_match_the_bench_camera():
+    K = S.intrinsics(64, 48)
+    assert torch.equal(get_ray_directions(48, 64, K), S.get_ray_directions(48, 64, K))
+    d = get_ray_directions(4, 4, K)
+    c2w = torch.eye(4)[:3]
+    o, r = get_rays(d, c2w)
+    assert torch.equal(r, d) and torch.equal(o, torch.zeros_like(d))
+
+
+def test_nerf_synthetic_loader(tmp_path):
+    angle = 0.6911112070083618  # Lego
+    rng = np.random.default_rng(1)
+    frames, imgs = [], []
+    for i in range(3):
+        th = 2 * math.pi * i / 3
+        c2w = np.eye(4)
+        c2w[:3, 3] = [4.0 * math.cos(th), 4.0 * math.sin(th), 1.0]  # blender units, radius != 1.5
+        frames.append({"file_path": f"./train/r_{i}", "transform_matrix": c2w.tolist()})
+        img = rng.integers(0, 256, (16, 16, 4), dtype=np.uint8)
+        (tmp_path / "train").mkdir(exist_ok=True)
+        write_png(str(tmp_path / "train" / f"r_{i}.png"), img)
+        imgs.append(img)
+    json.dump({"camera_angle_x": angle, "frames": frames}, open(tmp_path / "transforms_train.json", "w"))
+    ds = NeRFDataset(str(tmp_path), split='train', downsample=0.01)
+    assert ds.img_wh == (8, 8)
+    fx = 0.5 * 800 / np.tan(0.5 * angle) * 0.01
+    assert abs(float(ds.K[0, 0]) - fx) < 1e-4 and float(ds.K[0, 2]) == 4.0
+    assert ds.poses.shape == (3, 3, 4) and ds.rays.shape == (3, 64, 3)
+    # [right up back] -> [right down front], camera centre at radius 1.5
+    assert torch.allclose(ds.poses[:, :, 3].norm(dim=1), torch.full((3,), 1.5), atol=1e-5)
+    assert float(ds.poses[0, 1, 1]) == -1.0 and float(ds.poses[0, 2, 2]) == -1.0
+    # alpha blended onto white, then 16 -> 8 linear resize = 2x2 mean
+    f = imgs[0].astype(np.float32) / 255
+    rgb = f[..., :3] * f[..., 3:] + (1 - f[..., 3:])
+    want = rgb.reshape(8, 2, 8, 2, 3).mean((1, 3)).reshape(-1, 3)
+    np.testing.assert_allclose(ds.rays[0].numpy(), want, atol=1e-6)
+    assert ds.gt_u8().dtype == torch.uint8
+    try:
+        dataset_dict['colmap']('x')
+        raise AssertionError("expected NotImplementedError")
+    except NotImplementedError:
+        pass
