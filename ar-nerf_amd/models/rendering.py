@@ -42,11 +42,43 @@ def _background(kwargs, rays_d, default):
     return im if im is not None else default
 
 
+def _test_renderer(model, n_rays, esf, T_threshold, max_samples):
+    """TestRenderer cached on the model per (rays, loop settings, bitfield)."""
+    import renderer as RD
+    cache = model.__dict__.setdefault('_test_renderers', {})
+    key = (n_rays, float(esf), float(T_threshold), int(max_samples), model.density_bitfield.data_ptr())
+    rr = cache.get(key)
+    p16 = model._shadow.get()
+    if rr is None:
+        if len(cache) >= 4:
+            cache.clear()
+        rr = RD.TestRenderer(n_rays, model.grid, p16.clone(), model.density_bitfield, model.cascades, model.scale,
+                             model.grid_size, exp_step_factor=esf, T_threshold=T_threshold, max_samples=max_samples,
+                             iters_per_graph=16, iters_tail=8)
+        rr._src = None
+        cache[key] = rr
+    if rr._src is not p16:  # parameters changed since the last frame: refresh the renderer's copy
+        rr.params16.copy_(p16)
+        rr._src = p16
+    return rr
+
+
 @torch.no_grad()
 def __render_rays_test(model, rays_o, rays_d, hits_t, **kwargs):
     """models/rendering.py:162-253 (grows samples per alive ray, composites
-    until T < T_threshold; black background by default)."""
+    until T < T_threshold; black background by default).  For an NGP on the
+    GPU the loop runs device-resident in HIP graphs (renderer.TestRenderer,
+    bit-identical results); device_loop=False keeps the host-driven loop."""
     exp_step_factor = kwargs.get('exp_step_factor', 0.)
+    if kwargs.get('device_loop', True) and hasattr(model, '_shadow') and rays_o.is_cuda and len(rays_o) > 0:
+        rr = _test_renderer(model, len(rays_o), exp_step_factor, kwargs.get('T_threshold', 1e-4),
+                            kwargs.get('max_samples', MAX_SAMPLES))
+        out = rr.render(rays_o, rays_d, hits_t[:, 0])
+        results = {k: v.clone() for k, v in out.items()}
+        rgb_bg = _background(kwargs, rays_d, torch.zeros(3, device=rays_o.device))
+        if kwargs.get('blend_bkg', True):
+            results['rgb'] += rgb_bg * (1 - results['opacity'])[:, None]
+        return results
     results = {}
     N_rays = len(rays_o)
     device = rays_o.device

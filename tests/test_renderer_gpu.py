@@ -26,7 +26,7 @@ def _hits(model, o, d):
 
 def _host_loop(model, o, d, **kw):
     with torch.no_grad():
-        return render(model, o, d, test_time=True, **kw)
+        return render(model, o, d, test_time=True, device_loop=False, **kw)
 
 
 def _assert_same(res, ref):
@@ -78,6 +78,23 @@ def test_renderer_full_frame_bit_exact(scale, esf, occ):
     _assert_same(res, ref)
     assert rr.last_iterations > 2
     assert float(res["opacity"].max()) > 0
+
+
+def test_render_api_uses_the_device_loop_bit_exact():
+    """render(test_time=True) routes an NGP through the cached TestRenderer:
+    same pixels as the host loop, and a parameter update reaches it."""
+    fx = load("lego_test")
+    model = _product_model(fx)
+    o, d = torch.from_numpy(fx["rays_o"]).to(DEV), torch.from_numpy(fx["rays_d"]).to(DEV)
+    with torch.no_grad():
+        dev = render(model, o, d, test_time=True)
+    _assert_same(dev, _host_loop(model, o, d))
+    assert len(model._test_renderers) == 1
+    with torch.no_grad():
+        model.params.mul_(0.5)
+        dev2 = render(model, o, d, test_time=True)
+    _assert_same(dev2, _host_loop(model, o, d))
+    assert not torch.equal(dev2["rgb"], dev["rgb"])
 
 
 def test_render_pose_equals_rays_path():
