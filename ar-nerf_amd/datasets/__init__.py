@@ -1,8 +1,9 @@
 """datasets/__init__.py of the reference.  Implemented: 'nerf' (NeRF-synthetic
-/ Blender).  The other loaders of the reference (nsvf, colmap, colmap_exr,
+/ Blender) and 'nsvf' (Synthetic_NeRF & co.).  The other loaders of the reference (nsvf, colmap, colmap_exr,
 colmap_real_exr, myblender, nerfpp, rtmv) are SURVEY.md §8f rank-2 work not
 done yet; asking for one raises."""
 from .nerf import NeRFDataset
+from .nsvf import NSVFDataset
 
 
 class _Missing:
@@ -10,9 +11,9 @@ class _Missing:
         self.name = name
 
     def __call__(self, *a, **k):
-        raise NotImplementedError(f"dataset '{self.name}' is not implemented in this build (only 'nerf')")
+        raise NotImplementedError(f"dataset '{self.name}' is not implemented in this build (only 'nerf' and 'nsvf')")
 
 
-dataset_dict = {'nerf': NeRFDataset}
-for _n in ('nsvf', 'colmap', 'colmap_exr', 'colmap_real_exr', 'myblender', 'nerfpp', 'rtmv'):
+dataset_dict = {'nerf': NeRFDataset, 'nsvf': NSVFDataset}
+for _n in ('colmap', 'colmap_exr', 'colmap_real_exr', 'myblender', 'nerfpp', 'rtmv'):
     dataset_dict[_n] = _Missing(_n)

@@ -101,3 +101,28 @@ def test_nerf_synthetic_loader(tmp_path):
         raise AssertionError("expected NotImplementedError")
     except NotImplementedError:
         pass
+
+
+def test_nsvf_synthetic_loader(tmp_path):
+    root = tmp_path / "Synthetic_NeRF" / "Lego"
+    (root / "rgb").mkdir(parents=True)
+    (root / "pose").mkdir()
+    (root / "intrinsics.txt").write_text("1111.1110311937682 0. 0. 0.\n0. 1111.1110311937682 0. 0.\n")
+    (root / "bbox.txt").write_text("-0.6 -1.1 -0.4 0.6 1.1 1.0 0.1\n")
+    rng = np.random.default_rng(2)
+    for split, n in (("0", 2), ("1", 1), ("2", 1)):
+        for i in range(n):
+            c2w = np.eye(4)
+            c2w[:3, 3] = rng.uniform(-3, 3, 3)
+            np.savetxt(root / "pose" / f"{split}_{i:04d}.txt", c2w)
+            write_png(str(root / "rgb" / f"{split}_{i:04d}.png"), rng.integers(0, 256, (8, 8, 4), dtype=np.uint8))
+    ds = dataset_dict['nsvf'](str(root), split='train', downsample=0.01)
+    assert ds.img_wh == (8, 8) and abs(float(ds.K[0, 0]) - 11.111110311937682) < 1e-5
+    shift = np.array([0.0, 0.0, 0.3])
+    scale = 1.1 * 1.05 * 2.2 / 2  # largest side 2.2, x1.05, x1.1 for Lego
+    assert np.allclose(ds.shift, shift) and abs(ds.scale - scale) < 1e-9
+    raw = np.loadtxt(root / "pose" / "0_0000.txt")[:3]
+    want = (raw[:, 3] - shift) / (2 * scale)
+    assert np.allclose(ds.poses[0, :, 3].numpy(), want, atol=1e-6)
+    assert ds.rays.shape == (2, 64, 3)
+    assert dataset_dict['nsvf'](str(root), split='test', downsample=0.01).poses.shape == (1, 3, 4)
