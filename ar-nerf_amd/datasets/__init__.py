@@ -1,9 +1,10 @@
 """datasets/__init__.py of the reference.  Implemented: 'nerf' (NeRF-synthetic
-/ Blender) and 'nsvf' (Synthetic_NeRF & co.).  The other loaders of the reference (nsvf, colmap, colmap_exr,
+/ Blender) 'nsvf' (Synthetic_NeRF & co.) and 'colmap' (mip-NeRF 360).  The other loaders of the reference (nsvf, colmap, colmap_exr,
 colmap_real_exr, myblender, nerfpp, rtmv) are SURVEY.md §8f rank-2 work not
 done yet; asking for one raises."""
 from .nerf import NeRFDataset
 from .nsvf import NSVFDataset
+from .colmap import ColmapDataset
 
 
 class _Missing:
@@ -11,9 +12,9 @@ class _Missing:
         self.name = name
 
     def __call__(self, *a, **k):
-        raise NotImplementedError(f"dataset '{self.name}' is not implemented in this build (only 'nerf' and 'nsvf')")
+        raise NotImplementedError(f"dataset '{self.name}' is not implemented in this build (only 'nerf', 'nsvf', 'colmap')")
 
 
-dataset_dict = {'nerf': NeRFDataset, 'nsvf': NSVFDataset}
-for _n in ('colmap', 'colmap_exr', 'colmap_real_exr', 'myblender', 'nerfpp', 'rtmv'):
+dataset_dict = {'nerf': NeRFDataset, 'nsvf': NSVFDataset, 'colmap': ColmapDataset}
+for _n in ('colmap_exr', 'colmap_real_exr', 'myblender', 'nerfpp', 'rtmv'):
     dataset_dict[_n] = _Missing(_n)

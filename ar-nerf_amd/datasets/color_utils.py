@@ -34,7 +34,13 @@ def read_image(img_path, img_wh, blend_a=True, exr_file=False):
     """-> float32 (h*w, 3): RGBA blended onto white (blend_a) or black."""
     if exr_file:
         raise NotImplementedError("EXR images need OpenCV's OpenEXR reader (not available)")
-    img = read_png(img_path).astype(np.float32) / 255.0
+    if img_path.lower().endswith(".png"):
+        img = read_png(img_path).astype(np.float32) / 255.0
+    else:  # JPEG etc.: Pillow (what imageio itself uses for these formats)
+        from PIL import Image
+        img = np.asarray(Image.open(img_path)).astype(np.float32) / 255.0
+        if img.ndim == 2:
+            img = img[..., None].repeat(3, -1)
     if img.shape[2] == 4:  # blend A to RGB
         if blend_a:
             img = img[..., :3] * img[..., -1:] + (1 - img[..., -1:])

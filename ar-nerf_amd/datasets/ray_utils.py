@@ -1,4 +1,5 @@
-"""datasets/ray_utils.py:7-70 of the reference (kornia-free)."""
+"""datasets/ray_utils.py:7-214 of the reference (kornia-free)."""
+import numpy as np
 import torch
 
 
@@ -28,3 +29,42 @@ def get_rays(directions, c2w):
         rays_d = torch.einsum('nc,nac->na', directions, c2w[..., :3])
     rays_o = c2w[..., 3].expand_as(rays_d)
     return rays_o, rays_d
+
+
+def normalize(v):
+    return v / np.linalg.norm(v)
+
+
+def average_poses(poses, pts3d=None):
+    """ray_utils.py:108-147: centre = mean of the point cloud (or of the
+    cameras), z = mean z axis, x = y' x z, y = z x x."""
+    center = pts3d.mean(0) if pts3d is not None else poses[..., 3].mean(0)
+    z = normalize(poses[..., 2].mean(0))
+    y_ = poses[..., 1].mean(0)
+    x = normalize(np.cross(y_, z))
+    y = np.cross(z, x)
+    return np.stack([x, y, z, center], 1)
+
+
+def center_poses(poses, pts3d=None):
+    """ray_utils.py:150-178: poses (and points) in the average pose's frame."""
+    pose_avg = average_poses(poses, pts3d)
+    pose_avg_homo = np.eye(4)
+    pose_avg_homo[:3] = pose_avg
+    pose_avg_inv = np.linalg.inv(pose_avg_homo)
+    last_row = np.tile(np.array([0, 0, 0, 1]), (len(poses), 1, 1))
+    poses_centered = (pose_avg_inv @ np.concatenate([poses, last_row], 1))[:, :3]
+    if pts3d is not None:
+        return poses_centered, pts3d @ pose_avg_inv[:, :3].T + pose_avg_inv[:, 3:].T, pose_avg
+    return poses_centered, pose_avg
+
+
+def create_spheric_poses(radius, mean_h, n_poses=120):
+    """ray_utils.py:180-216: a circle of n_poses cameras around the z axis."""
+    def spheric_pose(theta, phi, radius):
+        trans_t = np.array([[1, 0, 0, 0], [0, 1, 0, 2 * mean_h], [0, 0, 1, -radius]])
+        rot_phi = np.array([[1, 0, 0], [0, np.cos(phi), -np.sin(phi)], [0, np.sin(phi), np.cos(phi)]])
+        rot_theta = np.array([[np.cos(theta), 0, -np.sin(theta)], [0, 1, 0], [np.sin(theta), 0, np.cos(theta)]])
+        c2w = rot_theta @ rot_phi @ trans_t
+        return np.array([[-1, 0, 0], [0, 0, 1], [0, 1, 0]]) @ c2w
+    return np.stack([spheric_pose(th, -np.pi / 12, radius) for th in np.linspace(0, 2 * np.pi, n_poses + 1)[:-1]], 0)

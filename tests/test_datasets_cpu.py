@@ -97,7 +97,7 @@ def test_nerf_synthetic_loader(tmp_path):
     np.testing.assert_allclose(ds.rays[0].numpy(), want, atol=1e-6)
     assert ds.gt_u8().dtype == torch.uint8
     try:
-        dataset_dict['colmap']('x')
+        dataset_dict['rtmv']('x')
         raise AssertionError("expected NotImplementedError")
     except NotImplementedError:
         pass
@@ -126,3 +126,46 @@ def test_nsvf_synthetic_loader(tmp_path):
     assert np.allclose(ds.poses[0, :, 3].numpy(), want, atol=1e-6)
     assert ds.rays.shape == (2, 64, 3)
     assert dataset_dict['nsvf'](str(root), split='test', downsample=0.01).poses.shape == (1, 3, 4)
+
+
+def test_colmap_model_and_loader(tmp_path):
+    from PIL import Image as PILImage
+
+    from datasets import colmap_utils as CU
+    from datasets.ray_utils import center_poses
+    root = tmp_path / "garden"
+    (root / "sparse" / "0").mkdir(parents=True)
+    (root / "images").mkdir()
+    rng = np.random.default_rng(3)
+    cams = {1: CU.Camera(1, "PINHOLE", 16, 12, np.array([20.0, 21.0, 8.0, 6.0]))}
+    ims = {}
+    for i in range(9):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        name = f"img_{8 - i:03d}.jpg"  # ids and names in opposite orders: poses are sorted by name
+        ims[i + 1] = CU.Image(i + 1, q, rng.normal(size=3) * 3, 1, name, np.zeros((0, 2)), np.zeros(0, np.int64))
+        PILImage.fromarray(rng.integers(0, 256, (12, 16, 3), dtype=np.uint8)).save(root / "images" / name, quality=95)
+    pts = {k: CU.Point3D(k, rng.normal(size=3), np.array([1, 2, 3]), 0.5, np.zeros(0), np.zeros(0)) for k in range(20)}
+    CU.write_model_binary(str(root / "sparse" / "0"), cams, ims, pts)
+    # readers round-trip the model
+    rc = CU.read_cameras_binary(str(root / "sparse/0/cameras.bin"))
+    ri = CU.read_images_binary(str(root / "sparse/0/images.bin"))
+    assert rc[1].model == "PINHOLE" and np.array_equal(rc[1].params, cams[1].params)
+    assert ri[3].name == ims[3].name and np.array_equal(ri[3].qvec, ims[3].qvec)
+    R = ri[3].qvec2rotmat()
+    assert np.allclose(R @ R.T, np.eye(3)) and abs(np.linalg.det(R) - 1) < 1e-9
+    ds = dataset_dict['colmap'](str(root), split='train')
+    assert ds.img_wh == (16, 12) and float(ds.K[0, 0]) == 20.0 and float(ds.K[1, 2]) == 6.0
+    assert ds.poses.shape == (7, 3, 4) and ds.rays.shape == (7, 192, 3)  # images 0 and 8 (i % 8 == 0) are test
+    # expected poses: c2w sorted by name, centred on the point cloud, closest camera at distance 1
+    order = sorted(ims, key=lambda k: ims[k].name)
+    c2w = []
+    for k in order:
+        w2c = np.eye(4)
+        w2c[:3, :3], w2c[:3, 3] = CU.qvec2rotmat(ims[k].qvec), ims[k].tvec
+        c2w.append(np.linalg.inv(w2c)[:3])
+    pc, _, _ = center_poses(np.stack(c2w), np.stack([p.xyz for p in pts.values()]))
+    pc[..., 3] /= np.linalg.norm(pc[..., 3], axis=-1).min()
+    np.testing.assert_allclose(ds.poses.numpy(), pc[[i for i in range(9) if i % 8 != 0]].astype(np.float32),
+                               rtol=1e-5, atol=1e-5)
+    assert dataset_dict["colmap"](str(root), split="test").poses.shape == (2, 3, 4)
