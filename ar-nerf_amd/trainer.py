@@ -44,7 +44,7 @@ class NGPTrainer:
     def __init__(self, scale=0.5, batch_size=8192, lr=1e-2, num_epochs=30, steps_per_epoch=1000, loss="raw",
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
-                 device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=128, bin_level_lo=8,
+                 device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=None, bin_level_lo=None,
                  chunk_first=64):
         self.dev = torch.device(device)
         self.scale = float(scale)
@@ -153,6 +153,15 @@ class NGPTrainer:
         # levels [0, bin_level_lo) atomic -- their in-wave run merge keeps the
         # requests few -- fine levels binned (DESIGN.md "hash backward").
         assert hash_backward in ("atomic", "binned", "hybrid")
+        # defaults by scene size (measured): one cascade (object scenes, ~70
+        # samples/ray) 8 atomic levels + 128 binned samples/ray; cascaded (unbounded) scenes
+        # have ~2x the gradient-carrying samples and 4 more hashed levels: all levels binned
+        # (+17 % at scale 16) with room for 512 samples/ray
+        big = self.cascades > 1
+        if bin_level_lo is None:
+            bin_level_lo = 0 if big else 8
+        if bin_samples_per_ray is None:
+            bin_samples_per_ray = 512 if big else 128
         self.hash_backward = hash_backward
         self.bin_level_lo = 0 if hash_backward == "binned" else bin_level_lo
         if hash_backward != "atomic":

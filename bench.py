@@ -82,7 +82,10 @@ def parse():
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--breakdown-steps", type=int, default=50, help="eager steps with per-kernel HIP events")
     ap.add_argument("--hash-backward", default="hybrid", choices=["hybrid", "binned", "atomic"])
-    ap.add_argument("--bin-level-lo", type=int, default=8, help="hybrid hash backward: first binned level")
+    ap.add_argument("--bin-level-lo", type=int, default=None,
+                    help="hybrid hash backward: first binned level (default: trainer's, 8 / 0 for cascaded scenes)")
+    ap.add_argument("--bin-samples-per-ray", type=int, default=None,
+                    help="binned hash-backward workspace per ray (default: trainer's, 128 / 512 for cascaded scenes)")
     ap.add_argument("--infer-frames", type=int, default=20, help="timed full-frame test renders (0: skip)")
     ap.add_argument("--infer-res", type=int, default=800)
     return ap.parse_args()
@@ -232,7 +235,7 @@ def main():
     directions = scene.directions.to(dev).contiguous()
     poses = scene.poses.to(dev).contiguous()
     trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward,
-                         bin_level_lo=args.bin_level_lo)
+                         bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray)
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
     R = args.batch
 
@@ -344,7 +347,7 @@ def main():
                        "graphs": trainer.use_graphs,
                        "chunk_first": trainer.chunk_first,
                        "parallelism": f"dp{world}", "last_loss": round(loss, 5),
-                       "hash_backward": args.hash_backward, "bin_level_lo": args.bin_level_lo,
+                       "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
             "roofline": dict(kernel=dominant, traffic=pmc_traffic(dominant), **kernels[dominant]),
             "kernels": kernels,
