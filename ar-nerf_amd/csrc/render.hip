@@ -98,6 +98,42 @@ __device__ __forceinline__ int64_t block_append(int cnt, unsigned long long* cou
     return off;
 }
 
+constexpr int CRPT = 4;  // rays per thread per composite pass
+
+// block_append for CRPT items per thread at positions n = base + k*256 + t:
+// offsets in (k, t) order, i.e. the survivors keep their alive-list order
+// within the block (the list order is what keeps neighbouring pixels' samples
+// adjacent for the encode's gathers), with ONE counter atomic.
+__device__ __forceinline__ void block_append_k(const int (&cnt)[CRPT], int64_t (&off)[CRPT],
+                                               unsigned long long* counter) {
+    __shared__ int wt[CRPT][4];
+    __shared__ int64_t boff;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl[CRPT];
+#pragma unroll
+    for (int k = 0; k < CRPT; ++k) {
+        incl[k] = wave_incl_scan(cnt[k]);
+        if (lane == 63) wt[k][w] = incl[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+#pragma unroll
+        for (int k = 0; k < CRPT; ++k) tot += wt[k][0] + wt[k][1] + wt[k][2] + wt[k][3];
+        boff = tot ? (int64_t)atomicAdd(counter, (unsigned long long)tot) : 0;
+    }
+    __syncthreads();
+    int64_t base = boff;
+#pragma unroll
+    for (int k = 0; k < CRPT; ++k) {
+        int before = 0;
+        for (int i = 0; i < w; ++i) before += wt[k][i];
+        off[k] = base + before + incl[k] - cnt[k];
+        base += wt[k][0] + wt[k][1] + wt[k][2] + wt[k][3];
+    }
+    __syncthreads();  // wt / boff are reused by the next call
+}
+
 // ---- wave-per-ray mode (SIMPLE launches, N_samples >= WAVE_NS) ----------
 // Late iterations have few alive rays with many samples each: one lane per
 // ray leaves most of the chip idle while each lane walks ~N_samples occupied
@@ -345,41 +381,58 @@ __global__ void __launch_bounds__(256) render_composite_kernel(const float* __re
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int my_total = 0;
-    for (int64_t bbase = (int64_t)blockIdx.x * blockDim.x; bbase < n_alive; bbase += stride) {  // block-uniform
-        const int64_t n = bbase + threadIdx.x;
-        bool keep = false;
-        int ne = 0;
-        int32_t r = -1;
-        if (n < n_alive) {
-            ne = n_eff[n];
-            r = alive_in[n];
-            if (ne > 0) {  // volumerendering.cu:221-224: no samples -> dead
-                keep = true;
-                float op = opacity[r], dp = depth[r], cr = rgb[3 * r], cg = rgb[3 * r + 1], cb = rgb[3 * r + 2];
-                float T = 1 - op;
-                for (int s = 0; s < ne; ++s) {  // volumerendering.cu:228-256
-                    const int64_t o = s * n_alive + n;  // sample-major slots (render_march_kernel)
-                    const float a = 1.0f - __expf(-sigmas[o] * deltas[o]);
-                    const float w = a * T;
-                    cr += w * rgbs[3 * o]; cg += w * rgbs[3 * o + 1]; cb += w * rgbs[3 * o + 2];
-                    dp += w * ts[o];
-                    op += w;
-                    T *= 1.0f - a;
-                    if (T <= T_thr) { keep = false; break; }
-                }
-                rgb[3 * r] = cr; rgb[3 * r + 1] = cg; rgb[3 * r + 2] = cb;
-                depth[r] = dp;
-                opacity[r] = op;
+    // CRPT rays per thread per pass (stride 256): one survivor append per
+    // 256*CRPT rays (same-address atomics serialise)
+    // (only while the alive rays outnumber the grid's threads: late iterations
+    // have few rays with many samples each and want one ray per thread)
+    const int rpt = n_alive > stride ? CRPT : 1;
+    for (int64_t bbase = (int64_t)blockIdx.x * blockDim.x * rpt; bbase < n_alive; bbase += stride * rpt) {
+        int32_t kept[CRPT];  // survivor ray or -1 (static indices: registers)
+#pragma unroll
+        for (int k = 0; k < CRPT; ++k) {  // block-uniform
+            kept[k] = -1;
+            const int64_t n = bbase + k * blockDim.x + threadIdx.x;
+            if (k >= rpt || n >= n_alive) continue;
+            const int ne = n_eff[n];
+            const int32_t r = alive_in[n];
+            my_total += ne;  // total_samples += N_eff_samples.sum() (rendering.py:199)
+            if (ne <= 0) continue;  // volumerendering.cu:221-224: no samples -> dead
+            bool keep = true;
+            float op = opacity[r], dp = depth[r], cr = rgb[3 * r], cg = rgb[3 * r + 1], cb = rgb[3 * r + 2];
+            float T = 1 - op;
+            for (int s = 0; s < ne; ++s) {  // volumerendering.cu:228-256
+                const int64_t o = s * n_alive + n;  // sample-major slots (render_march_kernel)
+                const float a = 1.0f - __expf(-sigmas[o] * deltas[o]);
+                const float w = a * T;
+                cr += w * rgbs[3 * o]; cg += w * rgbs[3 * o + 1]; cb += w * rgbs[3 * o + 2];
+                dp += w * ts[o];
+                op += w;
+                T *= 1.0f - a;
+                if (T <= T_thr) { keep = false; break; }
             }
+            rgb[3 * r] = cr; rgb[3 * r + 1] = cg; rgb[3 * r + 2] = cb;
+            depth[r] = dp;
+            opacity[r] = op;
+            if (keep) kept[k] = r;
         }
-        my_total += ne;  // total_samples += N_eff_samples.sum() (rendering.py:199)
-        const int64_t off = block_append(keep ? 1 : 0, reinterpret_cast<unsigned long long*>(&state[parity ^ 1]));
-        if (keep) alive_out[off] = r;
+        int cnt[CRPT];
+        int64_t off[CRPT];
+#pragma unroll
+        for (int k = 0; k < CRPT; ++k) cnt[k] = kept[k] >= 0;
+        block_append_k(cnt, off, reinterpret_cast<unsigned long long*>(&state[parity ^ 1]));
+#pragma unroll
+        for (int k = 0; k < CRPT; ++k)
+            if (kept[k] >= 0) alive_out[off[k]] = kept[k];
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) my_total += __shfl_xor(my_total, o, 64);
-    if (lane == 0 && my_total)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&state[RS_TOTAL]), (unsigned long long)my_total);
+    __shared__ int wsum[4];  // one total atomic per block, not per wave
+    if (lane == 0) wsum[threadIdx.x >> 6] = my_total;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (tot) atomicAdd(reinterpret_cast<unsigned long long*>(&state[RS_TOTAL]), (unsigned long long)tot);
+    }
 }
 
 // rendering.py:240-251: rgb += bg * (1 - opacity)
@@ -450,7 +503,7 @@ int ngp_render_test_composite(const float* sigmas, const float* rgbs, const floa
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(sigmas && rgbs && deltas && ts && n_eff && alive_in && alive_out && alive_in != alive_out &&
                   opacity && depth && rgb);
-    const unsigned blocks = std::min(nblk(n_rays, 256), 1024u);
+    const unsigned blocks = std::min(nblk(n_rays, 256 * CRPT), 1024u);
     render_composite_kernel<<<blocks, 256, 0, as_stream(stream)>>>(sigmas, rgbs, deltas, ts, n_eff, state, parity,
                                                                   alive_in, alive_out, T_threshold, opacity, depth,
                                                                   rgb);
