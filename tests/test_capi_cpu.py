@@ -71,3 +71,21 @@ def test_bad_arguments_return_einval():
     assert L.ngp_bitfield_summary(None, 256, 128, None, None) == -1
     # zero-size calls are no-ops
     assert L.ngp_morton3d(None, 0, None, None) == 0
+
+
+def test_new_entry_points_reject_bad_arguments_without_launching():
+    """Argument checks run before any launch (no GPU needed): NGP_EINVAL (-1)."""
+    import ctypes as C
+    L = HG._lib()
+    assert L.ngp_render_test_capacity(-1, 1) == -1 and L.ngp_render_test_capacity(10, 4) == 40
+    assert L.ngp_render_test_begin(-1, None, None, None, None, None, None) == -1
+    assert L.ngp_render_test_begin(4, None, None, None, None, None, None) == -1
+    assert L.ngp_render_test_composite(None, None, None, None, None, 4, 2, None, None, None, C.c_float(1e-4),
+                                       None, None, None, None) == -1
+    assert L.ngp_render_test_finish(None, 4, None, None, None) == -1
+    assert L.ngp_distortion_loss_fw(None, None, None, None, -1, None, None, None, None) == -1
+    assert L.ngp_distortion_loss_fw(None, None, None, None, 3, None, None, None, None) == -1
+    assert L.ngp_distortion_loss_bw(None, None, None, None, None, None, None, 3, None, None) == -1
+    assert L.ngp_distortion_loss_fw(None, None, None, None, 0, None, None, None, None) == 0  # empty: no-op
+    g = HG.HashGrid(0.5)
+    assert L.ngp_density_input_grad(None, 5, C.byref(g.desc), None, None, None, None, None) == -1
