@@ -331,18 +331,24 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
 }
 
 // --------------------------------------------------- occupancy grid update
-// density_grid_tmp[c, idx] = sigma (models/networks.py:268); duplicates keep
-// the max (the reference's last-writer-wins is order-undefined on a GPU).
-// sigma >= 0, so an unsigned-int max on the fp32 bits is a float max.
-// Negative indices are skipped (occupancy samples that do not exist: no
-// occupied cell to resample, see occ_sample_kernel).
-__global__ void scatter_max_kernel(const int64_t* __restrict__ idx, const float* __restrict__ sig, int64_t n,
-                                   float* __restrict__ tmp) {
+// density_grid_tmp[c, idx] = sigma (models/networks.py:268) as a torch
+// index_put_ over the cell list: with duplicate cells the LAST write in list
+// order wins (torch's sequential semantics; sample_uniform_and_occupied_cells
+// draws i.i.d., so a duplicated cell keeps its last draw's sigma, and a cell
+// drawn in both halves keeps the occupied-half draw).  Each sample i at list
+// position pos_base + i leaves the 64-bit key ((pos + 1) << 32 | sigma bits)
+// with a 64-bit atomicMax, so the largest position wins independently of
+// execution order; ranks sharding the list combine their key grids with a MAX
+// all-reduce, the same rule across ranks.  Negative indices are skipped
+// (occupancy samples that do not exist: no occupied cell to resample).
+__global__ void scatter_last_kernel(const int64_t* __restrict__ idx, const float* __restrict__ sig, int64_t n,
+                                    int64_t pos_base, unsigned long long* __restrict__ key) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t j = idx[i];
     if (j < 0) return;
-    atomicMax(reinterpret_cast<unsigned int*>(tmp) + j, __float_as_uint(fmaxf(sig[i], 0.f)));
+    const unsigned long long k = ((unsigned long long)(pos_base + i + 1) << 32) | __float_as_uint(fmaxf(sig[i], 0.f));
+    atomicMax(key + j, k);
 }
 
 // ---------------------------------------- occupancy cell sampling on device
@@ -564,21 +570,28 @@ __global__ void __launch_bounds__(OSC_T) occ_sample_sorted_kernel(
     }
 }
 
-// models/networks.py:273-278: grid = where(grid<0, grid, max(grid*decay, tmp));
+// models/networks.py:270-278: grid = where(grid<0, grid, max(grid*decay, tmp)),
+// decay per cell when decay_cells != nullptr (erode, networks.py:270-272:
+// clamp(decay**(1/count_grid), 0.1, 0.95), evaluated once per count grid by the
+// caller);
 // accumulates sum and count of grid > 0 for the mean, in fp64 so the mean is
 // the correctly rounded one whatever the summation order: at initialisation
 // every cell holds sigma ~= 1 and the threshold (= that mean) splits them, so
 // a last-digit difference in an fp32 sum flips thousands of cells and sends
 // training down a different trajectory.
-__global__ void __launch_bounds__(256) grid_ema_kernel(float* __restrict__ grid, float* __restrict__ tmp, int64_t n,
-                                                       float decay, double* __restrict__ sum_cnt) {
+__global__ void __launch_bounds__(256) grid_ema_kernel(float* __restrict__ grid, unsigned long long* __restrict__ key,
+                                                       int64_t n, float decay, const float* __restrict__ decay_cells,
+                                                       double* __restrict__ sum_cnt) {
     double s = 0.0, c = 0.0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const float gv = grid[i];
-        const float nv = gv < 0 ? gv : fmaxf(gv * decay, tmp[i]);
+        const float dc = decay_cells ? decay_cells[i] : decay;
+        const unsigned long long kv = key[i];
+        const float tv = kv ? __uint_as_float((uint32_t)kv) : 0.f;  // density_grid_tmp (zeros where unsampled)
+        const float nv = gv < 0 ? gv : fmaxf(gv * dc, tv);
         grid[i] = nv;
-        tmp[i] = 0.f;  // consumed: left zeroed for the next update
+        if (kv) key[i] = 0ull;  // consumed: left zeroed for the next update
         if (nv > 0) { s += (double)nv; c += 1.0; }
     }
 #pragma unroll
@@ -908,11 +921,13 @@ int ngp_counters_inc(int64_t* counters, int n, void* stream) {
     return ngp_launch_status();
 }
 
-int ngp_density_scatter_max(const int64_t* indices, const float* sigmas, int64_t n, float* grid_tmp, void* stream) {
-    NGP_CHECK_ARG(n >= 0);
+int ngp_density_scatter_last(const int64_t* indices, const float* sigmas, int64_t n, int64_t pos_base,
+                             uint64_t* grid_key, void* stream) {
+    NGP_CHECK_ARG(n >= 0 && pos_base >= 0 && pos_base + n < (1ll << 31));
     if (n == 0) return NGP_OK;
-    NGP_CHECK_ARG(indices && sigmas && grid_tmp);
-    scatter_max_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(indices, sigmas, n, grid_tmp);
+    NGP_CHECK_ARG(indices && sigmas && grid_key && ((uintptr_t)grid_key & 7) == 0);
+    scatter_last_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(
+        indices, sigmas, n, pos_base, reinterpret_cast<unsigned long long*>(grid_key));
     return ngp_launch_status();
 }
 
@@ -964,16 +979,18 @@ int ngp_occupancy_samples_sorted(uint64_t seed, const int64_t* counter_dev, int 
     return ngp_launch_status();
 }
 
-int ngp_density_grid_ema(float* density_grid, float* grid_tmp, int64_t n, float decay, float thr_max,
-                         void* sum_cnt_ws, float* threshold_out, void* stream) {
-    NGP_CHECK_ARG(n > 0 && density_grid && grid_tmp && sum_cnt_ws && threshold_out);
+int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, float decay, const float* decay_cells,
+                         float thr_max, void* sum_cnt_ws, float* threshold_out, void* stream) {
+    NGP_CHECK_ARG(n > 0 && density_grid && grid_key && sum_cnt_ws && threshold_out && ((uintptr_t)grid_key & 7) == 0);
     NGP_CHECK_ARG(((uintptr_t)sum_cnt_ws & 7) == 0);
     hipStream_t s = as_stream(stream);
     hipError_t e = hipMemsetAsync(sum_cnt_ws, 0, 2 * sizeof(double), s);
     if (e != hipSuccess) return (int)e;
     int64_t blocks = (n + 255) / 256;
     if (blocks > 512) blocks = 512;
-    grid_ema_kernel<<<(unsigned)blocks, 256, 0, s>>>(density_grid, grid_tmp, n, decay, (double*)sum_cnt_ws);
+    grid_ema_kernel<<<(unsigned)blocks, 256, 0, s>>>(density_grid, reinterpret_cast<unsigned long long*>(grid_key), n,
+                                                     decay, decay_cells,
+                                                     (double*)sum_cnt_ws);
     grid_threshold_kernel<<<1, 1, 0, s>>>((const double*)sum_cnt_ws, thr_max, threshold_out);
     return ngp_launch_status();
 }

@@ -7,10 +7,12 @@ from rank 0 every forward (SURVEY.md §2 "Collective call sites").  Here:
   * one all-reduce (SUM) of the flat fp32 gradient per step; the Adam kernel
     folds in the 1/world mean (grad_scale), so no extra pass;
   * no per-step buffer broadcast: the occupancy update is made identical on
-    every rank by construction -- each rank evaluates a disjoint 1/world
-    share of the sampled cells, one MAX all-reduce combines the cell maxima
-    (every 16 steps, C*128^3 fp32 = 8 MB), and rank 0's threshold is
-    broadcast (8 bytes) so all ranks pack the same bitfield.
+    every rank by construction -- all ranks draw the same cells and jitter
+    (rank-independent seeds), each evaluates a disjoint 1/world share of the
+    list, one MAX all-reduce of the 64-bit (list position, sigma) key grid
+    combines them with the reference's last-writer-wins rule (every 16
+    steps, C*128^3 x 8 B = 16 MB), and rank 0's threshold is broadcast
+    (8 bytes) so all ranks pack the same bitfield.
 All functions are no-ops for world_size 1 and work with gloo on CPU tensors.
 """
 import torch
@@ -41,8 +43,10 @@ def allreduce_grad_(grad, group=None):
 
 
 def combine_density_tmp_(tmp, group=None):
-    """Cell-wise MAX of the per-rank density_grid_tmp (unevaluated cells are 0,
-    sigma >= 0, so MAX == the union of all ranks' evaluations)."""
+    """Cell-wise MAX of the per-rank density_grid_tmp keys ((list position + 1)
+    << 32 | sigma bits, 0 = unevaluated; ngp_density_scatter_last): the
+    largest list position wins across ranks as within one, so the result
+    equals a single process evaluating the whole list."""
     if world_info(group)[1] > 1:
         dist.all_reduce(tmp, op=dist.ReduceOp.MAX, group=group)
     return tmp

@@ -162,9 +162,14 @@ class NGP(nn.Module):
             half_grid_size = s / self.grid_size
             xyzs_w = (coords / (self.grid_size - 1) * 2 - 1) * (s - half_grid_size)
             xyzs_w += (torch.rand_like(xyzs_w) * 2 - 1) * half_grid_size
-            density_grid_tmp[c, indices] = self.density(xyzs_w)
-        if erode:
-            decay = torch.clamp(decay ** (1 / self.count_grid), 0.1, 0.95)
+            # density_grid_tmp[c, indices] = density (last duplicate wins, deterministically)
+            vren.density_scatter_last(density_grid_tmp[c], indices, self.density(xyzs_w))
+        if erode:  # clamp(decay**(1/count_grid), 0.1, 0.95), evaluated once on the host (vren.erode_decay)
+            key = (self.count_grid.data_ptr(), self.count_grid._version, float(decay))
+            if getattr(self, "_erode_key", None) != key:
+                self._erode_decay = vren.erode_decay(self.count_grid, decay).to(self.count_grid.device)
+                self._erode_key = key
+            decay = self._erode_decay
         self.density_grid = torch.where(self.density_grid < 0, self.density_grid,
                                         torch.maximum(self.density_grid * decay, density_grid_tmp))
         pos = self.density_grid > 0

@@ -45,7 +45,7 @@ class NGPTrainer:
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
                  device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=None, bin_level_lo=None,
-                 chunk_first=64):
+                 chunk_first=64, erode=False):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
@@ -56,6 +56,12 @@ class NGPTrainer:
         # train.py:104-105
         self.esf = exp_step_factor if exp_step_factor is not None else (1 / 256 if scale > 0.5 else 0.0)
         self.G = grid_size
+        # erode (networks.py:270-272): per-cell decay from mark_invisible_cells'
+        # count_grid; train.py:178 turns it on for COLMAP scenes
+        self.erode = bool(erode)
+        self.count_grid = None
+        self.decay_cells = None
+        self._decay_for = None
         self.cascades = max(1 + int(np.ceil(np.log2(2 * scale))), 1)  # models/networks.py:27
         self.update_interval, self.warmup_steps, self.max_samples = update_interval, warmup_steps, max_samples
         self.pg = process_group
@@ -81,7 +87,8 @@ class NGPTrainer:
         self._sum_cnt = torch.zeros(2, dtype=torch.float64, device=dev)
         # device-side occupancy sampling buffers (update_density_grid)
         M2 = 2 * (self.G ** 3 // 4)
-        self._occ_tmp = torch.zeros_like(self.density_grid)
+        # density_grid_tmp as 64-bit (list position, sigma) keys: last writer wins (ngp_density_scatter_last)
+        self._occ_key = torch.zeros(self.density_grid.shape, dtype=torch.int64, device=dev)
         self._occ_list = torch.empty(self.G ** 3, dtype=torch.int32, device=dev)
         self._occ_count = torch.zeros(1, dtype=torch.int64, device=dev)
         self._occ_xyz = torch.empty(M2, 3, device=dev)
@@ -172,6 +179,11 @@ class NGPTrainer:
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(1000 + seed + self.rank)
         self.sample_seed = (1000003 * (seed + 1) + 7919 * self.rank) & 0xFFFFFFFFFFFFFFFF  # ngp_sample_batch key
+        # occupancy draws: rank-independent (every rank draws the same cells and
+        # jitter; each evaluates its shard), so any world size builds one grid
+        self.occ_seed = ((1000003 * (seed + 1)) ^ 0x5DEECE66D) & 0xFFFFFFFFFFFFFFFF
+        self.occ_gen = torch.Generator(device=dev)
+        self.occ_gen.manual_seed(2000 + seed)
         # device step counters: [0] Adam steps taken, [1] batches drawn (RNG
         # counter), [2] device-sampled occupancy updates (their RNG counter)
         self.dctr = torch.zeros(3, dtype=torch.int64, device=dev)
@@ -213,9 +225,12 @@ class NGPTrainer:
     # ------------------------------------------------------ occupancy grid
     @torch.no_grad()
     def mark_invisible_cells(self, K, poses, img_wh, chunk=64 ** 3):
-        """models/networks.py:209-250 (once, before training)."""
+        """models/networks.py:209-250 (once, before training): density -1 for
+        cells no camera sees (or too near one), and count_grid = the fraction
+        of cameras that see each cell, from which the erode decay is derived."""
         K, poses = K.to(self.dev), poses.to(self.dev)
         N_cams = poses.shape[0]
+        self.count_grid = torch.zeros_like(self.density_grid)
         w2c_R = poses[:, :3, :3].transpose(1, 2)
         w2c_T = -w2c_R @ poses[:, :3, 3:]
         for c in range(self.cascades):
@@ -232,30 +247,46 @@ class NGPTrainer:
                            (uv[:, 1] < img_wh[1])
                 covered_by_cam = (uvd[:, 2] >= NEAR_DISTANCE) & in_image
                 count = covered_by_cam.sum(0) / N_cams
+                self.count_grid[c, indices[i:i + chunk]] = count
                 too_near_to_any_cam = ((uvd[:, 2] < NEAR_DISTANCE) & in_image).any(0)
                 valid_mask = (count > 0) & (~too_near_to_any_cam)
                 self.density_grid[c, indices[i:i + chunk]] = torch.where(valid_mask, 0., -1.)
+        self.decay_cells = vren.erode_decay(self.count_grid).to(self.dev)
+        self._decay_for = 0.95
 
     @torch.no_grad()
-    def update_density_grid(self, density_threshold, warmup=False, decay=0.95):
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=None, jitter=None):
         """models/networks.py:252-281.  Past warmup the cells are drawn on device
         (ngp_occupied_cells + ngp_occupancy_samples: no host sync, so the update
         can sit inside a captured graph).  Multi-GPU: each rank evaluates its
         1/world share of the (identically drawn) cells and the cell maxima are
         combined with one MAX all-reduce, so every rank packs an identical
-        bitfield."""
+        bitfield.  erode (default: the trainer's setting) decays each cell by
+        clamp(decay**(1/count_grid), 0.1, 0.95) (networks.py:270-272).
+        jitter (tests): the warm-up's U[0,1) jitter per cell (C, G^3, 3) in
+        grid_coords order instead of the trainer's own draw."""
         C, G = self.cascades, self.G
+        erode = self.erode if erode is None else erode
+        if erode and self.decay_cells is None:
+            raise RuntimeError("update_density_grid(erode=True) needs count_grid: call mark_invisible_cells first")
+        if erode and decay != self._decay_for:  # (host evaluation: not inside a graph capture)
+            self.decay_cells = vren.erode_decay(self.count_grid, decay).to(self.dev)
+            self._decay_for = decay
         L, s = self.L, vren._stream()
-        tmp = self._occ_tmp  # zero on entry; the EMA consumes (re-zeroes) it
+        key = self._occ_key  # zero on entry; the EMA consumes (re-zeroes) it
         for c in range(C):
             sc = min(2 ** (c - 1), self.scale)
             half_grid_size = sc / G
             if warmup:  # get_all_cells (networks.py:167-179)
-                indices, coords = self.all_indices, self.grid_coords
-                if self.world > 1:  # each rank evaluates its share of the cells
-                    indices, coords = ddp.shard_cells(indices, coords, self.rank, self.world)
+                # the jitter is drawn for every cell from a rank-independent
+                # generator, then each rank evaluates its share of the cells:
+                # any world size builds the same grid
+                jit = (torch.rand(self.grid_coords.shape, device=self.dev, generator=self.occ_gen) if jitter is None
+                       else jitter[c].to(self.dev))
+                lo, hi = ddp.shard_range(self.grid_coords.shape[0], self.rank, self.world)
+                indices, coords = self.all_indices[lo:hi], self.grid_coords[lo:hi]
                 xyzs_w = (coords / (G - 1) * 2 - 1) * (sc - half_grid_size)
-                xyzs_w += (torch.rand(xyzs_w.shape, device=self.dev, generator=self.gen) * 2 - 1) * half_grid_size
+                xyzs_w += (jit[lo:hi] * 2 - 1) * half_grid_size
                 sig, _ = HG.density_forward(xyzs_w.float().contiguous(), self.grid, self.params16)
                 flat = (indices + c * G ** 3).contiguous()
                 n = flat.shape[0]
@@ -265,7 +296,7 @@ class NGPTrainer:
                                               _p(self._occ_list), _p(self._occ_count), s), "occupied_cells")
                 lo, hi = ddp.shard_range(2 * M, self.rank, self.world)
                 n = hi - lo
-                args = (self.sample_seed ^ 0x5DEECE66D, _p(self.dctr[2:]), c, G, M, ctypes_float(sc - half_grid_size),
+                args = (self.occ_seed, _p(self.dctr[2:]), c, G, M, ctypes_float(sc - half_grid_size),
                         ctypes_float(half_grid_size), _p(self._occ_list), _p(self._occ_count), lo, hi)
                 if self.occ_sorted:  # ascending cells: the density forward's waves stay cache-local
                     vren._ok(L.ngp_occupancy_samples_sorted(*args, _p(self._occ_ws), _p(self._occ_xyz),
@@ -284,12 +315,14 @@ class NGPTrainer:
                                                      _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16),
                                                      _p(self._occ_sig), None, s), "density_forward")
                 sig, flat = self._occ_sig, self._occ_flat
-            vren._ok(L.ngp_density_scatter_max(_p(flat), _p(sig), n, _p(tmp), s), "density_scatter_max")
+            # density_grid_tmp[c, indices] = sigma, list positions lo + i (rank shards)
+            vren._ok(L.ngp_density_scatter_last(_p(flat), _p(sig), n, lo, _p(key), s), "density_scatter_last")
         if not warmup:
             vren._ok(L.ngp_counters_inc(_p(self.dctr[2:]), 1, s), "counters_inc")
-        ddp.combine_density_tmp_(tmp, self.pg)
-        st = L.ngp_density_grid_ema(_p(self.density_grid), _p(tmp), self.density_grid.numel(), ctypes_float(decay),
-                                    ctypes_float(density_threshold), _p(self._sum_cnt), _p(self.threshold), s)
+        ddp.combine_density_tmp_(key, self.pg)
+        st = L.ngp_density_grid_ema(_p(self.density_grid), _p(key), self.density_grid.numel(), ctypes_float(decay),
+                                    _p(self.decay_cells) if erode else None, ctypes_float(density_threshold),
+                                    _p(self._sum_cnt), _p(self.threshold), s)
         vren._ok(st, "density_grid_ema")
         ddp.sync_threshold_(self.threshold, self.pg)  # identical threshold on every rank
         vren.packbits(self.density_grid, self.threshold[:1], self.density_bitfield)
@@ -729,3 +762,4 @@ class NGPTrainer:
 
 def ctypes_float(x):
     return HG.c_float(float(x))
+

@@ -73,8 +73,8 @@ def _declare(L):
         "ngp_ray_segments_capped": [vp, c_int64, c_int, vp, vp, vp, vp, vp],
         "ngp_adam_step": [vp, vp, vp, vp, vp, c_int64, c_float, c_float, c_float, c_float, c_int64, c_float, c_int,
                           vp],
-        "ngp_density_scatter_max": [vp, vp, c_int64, vp, vp],
-        "ngp_density_grid_ema": [vp, vp, c_int64, c_float, c_float, vp, vp, vp],
+        "ngp_density_scatter_last": [vp, vp, c_int64, c_int64, vp, vp],
+        "ngp_density_grid_ema": [vp, vp, c_int64, c_float, vp, c_float, vp, vp, vp],
         "ngp_distortion_loss_fw": [vp, vp, vp, vp, c_int64, vp, vp, vp, vp],
         "ngp_distortion_loss_bw": [vp, vp, vp, vp, vp, vp, vp, c_int64, vp, vp],
         "ngp_render_test_begin": [c_int64, vp, vp, vp, vp, vp, vp],
@@ -380,3 +380,33 @@ def distortion_loss_bw(dL_dloss, ws_inclusive_scan, wts_inclusive_scan, ws, delt
     dws = torch.zeros(ws.shape[0], device=ws.device)
     _ok(lib().ngp_distortion_loss_bw(*a, rays_a.shape[0], c_void_p(dws.data_ptr()), _stream()), "distortion_loss_bw")
     return dws
+
+
+def density_scatter_last(tmp, indices, sigmas):
+    """tmp.view(-1)[indices] = sigmas (models/networks.py:268) with torch's
+    sequential index_put_ semantics on duplicate indices (the last one in
+    list order wins), deterministically on the GPU (a device index_put_
+    leaves the winner to the scheduler): ngp_density_scatter_last's 64-bit
+    (position, sigma) keys, then the winners' sigmas into tmp (f32, in place;
+    cells not listed keep their value; sigma is clamped at 0)."""
+    _check("tmp", tmp, torch.float32)
+    idx = indices.reshape(-1).long().contiguous()
+    sig = sigmas.reshape(-1).float().contiguous()
+    key = torch.zeros(tmp.numel(), dtype=torch.int64, device=tmp.device)
+    _ok(lib().ngp_density_scatter_last(idx.data_ptr(), sig.data_ptr(), idx.numel(), 0, key.data_ptr(), _stream()),
+        "density_scatter_last")
+    hit = key != 0
+    val = (key & 0xFFFFFFFF).to(torch.int32).view(torch.float32)
+    flat = tmp.view(-1)
+    flat.copy_(torch.where(hit, val, flat))
+    return tmp
+
+
+def erode_decay(count_grid, decay=0.95):
+    """Per-cell erode decay clamp(decay**(1/count_grid), 0.1, 0.95)
+    (models/networks.py:270-272), for ngp_density_grid_ema's decay_cells.
+    count_grid is fixed once mark_invisible_cells ran, so this is evaluated
+    once, with torch on the host: the values are the reference expression's
+    CPU evaluation bit for bit (a device pow may differ in the last ulp).
+    Cells no camera sees (count 0 -> 0.1) hold density -1 and never decay."""
+    return torch.clamp(decay ** (1 / count_grid.detach().float().cpu()), 0.1, 0.95)

@@ -86,6 +86,9 @@ def parse():
                     help="hybrid hash backward: first binned level (default: trainer's, 8 / 0 for cascaded scenes)")
     ap.add_argument("--bin-samples-per-ray", type=int, default=None,
                     help="binned hash-backward workspace per ray (default: trainer's, 128 / 512 for cascaded scenes)")
+    ap.add_argument("--erode", default="auto", choices=["auto", "on", "off"],
+                    help="occupancy erode decay (networks.py:270-272); auto = on for cascaded (garden-shaped, "
+                         "COLMAP-like) scenes as train.py:178 does for colmap")
     ap.add_argument("--infer-frames", type=int, default=20, help="timed full-frame test renders (0: skip)")
     ap.add_argument("--infer-res", type=int, default=800)
     return ap.parse_args()
@@ -234,8 +237,9 @@ def main():
     gt_images = scene.gt_images(device=dev)  # (n_img, HW, 3) u8, resident in HBM
     directions = scene.directions.to(dev).contiguous()
     poses = scene.poses.to(dev).contiguous()
+    erode = args.erode == "on" or (args.erode == "auto" and args.scale > 0.5)
     trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward,
-                         bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray)
+                         bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray, erode=erode)
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
     R = args.batch
 
@@ -348,6 +352,7 @@ def main():
                        "chunk_first": trainer.chunk_first,
                        "parallelism": f"dp{world}", "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
+                       "erode": trainer.erode,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
             "roofline": dict(kernel=dominant, traffic=pmc_traffic(dominant), **kernels[dominant]),
             "kernels": kernels,

@@ -422,25 +422,33 @@ int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_av
 /* counters[i] += 1, i < n (n <= 64): advances the device step counters. */
 int ngp_counters_inc(int64_t* counters, int n, void* stream);
 
-/* Occupancy update (models/networks.py:252-281).  scatter_max: grid_tmp[idx[i]]
- * = max(grid_tmp[idx[i]], sigmas[i]) (flat cascade*G^3 indices, sigmas >= 0).
- * (negative indices skipped).  grid_ema: grid = where(grid<0, grid,
- * max(grid*decay, tmp)) in place (tmp is consumed: left zeroed), then
+/* Occupancy update (models/networks.py:252-281).  density_grid_tmp is kept as
+ * a 64-bit key grid (n = C*G^3 u64, 8-byte aligned, zero between updates):
+ * scatter_last: density_grid_tmp[idx[i]] = sigmas[i] (networks.py:268) with
+ * torch's sequential index_put_ semantics -- of duplicate cells the one at the
+ * largest list position pos_base + i wins, key = (pos+1) << 32 | sigma bits
+ * (sigma clamped at 0; negative indices skipped); ranks sharding one list
+ * combine key grids with a MAX all-reduce.  grid_ema: grid = where(grid<0,
+ * grid, max(grid*decay, tmp)) in place (the key grid is consumed: left
+ * zeroed); decay_cells (nullable, n floats) replaces the scalar decay per cell
+ * -- the erode branch (networks.py:270-272), decay_cells =
+ * clamp(decay**(1/count_grid), 0.1, 0.95); then
  * threshold_out[0] = min(mean(grid[grid>0]), thr_max) (NaN if none, as in
  * Python), threshold_out[1] = the mean; feed threshold_out to ngp_packbits'
  * threshold_dev.  sum_cnt_ws: 16 bytes of scratch (two fp64 accumulators, 8-byte
  * aligned; the mean is taken in fp64). */
-int ngp_density_scatter_max(const int64_t* indices, const float* sigmas, int64_t n, float* grid_tmp,
-                            void* stream);
-int ngp_density_grid_ema(float* density_grid, float* grid_tmp, int64_t n, float decay,
-                         float thr_max, void* sum_cnt_ws, float* threshold_out, void* stream);
+int ngp_density_scatter_last(const int64_t* indices, const float* sigmas, int64_t n, int64_t pos_base,
+                             uint64_t* grid_key, void* stream);
+int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, float decay,
+                         const float* decay_cells, float thr_max, void* sum_cnt_ws, float* threshold_out,
+                         void* stream);
 /* sample_uniform_and_occupied_cells (models/networks.py:181-207) on device,
  * no host sync: ngp_occupied_cells lists the cells of one cascade (n_cells
  * f32, Morton order) with density > threshold into list (capacity n_cells,
  * order unspecified), *count = their number (8-byte aligned).
  * ngp_occupancy_samples writes samples [lo, hi) of the 2*M list: sample i <
  * M a uniform cell, i >= M a cell drawn uniformly from the occupied list
- * (flat_idx = -1, skipped by ngp_density_scatter_max, when it is empty);
+ * (flat_idx = -1, skipped by ngp_density_scatter_last, when it is empty);
  * xyzs (hi-lo, 3) = (coords/(G-1)*2-1)*(s-hgs) + (U*2-1)*hgs (networks.py:
  * 262-266; s_minus_hgs, hgs as fp32), flat_idx (hi-lo) = cascade*G^3 +
  * Morton index.  Randoms from Philox keyed by (seed, *counter_dev, cascade,

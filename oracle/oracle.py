@@ -317,6 +317,41 @@ def mlp_forward(x16, Ws, out_act=None):
     return h
 
 
+U32 = 2.0 ** -24  # fp32 unit roundoff
+
+
+def ulp16(v):
+    """fp16 ulp at |v| (2^-24 in the subnormal range)."""
+    a = v.abs().clamp_min(2.0 ** -14)
+    return torch.exp2(torch.floor(torch.log2(a)) - 10)
+
+
+def mlp_forward_bound(x16, Ws):
+    """mlp_forward (ReLU hidden, no output activation) plus, per output, a
+    bound on |out - out'| for ANY implementation with the same fp16 storage
+    points (fp16 weights and layer outputs) that accumulates each dot
+    product in fp32 in any order (e.g. MFMA tiles vs this oracle's GEMM):
+    products of fp16 operands are exact in fp32; a length-n fp32 sum is off
+    by at most gamma_n * sum|terms| (gamma_n = n u / (1 - n u)); an error d
+    in a layer's inputs moves its outputs by at most |W| d; rounding to fp16
+    then adds at most one fp16 ulp (the two values may straddle a rounding
+    boundary); ReLU is 1-Lipschitz.  Returns (out, bound), both fp32."""
+    h = x16.float()
+    d = torch.zeros_like(h)
+    for i, W in enumerate(Ws):
+        W16 = rh(W.detach()).float()
+        n = W16.shape[1]
+        gam = n * U32 / (1 - n * U32)
+        z = h @ W16.t()
+        dz = d @ W16.abs().t() + gam * (h.abs() @ W16.abs().t())
+        if i < len(Ws) - 1:
+            z = torch.relu(z)
+        hn = rh(z)
+        d = dz + ulp16(z.abs() + dz)
+        h = hn
+    return h, d
+
+
 # density net 32->64->16, color net 32->64->64->16(pad; 3 used)
 DENSITY_DIMS = (32, 64, 16)
 COLOR_DIMS = (32, 64, 64, 16)
@@ -560,3 +595,37 @@ class OracleTrainer:
             g = p.grad if p.grad is not None else torch.zeros_like(p)
             adam_(p.data, g.contiguous(), m, v, self.lr, self.t)
         return float(loss.detach()), int(cnt[0])
+
+
+def mark_borderline_cells(K, poses, img_wh, grid_size, scale, cascades, near=0.01, rel=1e-5):
+    """(cascades, G^3) bool in Morton order: cells whose projection into some
+    camera lies within `rel` (relative, float64) of an image border, of the
+    near plane or of the camera plane -- there mark_invisible_cells'
+    in_image / covered tests (models/networks.py:229-248) depend on the last
+    bits of a float32 matmul whose summation order differs between devices
+    and BLAS builds; everywhere else they are decided with a margin.
+    Test infrastructure (tests/test_occupancy_gpu.py, make_golden.py)."""
+    G = grid_size
+    W, H = img_wh
+    ax = torch.arange(G, dtype=torch.int64)
+    coords = torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3)
+    idx = morton3D(coords.int()).long()
+    P = poses.double()
+    R = P[:, :3, :3].transpose(1, 2)
+    T = -R @ P[:, :3, 3:]
+    Kd = K.double()
+    out = torch.zeros(cascades, G ** 3, dtype=torch.bool)
+    for c in range(cascades):
+        s = min(2 ** (c - 1), scale)
+        hgs = s / G
+        for i in range(0, G ** 3, 1 << 18):
+            x = (coords[i:i + (1 << 18)].double() / (G - 1) * 2 - 1) * (s - hgs)
+            uvd = Kd @ (R @ x.T + T)  # (N_cams, 3, chunk)
+            dd = uvd[:, 2]
+            uv = uvd[:, :2] / torch.where(dd == 0, torch.full_like(dd, 1e-300), dd)[:, None]
+            bu = torch.minimum(uv[:, 0].abs(), (uv[:, 0] - W).abs()) / W
+            bv = torch.minimum(uv[:, 1].abs(), (uv[:, 1] - H).abs()) / H
+            scale_d = 1 + dd.abs()
+            b = (bu < rel) | (bv < rel) | ((dd - near).abs() < rel * scale_d) | (dd.abs() < rel * scale_d)
+            out[c, idx[i:i + (1 << 18)]] = b.any(0)
+    return out

@@ -39,7 +39,9 @@ def main(argv=None):
     test = dataset_dict[a.dataset](a.root, split='test', downsample=a.downsample)
     gt = train.gt_u8().to(dev)
     dirs, poses = train.directions.to(dev).contiguous(), train.poses.to(dev).contiguous()
-    tr = NGPTrainer(scale=a.scale, batch_size=a.batch, device=dev, num_epochs=max(1, a.steps // 1000))
+    # erode for COLMAP scenes, as train.py:176-178 passes erode=dataset_name=='colmap'
+    tr = NGPTrainer(scale=a.scale, batch_size=a.batch, device=dev, num_epochs=max(1, a.steps // 1000),
+                    erode=a.dataset == "colmap")
     tr.mark_invisible_cells(train.K.to(dev), poses, train.img_wh)  # train.py:169-172
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -159,6 +159,18 @@ def test_render_case(scale, amp, seed):
             "total_samples": int(res["total_samples"])}
 
 
+def pins(grid, thr, band=0.05):
+    """Cells whose density is within `band` of thr in log space, with their
+    values: the sampled update resamples torch.nonzero(grid > thr), so a test
+    pins these cells to the glue's values first, and the list it draws from
+    is the glue's (the product's densities differ from the oracle's within the
+    fp16 storage-point error bound, far below the band)."""
+    g = grid.reshape(-1)
+    near = (torch.log(g.clamp_min(1e-30)) - math.log(thr)).abs() < band
+    idx = torch.nonzero(near)[:, 0]
+    return idx.int().numpy(), g[idx].numpy()
+
+
 def density_case(seed, amp):
     from models.networks import NGP
     model = NGP(0.5)
@@ -173,14 +185,70 @@ def density_case(seed, amp):
     model.update_density_grid(thr, warmup=True)
     out["warm_bitfield"] = model.density_bitfield.numpy().copy()
     g = model.density_grid
+    out["warm_pin_idx"], out["warm_pin_val"] = pins(g, thr)
     out["warm_grid_sha"] = sha(g)
     out["warm_mean"] = float(g[g > 0].mean())
     torch.manual_seed(seed + 1)
     model.update_density_grid(thr, warmup=False)
     out["upd_bitfield_sha"] = sha(model.density_bitfield)
+    out["upd_bitfield"] = model.density_bitfield.numpy().copy()
     out["upd_popcount"] = int(np.unpackbits(model.density_bitfield.numpy()).sum())
     g = model.density_grid
     out["upd_mean"] = float(g[g > 0].mean())
+    return out
+
+
+def occupancy_case(seed, amp, n_cams=10, W=64, H=48):
+    """mark_invisible_cells (networks.py:209-250) on a Lego-sized (scale 0.5,
+    1 cascade) and a garden-sized (scale 16, 6 cascades) grid, then the erode
+    occupancy chain on the Lego grid (train.py:175-178 with erode=True):
+    two warm-up updates (the second one decays by the per-cell erode factor)
+    and one sampled update.  Grids are stored as sha256 + summaries (the
+    count grid takes n_cams+1 values: a histogram of count*n_cams); the final
+    bitfields in full."""
+    from models.networks import NGP
+    out = {"case": "occupancy_erode", "seed": seed, "amp": amp, "n_cams": n_cams, "W": W, "H": H}
+    thr = 0.01 * 1024 / 3 ** 0.5
+    for tag, scale in (("lego", 0.5), ("garden", 16.0)):
+        sc = S.AnalyticScene(W=W, H=H, n_images=n_cams, scale=scale)
+        model = NGP(scale)
+        G = model.grid_size
+        ax = torch.arange(G, dtype=torch.int32)
+        model.register_buffer("density_grid", torch.zeros(model.cascades, G ** 3))
+        model.register_buffer("grid_coords", torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3))
+        model.mark_invisible_cells(sc.K, sc.poses, (W, H))
+        cg = model.count_grid
+        k = torch.round(cg * n_cams).long()
+        assert torch.equal(cg, (k / n_cams).float()), "count grid values are k / n_cams"
+        out[f"{tag}_count_sha"] = sha(cg)  # torch CPU: k / n_cams correctly rounded
+        out[f"{tag}_k_sha"] = sha(k.to(torch.uint8))  # the number of covering cameras per cell
+        # cells whose projections sit on an image border / the near plane (fp64,
+        # oracle.mark_borderline_cells) depend on float32 matmul order: masked
+        bl = O.mark_borderline_cells(sc.K, sc.poses, (W, H), G, scale, model.cascades)
+        out[f"{tag}_n_borderline"] = int(bl.sum())
+        out[f"{tag}_k_masked_sha"] = sha(torch.where(bl, 255, k).to(torch.uint8))
+        out[f"{tag}_mark_masked_sha"] = sha(torch.where(bl, 7.0, model.density_grid))
+        out[f"{tag}_count_hist"] = torch.stack([torch.bincount(k[c], minlength=n_cams + 1)
+                                                for c in range(model.cascades)]).numpy()
+        out[f"{tag}_mark_sha"] = sha(model.density_grid)
+        out[f"{tag}_invisible"] = (model.density_grid < 0).sum(1).numpy()
+        if tag != "lego":
+            continue
+        table_override(model, 100 + seed, amp)
+        torch.manual_seed(seed)
+        model.update_density_grid(thr, warmup=True, erode=True)
+        model.update_density_grid(thr, warmup=True, erode=True)
+        g = model.density_grid
+        out["warm2_bitfield"] = model.density_bitfield.numpy().copy()
+        out["warm2_pin_idx"], out["warm2_pin_val"] = pins(g, thr)
+        out["warm2_grid_sha"] = sha(g)
+        out["warm2_mean"] = float(g[g > 0].mean())
+        torch.manual_seed(seed + 1)
+        model.update_density_grid(thr, warmup=False, erode=True)
+        g = model.density_grid
+        out["upd_bitfield"] = model.density_bitfield.numpy().copy()
+        out["upd_grid_sha"] = sha(g)
+        out["upd_mean"] = float(g[g > 0].mean())
     return out
 
 
@@ -191,8 +259,13 @@ def main():
         train_case("lego_train", 0.5, 0.0, 256, 1.0, 1),
         train_case("garden_train", 16.0, 1 / 256, 128, 1.0, 2),
         test_render_case(0.5, 1.0, 3),
-        density_case(4, 1.0),
     ]
+    # update_density_grid writes density_grid_tmp[c, indices] with duplicate
+    # cells: torch's parallel CPU index_put_ lets threads race on them, so
+    # the occupancy cases run on one thread (sequential: the last duplicate
+    # in list order wins, the semantics the product reproduces)
+    torch.set_num_threads(1)
+    cases += [density_case(4, 1.0), occupancy_case(5, 1.0)]
     for c in cases:
         path = os.path.join(HERE, f"{c['case']}.npz")
         np.savez_compressed(path, **{k: np.asarray(v) for k, v in c.items()})

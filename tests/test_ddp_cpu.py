@@ -19,6 +19,13 @@ def _free_port():
     return p
 
 
+def _cells():
+    g = torch.Generator().manual_seed(0)
+    idx = torch.randint(0, 4096, (3000,), generator=g)  # many duplicates
+    sig = torch.rand(3000, generator=g) * 10
+    return idx, sig
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -29,15 +36,17 @@ def _worker(rank, world, port, q):
         g = torch.arange(10, dtype=torch.float32) * (rank + 1)
         ddp.allreduce_grad_(g)
         out["grad"] = g
-        # 2) sharded occupancy evaluation + MAX combine == single-process result
-        n = 1000
-        idx = torch.randperm(4096, generator=torch.Generator().manual_seed(0))[:n]
-        coords = torch.stack([idx % 16, (idx // 16) % 16, idx // 256], 1)
-        si, sc = ddp.shard_cells(idx, coords, rank, world)
-        tmp = torch.zeros(4096)
-        tmp[si] = torch.sin(si.float()).abs() + sc.sum(1).float() * 1e-3
-        ddp.combine_density_tmp_(tmp)
-        out["tmp"] = tmp
+        # 2) sharded occupancy evaluation + MAX combine of the (position, sigma)
+        # keys == single-process last-writer-wins result (duplicate cells, some
+        # duplicated across the shard boundary)
+        idx, sig = _cells()
+        lo, hi = ddp.shard_range(idx.shape[0], rank, world)
+        key = torch.zeros(4096, dtype=torch.int64)
+        pos = torch.arange(lo, hi, dtype=torch.int64)
+        kv = ((pos + 1) << 32) | sig[lo:hi].view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        key.scatter_reduce_(0, idx[lo:hi], kv, reduce="amax")
+        ddp.combine_density_tmp_(key)
+        out["tmp"] = torch.where(key != 0, (key & 0xFFFFFFFF).to(torch.int32).view(torch.float32), 0.)
         # 3) threshold broadcast from rank 0
         thr = torch.tensor([1.0 + rank, 2.0])
         ddp.sync_threshold_(thr)
@@ -62,11 +71,11 @@ def test_ddp_pieces_world2():
     for r in range(2):
         torch.testing.assert_close(res[r]["grad"], base * 3)
         assert res[r]["thr"].tolist() == [1.0, 2.0]
-    idx = torch.randperm(4096, generator=torch.Generator().manual_seed(0))[:1000]
-    coords = torch.stack([idx % 16, (idx // 16) % 16, idx // 256], 1)
+    idx, sig = _cells()
+    torch.set_num_threads(1)  # torch's sequential index_put_: the last duplicate wins
     full = torch.zeros(4096)
-    full[idx] = torch.sin(idx.float()).abs() + coords.sum(1).float() * 1e-3
-    torch.testing.assert_close(res[0]["tmp"], full)
+    full[idx] = sig
+    assert torch.equal(res[0]["tmp"], full)
     assert torch.equal(res[0]["tmp"], res[1]["tmp"])
 
 

@@ -75,30 +75,4 @@ def test_product_test_render_matches_reference_glue():
     assert abs(int(res["total_samples"]) - int(fx["total_samples"])) <= 4
 
 
-def test_product_density_update_matches_reference_glue():
-    fx = load("density_update")
-    fm = FixtureModel(0.5, int(fx["seed"]), float(fx["amp"]))
-    m = NGP(0.5)
-    m.load_tcnn_params(fm.xyz_encoder.params.detach(), fm.rgb_net.params.detach())
-    G = m.grid_size
-    ax = torch.arange(G, dtype=torch.int32)
-    m.register_buffer("density_grid", torch.zeros(1, G ** 3))
-    m.register_buffer("grid_coords", torch.stack(torch.meshgrid(ax, ax, ax, indexing="ij"), -1).reshape(-1, 3))
-    m = m.to(DEV)
-    # the jitter of networks.py:267 is drawn with torch.rand_like: replay the
-    # reference run's CPU draw on the device
-    torch.manual_seed(int(fx["seed"]))
-    jit = torch.rand(G ** 3, 3)
-    orig = torch.rand_like
-    torch.rand_like = lambda x, **k: jit.to(x.device, x.dtype) if x.shape == jit.shape else orig(x, **k)
-    try:
-        m.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=True)
-    finally:
-        torch.rand_like = orig
-    ref = torch.from_numpy(fx["warm_bitfield"])
-    got = m.density_bitfield.cpu()
-    diff_bits = int(np.unpackbits((got ^ ref).numpy()).sum())
-    # cells whose density sits within fp16 rounding of the threshold may flip
-    assert diff_bits <= 1e-3 * 128 ** 3, diff_bits
-    g = m.density_grid
-    assert abs(float(g[g > 0].mean()) - float(fx["warm_mean"])) < 1e-2 * float(fx["warm_mean"])
+# the occupancy update vs the glue: tests/test_occupancy_gpu.py
