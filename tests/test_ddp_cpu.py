@@ -72,9 +72,13 @@ def test_ddp_pieces_world2():
         torch.testing.assert_close(res[r]["grad"], base * 3)
         assert res[r]["thr"].tolist() == [1.0, 2.0]
     idx, sig = _cells()
+    nt = torch.get_num_threads()
     torch.set_num_threads(1)  # torch's sequential index_put_: the last duplicate wins
-    full = torch.zeros(4096)
-    full[idx] = sig
+    try:
+        full = torch.zeros(4096)
+        full[idx] = sig
+    finally:
+        torch.set_num_threads(nt)
     assert torch.equal(res[0]["tmp"], full)
     assert torch.equal(res[0]["tmp"], res[1]["tmp"])
 
