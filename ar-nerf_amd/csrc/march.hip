@@ -121,9 +121,10 @@ __global__ void __launch_bounds__(256) raygen_aabb_kernel(
 // raygen_aabb_kernel) and the marcher's start perturbation noise ~ U[0,1)
 // (models/custom_functions.py:83), from Philox keyed by (seed, step).
 // gt_u8 (n_img, HW, 3) u8 -> rgb_gt = u8 / 255 (f32).
+template <typename GT>
 __global__ void __launch_bounds__(256) sample_batch_kernel(
-    uint64_t seed, uint64_t step, const int64_t* __restrict__ step_dev, const uint8_t* __restrict__ gt_u8, int64_t n_img,
-    int64_t hw,
+    uint64_t seed, uint64_t step, const int64_t* __restrict__ step_dev, int64_t ray_offset, const GT* __restrict__ gt,
+    int64_t n_img, int64_t hw,
     const float* __restrict__ directions, const float* __restrict__ poses, int64_t n_rays,
     const float* __restrict__ center, const float* __restrict__ half_size, float near, int64_t* __restrict__ img_idx,
     int64_t* __restrict__ pix_idx, float* __restrict__ rgb_gt, float* __restrict__ noise,
@@ -131,15 +132,21 @@ __global__ void __launch_bounds__(256) sample_batch_kernel(
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_rays) return;
     if (step_dev) step += (uint64_t)*step_dev;  // device counter + offset (graph replays)
-    const uint4 u = philox4x32(make_uint4((uint32_t)r, (uint32_t)(r >> 32), (uint32_t)step, (uint32_t)(step >> 32)),
+    const int64_t q = r + ray_offset;  // the ray's index in the global batch (data-parallel ranks)
+    const uint4 u = philox4x32(make_uint4((uint32_t)q, (uint32_t)(q >> 32), (uint32_t)step, (uint32_t)(step >> 32)),
                                make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
     const int64_t img = uniform_index(u.x, n_img), pix = uniform_index(u.y, hw);
     img_idx[r] = img;
     pix_idx[r] = pix;
     noise[r] = (float)(u.z >> 8) * (1.0f / 16777216.0f);
-    const uint8_t* g = gt_u8 + (img * hw + pix) * 3;
+    const GT* g = gt + (img * hw + pix) * 3;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) rgb_gt[3 * r + i] = (float)g[i] / 255.0f;
+    for (int i = 0; i < 3; ++i) {
+        if constexpr (sizeof(GT) == 1)
+            rgb_gt[3 * r + i] = (float)g[i] / 255.0f;  // read_image's astype(float32) / 255
+        else
+            rgb_gt[3 * r + i] = g[i];
+    }
     gen_ray(poses + img * 12, directions + pix * 3, center, half_size, near, rays_o + 3 * r, rays_d + 3 * r,
             hits_t + 2 * r);
 }
@@ -652,32 +659,44 @@ int ngp_raygen_aabb(const float* directions, const float* poses, const int64_t* 
     return ngp_launch_status();
 }
 
-int ngp_sample_batch(uint64_t seed, uint64_t step, const uint8_t* gt_u8, int64_t n_img, int64_t hw,
-                     const float* directions, const float* poses, int64_t n_rays, const float* center,
-                     const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
-                     float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream) {
-    NGP_CHECK_ARG(n_rays >= 0 && n_img >= 1 && hw >= 1);
+static int launch_sample_batch(uint64_t seed, uint64_t step, const int64_t* step_dev, int64_t ray_offset,
+                               const void* gt, int gt_f32, int64_t n_img, int64_t hw, const float* directions,
+                               const float* poses, int64_t n_rays, const float* center, const float* half_size,
+                               float near_distance, int64_t* img_idx, int64_t* pix_idx, float* rgb_gt, float* noise,
+                               float* rays_o, float* rays_d, float* hits_t, void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && n_img >= 1 && hw >= 1 && ray_offset >= 0 && (gt_f32 == 0 || gt_f32 == 1));
     if (n_rays == 0) return NGP_OK;
-    NGP_CHECK_ARG(gt_u8 && directions && poses && center && half_size && img_idx && pix_idx && rgb_gt && noise &&
+    NGP_CHECK_ARG(gt && directions && poses && center && half_size && img_idx && pix_idx && rgb_gt && noise &&
                   rays_o && rays_d && hits_t);
-    sample_batch_kernel<<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
-        seed, step, nullptr, gt_u8, n_img, hw, directions, poses, n_rays, center, half_size, near_distance, img_idx,
-        pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t);
+    if (gt_f32)
+        sample_batch_kernel<float><<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
+            seed, step, step_dev, ray_offset, (const float*)gt, n_img, hw, directions, poses, n_rays, center,
+            half_size, near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t);
+    else
+        sample_batch_kernel<uint8_t><<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
+            seed, step, step_dev, ray_offset, (const uint8_t*)gt, n_img, hw, directions, poses, n_rays, center,
+            half_size, near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t);
     return ngp_launch_status();
 }
 
-int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_add, const uint8_t* gt_u8, int64_t n_img,
-                         int64_t hw, const float* directions, const float* poses, int64_t n_rays, const float* center,
-                         const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
-                         float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream) {
-    NGP_CHECK_ARG(n_rays >= 0 && n_img >= 1 && hw >= 1 && step_dev);
-    if (n_rays == 0) return NGP_OK;
-    NGP_CHECK_ARG(gt_u8 && directions && poses && center && half_size && img_idx && pix_idx && rgb_gt && noise &&
-                  rays_o && rays_d && hits_t);
-    sample_batch_kernel<<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
-        seed, (uint64_t)step_add, step_dev, gt_u8, n_img, hw, directions, poses, n_rays, center, half_size,
-        near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t);
-    return ngp_launch_status();
+int ngp_sample_batch(uint64_t seed, uint64_t step, int64_t ray_offset, const void* gt, int gt_f32, int64_t n_img,
+                     int64_t hw, const float* directions, const float* poses, int64_t n_rays, const float* center,
+                     const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
+                     float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream) {
+    return launch_sample_batch(seed, step, nullptr, ray_offset, gt, gt_f32, n_img, hw, directions, poses, n_rays,
+                               center, half_size, near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d,
+                               hits_t, stream);
+}
+
+int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_add, int64_t ray_offset, const void* gt,
+                         int gt_f32, int64_t n_img, int64_t hw, const float* directions, const float* poses,
+                         int64_t n_rays, const float* center, const float* half_size, float near_distance,
+                         int64_t* img_idx, int64_t* pix_idx, float* rgb_gt, float* noise, float* rays_o,
+                         float* rays_d, float* hits_t, void* stream) {
+    NGP_CHECK_ARG(step_dev);
+    return launch_sample_batch(seed, (uint64_t)step_add, step_dev, ray_offset, gt, gt_f32, n_img, hw, directions,
+                               poses, n_rays, center, half_size, near_distance, img_idx, pix_idx, rgb_gt, noise,
+                               rays_o, rays_d, hits_t, stream);
 }
 
 int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, int grid_size, uint32_t* summary, void* stream) {

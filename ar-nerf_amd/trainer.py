@@ -178,7 +178,9 @@ class NGPTrainer:
         self.bg = torch.ones(3, **f) if self.esf == 0 else torch.zeros(3, **f)  # models/rendering.py:287-296
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(1000 + seed + self.rank)
-        self.sample_seed = (1000003 * (seed + 1) + 7919 * self.rank) & 0xFFFFFFFFFFFFFFFF  # ngp_sample_batch key
+        # ngp_sample_batch key: one seed for all ranks, rank r draws rays [r*R, (r+1)*R) of the global
+        # batch (independent uniform draws per ray, as the reference's per-rank DataLoaders)
+        self.sample_seed = (1000003 * (seed + 1)) & 0xFFFFFFFFFFFFFFFF
         # occupancy draws: rank-independent (every rank draws the same cells and
         # jitter; each evaluates its shard), so any world size builds one grid
         self.occ_seed = ((1000003 * (seed + 1)) ^ 0x5DEECE66D) & 0xFFFFFFFFFFFFFFFF
@@ -344,7 +346,9 @@ class NGPTrainer:
             if src[0] == "sample":
                 _, add, gt = src
                 n_img, hw = gt.shape[0], gt.shape[1]
-                vren._ok(L.ngp_sample_batch_dev(self.sample_seed, _p(self.dctr[1:]), add, _p(gt), n_img, hw,
+                assert gt.dtype in (torch.uint8, torch.float32) and gt.is_contiguous()
+                vren._ok(L.ngp_sample_batch_dev(self.sample_seed, _p(self.dctr[1:]), add, self.rank * R, _p(gt),
+                                                int(gt.dtype == torch.float32), n_img, hw,
                                                 _p(directions), _p(poses), R, _p(self.center), _p(self.half_size),
                                                 ctypes_float(NEAR_DISTANCE), _p(m["img_idxs"]), _p(m["pix_idxs"]),
                                                 _p(m["rgb_gt"]), _p(m["noise"]), _p(m["rays_o"]), _p(m["rays_d"]),
@@ -452,9 +456,10 @@ class NGPTrainer:
         return self._on_exec_stream(self._step, ("idx", img_idxs, pix_idxs, noise), rgb_gt, directions, poses,
                                     apply_adam, nxt)
 
-    def train_step(self, gt_u8, directions, poses):
+    def train_step(self, gt, directions, poses):
         """One training step on a batch drawn on device from the training set
-        (gt_u8 (n_img, HW, 3) u8 images, directions (HW,3), poses (n_img,3,4)):
+        (gt (n_img, HW, 3) u8 images -- or f32 colours, e.g. alpha-blended
+        data -- directions (HW,3), poses (n_img,3,4)):
         the reference's DataLoader + training_step with nothing on the host.
         The next step's batch is drawn and marched ahead on the side stream.
         Steady-state steps (batch already marched ahead, no occupancy update
@@ -464,9 +469,9 @@ class NGPTrainer:
         if (self.use_graphs and self._pending is not None and (gs % ui != 0 or self._updated_for == gs)
                 and gs >= self.warmup_steps and self.kernel_events is None and not self.random_bg
                 and not self.no_prefetch):
-            return self._replay(gt_u8, directions, poses, (gs + 1) % ui == 0)
-        return self._on_exec_stream(self._step, ("sample", 0, gt_u8), None, directions, poses, True,
-                                    ("sample", 1, gt_u8))
+            return self._replay(gt, directions, poses, (gs + 1) % ui == 0)
+        return self._on_exec_stream(self._step, ("sample", 0, gt), None, directions, poses, True,
+                                    ("sample", 1, gt))
 
     def _set_lr(self):
         lr = self.lr()
@@ -474,7 +479,7 @@ class NGPTrainer:
             self.lr_dev.fill_(lr)
             self._lr_set = lr
 
-    def _replay(self, gt_u8, directions, poses, update_after):
+    def _replay(self, gt, directions, poses, update_after):
         """Graph-replayed steady-state step for the batch pending in set k.
         Plain variant: the step's kernels on the capture stream, the next
         batch's march forked onto the side stream and joined before the end,
@@ -486,14 +491,14 @@ class NGPTrainer:
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
         self._set_lr()
-        key = (k, bool(update_after), gt_u8.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt_u8.shape)
+        key = (k, bool(update_after), gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype)
         g = self._graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
             # capture on a side stream, ordered after everything enqueued so far
             torch.cuda.current_stream().synchronize()
             with torch.cuda.graph(g):
-                self._graph_body(k, gt_u8, directions, poses, update_after)
+                self._graph_body(k, gt, directions, poses, update_after)
             self._graphs[key] = g
         g.replay()
         self.cur = k
@@ -505,14 +510,14 @@ class NGPTrainer:
             self._updated_for = self.global_step
         return self.out_loss
 
-    def _graph_body(self, k, gt_u8, directions, poses, update_after=False):
+    def _graph_body(self, k, gt, directions, poses, update_after=False):
         self.cur = k
         self._bind(self.msets[k])
         cs = torch.cuda.current_stream()
         if not update_after:
             def fork():
                 self.march_stream.wait_stream(cs)
-                self._march(1 - k, ("sample", 1, gt_u8), directions, poses, self.march_stream)
+                self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
 
             self._compute(self.rgb_gt, True, fork)
             cs.wait_stream(self.march_stream)
@@ -521,7 +526,7 @@ class NGPTrainer:
             self._compute(self.rgb_gt, True, None)
             vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
             self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=False)
-            self._march(1 - k, ("sample", 0, gt_u8), directions, poses, cs)
+            self._march(1 - k, ("sample", 0, gt), directions, poses, cs)
 
     def _step(self, src, rgb_gt, directions, poses, apply_adam, next_src):
         self._ev("occupancy_update", 0)

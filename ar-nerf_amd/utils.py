@@ -15,6 +15,10 @@ or save state_dict only, as ModelCheckpoint(save_weights_only=True) does).
 import torch
 
 TCNN_KEYS = ("xyz_encoder.params", "rgb_net.params")
+# tcnn modules without trainable state still register an (empty) `params`
+# Parameter -- the SH dir_encoder (models/networks.py:59-66) -- so every
+# reference checkpoint holds 'model.dir_encoder.params' of shape [0]
+EMPTY_TCNN_KEYS = ("dir_encoder.params",)
 
 
 def _load(ckpt_path):
@@ -43,6 +47,7 @@ def tcnn_state_dict(model):
     xyz, rgb = model.tcnn_params()
     sd['xyz_encoder.params'] = xyz.clone()
     sd['rgb_net.params'] = rgb.clone()
+    sd['dir_encoder.params'] = torch.zeros(0, dtype=rgb.dtype)
     for name in ('density_grid', 'grid_coords'):
         if hasattr(model, name) and name not in sd:
             sd[name] = getattr(model, name)
@@ -60,6 +65,11 @@ def load_ckpt(model, ckpt_path, model_name='model', prefixes_to_ignore=[]):
     ck = extract_model_state_dict(ckpt_path, model_name, prefixes_to_ignore)
     if all(k in ck for k in TCNN_KEYS):
         model.load_tcnn_params(ck.pop(TCNN_KEYS[0]), ck.pop(TCNN_KEYS[1]))
+    for k in EMPTY_TCNN_KEYS:  # parameter-free tcnn encodings: nothing to load
+        if k in ck:
+            if ck[k].numel() != 0:
+                raise RuntimeError(f"checkpoint entry {k} should be empty, has {ck[k].numel()} values")
+            ck.pop(k)
     for name in ('density_grid', 'grid_coords'):
         if name in ck and name not in dict(model.named_buffers()):
             if hasattr(model, name):

@@ -39,10 +39,10 @@ def _declare(L):
     sig = {
         "ngp_ray_aabb_intersect": [vp, vp, c_int64, vp, vp, c_int, c_int, vp, vp, vp, vp],
         "ngp_raygen_aabb": [vp, vp, vp, vp, c_int64, vp, vp, c_float, vp, vp, vp, vp],
-        "ngp_sample_batch": [ctypes.c_uint64, ctypes.c_uint64, vp, c_int64, c_int64, vp, vp, c_int64, vp, vp,
-                             c_float, vp, vp, vp, vp, vp, vp, vp, vp],
-        "ngp_sample_batch_dev": [ctypes.c_uint64, vp, c_int64, vp, c_int64, c_int64, vp, vp, c_int64, vp, vp,
-                                 c_float, vp, vp, vp, vp, vp, vp, vp, vp],
+        "ngp_sample_batch": [ctypes.c_uint64, ctypes.c_uint64, c_int64, vp, c_int, c_int64, c_int64, vp, vp, c_int64,
+                             vp, vp, c_float, vp, vp, vp, vp, vp, vp, vp, vp],
+        "ngp_sample_batch_dev": [ctypes.c_uint64, vp, c_int64, c_int64, vp, c_int, c_int64, c_int64, vp, vp, c_int64,
+                                 vp, vp, c_float, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_adam_step_dev": [vp, vp, vp, vp, vp, c_int64, vp, c_float, c_float, c_float, vp, c_float, c_int, vp],
         "ngp_counters_inc": [vp, c_int, vp],
         "ngp_occupied_cells": [vp, c_int64, c_float, vp, vp, vp],

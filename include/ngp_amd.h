@@ -58,21 +58,25 @@ int ngp_raygen_aabb(const float* directions, const float* poses, const int64_t* 
  * BaseDataset.__getitem__, datasets/base.py:22-35, the batch gathers of
  * train.py:85-97 and the marcher's torch.rand noise, custom_functions.py:83):
  * img_idx ~ U{0..n_img-1}, pix_idx ~ U{0..hw-1}, noise ~ U[0,1) from
- * Philox-4x32-10 keyed by (seed, step) -- a pure function of (seed, step, ray);
- * rgb_gt (n_rays,3) = gt_u8[img, pix, :] / 255 with gt_u8 (n_img,hw,3) u8;
+ * Philox-4x32-10 keyed by (seed, step, ray_offset + ray) -- a pure function of
+ * those, so ranks drawing rays [rank*R, (rank+1)*R) of one global batch
+ * (ray_offset = rank*R) together draw exactly the single-process batch;
+ * rgb_gt (n_rays,3) = gt[img, pix, :] with gt (n_img,hw,3) either u8
+ * (gt_f32 = 0; value / 255 in fp32, read_image's astype(float32)/255) or
+ * f32 (gt_f32 = 1; e.g. alpha-blended images, datasets/color_utils.py);
  * rays and hits_t as ngp_raygen_aabb. */
-int ngp_sample_batch(uint64_t seed, uint64_t step, const uint8_t* gt_u8, int64_t n_img, int64_t hw,
-                     const float* directions, const float* poses, int64_t n_rays, const float* center,
+int ngp_sample_batch(uint64_t seed, uint64_t step, int64_t ray_offset, const void* gt, int gt_f32, int64_t n_img,
+                     int64_t hw, const float* directions, const float* poses, int64_t n_rays, const float* center,
                      const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
                      float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream);
 
 /* ngp_sample_batch with the RNG counter in device memory: step = *step_dev +
  * step_add (a captured graph replays with the counter advanced on device). */
-int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_add, const uint8_t* gt_u8,
-                         int64_t n_img, int64_t hw, const float* directions, const float* poses,
-                         int64_t n_rays, const float* center, const float* half_size,
-                         float near_distance, int64_t* img_idx, int64_t* pix_idx, float* rgb_gt,
-                         float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream);
+int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_add, int64_t ray_offset, const void* gt,
+                         int gt_f32, int64_t n_img, int64_t hw, const float* directions, const float* poses,
+                         int64_t n_rays, const float* center, const float* half_size, float near_distance,
+                         int64_t* img_idx, int64_t* pix_idx, float* rgb_gt, float* noise, float* rays_o,
+                         float* rays_d, float* hits_t, void* stream);
 
 /* ------------------------------------------------- occupancy grid utils */
 /* Replaces vren.morton3D (binding.cpp:36-40 -> raymarching.cu:62-88). */

@@ -37,7 +37,7 @@ def main(argv=None):
     torch.cuda.set_device(dev)
     train = dataset_dict[a.dataset](a.root, split='train', downsample=a.downsample)
     test = dataset_dict[a.dataset](a.root, split='test', downsample=a.downsample)
-    gt = train.gt_u8().to(dev)
+    gt = train.gt_f32().to(dev)  # float targets, as the reference's loss sees them
     dirs, poses = train.directions.to(dev).contiguous(), train.poses.to(dev).contiguous()
     # erode for COLMAP scenes, as train.py:176-178 passes erode=dataset_name=='colmap'
     tr = NGPTrainer(scale=a.scale, batch_size=a.batch, device=dev, num_epochs=max(1, a.steps // 1000),

@@ -50,3 +50,21 @@ def test_slim_ckpt_pops_training_entries(tmp_path):
     m2 = NGP(0.5, seed=9)
     utils.load_ckpt(m2, path)
     assert torch.equal(m2.params, m.params)
+
+
+def test_reference_checkpoint_with_empty_dir_encoder_params(tmp_path):
+    """The reference's tcnn SH encoding registers an empty `params` Parameter,
+    so its checkpoints hold 'model.dir_encoder.params' of shape [0]."""
+    src = NGP(0.5, seed=3)
+    ck = _ref_ckpt(src)
+    assert ck['state_dict']['model.dir_encoder.params'].shape == (0,)
+    path = str(tmp_path / "ref.ckpt")
+    torch.save(ck, path)
+    dst = NGP(0.5, seed=4)
+    utils.load_ckpt(dst, path)
+    assert torch.equal(dst.params, src.params)
+    ck['state_dict']['model.dir_encoder.params'] = torch.zeros(3)
+    torch.save(ck, path)
+    import pytest
+    with pytest.raises(RuntimeError, match="dir_encoder.params"):
+        utils.load_ckpt(NGP(0.5), path)

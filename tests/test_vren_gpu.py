@@ -75,8 +75,10 @@ def test_raygen_aabb_matches_host_rays():
 def test_sample_batch_on_device():
     """ngp_sample_batch (datasets/base.py:22-35 + get_rays + AABB + noise on
     device): the rays equal raygen_aabb on the drawn pixels bit for bit, the
-    ground truth is the u8 gather / 255, indices and noise are in range and
-    roughly uniform, and the draw is a pure function of (seed, step)."""
+    ground truth is the u8 gather / 255 (or the f32 gather), indices and
+    noise are in range and roughly uniform, the draw is a pure function of
+    (seed, step, global ray index): two ranks with ray_offset 0 / R/2 draw
+    the two halves of the single-process batch."""
     import ctypes
     sc = S.SyntheticScene(W=200, H=200, n_images=20, scale=0.5)
     gt = torch.randint(0, 256, (20, 200 * 200, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(0)).to(DEV)
@@ -84,14 +86,17 @@ def test_sample_batch_on_device():
     center = torch.zeros(1, 3, device=DEV); half = torch.ones(1, 3, device=DEV) * 0.5
     R = 1 << 16
 
-    def draw(seed, step):
-        out = dict(img=torch.empty(R, dtype=torch.int64, device=DEV), pix=torch.empty(R, dtype=torch.int64, device=DEV),
-                   rgb=torch.empty(R, 3, device=DEV), noise=torch.empty(R, device=DEV),
-                   o=torch.empty(R, 3, device=DEV), d=torch.empty(R, 3, device=DEV), ht=torch.empty(R, 2, device=DEV))
+    gtf = torch.rand(20, 200 * 200, 3, generator=torch.Generator().manual_seed(1)).to(DEV)
+
+    def draw(seed, step, n=R, offset=0, g=gt):
+        out = dict(img=torch.empty(n, dtype=torch.int64, device=DEV), pix=torch.empty(n, dtype=torch.int64, device=DEV),
+                   rgb=torch.empty(n, 3, device=DEV), noise=torch.empty(n, device=DEV),
+                   o=torch.empty(n, 3, device=DEV), d=torch.empty(n, 3, device=DEV), ht=torch.empty(n, 2, device=DEV))
         p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        vren._ok(vren.lib().ngp_sample_batch(seed, step, p(gt), 20, 200 * 200, p(dirs), p(poses), R, p(center),
-                                             p(half), 0.01, p(out["img"]), p(out["pix"]), p(out["rgb"]),
-                                             p(out["noise"]), p(out["o"]), p(out["d"]), p(out["ht"]), vren._stream()),
+        vren._ok(vren.lib().ngp_sample_batch(seed, step, offset, p(g), int(g.dtype == torch.float32), 20, 200 * 200,
+                                             p(dirs), p(poses), n, p(center), p(half), 0.01, p(out["img"]),
+                                             p(out["pix"]), p(out["rgb"]), p(out["noise"]), p(out["o"]), p(out["d"]),
+                                             p(out["ht"]), vren._stream()),
                  "sample_batch")
         return out
 
@@ -108,6 +113,11 @@ def test_sample_batch_on_device():
     ro, rd, ht = vren.raygen_aabb(dirs, poses, a["img"], a["pix"], center, half, 0.01)
     assert torch.equal(ro, a["o"]) and torch.equal(rd, a["d"]) and torch.equal(ht, a["ht"])
     assert torch.equal(a["rgb"], _true_div255(gt[a["img"], a["pix"]]))
+    h0, h1 = draw(5, 1, R // 2, 0), draw(5, 1, R // 2, R // 2)
+    for k in a:
+        assert torch.equal(torch.cat([h0[k], h1[k]]), a[k])
+    f = draw(5, 1, g=gtf)
+    assert torch.equal(f["pix"], a["pix"]) and torch.equal(f["rgb"], gtf[a["img"], a["pix"]])
 
 
 def test_morton_packbits():
