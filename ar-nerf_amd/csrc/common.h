@@ -19,6 +19,15 @@ static inline int ngp_launch_status() {
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Kernel timing hook (ngp_timing_set, host.hip): HIP events around one launch.
+void ngp_timing_mark(int id, int end, hipStream_t s);
+#define NGP_TIMED(id, s, ...)          \
+    do {                               \
+        ngp_timing_mark((id), 0, (s)); \
+        __VA_ARGS__;                   \
+        ngp_timing_mark((id), 1, (s)); \
+    } while (0)
+
 // Workgroups of `kernel` that fit on the whole device at once (occupancy x
 // CUs): the grid of a persistent kernel, so per-block prologues (LDS weight
 // images) are paid once per resident block, not once per tile.

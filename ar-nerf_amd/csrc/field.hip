@@ -939,16 +939,16 @@ int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const in
     static const bool xcd = getenv("NGP_ENCODE_XCD") && getenv("NGP_ENCODE_XCD")[0] == '1';  // diagnostic
     if (!xcd) {
         static const unsigned cap = resident_blocks(hash_encode_kernel<true>, 256, 0);
-        hash_encode_kernel<true><<<std::max(1u, std::min(cap, (unsigned)((n + 255) / 256))), 256, 0,
+        NGP_TIMED(NGP_K_HASH_ENCODE, as_stream(stream), hash_encode_kernel<true><<<std::max(1u, std::min(cap, (unsigned)((n + 255) / 256))), 256, 0,
                                    as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16,
-                                                        (_Float16*)enc_pm);
+                                                        (_Float16*)enc_pm));
         return ngp_launch_status();
     }
     static const unsigned cap = resident_blocks(hash_encode_kernel<false>, 256, 0);
     const unsigned per_pair = std::max(1u, std::min(cap / 8, (unsigned)((n + 255) / 256)));
-    hash_encode_kernel<false><<<8 * per_pair, 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga,
+    NGP_TIMED(NGP_K_HASH_ENCODE, as_stream(stream), hash_encode_kernel<false><<<8 * per_pair, 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga,
                                                                            (const uint32_t*)table_f16,
-                                                                           (_Float16*)enc_pm);
+                                                                           (_Float16*)enc_pm));
     return ngp_launch_status();
 }
 
@@ -962,15 +962,17 @@ int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, cons
     GridArgs ga{};
     if (!dirs) {  // density net only (occupancy updates)
         static const unsigned capd = resident_blocks(field_fwd_kernel<false, true>, 256, 0);
-        field_fwd_kernel<false, true><<<persistent_blocks(n, 64, capd), 256, 0, as_stream(stream)>>>(
-            nullptr, nullptr, n, n_dev, ga, nullptr, (const _Float16*)mlp_f16, sigmas, nullptr, nullptr,
-            (_Float16*)h_f16, (const _Float16*)enc_pm, n, sample_idx);
+        NGP_TIMED(NGP_K_FIELD_MLP, as_stream(stream),
+                  field_fwd_kernel<false, true><<<persistent_blocks(n, 64, capd), 256, 0, as_stream(stream)>>>(
+                      nullptr, nullptr, n, n_dev, ga, nullptr, (const _Float16*)mlp_f16, sigmas, nullptr, nullptr,
+                      (_Float16*)h_f16, (const _Float16*)enc_pm, n, sample_idx));
         return ngp_launch_status();
     }
     static const unsigned cap = resident_blocks(field_fwd_kernel<true, true>, 256, 0);
-    field_fwd_kernel<true, true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
-        nullptr, dirs, n, n_dev, ga, nullptr, (const _Float16*)mlp_f16, sigmas, rgbs, nullptr, (_Float16*)h_f16,
-        (const _Float16*)enc_pm, n, sample_idx);
+    NGP_TIMED(NGP_K_FIELD_MLP, as_stream(stream),
+              field_fwd_kernel<true, true><<<persistent_blocks(n, 64, cap), 256, 0, as_stream(stream)>>>(
+                  nullptr, dirs, n, n_dev, ga, nullptr, (const _Float16*)mlp_f16, sigmas, rgbs, nullptr,
+                  (_Float16*)h_f16, (const _Float16*)enc_pm, n, sample_idx));
     return ngp_launch_status();
 }
 
@@ -990,9 +992,9 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
             return NGP_ERANGE;
         attr_set = true;
     }
-    field_bwd_mlp_kernel<<<persistent_blocks(n, 64, 256), 256, lds, as_stream(stream)>>>(
+    NGP_TIMED(NGP_K_MLP_BWD, as_stream(stream), field_bwd_mlp_kernel<<<persistent_blocks(n, 64, 256), 256, lds, as_stream(stream)>>>(
         dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
-        grad_mlp, enc_pm_stride);
+        grad_mlp, enc_pm_stride));
     return ngp_launch_status();
 }
 
@@ -1004,8 +1006,8 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && denc && grad_table && ((uintptr_t)denc & 15) == 0);
-    hash_bwd_kernel<0><<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx,
-                                                                                     ga, denc, grad_table, 0, L);
+    NGP_TIMED(NGP_K_HASH_BWD_COARSE, as_stream(stream), hash_bwd_kernel<0><<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx,
+                                                                                     ga, denc, grad_table, 0, L));
     return ngp_launch_status();
 }
 
@@ -1025,15 +1027,15 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
     const unsigned blocks = persistent_blocks(n, 64, cap);
     hipStream_t s = as_stream(stream);
     if (mode == 1)
-        hash_bwd_kernel<1><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<1><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
     else if (mode == 2)
-        hash_bwd_kernel<2><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<2><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
     else if (mode == 4)
-        hash_bwd_kernel<4><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<4><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
     else if (mode == 3)
-        hash_bwd_kernel<3><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<3><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
     else
-        hash_bwd_kernel<0><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi);
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<0><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
     return ngp_launch_status();
 }
 

@@ -486,14 +486,14 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
     hipStream_t s = as_stream(stream);
     if (phase & 1) {
         static const unsigned capC = resident_blocks(hash_count_kernel, 256, 0);
-        hash_count_kernel<<<persistent_blocks(n, TILE, capC), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, ws);
-        hash_scan_kernel<<<NSLOT, 256, 0, s>>>(n_dev, n, ba, ws);
-        hash_plan_kernel<<<1, MAXB, 0, s>>>(nbt, ws);
+        NGP_TIMED(NGP_K_HASH_COUNT, s, hash_count_kernel<<<persistent_blocks(n, TILE, capC), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, ws));
+        NGP_TIMED(NGP_K_HASH_SCAN, s, hash_scan_kernel<<<NSLOT, 256, 0, s>>>(n_dev, n, ba, ws));
+        NGP_TIMED(NGP_K_HASH_PLAN, s, hash_plan_kernel<<<1, MAXB, 0, s>>>(nbt, ws));
     }
     if (phase & 2) {
         static const unsigned capW = resident_blocks(hash_write_kernel<2>, 256, 0);
-        hash_write_kernel<2><<<persistent_blocks(n, TILE, capW), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba,
-                                                                           denc, grad_table, ws);
+        NGP_TIMED(NGP_K_HASH_WRITE, s, hash_write_kernel<2><<<persistent_blocks(n, TILE, capW), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba,
+                                                                           denc, grad_table, ws));
         static bool attr = false;
         const size_t lds = (size_t)BENT * 2 * sizeof(double);
         if (!attr) {
@@ -503,7 +503,7 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
             attr = true;
         }
         static const unsigned capB = resident_blocks(hash_accum_kernel<0>, 1024, lds);
-        hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws);
+        NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws));
     }
     return ngp_launch_status();
 }

@@ -3,9 +3,63 @@
 
 #include "common.h"
 
+// Kernel timing hook (ngp_timing_set): a one-lane kernel before and after
+// each instrumented launch stores the GPU wall clock into the caller's stamp
+// table, row = *step_dev % ring -- plain kernel nodes, so a captured HIP
+// graph times its kernels on every replay (HIP event nodes inside captured
+// graphs are not available with the HIP runtime torch ships).
+static uint64_t* g_stamps = nullptr;
+static const int64_t* g_step = nullptr;
+static int64_t g_ring = 0;
+static int g_ids = 0, g_per = 0;
+static uint64_t g_begin = 0, g_end = 0;  // ids bracketed before / after
+static int32_t g_count[64];
+
+__global__ void stamp_kernel(uint64_t* __restrict__ stamps, const int64_t* __restrict__ step, int64_t ring,
+                             int64_t row_len, int64_t col) {
+    if (threadIdx.x == 0) stamps[(*step % ring) * row_len + col] = wall_clock64();
+}
+
+void ngp_timing_mark(int id, int end, hipStream_t s) {
+    if (!g_stamps || id < 0 || id >= g_ids) return;
+    const int i = g_count[id];
+    if (end) g_count[id] = i + 1;
+    if (i >= g_per || !(((end ? g_end : g_begin) >> id) & 1ull)) return;
+    stamp_kernel<<<1, 64, 0, s>>>(g_stamps, g_step, g_ring, (int64_t)g_ids * g_per * 2,
+                                  ((int64_t)id * g_per + i) * 2 + (end ? 1 : 0));
+}
+
 extern "C" {
 
-const char* ngp_version(void) { return "ngp_amd 0.1 gfx950"; }
+const char* ngp_version(void) { return "ngp_amd 0.2 gfx950"; }
+
+int ngp_timing_set(uint64_t* stamps, const int64_t* step_dev, int64_t ring, int n_ids, int per_id, uint64_t begin_mask,
+                   uint64_t end_mask) {
+    if (stamps && (!step_dev || ring < 1 || n_ids < 1 || n_ids > 64 || per_id < 1)) return NGP_EINVAL;
+    g_stamps = stamps;
+    g_step = stamps ? step_dev : nullptr;
+    g_ring = stamps ? ring : 0;
+    g_ids = stamps ? n_ids : 0;
+    g_per = stamps ? per_id : 0;
+    g_begin = begin_mask;
+    g_end = end_mask;
+    for (int i = 0; i < 64; ++i) g_count[i] = 0;
+    return NGP_OK;
+}
+
+int ngp_timing_counts(int32_t* counts, int n_ids) {
+    if (!counts || n_ids < 0 || n_ids > 64) return NGP_EINVAL;
+    for (int i = 0; i < n_ids; ++i) counts[i] = g_count[i];
+    return NGP_OK;
+}
+
+double ngp_timing_tick_ns(void) {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+        return 0.0;
+    return 1e6 / (double)khz;
+}
 
 // Level table of tcnn's Grid/Hash encoding as the reference configures it
 // (models/networks.py:33-49): computed in fp32 the way tcnn does

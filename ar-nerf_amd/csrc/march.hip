@@ -669,13 +669,13 @@ static int launch_sample_batch(uint64_t seed, uint64_t step, const int64_t* step
     NGP_CHECK_ARG(gt && directions && poses && center && half_size && img_idx && pix_idx && rgb_gt && noise &&
                   rays_o && rays_d && hits_t);
     if (gt_f32)
-        sample_batch_kernel<float><<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
+        NGP_TIMED(NGP_K_SAMPLE_BATCH, as_stream(stream), sample_batch_kernel<float><<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
             seed, step, step_dev, ray_offset, (const float*)gt, n_img, hw, directions, poses, n_rays, center,
-            half_size, near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t);
+            half_size, near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t));
     else
-        sample_batch_kernel<uint8_t><<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
+        NGP_TIMED(NGP_K_SAMPLE_BATCH, as_stream(stream), sample_batch_kernel<uint8_t><<<nblk(n_rays, 256), 256, 0, as_stream(stream)>>>(
             seed, step, step_dev, ray_offset, (const uint8_t*)gt, n_img, hw, directions, poses, n_rays, center,
-            half_size, near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t);
+            half_size, near_distance, img_idx, pix_idx, rgb_gt, noise, rays_o, rays_d, hits_t));
     return ngp_launch_status();
 }
 
@@ -708,9 +708,9 @@ int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, int grid_size
     const int64_t bpc = (int64_t)grid_size * grid_size * grid_size / 64;
     const bool dil = grid_size >= 4 && (grid_size & (grid_size - 1)) == 0 && bpc > 0 && n_words % bpc == 0 &&
                      n_words % 64 == 0;
-    bitfield_summary_kernel<<<nblk(n_words, 256), 256, 0, as_stream(stream)>>>(
+    NGP_TIMED(NGP_K_SUMMARY, as_stream(stream), bitfield_summary_kernel<<<nblk(n_words, 256), 256, 0, as_stream(stream)>>>(
         reinterpret_cast<const uint64_t*>(bitfield), n_words, dil ? bpc : 1, dil ? grid_size / 4 : 0, summary,
-        summary + (n_words + 31) / 32);
+        summary + (n_words + 31) / 32));
     return ngp_launch_status();
 }
 
@@ -755,7 +755,7 @@ int ngp_march_train_count(const float* rays_o, const float* rays_d, const float*
         if (march_simple(p)) march_count_kernel<true><<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts);
         else march_count_kernel<false><<<nblk(n_rays, 64), 64, 0, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts);
     }
-    scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total);
+    NGP_TIMED(NGP_K_SCAN_RAYS, s, scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total));
     return ngp_launch_status();
 }
 
@@ -806,23 +806,23 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
             const char* edg = getenv("NGP_MARCH_DIAG");
             const int dg = edg ? atoi(edg) : 0;
             if (dg == 1)
-                march_slots_wave_kernel<1><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
-                                                                            counts, slot_t, slot_dt);
+                NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<1><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
+                                                                            counts, slot_t, slot_dt));
             else if (dg == 2)
-                march_slots_wave_kernel<2><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
-                                                                            counts, slot_t, slot_dt);
+                NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<2><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
+                                                                            counts, slot_t, slot_dt));
             else
-                march_slots_wave_kernel<0><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
-                                                                            counts, slot_t, slot_dt);
+                NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<0><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
+                                                                            counts, slot_t, slot_dt));
         } else if (march_simple(p)) {
-            if (stage) march_slots_kernel<true, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
-            else march_slots_kernel<true, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
+            if (stage) NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<true, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw));
+            else NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<true, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw));
         } else {
-            if (stage) march_slots_kernel<false, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
-            else march_slots_kernel<false, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw);
+            if (stage) NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw));
+            else NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw));
         }
     }
-    scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total);
+    NGP_TIMED(NGP_K_SCAN_RAYS, s, scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total));
     return ngp_launch_status();
 }
 
@@ -832,8 +832,8 @@ int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int6
     NGP_CHECK_ARG(n_rays >= 0 && max_samples >= 1);
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_o && rays_d && rays_a && slot_t && slot_dt && xyzs && dirs && deltas && ts);
-    march_compact_kernel<<<nblk(n_rays, 4), 256, 0, as_stream(stream)>>>(rays_o, rays_d, rays_a, n_rays, slot_t,
-                                                                        slot_dt, max_samples, xyzs, dirs, deltas, ts);
+    NGP_TIMED(NGP_K_COMPACT, as_stream(stream), march_compact_kernel<<<nblk(n_rays, 4), 256, 0, as_stream(stream)>>>(rays_o, rays_d, rays_a, n_rays, slot_t,
+                                                                        slot_dt, max_samples, xyzs, dirs, deltas, ts));
     return ngp_launch_status();
 }
 

@@ -756,11 +756,11 @@ static void launch_segments(const int32_t* counts, const int64_t* rays_a, int64_
                             hipStream_t s) {
     const unsigned blocks = (unsigned)((n_rows + SEG_ROWS - 1) / SEG_ROWS);
     if (cap > 0)
-        segments_kernel<true><<<blocks, SEG_THREADS, 0, s>>>(nullptr, rays_a, n_rows, cap, first, start_ws, total,
-                                                             total_acc, sample_idx);
+        NGP_TIMED(NGP_K_SEGMENTS, s, segments_kernel<true><<<blocks, SEG_THREADS, 0, s>>>(nullptr, rays_a, n_rows, cap, first, start_ws, total,
+                                                             total_acc, sample_idx));
     else
-        segments_kernel<false><<<blocks, SEG_THREADS, 0, s>>>(counts, rays_a, n_rows, 0, first, start_ws, total,
-                                                              total_acc, sample_idx);
+        NGP_TIMED(NGP_K_SEGMENTS, s, segments_kernel<false><<<blocks, SEG_THREADS, 0, s>>>(counts, rays_a, n_rows, 0, first, start_ws, total,
+                                                              total_acc, sample_idx));
 }
 
 // ------------------------------------------- chunked forward (training)
@@ -823,9 +823,9 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
     LossArgs la{loss_type, lambda_opacity, lambda_depth, depth_scale, 1.0f / (float)n_rays, T_threshold};
     // one row per wave: every row's dependent load chain in flight at once
     // (a few rows per wave serialised their memory latencies)
-    composite_loss_wave_kernel<<<(unsigned)std::min<int64_t>((n_rays + 3) / 4, 1 << 20), 256, 0, as_stream(stream)>>>(
+    NGP_TIMED(NGP_K_COMPOSITE, as_stream(stream), composite_loss_wave_kernel<<<(unsigned)std::min<int64_t>((n_rays + 3) / 4, 1 << 20), 256, 0, as_stream(stream)>>>(
         sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
-        out_depth, out_loss, n_active, sample_idx, (unsigned long long*)alloc_ws, n_active_total, stats);
+        out_depth, out_loss, n_active, sample_idx, (unsigned long long*)alloc_ws, n_active_total, stats));
     return ngp_launch_status();
 }
 
@@ -834,12 +834,12 @@ int ngp_chunk_counts(const int64_t* rays_a, int64_t n_rows, int first, const flo
     NGP_CHECK_ARG(n_rows >= 0 && first >= 1 && counts && rays_a);
     if (n_rows == 0) return NGP_OK;
     if (!sigmas) {
-        chunk_first_kernel<<<(unsigned)((n_rows + 255) / 256), 256, 0, as_stream(stream)>>>(rays_a, n_rows, first,
-                                                                                           counts);
+        NGP_TIMED(NGP_K_CHUNK, as_stream(stream), chunk_first_kernel<<<(unsigned)((n_rows + 255) / 256), 256, 0, as_stream(stream)>>>(rays_a, n_rows, first,
+                                                                                           counts));
     } else {
         NGP_CHECK_ARG(deltas != nullptr);
-        chunk_rest_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, as_stream(stream)>>>(sigmas, deltas, rays_a, n_rows,
-                                                                                      first, T_threshold, counts);
+        NGP_TIMED(NGP_K_CHUNK, as_stream(stream), chunk_rest_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, as_stream(stream)>>>(sigmas, deltas, rays_a, n_rows,
+                                                                                      first, T_threshold, counts));
     }
     return ngp_launch_status();
 }
@@ -887,9 +887,9 @@ int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
     const int64_t n4 = n / 4;
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
+    NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, lr, beta1, beta2, eps, bc1,
-                                                                 bc2, grad_scale, zero_grad, nullptr, nullptr);
+                                                                 bc2, grad_scale, zero_grad, nullptr, nullptr));
     return ngp_launch_status();
 }
 
@@ -903,9 +903,9 @@ int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_av
     const int64_t n4 = n / 4;
     int64_t blocks = (n4 + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
+    NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
-                                                                 1.f, grad_scale, zero_grad, lr_dev, step_dev);
+                                                                 1.f, grad_scale, zero_grad, lr_dev, step_dev));
     return ngp_launch_status();
 }
 

@@ -1,0 +1,102 @@
+"""Per-kernel timing of the training step inside the captured HIP graphs
+(libngp_amd.so's ngp_timing_set hook: every instrumented launch is
+bracketed by two one-lane kernels that store the GPU wall clock into a
+stamp table on the device, row = the trainer's device step counter, so a
+replayed graph times every one of its kernels; HIP event nodes inside
+captured graphs are not available with the HIP runtime torch ships).
+
+A stamp pair measures from the end of the kernel before the launch (the
+stamp kernel runs when its predecessor in the stream has finished) to the
+end of the launch: the kernel's execution plus its dispatch gap, like a HIP
+event pair around it.  Measurement plumbing only (bench.py, scripts/); the
+product path never arms it."""
+from __future__ import annotations
+
+import ctypes
+import itertools
+from ctypes import c_double, c_int, c_int32, c_int64, c_uint64, c_void_p
+
+import torch
+
+import vren
+
+NAMES = ["sample_batch", "bitfield_summary", "march", "scan_rays", "march_compact", "segments", "hash_encode",
+         "field_mlp", "chunk_rest", "composite_loss", "hash_count", "hash_scan", "hash_plan", "mlp_bwd",
+         "hash_bwd_coarse", "hash_write", "hash_accum", "adam"]  # include/ngp_amd.h NGP_K_* order
+_UID = itertools.count(1)
+PER_ID = 4  # launches per kernel id per step (segments runs 3x, encode / MLP 2x, +1 in occupancy updates)
+
+
+def _lib():
+    L = vren.lib()
+    L.ngp_timing_set.argtypes = [c_void_p, c_void_p, c_int64, c_int, c_int, c_uint64, c_uint64]
+    L.ngp_timing_counts.argtypes = [c_void_p, c_int]
+    L.ngp_timing_tick_ns.restype = c_double
+    return L
+
+
+class KernelTimer:
+    """Stamp table for `rows` steps (row = step counter % rows) of the kernels
+    `names` (None: all).  trainer.timer = KernelTimer(...) makes NGPTrainer
+    capture (and replay) graphs with the stamps inside; read() after a
+    synchronize returns per-launch durations of every step that ran.
+    span=(first, last): only a stamp before `first` and one after `last`
+    (consecutive launches on one stream timed together: read_span())."""
+
+    def __init__(self, step_counter, rows=4096, names=None, device="cuda", span=None):
+        self.step = step_counter  # int64 device scalar: the row of the running step
+        self.rows = rows
+        self.row_len = len(NAMES) * PER_ID * 2
+        self.stamps = torch.zeros(rows, self.row_len, dtype=torch.int64, device=device)
+        ids = range(len(NAMES)) if names is None else [NAMES.index(n) for n in names]
+        self.begin_mask = self.end_mask = sum(1 << i for i in ids)
+        self.span = span
+        if span is not None:
+            self.begin_mask, self.end_mask = 1 << NAMES.index(span[0]), 1 << NAMES.index(span[1])
+        self.tick_ns = _lib().ngp_timing_tick_ns()
+        self.uid = next(_UID)  # graphs captured with this table are keyed by it (never reused)
+
+    def arm(self):
+        vren._ok(_lib().ngp_timing_set(self.stamps.data_ptr(), self.step.data_ptr(), self.rows, len(NAMES), PER_ID,
+                                       self.begin_mask, self.end_mask), "timing_set")
+
+    def disarm(self):
+        """-> launches per kernel id bracketed since arm()"""
+        c = (c_int32 * len(NAMES))()
+        vren._ok(_lib().ngp_timing_counts(c, len(NAMES)), "timing_counts")
+        vren._ok(_lib().ngp_timing_set(None, None, 0, 0, 0, 0, 0), "timing_set")
+        return list(c)
+
+    def reset(self):
+        self.stamps.zero_()
+
+    def read(self):
+        """{kernel: [ms per launch, ...]} over the rows written since reset()"""
+        st = self.stamps.cpu().view(self.rows, len(NAMES), PER_ID, 2)
+        a, b = st[..., 0], st[..., 1]
+        ok = (a > 0) & (b >= a)
+        ms = (b - a).double() * self.tick_ns * 1e-6
+        out = {}
+        for k, n in enumerate(NAMES):
+            m = ok[:, k, :]
+            if m.any():
+                out[n] = ms[:, k, :][m].tolist()
+        return out
+
+    def read_span(self):
+        """[ms per step] from the stamp before span[0]'s first launch to the
+        one after span[1]'s first launch, over the rows written"""
+        st = self.stamps.cpu().view(self.rows, len(NAMES), PER_ID, 2)
+        a = st[:, NAMES.index(self.span[0]), 0, 0]
+        b = st[:, NAMES.index(self.span[1]), 0, 1]
+        ok = (a > 0) & (b >= a)
+        return ((b - a)[ok].double() * self.tick_ns * 1e-6).tolist()
+
+    def steps(self):
+        st = self.stamps.view(self.rows, -1)
+        return int((st > 0).any(1).sum())
+
+    def summary(self):
+        """{kernel: (avg ms per launch, launches per step)} over the steps recorded"""
+        n = max(1, self.steps())
+        return {k: (sum(v) / len(v), len(v) / n) for k, v in self.read().items()}

@@ -197,8 +197,10 @@ class NGPTrainer:
         self._graphs = {}
         self.L = vren.lib()
         HG._lib()
-        # {"field_fwd"|"mlp_bwd"|"hash_bwd"|stage: (start, end) torch.cuda.Event} (bench)
+        # {"field_fwd"|"mlp_bwd"|"hash_bwd"|stage: (start, end) torch.cuda.Event} (eager diagnostics)
         self.kernel_events = None
+        # ktimer.KernelTimer (bench): graph replays carry HIP events around every kernel
+        self.timer = None
 
     @staticmethod
     def _march_buffers(R, cap, f, cap_bits):
@@ -492,15 +494,23 @@ class NGPTrainer:
             torch.cuda.current_stream().wait_event(ev)
         self._set_lr()
         key = (k, bool(update_after), gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype)
-        g = self._graphs.get(key)
-        if g is None:
+        tm = self.timer  # (measurement) graphs with wall-clock stamp kernels around every kernel
+        if tm is not None:
+            key = key + (tm.uid,)
+        if key not in self._graphs:
             g = torch.cuda.CUDAGraph()
             # capture on a side stream, ordered after everything enqueued so far
             torch.cuda.current_stream().synchronize()
-            with torch.cuda.graph(g):
-                self._graph_body(k, gt, directions, poses, update_after)
+            if tm is not None:
+                tm.arm()
+            try:
+                with torch.cuda.graph(g):
+                    self._graph_body(k, gt, directions, poses, update_after)
+            finally:
+                if tm is not None:
+                    tm.disarm()
             self._graphs[key] = g
-        g.replay()
+        self._graphs[key].replay()
         self.cur = k
         self._bind(self.msets[k])
         self._pending = (1 - k, None)  # marched (and joined) inside the graph

@@ -33,36 +33,47 @@ sys.path[:0] = [os.path.join(ROOT, "ar-nerf_amd")]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-import hashgrid as HG  # noqa: E402
+import ktimer as KT  # noqa: E402
 import synthetic as S  # noqa: E402
 from trainer import NGPTrainer  # noqa: E402
 
 with open(os.path.join(ROOT, "BASELINE.json")) as f:
     BASELINE = json.load(f)
 
-# Algorithmic work per unit of the per-kernel breakdown:
-#  hash_encode (unit: field-evaluated sample): 16 levels x 8 corners x fp16x2
-#      gathered (512 B) + xyz (12 B) + list index (4 B) read + fp16 encoding
-#      (64 B) written                                              -> bytes
-#  field_mlp (evaluated sample): density 32-64-16 + colour 32-64-64-16 forward
-#      (2 x (3072 + 7168) FLOP)                                    -> FLOPs
-#  mlp_bwd (gradient-carrying sample): forward recompute + dX + dW of both
-#      MLPs (16-row output layers as computed)                     -> FLOPs
-#  hash_bwd_coarse (gradient-carrying sample, levels 0-7): xyz + index (16 B)
-#      + dL/denc (64 B) read + read-modify-write of 8 x 8 x 2 fp32 table
-#      gradients (2 x 512 B)                                       -> bytes
-#  adam (parameter): p, g, m, v read; p, m, v, fp16 p written, g zeroed (34 B)
+# Algorithmic work per unit, per kernel of the step (SURVEY.md
+# §8(d)).  Units: "marched" / "evaluated" (field-evaluated) / "composited" /
+# "active" (gradient-carrying) samples of the step, "params" of the model.
+# bound: "hbm" (algorithmic bytes vs 8 TB/s), "mfma" (dense fp16 FLOPs vs
+# 2.5 PFLOP/s), "atomic" (bytes added by memory-side float atomics vs the
+# chip-wide ~1.3 TB/s of MI355X_MICROARCH.md "Global float atomics"),
+# "latency" (small scans / list builders: time only).
+#  hash_encode: 16 levels x 8 corners x fp16x2 gathered (512 B) + xyz 12 B +
+#      list index 4 B read + fp16 encoding 64 B written            -> 592 B
+#  field_mlp: density 32-64-16 + colour 32-64-64-16 forward       -> 20,480 FLOP
+#  mlp_bwd: forward recompute + dX + dW of both MLPs               -> 59,392 FLOP
+#  hash_bwd_coarse (levels 0-7, atomic): 8 x 8 corners x 2 fp32 gradients
+#      added (512 B of atomics per sample)                         -> 512 B
+#  hash_bwd_fine = hash_write + hash_accum (levels 8-15, counting sort +
+#      LDS accumulation): xyz + index 16 B + dL/denc 64 B read + read-modify-
+#      write of 8 x 8 x 2 fp32 table gradients (2 x 512 B)         -> 1,104 B
+#  march + march_compact: xyz, dir, t, dt written (32 B / marched sample)
+#  composite_loss: fwd 28 B + bwd 48 B per composited sample      -> 76 B
+#  adam: p, g, m, v read; p, m, v, fp16 p written, g zeroed        -> 34 B / param
 _MLP_FWD = 2 * (32 * 64 + 64 * 16) + 2 * (32 * 64 + 64 * 64 + 64 * 16)
-KERNEL_WORK = {
-    "hash_encode": ("hbm", 16 * 8 * 4 + 12 + 4 + 64, "GB/s", "evaluated"),
-    "field_mlp": ("mfma", _MLP_FWD, "TFLOP/s", "evaluated"),
-    "mlp_bwd": ("mfma", 2 * (32 * 64 + 64 * 16 + 32 * 64 + 64 * 64 + 64 * 16)
-                + 2 * (16 * 64 + 64 * 64 + 64 * 16 + 16 * 64 + 64 * 32)
-                + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32), "TFLOP/s", "active"),
-    "hash_bwd_coarse": ("hbm", 16 + 64 + 2 * 8 * 8 * 2 * 4, "GB/s", "active"),
-    "adam": ("hbm", 34, "GB/s", "params"),
+_MLP_BWD = (2 * (32 * 64 + 64 * 16 + 32 * 64 + 64 * 64 + 64 * 16)
+            + 2 * (16 * 64 + 64 * 64 + 64 * 16 + 16 * 64 + 64 * 32)
+            + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32))
+KERNEL_WORK = {  # name: (bound, work per unit, unit basis, member kernels)
+    "hash_encode": ("hbm", 16 * 8 * 4 + 12 + 4 + 64, "evaluated", ["hash_encode"]),
+    "field_mlp": ("mfma", _MLP_FWD, "evaluated", ["field_mlp"]),
+    "mlp_bwd": ("mfma", _MLP_BWD, "active", ["mlp_bwd"]),
+    "hash_bwd_coarse": ("atomic", 8 * 8 * 2 * 4, "active", ["hash_bwd_coarse"]),
+    "hash_bwd_fine": ("hbm", 16 + 64 + 2 * 8 * 8 * 2 * 4, "active", ["hash_write", "hash_accum"]),
+    "march": ("hbm", 32, "marched", ["march", "march_compact"]),
+    "composite_loss": ("hbm", 76, "composited", ["composite_loss"]),
+    "adam": ("hbm", 34, "params", ["adam"]),
 }
-PEAK = {"hbm": 8000.0, "mfma": 2500.0}  # MI355X: HBM3E GB/s; dense fp16 MFMA TFLOP/s
+PEAK = {"hbm": (8000.0, "GB/s"), "mfma": (2500.0, "TFLOP/s"), "atomic": (1300.0, "GB/s")}
 
 
 def parse():
@@ -78,9 +89,9 @@ def parse():
     ap.add_argument("--psnr-views", type=int, default=2)
     ap.add_argument("--psnr-res", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--quiet", action="store_true")
-    ap.add_argument("--breakdown-steps", type=int, default=50, help="eager steps with per-kernel HIP events")
+    ap.add_argument("--breakdown-steps", type=int, default=100,
+                    help="graph-replayed steps with HIP events around every kernel (per-kernel breakdown)")
     ap.add_argument("--hash-backward", default="hybrid", choices=["hybrid", "binned", "atomic"])
     ap.add_argument("--bin-level-lo", type=int, default=None,
                     help="hybrid hash backward: first binned level (default: trainer's, 8 / 0 for cascaded scenes)")
@@ -175,57 +186,71 @@ def inference_bench(trainer, res, frames, world, rank):
                         "iteration in HIP graphs (16 iterations, then 8 per replay while rays remain), one host sync per graph"}
 
 
-def cpu_baseline(trainer, scene, gt_images, budget_s, batch):
-    """The oracle (oracle/, CPU restatement) timed on this host on the same
-    workload: full training steps on 8192-ray batches from the same model
-    state, as many as fit ~budget_s (at least 1)."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(trainer, scene, gt_images, batch, warm=3, timed=20):
+    """The oracle (oracle/, the CPU restatement of the reference's kernels +
+    torch fp32 autograd MLPs) timed on this host on the same workload: full
+    training steps on `batch`-ray batches from the trained model state,
+    `warm` untimed then `timed` timed, median step time.
+    Threads: the host cores this process may use (OMP_NUM_THREADS when set --
+    the GPU box's share -- else all cores)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # test/baseline infrastructure only
-    threads = int(os.environ.get("OMP_NUM_THREADS", min(16, os.cpu_count() or 1)))
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(threads)
     ot = O.OracleTrainer(trainer.params, scene.scale, trainer.density_bitfield, trainer.cascades)
     gen = torch.Generator().manual_seed(77)
     c = torch.zeros(1, 3); h = torch.ones(1, 3) * scene.scale
-    steps, t_total, samples = 0, 0.0, 0
-    while steps < 5 and (steps == 0 or t_total < budget_s):
+    times, samples = [], 0
+    for i in range(warm + timed):
         img, pix = scene.sample_batch(batch, gen)
         o, d = scene.rays(img, pix)
         _, ht, _ = O.ray_aabb_intersect(o, d, c, h, 1)
         ht = ht[:, 0].contiguous()
         ht[(ht[:, 0] >= 0) & (ht[:, 0] < 0.01), 0] = 0.01
-        gt = gt_images[img, pix].float().cpu() / 255
+        gt = gt_images[img.to(gt_images.device), pix.to(gt_images.device)].float().cpu() / 255
         noise = torch.rand(batch, generator=gen)
         t0 = time.perf_counter()
         _, n = ot.step(o.contiguous(), d.contiguous(), ht, gt, noise, torch.ones(3))
-        t_total += time.perf_counter() - t0
-        steps += 1
-        samples += n
-    return {"value": round(batch * steps / t_total, 1), "unit": "rays/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} full training step(s) of the {batch}-ray batch on the oracle "
-                      f"(C march/composite/hash + torch fp32 MLP autograd + C Adam over all params), "
-                      f"{samples / max(1, steps) / batch:.1f} samples/ray, {t_total:.1f} s"}
+        if i >= warm:
+            times.append(time.perf_counter() - t0)
+            samples += n
+    times.sort()
+    med = times[len(times) // 2] if len(times) % 2 else 0.5 * (times[len(times) // 2 - 1] + times[len(times) // 2])
+    return {"value": round(batch / med, 1), "unit": "rays/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"median of {timed} full training steps of the {batch}-ray batch after {warm} warm-up steps "
+                      f"on the oracle (C march/composite/hash + torch fp32 MLP autograd + C Adam over all "
+                      f"{trainer.params.numel()} params), {samples / max(1, timed) / batch:.1f} samples/ray, "
+                      f"{sum(times):.1f} s timed"}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
+def pmc_traffic(members, launches):
+    """HBM bytes per step of the op made of kernels `members` (launches per
+    step from the breakdown), from the committed PMC summary
     (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
     corrected per MI355X_MICROARCH.md "HBM"), or None if not measured."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            t = json.load(f).get(kernel)
+            t = json.load(f)
     except (OSError, ValueError):
         return None
-    return None if t is None else t.get("bytes_per_launch")
-
-
-def _recorded(event):
-    try:
-        event.elapsed_time(event)
-        return True
-    except (RuntimeError, ValueError):
-        return False
+    if not all(m in t and m in launches for m in members):
+        return None
+    return round(sum(t[m]["bytes_per_launch"] * launches[m][1] for m in members))
 
 
 def main():
@@ -243,13 +268,11 @@ def main():
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
     R = args.batch
 
-    def run(n, events=None):
+    def run(n):
         """n training steps, each on a batch drawn on device (trainer.train_step:
         pixels, ground truth and noise from a counter-based RNG); batch i+1 is
         drawn and marched on the side stream during step i."""
         for i in range(n):
-            if events is not None:
-                trainer.kernel_events = events[i]
             trainer.train_step(gt_images, directions, poses)
         trainer.drain()
 
@@ -258,9 +281,48 @@ def main():
     torch.cuda.synchronize()
     log(rank, f"[bench] pretrain {args.pretrain} steps in {time.time() - t0:.1f}s, "
               f"samples last batch {int(trainer.n_samples.item())}")
+    # ---- breakdown region: graph replays whose graphs carry HIP events
+    # around every kernel (ktimer: external event nodes, read back one ring
+    # slot behind); per-kernel durations of the step as it runs in the graphs
+    n_bd = max(1, args.breakdown_steps)
+    full = KT.KernelTimer(trainer.dctr, rows=max(4096, 2 * n_bd))
+    trainer.timer = full
+    run(64)  # capture this timer's graph variants
+    torch.cuda.synchronize()
+    full.reset()
+    trainer.stats.zero_()
+    t_bd = time.perf_counter()
+    run(n_bd)
+    torch.cuda.synchronize()
+    t_bd = (time.perf_counter() - t_bd) / n_bd
+    trainer.timer = None
+    bd_summary, bd_steps = full.summary(), full.steps()
+    marched_bd, composited_bd, active_bd, evaluated_bd = trainer.stat_totals()
+    if trainer.chunk_first <= 0:
+        evaluated_bd = marched_bd
+    units_bd = {"marched": marched_bd / n_bd, "evaluated": evaluated_bd / n_bd, "composited": composited_bd / n_bd,
+                "active": active_bd / n_bd, "params": trainer.params.numel()}
+
+    def op_row(name, summary, units):
+        bound, per_unit, basis, members = KERNEL_WORK[name]
+        ms = sum(summary[m][0] * summary[m][1] for m in members if m in summary)  # per step
+        if ms <= 0:
+            return None
+        work = units[basis] * per_unit  # per step
+        peak, unit = PEAK[bound]
+        achieved = work / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
+        return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 4), "ms_per_step": round(ms, 4),
+                "work_per_unit": per_unit, "units_per_step": round(units[basis], 1), "unit_basis": basis,
+                "kernels": members}
+
+    ops = {k: r for k in KERNEL_WORK if (r := op_row(k, bd_summary, units_bd)) is not None}
+    dominant = max(ops, key=lambda k: ops[k]["ms_per_step"])
+    kernels = {k: {"avg_launch_ms": round(v[0], 4), "launches_per_step": round(v[1], 2),
+                   "ms_per_step": round(v[0] * v[1], 4)} for k, v in sorted(bd_summary.items(), key=lambda kv: -kv[1][0] * kv[1][1])}
+    # ---- timed region: plain graph replays (no instrumentation: even two
+    # stamp kernels per step cost ~3 %)
     run(args.warmup)
-    # ---- timed region: steady-state steps replay captured HIP graphs
-    # (trainer.train_step); no per-kernel instrumentation inside
     trainer.stats.zero_()
     if world > 1:
         dist.barrier()
@@ -272,75 +334,67 @@ def main():
     if world > 1:
         dist.barrier()
     t_el = time.perf_counter() - t_start
+    marched, composited, active, evaluated = trainer.stat_totals()
+    # ---- roofline region: the same number of graph-replayed steps again, with
+    # one stamp before the dominant op's first kernel and one after its last
+    # (consecutive on the main stream)
+    members = KERNEL_WORK[dominant][3]
+    dom = KT.KernelTimer(trainer.dctr, rows=max(4096, 2 * args.steps), span=(members[0], members[-1]))
+    trainer.timer = dom
+    run(64)  # capture this timer's graph variants
+    torch.cuda.synchronize()
+    dom.reset()
+    trainer.stats.zero_()
+    t_rf = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    t_rf = (time.perf_counter() - t_rf) / args.steps
+    trainer.timer = None
+    span = dom.read_span()
+    dom_summary = {members[0]: (sum(span) / len(span), 1.0)} if span else bd_summary
+    m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
+    if trainer.chunk_first <= 0:
+        e_rf = m_rf
+    units_rf = {"marched": m_rf / args.steps, "evaluated": e_rf / args.steps, "composited": c_rf / args.steps,
+                "active": a_rf / args.steps, "params": trainer.params.numel()}
     t_max = torch.tensor([t_el], device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     t_el = float(t_max.item())
     total_rays = R * args.steps * world
     value = total_rays / t_el
-    marched, composited, active, evaluated = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         evaluated = marched
-    rm_s = marched / (R * args.steps)
-    vr_s = composited / (R * args.steps)
-    ev_s = evaluated / (R * args.steps)
-    # ---- breakdown region: the same steps run eagerly with HIP events around
-    # each kernel / stage, on the stream each is launched on (events cannot
-    # sit between the nodes of a replayed graph); per-kernel durations and the
-    # roofline come from here
-    n_bd = max(1, min(args.steps, args.breakdown_steps))
-    # raygen_march = inline march on the main stream (steps after an occupancy
-    # update); march_side = the next batch's march on the side stream, which
-    # overlaps the step's compute (averaged over the steps that launched one)
-    stages = ["occupancy_update", "raygen_march", "march_side", "field_fwd", "composite_loss", "composite", "mlp_bwd",
-              "hash_bwd",
-              "hash_binned_apply", "allreduce", "adam"]
-    ev = [dict() for _ in range(n_bd)]
-    trainer.stats.zero_()
-    torch.cuda.synchronize()
-    t_bd = time.perf_counter()
-    run(n_bd, ev)
-    torch.cuda.synchronize()
-    t_bd = time.perf_counter() - t_bd
-    trainer.kernel_events = None
-    marched_bd, _, active_bd, evaluated_bd = trainer.stat_totals()
-    if trainer.chunk_first <= 0:
-        evaluated_bd = marched_bd
-
-    def durations(name):
-        return [p[0].elapsed_time(p[1]) for e in ev for p in e.get(name, []) if _recorded(p[1])]
-
-    per_step = {"evaluated": evaluated_bd / n_bd, "active": active_bd / n_bd, "params": trainer.params.numel()}
-    kernels = {}
-    for k, (bound, per_unit, unit, basis) in KERNEL_WORK.items():
-        d = durations(k)
-        if not d:
-            continue
-        ms = sum(d) / len(d)
-        launches = len(d) / n_bd
-        units = per_step[basis] / launches if basis != "params" else per_step[basis] / launches
-        achieved = units * per_unit / (ms * 1e-3) / (1e9 if bound == "hbm" else 1e12)
-        kernels[k] = {"bound": bound, "achieved": round(achieved, 2), "peak": PEAK[bound], "unit": unit,
-                      "frac": round(achieved / PEAK[bound], 4), "avg_launch_ms": round(ms, 4),
-                      "launches_per_step": round(launches, 2), "work_per_unit": per_unit,
-                      "units_per_launch": round(units, 1), "unit_basis": basis}
-    dominant = max(kernels, key=lambda k: kernels[k]["avg_launch_ms"])
-    stage_ms = {}
-    for k in stages:
-        d = durations(k)
-        if d:  # per step (march_side: per launch, over the steps that launched one)
-            stage_ms[k] = round(sum(d) / (len(d) if k == "march_side" else n_bd), 4)
+    units = {"marched": marched / args.steps, "evaluated": evaluated / args.steps,
+             "composited": composited / args.steps, "active": active / args.steps, "params": trainer.params.numel()}
+    rm_s, vr_s, ev_s = units["marched"] / R, units["composited"] / R, units["evaluated"] / R
+    roof = op_row(dominant, dom_summary, units_rf)
+    roof = dict(op=dominant, traffic=pmc_traffic(members, bd_summary), traffic_unit="bytes per step", **roof,
+                measured=f"device wall-clock stamps before / after the op inside the captured graphs of "
+                         f"{args.steps} graph-replayed steps run right after the timed ones "
+                         f"({t_rf * 1e3:.4f} ms/step with the 2 stamps; ktimer)")
+    # step-level bound: every op's algorithmic bytes at HBM peak + MLP FLOPs at MFMA peak
+    hbm_bytes = sum(units[KERNEL_WORK[k][2]] * KERNEL_WORK[k][1] for k in KERNEL_WORK if KERNEL_WORK[k][0] != "mfma")
+    flops = sum(units[KERNEL_WORK[k][2]] * KERNEL_WORK[k][1] for k in KERNEL_WORK if KERNEL_WORK[k][0] == "mfma")
+    bound_ms = hbm_bytes / 8000e9 * 1e3 + flops / 2500e12 * 1e3
+    adam_ms = units["params"] * 34 / 8000e9 * 1e3
+    step_bound = {"hbm_bytes_per_step": round(hbm_bytes), "mlp_flops_per_step": round(flops),
+                  "ms_per_step_at_peak": round(bound_ms, 4), "rays_per_s_at_peak": round(R / (bound_ms * 1e-3)),
+                  "adam_ms_at_peak": round(adam_ms, 4),
+                  "note": "sum of the ops' algorithmic work at HBM / MFMA peak, serial; dense FusedAdam alone "
+                          "(34 B/param) costs adam_ms_at_peak per step"}
     loss = float(trainer.out_loss.sum().item())
     psnr = psnr_eval(trainer, scene, args.psnr_views, args.psnr_res) if (rank == 0 and args.psnr_views > 0) else None
     infer = inference_bench(trainer, args.infer_res, args.infer_frames, world, rank) if args.infer_frames > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(trainer, scene, gt_images, args.cpu_budget_s, R)
+        cpu = cpu_baseline(trainer, scene, gt_images, R)
     if rank == 0:
         out = {
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_el / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16/fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp16 field (MLP weight gradients on bf16 MFMA operands) / fp32 march, composite, Adam",
             "data": "synthetic (analytic sphere+box scene, 100 views 800x800, Lego intrinsics; random-init weights "
                     f"trained {args.pretrain} setup steps)",
             "config": {"workload": "lego-shaped training step: 8192 rays/rank, scale 0.5, 128^3 grid, L=16 F=2 "
@@ -354,13 +408,14 @@ def main():
                        "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
                        "erode": trainer.erode,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
-            "roofline": dict(kernel=dominant, traffic=pmc_traffic(dominant), **kernels[dominant]),
+            "roofline": roof,
+            "ops": ops,
             "kernels": kernels,
-            "stage_ms": stage_ms,
+            "step_bound": step_bound,
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
-            "breakdown_note": (f"kernels / stage_ms / roofline: HIP-event averages over {n_bd} eagerly run steps after "
-                               f"the timed region ({t_bd / n_bd * 1e3:.3f} ms/step eager); the timed steps replay "
-                               "captured HIP graphs"),
+            "breakdown_note": (f"ops / kernels: wall-clock stamps around every kernel inside the captured graphs "
+                               f"over {bd_steps} replayed steps ({t_bd * 1e3:.3f} ms/step with all stamps); roofline: "
+                               f"see roofline.measured"),
             "cpu_baseline": cpu,
             "inference": infer,
         }

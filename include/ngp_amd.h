@@ -33,6 +33,31 @@ extern "C" {
 /* Library build tag (gfx950 code object version string). */
 const char* ngp_version(void);
 
+/* ------------------------------------------------------ kernel timing */
+/* Measurement hook (bench.py, scripts/): when a table is set, every
+ * instrumented kernel launch is bracketed by two one-lane kernels on its
+ * stream that store the GPU wall clock (wall_clock64) into
+ * stamps[(*step_dev % ring) * (n_ids * per_id * 2) + (id * per_id + i) * 2 +
+ * {0 = before, 1 = after}] for the i-th launch of kernel id since this call
+ * (launches beyond per_id and ids >= n_ids are not stamped; the stamp before
+ * a launch of id only if bit id of begin_mask is set, the one after only if
+ * bit id of end_mask is: one stamp before the first and one after the last
+ * of consecutive launches times them together with the least perturbation).  Captured into a HIP graph, the stamps time every
+ * kernel of every replay, the row chosen by the device step counter at run
+ * time.  stamps == NULL disables the hook.  Host-side global state: not for
+ * concurrent callers.  ngp_timing_counts: launches bracketed per id since
+ * ngp_timing_set; ngp_timing_tick_ns: ns per wall-clock tick. */
+enum {
+    NGP_K_SAMPLE_BATCH = 0, NGP_K_SUMMARY, NGP_K_MARCH, NGP_K_SCAN_RAYS, NGP_K_COMPACT, NGP_K_SEGMENTS,
+    NGP_K_HASH_ENCODE, NGP_K_FIELD_MLP, NGP_K_CHUNK, NGP_K_COMPOSITE, NGP_K_HASH_COUNT, NGP_K_HASH_SCAN,
+    NGP_K_HASH_PLAN, NGP_K_MLP_BWD, NGP_K_HASH_BWD_COARSE, NGP_K_HASH_WRITE, NGP_K_HASH_ACCUM, NGP_K_ADAM,
+    NGP_K_COUNT
+};
+int ngp_timing_set(uint64_t* stamps, const int64_t* step_dev, int64_t ring, int n_ids, int per_id, uint64_t begin_mask,
+                   uint64_t end_mask);
+int ngp_timing_counts(int32_t* counts, int n_ids);
+double ngp_timing_tick_ns(void);
+
 /* ---------------------------------------------------------------- rays */
 /* Replaces vren.ray_aabb_intersect (binding.cpp:9-20 -> intersection.cu:59-100).
  * rays_o/rays_d (n_rays,3) f32; centers/half_sizes (n_voxels,3) f32.

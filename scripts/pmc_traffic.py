@@ -12,7 +12,9 @@ import os
 import sys
 
 NAMES = {"hash_bwd_kernel": "hash_bwd_coarse", "field_bwd_mlp_kernel": "mlp_bwd", "hash_encode_kernel": "hash_encode",
-         "adam_kernel": "adam", "field_fwd_kernel": "field_mlp"}
+         "adam_kernel": "adam", "field_fwd_kernel": "field_mlp", "hash_write_kernel": "hash_write",
+         "hash_accum_kernel": "hash_accum", "hash_count_kernel": "hash_count", "march_slots_wave_kernel": "march",
+         "march_compact_kernel": "march_compact", "composite_loss_wave_kernel": "composite_loss"}  # ktimer names
 
 
 def parse(path):
