@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import itertools
-from ctypes import c_double, c_int, c_int32, c_int64, c_uint64, c_void_p
+from ctypes import c_int32
 
 import torch
 
@@ -28,11 +28,7 @@ PER_ID = 4  # launches per kernel id per step (segments runs 3x, encode / MLP 2x
 
 
 def _lib():
-    L = vren.lib()
-    L.ngp_timing_set.argtypes = [c_void_p, c_void_p, c_int64, c_int, c_int, c_uint64, c_uint64]
-    L.ngp_timing_counts.argtypes = [c_void_p, c_int]
-    L.ngp_timing_tick_ns.restype = c_double
-    return L
+    return vren.lib()  # signatures declared in vren._declare
 
 
 class KernelTimer:
