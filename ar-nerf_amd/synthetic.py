@@ -183,3 +183,36 @@ class AnalyticScene(SyntheticScene):
                 o = P[:, 3].expand_as(d)
                 out[i, s:s + chunk] = (self.gt_rgb_rays(o, d) * 255 + 0.5).to(torch.uint8)
         return out
+
+
+def write_nsvf_scene(root, res=100, n_train=24, n_test=2, seed=7):
+    """The analytic scene as an NSVF-format dataset on disk (the Synthetic-
+    NeRF layout datasets/nsvf.py reads): rgb/{0,2}_XXXX.png (split 0 = train,
+    2 = test), pose/*.txt (4x4 c2w), intrinsics.txt, bbox.txt -- so the whole
+    ingest -> train -> test-PSNR flow of train.py runs on it.  The reader
+    assumes 800-px Synthetic-NeRF frames scaled by its `downsample`: read the
+    scene with downsample = res / 800."""
+    import os
+
+    from datasets.png import write_png
+    os.makedirs(os.path.join(root, "rgb"), exist_ok=True)
+    os.makedirs(os.path.join(root, "pose"), exist_ok=True)
+    fx = 0.5 * 800 / np.tan(0.5 * 0.6911112070083618)  # of the 800-px frame
+    with open(os.path.join(root, "intrinsics.txt"), "w") as f:
+        f.write(f"{fx} 0. 0. 0.\n")
+    b = 0.5 / 1.05  # NSVF scale = 1.05 * half side = 0.5, shift 0: poses unchanged
+    with open(os.path.join(root, "bbox.txt"), "w") as f:
+        f.write(f"{-b} {-b} {-b} {b} {b} {b} 0.01\n")
+    sc = AnalyticScene(W=res, H=res, n_images=n_train + n_test, seed=seed)
+    for i in range(n_train + n_test):
+        split = "0" if i < n_train else "2"
+        P = sc.poses[i]
+        d = sc.directions @ P[:, :3].t()
+        o = P[:, 3].expand_as(d)
+        rgb = sc.gt_rgb_rays(o.contiguous(), d.contiguous()).reshape(res, res, 3)
+        write_png(os.path.join(root, "rgb", f"{split}_{i:04d}.png"),
+                  (rgb.clamp(0, 1) * 255 + 0.5).to(torch.uint8).numpy())
+        c2w = np.eye(4)
+        c2w[:3] = P.numpy()
+        np.savetxt(os.path.join(root, "pose", f"{split}_{i:04d}.txt"), c2w)
+    return root

@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--erode", default="auto", choices=["auto", "on", "off"],
                     help="occupancy erode decay (networks.py:270-272); auto = on for cascaded (garden-shaped, "
                          "COLMAP-like) scenes as train.py:178 does for colmap")
+    ap.add_argument("--quality-steps", type=int, default=30000,
+                    help="test-PSNR check after the reference schedule (scripts/quality_30k.py: product defaults vs "
+                         "exact mode, each in a child process; 0: skip)")
     ap.add_argument("--infer-frames", type=int, default=20, help="timed full-frame test renders (0: skip)")
     ap.add_argument("--infer-res", type=int, default=800)
     return ap.parse_args()
@@ -389,6 +392,11 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(trainer, scene, gt_images, R)
+    quality = None
+    if rank == 0 and world == 1 and args.quality_steps > 0:
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import quality_30k
+        quality = quality_30k.run(steps=args.quality_steps)
     if rank == 0:
         out = {
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
@@ -417,6 +425,7 @@ def main():
                                f"over {bd_steps} replayed steps ({t_bd * 1e3:.3f} ms/step with all stamps); roofline: "
                                f"see roofline.measured"),
             "cpu_baseline": cpu,
+            "quality": quality,
             "inference": infer,
         }
         print(json.dumps(out), flush=True)

@@ -7,4 +7,4 @@ TAG=${1:-quick}; shift || true
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --psnr-views 0 "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --psnr-views 0 --quality-steps 0 "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"

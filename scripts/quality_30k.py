@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Quality after the reference schedule (SURVEY.md §0 / north_star "PSNR
+within 0.2 dB of reference after 30k steps"): the analytic scene written as
+an NSVF-format dataset (synthetic.write_nsvf_scene) -> scripts/train_scene.py
+(train.py's flow: mark_invisible_cells, 8192-ray batches, occupancy updates
+every 16 steps with 256 warm-up steps, Adam lr 1e-2 cosine-annealed per
+epoch to lr/30 over 30 epochs x 1000 steps, the 'raw' loss) -> mean test
+PSNR, twice: the product defaults (chunked field evaluation, binned
+fine-level hash backward) and the exact mode (every marched sample through
+the field, per-sample atomic hash backward).  The reference itself cannot
+run here (CUDA), so "reference" = the exact mode of the same kernels.
+Prints one JSON line."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "ar-nerf_amd")]
+
+
+def _train(args):
+    """scripts/train_scene.py in a child process of its own (one trainer per
+    process, as in training; the GPU state of one run cannot touch the next)"""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_scene.py")] + args,
+                         check=True, stdout=subprocess.PIPE, text=True).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def run(steps=30000, res=400, n_train=100, n_test=10, seed=4, root=None):
+    import synthetic as S
+    with tempfile.TemporaryDirectory() as tmp:
+        scene = root or os.path.join(tmp, "Synthetic_NeRF", "Analytic")
+        if root is None:
+            S.write_nsvf_scene(scene, res=res, n_train=n_train, n_test=n_test)
+        args = ["--dataset", "nsvf", "--root", scene, "--downsample", str(res / 800), "--steps", str(steps),
+                "--seed", str(seed)]
+        default = _train(args)
+        exact = _train(args + ["--exact"])
+    return {"steps": steps, "schedule": "30 epochs x 1000 steps (scaled to steps), lr 1e-2 cosine to lr/30, raw loss",
+            "scene": f"analytic sphere+box as NSVF, {n_train} train / {n_test} test views at {res}x{res}",
+            "psnr_default": default["test_psnr"], "psnr_exact": exact["test_psnr"],
+            "delta_db": round(default["test_psnr"] - exact["test_psnr"], 3),
+            "train_rays_per_s_default": default["train_rays_per_s"],
+            "train_rays_per_s_exact": exact["train_rays_per_s"]}
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=30000)
+    ap.add_argument("--res", type=int, default=400)
+    ap.add_argument("--root", default=None, help="an existing NSVF scene instead of the synthetic one")
+    a = ap.parse_args()
+    print(json.dumps(run(a.steps, a.res, root=a.root)))

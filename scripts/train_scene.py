@@ -30,6 +30,11 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=30000)
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--test-views", type=int, default=0, help="0 = all")
+    ap.add_argument("--exact", action="store_true",
+                    help="exact mode: every marched sample through the field (chunk_first=0) and the per-sample "
+                         "atomic hash backward, instead of the chunked field + binned fine-level backward")
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--sync-every", type=int, default=0, help="(diagnostics) synchronize + report every N steps")
     a = ap.parse_args(argv)
     from datasets import dataset_dict
     from trainer import NGPTrainer
@@ -40,13 +45,17 @@ def main(argv=None):
     gt = train.gt_f32().to(dev)  # float targets, as the reference's loss sees them
     dirs, poses = train.directions.to(dev).contiguous(), train.poses.to(dev).contiguous()
     # erode for COLMAP scenes, as train.py:176-178 passes erode=dataset_name=='colmap'
+    mode = dict(chunk_first=0, hash_backward="atomic") if a.exact else {}
     tr = NGPTrainer(scale=a.scale, batch_size=a.batch, device=dev, num_epochs=max(1, a.steps // 1000),
-                    erode=a.dataset == "colmap")
+                    erode=a.dataset == "colmap", seed=a.seed, **mode)
     tr.mark_invisible_cells(train.K.to(dev), poses, train.img_wh)  # train.py:169-172
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for it in range(a.steps):
         tr.train_step(gt, dirs, poses)
+        if a.sync_every and (it + 1) % a.sync_every == 0:
+            torch.cuda.synchronize()
+            print(f"[train_scene] step {it + 1} ok, samples {int(tr.n_samples.item())}", file=sys.stderr, flush=True)
     tr.drain()
     torch.cuda.synchronize()
     t_train = time.perf_counter() - t0
@@ -60,7 +69,7 @@ def main(argv=None):
         out = tr.render(o, d, bg=1.0 if tr.esf == 0 else 0.0)
         mse = torch.mean((out["rgb"].clamp(0, 1) - test.rays[i].to(dev)) ** 2).item()
         psnrs.append(-10 * math.log10(max(mse, 1e-12)))
-    res = {"dataset": a.dataset, "root": a.root, "steps": a.steps,
+    res = {"dataset": a.dataset, "root": a.root, "steps": a.steps, "mode": "exact" if a.exact else "default",
            "train_rays_per_s": round(a.steps * a.batch / t_train, 1),
            "test_psnr": round(sum(psnrs) / max(1, len(psnrs)), 3), "test_views": n}
     print(json.dumps(res))
