@@ -39,7 +39,9 @@ __device__ __forceinline__ uint32_t corner_index(uint32_t px, uint32_t py, uint3
     // one conditional subtract; a real division only for other tables.
     if (pow2) return idx & (size - 1u);
     if (idx >= size) {
-        if (dense) return idx - size;
+        if (dense) idx -= size;
+        // (coordinates outside [0, res] -- inputs outside the grid's box:
+        // the full modulo keeps every index inside the table)
         if (__builtin_expect(idx >= size, 0)) idx %= size;
     }
     return idx;

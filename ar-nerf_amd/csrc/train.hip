@@ -387,10 +387,13 @@ __global__ void __launch_bounds__(1024) occ_list_kernel(const float* __restrict_
         base = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
     }
     __syncthreads();
+    // (the list holds at most n_cells entries: a reservation past that can
+    // only come from a corrupted count -- dropped instead of written)
+    if (base > (unsigned long long)n_cells) return;
     int64_t pos = (int64_t)base + wcnt[wid] + incl - mine;
 #pragma unroll
     for (int k = 0; k < PER; ++k)
-        if (hit[k]) list[pos++] = (int32_t)(c0 + k);
+        if (hit[k] && pos < n_cells) list[pos++] = (int32_t)(c0 + k);
 }
 
 __global__ void __launch_bounds__(256) occ_sample_kernel(uint64_t seed, const int64_t* __restrict__ ctr, int cascade,

@@ -4,8 +4,14 @@
 The reference's only parallelism is Lightning DDP over per-rank 8192-ray
 batches (train.py:288): gradients all-reduced every step, buffers broadcast
 from rank 0 every forward (SURVEY.md §2 "Collective call sites").  Here:
-  * one all-reduce (SUM) of the flat fp32 gradient per step; the Adam kernel
-    folds in the 1/world mean (grad_scale), so no extra pass;
+  * ZeRO-1 over the flat parameter vector: the fp32 gradient is
+    reduce-scattered (SUM) in two buckets -- [MLP | coarse hash levels] and
+    [fine hash levels] -- each rank runs FusedAdam on its 1/world shard of
+    every bucket only (fp32 master, moments; the 1/world mean is folded into
+    Adam), and the updated fp16 shadow the kernels read is all-gathered.
+    Exact per element (the same Adam on the same summed gradient), a third
+    less traffic than an all-reduce of the fp32 gradient (RS fp32 + AG fp16)
+    and 1/world of the Adam work per rank;
   * no per-step buffer broadcast: the occupancy update is made identical on
     every rank by construction -- all ranks draw the same cells and jitter
     (rank-independent seeds), each evaluates a disjoint 1/world share of the
@@ -13,7 +19,9 @@ from rank 0 every forward (SURVEY.md §2 "Collective call sites").  Here:
     combines them with the reference's last-writer-wins rule (every 16
     steps, C*128^3 x 8 B = 16 MB), and rank 0's threshold is broadcast
     (8 bytes) so all ranks pack the same bitfield.
-All functions are no-ops for world_size 1 and work with gloo on CPU tensors.
+All functions are no-ops for world_size 1.  With the gloo backend (CPU
+tests, and the 2-process test on one GPU) device tensors are staged through
+host memory.
 """
 import torch
 import torch.distributed as dist
@@ -35,10 +43,58 @@ def shard_cells(indices, coords, rank, world):
     return indices[lo:hi], coords[lo:hi]
 
 
+def zero_buckets(n_params, split, world, align=4):
+    """ZeRO-1 bucket bounds over a flat vector padded to n_pad: bucket 0 =
+    [0, s1), bucket 1 = [s1, n_pad), both multiples of world*align (equal
+    16-byte aligned shards); s1 = split rounded DOWN, so bucket 0 holds only
+    entries complete at `split` (a few of them fall into bucket 1)."""
+    q = world * align
+    s1 = (split // q) * q
+    n_pad = ((n_params + q - 1) // q) * q
+    return n_pad, [(0, s1), (s1, n_pad)] if s1 > 0 else [(0, n_pad)]
+
+
+def _gloo(group):
+    return dist.get_backend(group) == "gloo"
+
+
+def reduce_scatter_(full, out, group=None):
+    """out (len/world) = this rank's shard of SUM over ranks of full (len)."""
+    if world_info(group)[1] == 1:
+        out.copy_(full)
+        return out
+    if _gloo(group) and full.is_cuda:
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.reduce_scatter_tensor(o, full.cpu(), op=dist.ReduceOp.SUM, group=group)
+        out.copy_(o)
+    else:
+        dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=group)
+    return out
+
+
+def all_gather_(full, shard, group=None):
+    """full (len) = concatenation over ranks of shard (len/world)."""
+    if world_info(group)[1] == 1:
+        full.copy_(shard)
+        return full
+    if _gloo(group) and full.is_cuda:
+        f = torch.empty(full.shape, dtype=full.dtype)
+        dist.all_gather_into_tensor(f, shard.cpu(), group=group)
+        full.copy_(f)
+    else:
+        dist.all_gather_into_tensor(full, shard, group=group)
+    return full
+
+
 def allreduce_grad_(grad, group=None):
     """Sum the flat gradient over ranks (the mean is applied in Adam)."""
     if world_info(group)[1] > 1:
-        dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
+        if _gloo(group) and grad.is_cuda:
+            g = grad.cpu()
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+            grad.copy_(g)
+        else:
+            dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=group)
     return grad
 
 
@@ -48,12 +104,23 @@ def combine_density_tmp_(tmp, group=None):
     largest list position wins across ranks as within one, so the result
     equals a single process evaluating the whole list."""
     if world_info(group)[1] > 1:
-        dist.all_reduce(tmp, op=dist.ReduceOp.MAX, group=group)
+        if _gloo(group) and tmp.is_cuda:
+            t = tmp.cpu()
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            tmp.copy_(t)
+        else:
+            dist.all_reduce(tmp, op=dist.ReduceOp.MAX, group=group)
     return tmp
 
 
 def sync_threshold_(thr, group=None):
     """Broadcast rank 0's occupancy threshold so bitfields are identical."""
     if world_info(group)[1] > 1:
-        dist.broadcast(thr, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        if _gloo(group) and thr.is_cuda:
+            t = thr.cpu()
+            dist.broadcast(t, src=src, group=group)
+            thr.copy_(t)
+        else:
+            dist.broadcast(thr, src=src, group=group)
     return thr

@@ -38,6 +38,7 @@ def _p(t):
 
 
 STAT_STRIPES, STAT_STRIDE = 32, 16  # include/ngp_amd.h NGP_STAT_*
+THROTTLE_EVERY, THROTTLE_DEPTH = 32, 4  # host run-ahead bound: <= 160 steps enqueued
 
 
 class NGPTrainer:
@@ -70,11 +71,27 @@ class NGPTrainer:
         dev = self.dev
         # ---- field parameters: fp32 master, fp16 shadow, Adam state, grad
         self.grid = HG.HashGrid(scale)
-        self.params = HG.init_params(self.grid, seed=seed, device=dev)
-        self.params16 = self.params.half()
-        self.grad = torch.zeros_like(self.params)
-        self.exp_avg = torch.zeros_like(self.params)
-        self.exp_avg_sq = torch.zeros_like(self.params)
+        init = HG.init_params(self.grid, seed=seed, device=dev)
+        self.n_params = n = init.numel()
+        # ZeRO-1 layout (ddp.zero_buckets): buffers padded to n_pad, two
+        # buckets [MLP | coarse levels] [fine levels] split where the coarse
+        # gradient is complete; rank r owns shard r of each bucket
+        lo_level = 8 if bin_level_lo is None else bin_level_lo
+        split = HG.MLP_PARAMS + 2 * int(self.grid.offsets[min(max(lo_level, 0), len(self.grid.offsets) - 1)])
+        self.n_pad, self.buckets = ddp.zero_buckets(n, split, self.world)
+        pb = torch.zeros(self.n_pad, device=dev)
+        pb[:n] = init
+        self._pbuf = pb
+        self.params = pb[:n]  # fp32 master (a rank updates its shards only when world > 1)
+        self._p16buf = pb.half()
+        self.params16 = self._p16buf[:n]
+        self._gbuf = torch.zeros(self.n_pad, device=dev)
+        self.grad = self._gbuf[:n]
+        self.exp_avg = torch.zeros(self.n_pad, device=dev)
+        self.exp_avg_sq = torch.zeros(self.n_pad, device=dev)
+        self.shards = [(a + (b - a) * self.rank // self.world, a + (b - a) * (self.rank + 1) // self.world)
+                       for a, b in self.buckets]
+        self._gshard = [torch.zeros(hi - lo, device=dev) for lo, hi in self.shards] if self.world > 1 else None
         self.global_step = 0
         # ---- occupancy (models/networks.py:20-30, train.py:78-82)
         self.center = torch.zeros(1, 3, device=dev)
@@ -201,6 +218,9 @@ class NGPTrainer:
         self.kernel_events = None
         # ktimer.KernelTimer (bench): graph replays carry HIP events around every kernel
         self.timer = None
+        # world > 1 graph replays run as segments with the collectives between them
+        self._segmented = False
+        self._throttle_q = []  # events of every THROTTLE_EVERY-th step (train_step)
 
     @staticmethod
     def _march_buffers(R, cap, f, cap_bits):
@@ -468,12 +488,29 @@ class NGPTrainer:
         now or next step) replay a captured HIP graph of the whole step
         (NGP_GRAPHS=0: always eager)."""
         gs, ui = self.global_step, self.update_interval
+        self._throttle()
         if (self.use_graphs and self._pending is not None and (gs % ui != 0 or self._updated_for == gs)
                 and gs >= self.warmup_steps and self.kernel_events is None and not self.random_bg
                 and not self.no_prefetch):
             return self._replay(gt, directions, poses, (gs + 1) % ui == 0)
         return self._on_exec_stream(self._step, ("sample", 0, gt), None, directions, poses, True,
                                     ("sample", 1, gt))
+
+    def _throttle(self):
+        """Bound how far the host runs ahead of the GPU: an event every
+        THROTTLE_EVERY steps, and before enqueueing more the host waits for
+        the one THROTTLE_DEPTH events back (that step finished long ago when
+        the GPU is the bottleneck, so the queue never drains).  Thousands of
+        enqueued graph replays outstanding at once were followed by memory
+        faults in long runs (30k steps without a host sync); with the host
+        kept within a few hundred steps they ran clean."""
+        if self.global_step % THROTTLE_EVERY:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self._throttle_q.append(ev)
+        if len(self._throttle_q) > THROTTLE_DEPTH:
+            self._throttle_q.pop(0).synchronize()
 
     def _set_lr(self):
         lr = self.lr()
@@ -494,6 +531,28 @@ class NGPTrainer:
             torch.cuda.current_stream().wait_event(ev)
         self._set_lr()
         key = (k, bool(update_after), gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype)
+        if self.world == 1:
+            self._run_graph(key, lambda: self._graph_body(k, gt, directions, poses, update_after))
+        else:  # collectives between graph segments (no RCCL inside captures)
+            self._run_graph(key + ("compute",), lambda: self._segment_compute(k, gt, directions, poses, update_after))
+            self._reduce_grads()
+            self._run_graph(key + ("adam",), self._segment_adam)
+            self._gather_params16()
+            if update_after:  # (every 16 steps) eager: the update has its own collectives
+                self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=False)
+                self._march(1 - k, ("sample", 0, gt), directions, poses, torch.cuda.current_stream())
+        self.cur = k
+        self._bind(self.msets[k])
+        self._pending = (1 - k, None)  # marched (and joined) inside the graph
+        self.n_prefetched += 1
+        self.global_step += 1
+        if update_after:
+            self._updated_for = self.global_step
+        return self.out_loss
+
+    def _run_graph(self, key, body):
+        """Replay the graph captured for `key` (capturing body() first if new;
+        with a measurement timer set, one with its stamps)."""
         tm = self.timer  # (measurement) graphs with wall-clock stamp kernels around every kernel
         if tm is not None:
             key = key + (tm.uid,)
@@ -505,20 +564,35 @@ class NGPTrainer:
                 tm.arm()
             try:
                 with torch.cuda.graph(g):
-                    self._graph_body(k, gt, directions, poses, update_after)
+                    body()
             finally:
                 if tm is not None:
                     tm.disarm()
             self._graphs[key] = g
         self._graphs[key].replay()
+
+    def _segment_compute(self, k, gt, directions, poses, update_after):
+        """world > 1, first segment: the step up to the gradient (and the next
+        batch's march on the side stream, joined, unless an update follows)."""
         self.cur = k
         self._bind(self.msets[k])
-        self._pending = (1 - k, None)  # marched (and joined) inside the graph
-        self.n_prefetched += 1
-        self.global_step += 1
-        if update_after:
-            self._updated_for = self.global_step
-        return self.out_loss
+        cs = torch.cuda.current_stream()
+        fork = None
+        if not update_after:
+            def fork():
+                self.march_stream.wait_stream(cs)
+                self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
+        self._segmented = True
+        try:
+            self._compute(self.rgb_gt, True, fork)
+        finally:
+            self._segmented = False
+        if fork is not None:
+            cs.wait_stream(self.march_stream)
+
+    def _segment_adam(self):
+        self._adam_shards()
+        vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
 
     def _graph_body(self, k, gt, directions, poses, update_after=False):
         self.cur = k
@@ -691,15 +765,51 @@ class NGPTrainer:
                                            HG.ctypes.byref(self.grid.desc),
                                            _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
         self._ev("hash_bwd", 1)
-        self._ev("allreduce", 0)
-        ddp.allreduce_grad_(self.grad, self.pg)  # DDP gradient all-reduce (RCCL over xGMI)
-        self._ev("allreduce", 1)
-        if not apply_adam:  # (tests) leave the summed gradient in self.grad
-            return self.out_loss
-        self._ev("adam", 0)
-        self._adam(0, self.params.numel(), s)
-        self._ev("adam", 1)
+        if self.world == 1 and apply_adam:
+            self._ev("adam", 0)
+            self._adam(0, self.n_params, s)
+            self._ev("adam", 1)
+        elif self.world > 1 and not self._segmented:
+            self._reduce_grads()
+            if apply_adam:
+                self._adam_shards()
+                self._gather_params16()
         return self.out_loss
+
+    # ------------------------------------------------- data parallel (ZeRO-1)
+    def _reduce_grads(self):
+        """Reduce-scatter (SUM) of each gradient bucket into this rank's shard
+        buffers, then the local gradient is zeroed for the next step (RCCL over
+        xGMI; outside graph captures).  apply_adam=False callers (tests) find
+        the summed shards in _gshard."""
+        for (a, b), gs in zip(self.buckets, self._gshard):
+            ddp.reduce_scatter_(self._gbuf[a:b], gs, self.pg)
+        self._gbuf.zero_()
+
+    def _adam_shards(self):
+        """FusedAdam on this rank's shard of every bucket: fp32 master,
+        moments and fp16 shadow of the shard, from the reduced gradient shard
+        (the 1/world mean folded in; the shard buffer zeroed)."""
+        s = vren._stream()
+        for (lo, hi), gs in zip(self.shards, self._gshard):
+            q = lambda t: _p(t[lo:hi])  # noqa: E731
+            vren._ok(self.L.ngp_adam_step_dev(q(self._pbuf), _p(gs), q(self.exp_avg), q(self.exp_avg_sq),
+                                              q(self._p16buf), hi - lo, _p(self.lr_dev), ctypes_float(0.9),
+                                              ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                                              ctypes_float(1.0 / self.world), 1, s), "adam")
+
+    def _gather_params16(self):
+        """All-gather of the updated fp16 shadow the kernels read."""
+        for (a, b), (lo, hi) in zip(self.buckets, self.shards):
+            ddp.all_gather_(self._p16buf[a:b], self._p16buf[lo:hi], self.pg)
+
+    def full_params(self):
+        """The fp32 master vector, complete on every rank (world > 1: each rank
+        updates only its shards; this all-gathers them -- checkpoints, tests)."""
+        if self.world > 1:
+            for (a, b), (lo, hi) in zip(self.buckets, self.shards):
+                ddp.all_gather_(self._pbuf[a:b], self._pbuf[lo:hi].clone(), self.pg)
+        return self.params
 
     def _adam(self, lo, hi, s):
         """FusedAdam over params[lo:hi] (16-byte aligned bounds).  lr and the

@@ -55,7 +55,8 @@ def main(argv=None):
         tr.train_step(gt, dirs, poses)
         if a.sync_every and (it + 1) % a.sync_every == 0:
             torch.cuda.synchronize()
-            print(f"[train_scene] step {it + 1} ok, samples {int(tr.n_samples.item())}", file=sys.stderr, flush=True)
+            print(f"[train_scene] step {it + 1} ok, samples {int(tr.n_samples.item())}, occupied-cell count "
+                  f"{int(tr._occ_count.item())}", file=sys.stderr, flush=True)
     tr.drain()
     torch.cuda.synchronize()
     t_train = time.perf_counter() - t0
