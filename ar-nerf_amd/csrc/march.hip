@@ -151,6 +151,20 @@ __global__ void __launch_bounds__(256) sample_batch_kernel(
             hits_t + 2 * r);
 }
 
+// random_bg (models/rendering.py:287-288: rgb_bg = torch.rand(3) per batch),
+// drawn on device from Philox keyed by (seed, *counter_dev + add) so that a
+// replayed graph draws a fresh colour per batch.
+__global__ void random_bg_kernel(uint64_t seed, const int64_t* __restrict__ counter_dev, int64_t add,
+                                 float* __restrict__ bg) {
+    const uint64_t c = (uint64_t)(*counter_dev + add);
+    const uint4 u = philox4x32(make_uint4(0x62u, 0x67u, (uint32_t)c, (uint32_t)(c >> 32)),
+                               make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    if (threadIdx.x < 3) {
+        const uint32_t v = threadIdx.x == 0 ? u.x : threadIdx.x == 1 ? u.y : u.z;
+        bg[threadIdx.x] = (float)(v >> 8) * (1.0f / 16777216.0f);
+    }
+}
+
 // Bitfield summary: bit w of summary = (64-bit bitfield word w != 0), i.e.
 // whether the Morton-aligned 4x4x4 cell block w holds any occupied cell;
 // bit w of dilated = OR of that over block w and its 26 neighbours (same
@@ -697,6 +711,12 @@ int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_ad
     return launch_sample_batch(seed, (uint64_t)step_add, step_dev, ray_offset, gt, gt_f32, n_img, hw, directions,
                                poses, n_rays, center, half_size, near_distance, img_idx, pix_idx, rgb_gt, noise,
                                rays_o, rays_d, hits_t, stream);
+}
+
+int ngp_random_bg(uint64_t seed, const int64_t* counter_dev, int64_t add, float* bg, void* stream) {
+    NGP_CHECK_ARG(counter_dev && bg);
+    random_bg_kernel<<<1, 64, 0, as_stream(stream)>>>(seed, counter_dev, add, bg);
+    return ngp_launch_status();
 }
 
 int ngp_bitfield_summary(const uint8_t* bitfield, int64_t n_bytes, int grid_size, uint32_t* summary, void* stream) {

@@ -15,13 +15,17 @@ namespace ngp {
 // with the reference's early break;
 // then the background blend (models/rendering.py:287-296) and NeRFLoss
 // (losses.py:63-82: rgb loss of type `loss_type`, opacity entropy, depth
-// term) with its analytic gradient; pass 2 = composite_train_bw
-// (volumerendering.cu:86-150) with dL/dws = 0 (no distortion loss).
+// term, distortion term when lambda_distortion > 0) with its analytic
+// gradient; pass 2 = composite_train_bw (volumerendering.cu:86-150) with
+// dL/dws from the distortion loss (DistortionLoss fw / bw, losses.cu:8-140,
+// over the ray's composited samples: the others have ws = 0 and the
+// compositing backward stops at the termination anyway).
 // Per-ray outputs: rgb (after bg), opacity, depth, loss contribution
 // (already divided by the batch means' denominators).
 struct LossArgs {
     int loss_type;  // 0 raw (default, opt.py:34), 1 mse (upstream ngp_pl), 2 log, 3 tanh
     float lambda_opacity, lambda_depth, depth_scale, inv_n_rays, T_thr;
+    float lambda_dist;  // losses.py:77-80 (0: off, the default)
 };
 
 __device__ __forceinline__ void rgb_loss(int type, float x, float y, float& l, float& dldx) {
@@ -173,6 +177,43 @@ __device__ __forceinline__ int64_t composite_loss_ray(
         loss += -la.lambda_depth * logf(fminf(v, 1.0f)) * la.inv_n_rays;
         if (v < 1.0f) gdep = -la.lambda_depth / v / la.depth_scale * la.inv_n_rays;
     }
+    // ---- distortion loss (losses.py:77-80): its forward over the composited
+    // samples (W_tot = O, WT_tot = D are the ray's sums of ws and ws*ts) and
+    // dL/dws per sample (losses.cu:110-140); the ray's sum of dL/dws * ws is
+    // needed before the compositing backward's first sample: a pass of its own.
+    // Rows longer than two chunks park dL/dws in dL_dsig[s] (overwritten by
+    // pass 2 after it is read).
+    float gws_c[2] = {0.f, 0.f}, S_ws = 0.f;
+    if (la.lambda_dist != 0.f) {
+        const float gd2 = (la.lambda_dist * la.inv_n_rays) * 2;
+        float cw = 0.f, cwt = 0.f, ld = 0.f;
+        auto dist_chunk = [&](int64_t k0, const Chunk& c) {
+            const int cnt = (int)(na - k0 < 64 ? na - k0 : 64);
+            const bool in = lane < cnt;
+            const float w = in ? c.w : 0.f, wt = w * c.tt;
+            const float a = cw + wave_incl_scan(w, lane), b = cwt + wave_incl_scan(wt, lane);
+            const float we = a - w, wte = b - wt;  // exclusive sums (the reference's serial fold values)
+            const float l = 2 * (b * we - a * wte) + ((w * (1.0f / 3)) * w) * c.dl;
+            ld += wave_sum(in ? l : 0.f);
+            const float A = c.tt * we - wte, Bv = (D - b) - c.tt * (O - a);
+            const float gw = in ? gd2 * (A + Bv) + ((gd2 / 3.0f) * w) * c.dl : 0.f;
+            S_ws += wave_sum(gw * w);
+            cw = __shfl(a, 63, 64); cwt = __shfl(b, 63, 64);
+            return gw;
+        };
+        if (na > 0) gws_c[0] = dist_chunk(0, c0);
+        if (na > 64) gws_c[1] = dist_chunk(64, c1);
+        for (int64_t k0 = 128; k0 < na; k0 += 64) {
+            Chunk c;
+            load(k0, c);
+            const int64_t s = start + k0 + lane;
+            c.w = 0.f;
+            if (k0 + lane < na) c.w = dL_drgbs[3 * s];
+            const float gw = dist_chunk(k0, c);
+            if (k0 + lane < na) dL_dsig[s] = gw;
+        }
+        loss += la.lambda_dist * ld * la.inv_n_rays;
+    }
     if (lane == 0) {
         out_rgb[3 * ray] = xc[0]; out_rgb[3 * ray + 1] = xc[1]; out_rgb[3 * ray + 2] = xc[2];
         out_op[ray] = O;
@@ -181,32 +222,42 @@ __device__ __forceinline__ int64_t composite_loss_ray(
         if (n_active) n_active[n] = (int32_t)na;
     }
     na_out = na;
-    // ---- backward over the na composited samples (dL/dws = 0)
+    // ---- backward over the na composited samples
     const float gs = gop * (1 - O);
-    float rc = 0.f, gc = 0.f, bc = 0.f, dc = 0.f;
-    auto bw_chunk = [&](int64_t k0, const Chunk& c) {
+    float rc = 0.f, gc = 0.f, bc = 0.f, dc = 0.f, wc = 0.f;
+    auto bw_chunk = [&](int64_t k0, const Chunk& c, float gw) {
         const int cnt = (int)(na - k0 < 64 ? na - k0 : 64);
         const bool in = lane < cnt;
         const int64_t s = start + k0 + lane;
         const float w = in ? c.w : 0.f, Ta = c.Ta;
         const float pr = rc + wave_incl_scan(w * c.cr, lane), pg = gc + wave_incl_scan(w * c.cg, lane);
         const float pb = bc + wave_incl_scan(w * c.cb, lane), pd = dc + wave_incl_scan(w * c.tt, lane);
+        float ws_term = 0.f;
+        if (la.lambda_dist != 0.f) {  // + T g_ws - (S - prefix(g_ws ws)) (volumerendering.cu:138-146)
+            const float pw = wc + wave_incl_scan(in ? gw * w : 0.f, lane);
+            ws_term = Ta * gw - (S_ws - pw);
+            wc = __shfl(pw, 63, 64);
+        }
         if (in) {
             dL_drgbs[3 * s] = g[0] * w; dL_drgbs[3 * s + 1] = g[1] * w; dL_drgbs[3 * s + 2] = g[2] * w;
             dL_dsig[s] = c.dl * (g[0] * (c.cr * Ta - (R - pr)) + g[1] * (c.cg * Ta - (G - pg)) +
-                                 g[2] * (c.cb * Ta - (B - pb)) + gs + gdep * (c.tt * Ta - (D - pd)));
+                                 g[2] * (c.cb * Ta - (B - pb)) + gs + gdep * (c.tt * Ta - (D - pd)) + ws_term);
         }
         rc = __shfl(pr, 63, 64); gc = __shfl(pg, 63, 64); bc = __shfl(pb, 63, 64); dc = __shfl(pd, 63, 64);
     };
-    if (na > 0) bw_chunk(0, c0);
-    if (na > 64) bw_chunk(64, c1);
+    if (na > 0) bw_chunk(0, c0, gws_c[0]);
+    if (na > 64) bw_chunk(64, c1, gws_c[1]);
     for (int64_t k0 = 128; k0 < na; k0 += 64) {
         Chunk c;
         load(k0, c);
         const int64_t s = start + k0 + lane;
         c.w = 0.f; c.Ta = 0.f;
-        if (k0 + lane < na) { c.w = dL_drgbs[3 * s]; c.Ta = dL_drgbs[3 * s + 1]; }
-        bw_chunk(k0, c);
+        float gw = 0.f;
+        if (k0 + lane < na) {
+            c.w = dL_drgbs[3 * s]; c.Ta = dL_drgbs[3 * s + 1];
+            if (la.lambda_dist != 0.f) gw = dL_dsig[s];
+        }
+        bw_chunk(k0, c, gw);
     }
     return samples;
 }
@@ -815,7 +866,8 @@ extern "C" {
 
 int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
                        const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg, int loss_type,
-                       float lambda_opacity, float lambda_depth, float depth_scale, float T_threshold,
+                       float lambda_opacity, float lambda_depth, float lambda_distortion, float depth_scale,
+                       float T_threshold,
                        float* dL_dsigmas, float* dL_drgbs, float* out_rgb, float* out_opacity, float* out_depth,
                        float* out_loss, int32_t* n_active, int32_t* sample_idx, void* alloc_ws,
                        int64_t* n_active_total, int64_t* stats, void* stream) {
@@ -823,7 +875,8 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_a && rgb_gt && bg && out_rgb && out_opacity && out_depth && out_loss);
     NGP_CHECK_ARG(!sample_idx || (alloc_ws && n_active_total && ((uintptr_t)alloc_ws & 7) == 0));
-    LossArgs la{loss_type, lambda_opacity, lambda_depth, depth_scale, 1.0f / (float)n_rays, T_threshold};
+    LossArgs la{loss_type, lambda_opacity, lambda_depth, depth_scale, 1.0f / (float)n_rays, T_threshold,
+                lambda_distortion};
     // one row per wave: every row's dependent load chain in flight at once
     // (a few rows per wave serialised their memory latencies)
     NGP_TIMED(NGP_K_COMPOSITE, as_stream(stream), composite_loss_wave_kernel<<<(unsigned)std::min<int64_t>((n_rays + 3) / 4, 1 << 20), 256, 0, as_stream(stream)>>>(

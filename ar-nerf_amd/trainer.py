@@ -46,13 +46,14 @@ class NGPTrainer:
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
                  device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=None, bin_level_lo=None,
-                 chunk_first=64, erode=False):
+                 chunk_first=64, erode=False, lambda_distortion=0.0):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
         self.lr0, self.num_epochs, self.steps_per_epoch = lr, num_epochs, steps_per_epoch
         self.loss_type = LOSS_TYPES[loss]
         self.lambda_opacity, self.lambda_depth = lambda_opacity, lambda_depth
+        self.lambda_distortion = float(lambda_distortion)  # losses.py:77-80 (opt.py:25 default 0)
         self.random_bg = random_bg
         # train.py:104-105
         self.esf = exp_step_factor if exp_step_factor is not None else (1 / 256 if scale > 0.5 else 0.0)
@@ -193,6 +194,7 @@ class NGPTrainer:
             nbytes = HG._lib().ngp_hash_backward_binned_workspace(self.bin_max_samples)
             self.bin_ws = torch.empty((nbytes + 255) // 256, 64, dtype=torch.int32, device=dev)
         self.bg = torch.ones(3, **f) if self.esf == 0 else torch.zeros(3, **f)  # models/rendering.py:287-296
+        self._bg_rand = torch.zeros(3, **f)
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(1000 + seed + self.rank)
         # ngp_sample_batch key: one seed for all ranks, rank r draws rays [r*R, (r+1)*R) of the global
@@ -490,8 +492,7 @@ class NGPTrainer:
         gs, ui = self.global_step, self.update_interval
         self._throttle()
         if (self.use_graphs and self._pending is not None and (gs % ui != 0 or self._updated_for == gs)
-                and gs >= self.warmup_steps and self.kernel_events is None and not self.random_bg
-                and not self.no_prefetch):
+                and gs >= self.warmup_steps and self.kernel_events is None and not self.no_prefetch):
             return self._replay(gt, directions, poses, (gs + 1) % ui == 0)
         return self._on_exec_stream(self._step, ("sample", 0, gt), None, directions, poses, True,
                                     ("sample", 1, gt))
@@ -684,12 +685,16 @@ class NGPTrainer:
                      "field_forward")
         self._ev("field_fwd", 1)
         at("after_fwd")
-        bg = torch.rand(3, device=self.dev, generator=self.gen) if self.random_bg else self.bg
+        bg = self.bg
+        if self.random_bg:  # rendering.py:287-288, one colour per batch, drawn on device (graph-safe)
+            bg = self._bg_rand
+            vren._ok(L.ngp_random_bg(self.sample_seed ^ 0x6267, _p(self.dctr[1:]), 0, _p(bg), s), "random_bg")
         self._ev("composite_loss", 0)
         self._ev("composite", 0)
         vren._ok(L.ngp_composite_loss(_p(self.sigmas), _p(self.rgbs), _p(self.deltas), _p(self.ts), _p(self.rays_a), R,
                                       _p(rgb_gt), _p(bg), self.loss_type, ctypes_float(self.lambda_opacity),
-                                      ctypes_float(self.lambda_depth), ctypes_float(self.scale), ctypes_float(1e-4),
+                                      ctypes_float(self.lambda_depth), ctypes_float(self.lambda_distortion),
+                                      ctypes_float(self.scale), ctypes_float(1e-4),
                                       _p(self.dsig), _p(self.drgb), _p(self.out_rgb), _p(self.out_op),
                                       _p(self.out_depth), _p(self.out_loss), _p(self.n_active), None, None, None,
                                       _p(self.stats), s), "composite_loss")

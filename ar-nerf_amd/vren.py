@@ -45,6 +45,7 @@ def _declare(L):
                                  vp, vp, c_float, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_adam_step_dev": [vp, vp, vp, vp, vp, c_int64, vp, c_float, c_float, c_float, vp, c_float, c_int, vp],
         "ngp_counters_inc": [vp, c_int, vp],
+        "ngp_random_bg": [ctypes.c_uint64, vp, c_int64, vp, vp],
         "ngp_occupied_cells": [vp, c_int64, c_float, vp, vp, vp],
         "ngp_occupancy_samples": [ctypes.c_uint64, vp, c_int, c_int, c_int64, c_float, c_float, vp, vp, c_int64,
                                   c_int64, vp, vp, vp],
@@ -65,7 +66,8 @@ def _declare(L):
         "ngp_composite_train_fw": [vp, vp, vp, vp, vp, c_int64, c_float, vp, vp, vp, vp, vp, vp],
         "ngp_composite_train_bw": [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, c_int64, vp, vp, vp, c_float, vp, vp, vp],
         "ngp_composite_test_fw": [vp, vp, vp, vp, c_int64, c_int, vp, c_float, vp, vp, vp, vp, vp],
-        "ngp_composite_loss": [vp, vp, vp, vp, vp, c_int64, vp, vp, c_int, c_float, c_float, c_float, c_float, vp,
+        "ngp_composite_loss": [vp, vp, vp, vp, vp, c_int64, vp, vp, c_int, c_float, c_float, c_float, c_float, c_float,
+                               vp,
                                vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_active_samples": [vp, vp, c_int64, vp, vp, vp, vp],
         "ngp_chunk_counts": [vp, c_int64, c_int, vp, vp, c_float, vp, vp],

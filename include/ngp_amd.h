@@ -95,6 +95,11 @@ int ngp_sample_batch(uint64_t seed, uint64_t step, int64_t ray_offset, const voi
                      const float* half_size, float near_distance, int64_t* img_idx, int64_t* pix_idx,
                      float* rgb_gt, float* noise, float* rays_o, float* rays_d, float* hits_t, void* stream);
 
+/* random_bg (models/rendering.py:287-288: one U[0,1)^3 background colour per
+ * training batch) drawn on device: bg (3) f32 from Philox keyed by (seed,
+ * *counter_dev + add) -- graph replays draw a fresh colour per batch. */
+int ngp_random_bg(uint64_t seed, const int64_t* counter_dev, int64_t add, float* bg, void* stream);
+
 /* ngp_sample_batch with the RNG counter in device memory: step = *step_dev +
  * step_add (a captured graph replays with the counter advanced on device). */
 int ngp_sample_batch_dev(uint64_t seed, const int64_t* step_dev, int64_t step_add, int64_t ray_offset, const void* gt,
@@ -380,8 +385,10 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
  * composite_train_fw (volumerendering.cu:5-44), background blend
  * (models/rendering.py:287-296, bg = 3 device floats), NeRFLoss
  * (losses.py:63-82; loss_type 0 raw (default), 1 mse, 2 log, 3 tanh;
- * opacity entropy lambda_opacity; depth term lambda_depth with depth_scale)
- * and composite_train_bw with dL/dws = 0.  rgb_gt (n_rays,3).
+ * opacity entropy lambda_opacity; depth term lambda_depth with depth_scale;
+ * distortion term lambda_distortion, losses.py:77-80 + losses.cu:8-140,
+ * 0 = off) and composite_train_bw with dL/dws from the distortion term.
+ * rgb_gt (n_rays,3).
  * Out: dL_dsigmas (N), dL_drgbs (N,3) for each row's first n_active samples
  * (later entries are left unwritten: their gradient is exactly zero); per
  * ray out_rgb (n_rays,3) (after bg), out_opacity, out_depth, out_loss
@@ -401,8 +408,8 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
 #define NGP_STAT_STRIDE 16
 int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* deltas, const float* ts,
                        const int64_t* rays_a, int64_t n_rays, const float* rgb_gt, const float* bg,
-                       int loss_type, float lambda_opacity, float lambda_depth, float depth_scale,
-                       float T_threshold, float* dL_dsigmas, float* dL_drgbs, float* out_rgb,
+                       int loss_type, float lambda_opacity, float lambda_depth, float lambda_distortion,
+                       float depth_scale, float T_threshold, float* dL_dsigmas, float* dL_drgbs, float* out_rgb,
                        float* out_opacity, float* out_depth, float* out_loss, int32_t* n_active,
                        int32_t* sample_idx, void* alloc_ws, int64_t* n_active_total, int64_t* stats,
                        void* stream);

@@ -33,7 +33,7 @@ def main():
     for name, with_idx in (("plain", False), ("compact", True)):
         def f():
             vren._ok(L.ngp_composite_loss(p(tr.sigmas), p(tr.rgbs), p(tr.deltas), p(tr.ts), p(tr.rays_a), 8192,
-                                          p(tr.rgb_gt), p(tr.bg), 0, ctypes_float(1e-3), ctypes_float(0.0),
+                                          p(tr.rgb_gt), p(tr.bg), 0, ctypes_float(1e-3), ctypes_float(0.0), ctypes_float(0.0),
                                           ctypes_float(0.5), ctypes_float(1e-4), p(tr.dsig), p(tr.drgb), p(tr.out_rgb),
                                           p(tr.out_op), p(tr.out_depth), p(tr.out_loss), p(tr.n_active),
                                           p(tr.sample_idx) if with_idx else None, p(tr._alloc_ws),

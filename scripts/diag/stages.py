@@ -82,7 +82,7 @@ def main():
     st["chunk2_n"] = int(tr.eval_total.item())
     st["composite"] = timed(lambda: vren._ok(L.ngp_composite_loss(
         p(tr.sigmas), p(tr.rgbs), p(tr.deltas), p(tr.ts), p(tr.rays_a), R, p(tr.rgb_gt), p(tr.bg), 0,
-        ctypes_float(1e-3), ctypes_float(0.0), ctypes_float(0.5), ctypes_float(1e-4), p(tr.dsig), p(tr.drgb),
+        ctypes_float(1e-3), ctypes_float(0.0), ctypes_float(0.0), ctypes_float(0.5), ctypes_float(1e-4), p(tr.dsig), p(tr.drgb),
         p(tr.out_rgb), p(tr.out_op), p(tr.out_depth), p(tr.out_loss), p(tr.n_active), None, None, None, None, vren._stream()), "cl"))
     st["active_samples"] = timed(lambda: vren._ok(L.ngp_active_samples(
         p(tr.n_active), p(tr.rays_a), R, p(tr.act_start), p(tr.n_active_total), p(tr.sample_idx), vren._stream()), "as"))

@@ -44,16 +44,36 @@ def _rows(seed, n_rows=2000):
     return sig, rgbs, deltas, ts, rays_a, gt
 
 
-@pytest.mark.parametrize("seed", [0, 1])
-def test_composite_loss_matches_oracle(seed):
+class _DistortionCPU(torch.autograd.Function):
+    """losses.py:7-38 DistortionLoss on the oracle's restatement of losses.cu."""
+
+    @staticmethod
+    def forward(ctx, ws, deltas, ts, rays_a):
+        loss, wsi, wtsi = O.distortion_loss_fw(ws, deltas, ts, rays_a)
+        ctx.save_for_backward(wsi, wtsi, ws, deltas, ts, rays_a)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        wsi, wtsi, ws, deltas, ts, rays_a = ctx.saved_tensors
+        return O.distortion_loss_bw(g, wsi, wtsi, ws, deltas, ts, rays_a), None, None, None
+
+
+@pytest.mark.parametrize("seed,lam_d", [(0, 0.0), (1, 0.0), (2, 1e-2)])
+def test_composite_loss_matches_oracle(seed, lam_d):
+    """lam_d > 0: NeRFLoss's distortion term (losses.py:77-80) fused in, vs
+    the reference's autograd chain VolumeRenderer -> DistortionLoss (oracle
+    losses.cu restatement) -> composite_train_bw with dL/dws."""
     sig, rgbs, deltas, ts, rays_a, gt = _rows(seed)
     n_rows, n = rays_a.shape[0], sig.shape[0]
     T_thr, lam_op = 1e-4, 1e-3
     # oracle: VolumeRenderer (serial) + bg 0 + NeRFLoss raw, autograd backward
     s_ = sig.clone().requires_grad_(True)
     c_ = rgbs.clone().requires_grad_(True)
-    _, op, dep, rgb, _ = O._VolumeRendererCPU.apply(s_, c_, deltas, ts, rays_a, T_thr)
+    _, op, dep, rgb, ws = O._VolumeRendererCPU.apply(s_, c_, deltas, ts, rays_a, T_thr)
     loss = O.nerf_loss_raw(rgb, gt, op, lam_op)
+    if lam_d > 0:
+        loss = loss + (lam_d * _DistortionCPU.apply(ws, deltas, ts, rays_a)).mean()
     loss.backward()
     tot, _, _, _, _ = O.composite_train_fw(sig, rgbs, deltas, ts, rays_a, T_thr)
     # GPU
@@ -67,7 +87,7 @@ def test_composite_loss_matches_oracle(seed):
     n_active = torch.empty(n_rows, dtype=torch.int32, device=DEV)
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     L = vren.lib()
-    vren._ok(L.ngp_composite_loss(p(S), p(C), p(Dl), p(Ts), p(RA), n_rows, p(GT), p(bg), 0, lam_op, 0.0, 1.0, T_thr,
+    vren._ok(L.ngp_composite_loss(p(S), p(C), p(Dl), p(Ts), p(RA), n_rows, p(GT), p(bg), 0, lam_op, 0.0, lam_d, 1.0, T_thr,
                                   p(dsig), p(drgb), p(o_rgb), p(o_op), p(o_dep), p(o_loss), p(n_active), None, None,
                                   None, None, vren._stream()), "composite_loss")
     torch.cuda.synchronize()

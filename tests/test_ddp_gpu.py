@@ -1,19 +1,20 @@
 """Data-parallel training step on the device: two
 processes on the one GPU (gloo backend, device tensors staged through the
 host; the graph replays run in segments with the collectives between them)
-train the ZeRO-1 path (reduce-scatter of the gradient buckets, Adam on each
+run the ZeRO-1 path (reduce-scatter of the gradient buckets, Adam on each
 rank's shards, all-gather of the fp16 shadow, sharded occupancy updates with
-the MAX-combined key grid).  Against one process training the concatenated
-batch (rank r draws rays [r*R, (r+1)*R) of the same global batch):
+the MAX-combined key grid), against one process on the concatenated batch
+(rank r takes rays [r*R, (r+1)*R) of the same global batch):
 
-* both ranks hold identical fp16 shadows and identical bitfields every
-  checked step;
-* the per-step losses agree (the loss is a mean over rays: rank means
-  averaged by the 1/world folded into Adam = the 2R-ray mean);
-* the parameters agree up to summation order: gradients are sums of fp32
-  atomics whose order differs, and Adam maps a tiny-gradient element's
-  noise to a +-lr step, so a small fraction of elements may differ by up to
-  2*lr per step while the rest agree to fp32 rounding.
+* one step from the same state: the reduced gradient (rank sum / world) equals
+  the one-process gradient up to fp32 summation order (relative L2 per
+  parameter group);
+* 300 training steps: both ranks hold identical fp16 shadows, fp32 masters
+  and bitfields; the per-step losses agree with the one-process run's at
+  step 0 to summation order and stay within a few per cent on average --
+  NeRF training is chaotic (an occupancy cell flipped by rounding changes
+  the samples of every later step), so parameters are compared only
+  through that.
 """
 import os
 import socket
@@ -54,6 +55,31 @@ def _train(batch, steps):
     return tr, torch.stack(losses).cpu(), [b.cpu() for b in bitfields]
 
 
+def _grad_step(batch, rank=0):
+    """one step without Adam on rows [rank*batch, (rank+1)*batch) of a
+    2*R-ray global batch (host-drawn pixels / noise) -> the gradient"""
+    import synthetic as S
+    from trainer import NGPTrainer
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    dev = torch.device("cuda", 0)
+    tr = NGPTrainer(scale=0.5, batch_size=batch, device=dev, seed=3)
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(11)
+        tr.params[10240:] = ((torch.rand(tr.n_params - 10240, generator=g) * 2 - 1) * 0.5).to(dev)
+        tr.params16.copy_(tr.params.half())
+    tr.density_bitfield.copy_(sc.bitfield.to(dev))
+    tr.global_step = 1
+    gen = torch.Generator().manual_seed(5)
+    img, pix = sc.sample_batch(2 * R, gen)
+    noise = torch.rand(2 * R, generator=gen)
+    sl = slice(rank * batch, (rank + 1) * batch)
+    o, d = sc.rays(img[sl], pix[sl])
+    tr.step(img[sl].to(dev), pix[sl].to(dev), sc.gt_rgb_rays(o, d).to(dev), sc.directions.to(dev),
+            sc.poses.to(dev), noise=noise[sl].to(dev), apply_adam=False)
+    torch.cuda.synchronize()
+    return tr
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -63,12 +89,17 @@ def _worker(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        t1 = _grad_step(R, rank)  # reduced gradient shards in t1._gshard
+        shards = [g.cpu().numpy() for g in t1._gshard]
+        bounds = t1.buckets
+        del t1
         tr, losses, bfs = _train(R, STEPS)
         p = tr.full_params().cpu().clone()
         # numpy: pickled by value (a torch CPU tensor would travel as a shared-memory fd the exiting
         # child could no longer serve)
         q.put((rank, {"params": p.numpy(), "p16": tr.params16.cpu().numpy(), "losses": losses.numpy(),
-                      "bitfields": [b.numpy() for b in bfs], "prefetched": tr.n_prefetched}))
+                      "bitfields": [b.numpy() for b in bfs], "prefetched": tr.n_prefetched,
+                      "shards": shards, "buckets": bounds}))
     finally:
         dist.destroy_process_group()
 
@@ -81,8 +112,9 @@ def test_two_ranks_match_one_process_on_the_concatenated_batch():
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
-    res = {r: {k: (v if k == "prefetched" else [torch.from_numpy(x) for x in v] if k == "bitfields"
-                   else torch.from_numpy(v)) for k, v in d.items()} for r, d in res.items()}
+    res = {r: {k: (v if k in ("prefetched", "buckets") else [torch.from_numpy(x) for x in v]
+                   if k in ("bitfields", "shards") else torch.from_numpy(v)) for k, v in d.items()}
+           for r, d in res.items()}
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -92,8 +124,29 @@ def test_two_ranks_match_one_process_on_the_concatenated_batch():
         assert torch.equal(a, b)
     assert torch.equal(r0["params"], r1["params"])
     assert r0["prefetched"] > STEPS // 2  # the segmented graph replays ran
+    # (1) the reduced gradient of one step vs the one-process gradient
+    import hashgrid as HG
+    one = _grad_step(2 * R)
+    g1 = one.grad.cpu()
+    n = g1.numel()
+    full = torch.zeros(max(b for _, b in r0["buckets"]))
+    for i, (a, b) in enumerate(r0["buckets"]):
+        h = (b - a) // 2
+        full[a:a + h] = r0["shards"][i]
+        full[a + h:b] = r1["shards"][i]
+    g2 = full[:n] / 2  # rank sum -> mean (Adam's 1/world)
+    offs = [0, 3072, HG.MLP_PARAMS] + [HG.MLP_PARAMS + 2 * int(o) for o in one.grid.offsets[1:]]
+    worst = 0.0
+    for a, b in zip(offs[:-1], offs[1:]):
+        ref = g1[a:b].double()
+        if float(ref.norm()) == 0:
+            continue
+        worst = max(worst, float((g2[a:b].double() - ref).norm() / ref.norm()))
+    print(f"one step: reduced gradient vs one process, worst group relative L2 {worst:.2e}")
+    assert worst < 1e-4
+    del one
+    # (2) training
     tr, losses, bfs = _train(2 * R, STEPS)
-    one = tr.params.cpu()
     # loss of the concatenated batch = mean of the ranks' losses
     two = (r0["losses"] + r1["losses"]) / 2  # each rank's loss is the mean over its rays
     rel = (two - losses).abs() / losses.abs()
@@ -102,13 +155,6 @@ def test_two_ranks_match_one_process_on_the_concatenated_batch():
     assert float(rel[0]) < 1e-5  # same parameters, same rays: only summation order differs
     assert float(rel[:20].max()) < 1e-3
     assert float(rel.mean()) < 2e-2
-    d = (r0["params"] - one).abs()
-    frac = float((d > 1e-5).float().mean())
-    print(f"params: {frac:.2e} of elements differ by > 1e-5, max {float(d.max()):.2e}, "
-          f"relative L2 {float((r0['params'] - one).norm() / one.norm()):.2e}")
-    assert frac < 5e-2
-    assert float((r0["params"] - one).norm() / one.norm()) < 5e-2
-    assert float(d.max()) <= 2 * 1e-2 * STEPS
     for a, b in zip(r0["bitfields"], bfs):
         flips = int(np.unpackbits(torch.bitwise_xor(a, b).numpy()).sum())
         print(f"bitfield: {flips} of {a.numel() * 8} cells differ from the one-process run")
