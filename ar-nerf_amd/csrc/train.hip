@@ -9,6 +9,19 @@
 
 namespace ngp {
 
+// Zeroes n 64-bit words in stream order.  Used instead of hipMemsetAsync for
+// the small counters zeroed inside captured graphs: in the exact-mode step
+// graph a captured 8-byte memset was not reliably ordered before the kernel
+// that reads the counter (ngp_guard_hits counted the fallout), a kernel node
+// is.
+__global__ void zero_words_kernel(unsigned long long* __restrict__ p, int n) {
+    if ((int)threadIdx.x < n) p[threadIdx.x] = 0ull;
+}
+
+// Guard trips of the occupancy-list kernels (a reservation past the list's
+// capacity: only a corrupted count can cause one) -- ngp_guard_hits().
+__device__ unsigned long long g_guard_hits = 0ull;
+
 // ------------------------------------------------------ composite + loss
 // One wave per ray.  Pass 1 = composite_train_fw (volumerendering.cu:5-44),
 // the transmittance chain walked sample by sample in lane order (readlane)
@@ -440,7 +453,10 @@ __global__ void __launch_bounds__(1024) occ_list_kernel(const float* __restrict_
     __syncthreads();
     // (the list holds at most n_cells entries: a reservation past that can
     // only come from a corrupted count -- dropped instead of written)
-    if (base > (unsigned long long)n_cells) return;
+    if (base > (unsigned long long)n_cells) {
+        if (tid == 0) atomicAdd(&g_guard_hits, 1ull);
+        return;
+    }
     int64_t pos = (int64_t)base + wcnt[wid] + incl - mine;
 #pragma unroll
     for (int k = 0; k < PER; ++k)
@@ -466,7 +482,7 @@ __global__ void __launch_bounds__(256) occ_sample_kernel(uint64_t seed, const in
         idx = (int32_t)morton3((uint32_t)uniform_index(v.x, G), (uint32_t)uniform_index(v.y, G),
                                (uint32_t)uniform_index(v.z, G));
     } else {  // a cell drawn from the occupied list
-        const unsigned long long cnt = *count;
+        const unsigned long long cnt = min(*count, (unsigned long long)G * G * G);  // (guard: list capacity)
         if (cnt == 0) {
             flat[o] = -1;
             xyzs[3 * o] = 0.f; xyzs[3 * o + 1] = 0.f; xyzs[3 * o + 2] = 0.f;
@@ -591,9 +607,9 @@ __global__ void __launch_bounds__(OSC_T) occ_sample_sorted_kernel(
     for (int q = 0; q < w; ++q) run += wsum[q];
     run += incl - loc;
     const double inv_tot = 1.0 / sums[2 * nb + half];
-    const unsigned long long cnt = half ? *count : 0ull;
-    const float gm1 = (float)(G - 1);
     const int64_t n_cells = (int64_t)G * G * G;
+    const unsigned long long cnt = half ? min(*count, (unsigned long long)n_cells) : 0ull;  // (guard: capacity)
+    const float gm1 = (float)(G - 1);
 #pragma unroll 1
     for (int j = 0; j < OSC_PER; ++j) {
         run += e[j];
@@ -977,6 +993,12 @@ int ngp_counters_inc(int64_t* counters, int n, void* stream) {
     return ngp_launch_status();
 }
 
+unsigned long long ngp_guard_hits(void) {
+    unsigned long long v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_guard_hits), sizeof(v)) != hipSuccess) return ~0ull;
+    return v;
+}
+
 int ngp_density_scatter_last(const int64_t* indices, const float* sigmas, int64_t n, int64_t pos_base,
                              uint64_t* grid_key, void* stream) {
     NGP_CHECK_ARG(n >= 0 && pos_base >= 0 && pos_base + n < (1ll << 31));
@@ -991,8 +1013,7 @@ int ngp_occupied_cells(const float* grid_cascade, int64_t n_cells, float thresho
                        void* stream) {
     NGP_CHECK_ARG(n_cells > 0 && grid_cascade && list && count && ((uintptr_t)count & 7) == 0);
     hipStream_t s = as_stream(stream);
-    hipError_t e = hipMemsetAsync(count, 0, sizeof(int64_t), s);
-    if (e != hipSuccess) return (int)e;
+    zero_words_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(count), 1);
     occ_list_kernel<<<(unsigned)((n_cells + 8191) / 8192), 1024, 0, s>>>(grid_cascade, n_cells, threshold, list,
                                                                         (unsigned long long*)count);
     return ngp_launch_status();
@@ -1040,8 +1061,7 @@ int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, flo
     NGP_CHECK_ARG(n > 0 && density_grid && grid_key && sum_cnt_ws && threshold_out && ((uintptr_t)grid_key & 7) == 0);
     NGP_CHECK_ARG(((uintptr_t)sum_cnt_ws & 7) == 0);
     hipStream_t s = as_stream(stream);
-    hipError_t e = hipMemsetAsync(sum_cnt_ws, 0, 2 * sizeof(double), s);
-    if (e != hipSuccess) return (int)e;
+    zero_words_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(sum_cnt_ws), 2);
     int64_t blocks = (n + 255) / 256;
     if (blocks > 512) blocks = 512;
     grid_ema_kernel<<<(unsigned)blocks, 256, 0, s>>>(density_grid, reinterpret_cast<unsigned long long*>(grid_key), n,

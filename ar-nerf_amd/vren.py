@@ -96,6 +96,8 @@ def _declare(L):
     L.ngp_occupancy_sorted_workspace.restype = ctypes.c_size_t
     L.ngp_render_test_capacity.argtypes = [c_int64, c_int]
     L.ngp_render_test_capacity.restype = c_int64
+    L.ngp_guard_hits.argtypes = []
+    L.ngp_guard_hits.restype = ctypes.c_ulonglong
     # measurement hook (ktimer.py)
     L.ngp_timing_set.argtypes = [vp, vp, c_int64, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64]
     L.ngp_timing_set.restype = c_int

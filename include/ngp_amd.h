@@ -473,6 +473,10 @@ int ngp_counters_inc(int64_t* counters, int n, void* stream);
  * Python), threshold_out[1] = the mean; feed threshold_out to ngp_packbits'
  * threshold_dev.  sum_cnt_ws: 16 bytes of scratch (two fp64 accumulators, 8-byte
  * aligned; the mean is taken in fp64). */
+/* Number of times an occupancy-list kernel found its cell count past the
+ * list's capacity and dropped the batch instead of writing out of bounds
+ * (diagnostic: nonzero means a corrupted count; synchronises the device). */
+unsigned long long ngp_guard_hits(void);
 int ngp_density_scatter_last(const int64_t* indices, const float* sigmas, int64_t n, int64_t pos_base,
                              uint64_t* grid_key, void* stream);
 int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, float decay,

@@ -3,4 +3,4 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/xf
 python3 -c "import sys; sys.path.insert(0, 'ar-nerf_amd'); import synthetic as S; S.write_nsvf_scene('/tmp/Synthetic_NeRF/Analytic', res=400, n_train=100, n_test=10)"
-timeout -k 10 400 python3 -u scripts/train_scene.py --dataset nsvf --root /tmp/Synthetic_NeRF/Analytic --downsample 0.5 --steps 30000 --exact --sync-every 5000 > gpurun_out/xf/out3.json 2> gpurun_out/xf/err3.log
+timeout -k 10 400 python3 -u scripts/train_scene.py --dataset nsvf --root /tmp/Synthetic_NeRF/Analytic --downsample 0.5 --steps 30000 --exact > gpurun_out/xf/out3.json 2> gpurun_out/xf/err3.log

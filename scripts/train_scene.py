@@ -70,7 +70,9 @@ def main(argv=None):
         out = tr.render(o, d, bg=1.0 if tr.esf == 0 else 0.0)
         mse = torch.mean((out["rgb"].clamp(0, 1) - test.rays[i].to(dev)) ** 2).item()
         psnrs.append(-10 * math.log10(max(mse, 1e-12)))
+    import vren
     res = {"dataset": a.dataset, "root": a.root, "steps": a.steps, "mode": "exact" if a.exact else "default",
+           "guard_hits": int(vren.lib().ngp_guard_hits()),
            "train_rays_per_s": round(a.steps * a.batch / t_train, 1),
            "test_psnr": round(sum(psnrs) / max(1, len(psnrs)), 3), "test_views": n}
     print(json.dumps(res))

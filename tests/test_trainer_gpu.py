@@ -194,3 +194,24 @@ def test_repeated_step_gradients_agree_per_level():
         for a, b in zip(off[:-1], off[1:]):
             ref = grads[0][a:b]
             assert float((g[a:b] - ref).norm()) <= 1e-5 * float(ref.norm()) + 1e-12, (a, b)
+
+
+def test_exact_mode_graph_replays_keep_the_occupancy_counters():
+    """Exact mode (every marched sample through the field, per-sample atomic
+    hash backward) in captured graphs: the occupancy update's counters are
+    zeroed in stream order inside the graph (a captured hipMemsetAsync was
+    not -- the occupied-cell list kernel then found stale counts; its guard
+    counts such events, ngp_guard_hits)."""
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    before = int(vren.lib().ngp_guard_hits())
+    tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, chunk_first=0, hash_backward="atomic")
+    tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
+    for _ in range(600):
+        tr.train_step(gt_img, dirs, poses)
+    tr.drain()
+    torch.cuda.synchronize()
+    assert tr.n_prefetched > 300  # graph replays ran
+    assert int(vren.lib().ngp_guard_hits()) == before
+    assert torch.isfinite(tr.params).all()
