@@ -33,6 +33,18 @@
 // A dense-level pair split by a bucket boundary adds its x+1 corner with a
 // global atomic (and flags the bucket); samples beyond the workspace capacity
 // take the per-sample atomic path (and flag every bucket): exact either way.
+//
+// Run merging (levels of merge_mask, the coarse ones): consecutive samples of
+// a ray share a level's cell for dt * res_l < 1 (40 samples per cell at level
+// 0, ~6 at level 7 on Lego), i.e. the same (x, x+1) corner pair per y/z
+// corner.  Lanes 4 apart in a wave hold consecutive samples of the same y/z
+// corner, so the write kernel sums each run of equal pairs in registers
+// (segmented suffix sums, as the accumulation does) and its head emits two
+// single-entry records {i | F_SINGLE, sum_x, sum_y, 0} -- one per corner of
+// the pair, each in its own bucket (no split pair) -- for the whole run; a
+// run of one sample emits its pair record as usual.  Records per
+// (sample, level) stay <= 4 (a run of L >= 2 samples emits 2), and the count
+// kernel makes the same run decisions from the same keys.
 #pragma clang fp contract(off)
 
 #include "common.h"
@@ -40,17 +52,21 @@
 
 namespace ngp {
 
-constexpr int BSHIFT = 13, BENT = 1 << BSHIFT;  // entries per bucket (fp64 LDS image: 128 KB)
+// entries per bucket (fp64 LDS image: 2 x BENT x 8 B = 128 KB, one accumulating workgroup per CU;
+// 4096-entry buckets at two per CU measured the same accumulation time and a slower count pass)
+constexpr int BSHIFT = 13, BENT = 1 << BSHIFT;
 constexpr int NBL = 64;                          // bucket slots per level (2^19 / BENT)
 constexpr int NSLOT = L * NBL;                   // (level, bucket) slots per tile row
-constexpr int MAXB = 1024;                       // buckets over all levels
+constexpr int MAXB = 2048;                       // buckets over all levels
 constexpr int TILE = 256;                        // samples per count/write tile
 constexpr int RPT = TILE * 4 / 256;              // records per thread per level
 constexpr uint32_t CH = 32768;                   // records per pass-5 chunk
 constexpr uint32_t F_C0 = 1u << 28;              // record carries corner x only (pair split)
+constexpr uint32_t F_SINGLE = 1u << 29;          // record {i0 | F_SINGLE, g0, g1, 0}: one entry, summed run
 
 struct BinArgs {
     int lo;                 // levels [lo, L) are binned (the others have no buckets)
+    uint32_t merge;         // bit l: runs of equal corner pairs are merged at level l
     uint32_t bbase[L + 1];  // first bucket of level l
     int64_t tiles_cap;      // tiles the workspace holds
 };
@@ -118,6 +134,25 @@ __device__ __forceinline__ Rec make_rec(const float in[3], float2 gd, int cy, in
     return r;
 }
 
+// Run structure of one level across the wave: lanes 4 apart hold consecutive
+// samples of one y/z corner.  head: the lane starts a run of equal (e0, e1)
+// (lanes 0-3, an invalid lane or its successor, a changed pair); longrun: a
+// head whose run continues to lane + 4.
+struct RunInfo {
+    bool head, longrun;
+    uint64_t heads;
+};
+__device__ __forceinline__ RunInfo run_info(bool valid, uint32_t e0, uint32_t e1) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t k0 = valid ? e0 : 0xffffffffu, k1 = valid ? e1 : (0xfffffff0u | (uint32_t)lane);
+    const uint32_t p0 = __shfl_up(k0, 4, 64), p1 = __shfl_up(k1, 4, 64);
+    RunInfo r;
+    r.head = lane < 4 || !valid || p0 != k0 || p1 != k1;
+    r.heads = __ballot(r.head);
+    r.longrun = r.head && valid && lane + 4 < 64 && !((r.heads >> (lane + 4)) & 1ull);
+    return r;
+}
+
 __device__ __forceinline__ void tile_inputs(const float* __restrict__ xyzs, const int32_t* __restrict__ sidx,
                                             const GridArgs& ga, int64_t j0, int64_t N, float in[RPT][3],
                                             bool valid[RPT]) {
@@ -153,10 +188,18 @@ __global__ void __launch_bounds__(256) hash_count_kernel(const float* __restrict
         tile_inputs(xyzs, sidx, ga, tile * TILE, N, in, valid);
 #pragma unroll 1
         for (int l = ba.lo; l < L; ++l) {
+            const bool merge = (ba.merge >> l) & 1u;
 #pragma unroll
             for (int k = 0; k < RPT; ++k) {
-                if (!valid[k]) continue;
                 const Rec r = make_rec(in[k], g0, cy, cz, lv, l);
+                if (merge) {  // the write kernel's run decisions, from the same keys
+                    const RunInfo ri = run_info(valid[k], r.e0, r.e1);
+                    if (!valid[k] || !ri.head) continue;
+                    atomicAdd(&cnt[l * NBL + (r.e0 >> BSHIFT)], 1u);
+                    if (ri.longrun) atomicAdd(&cnt[l * NBL + (r.e1 >> BSHIFT)], 1u);
+                    continue;
+                }
+                if (!valid[k]) continue;
                 atomicAdd(&cnt[l * NBL + (r.e0 >> BSHIFT)], 1u);
             }
         }
@@ -198,24 +241,27 @@ __global__ void __launch_bounds__(256) hash_scan_kernel(const int64_t* __restric
     if (t == 0) ws.tot[ba.bbase[l] + lb] = carry;
 }
 
-// bucket regions + chunk items (one workgroup of MAXB threads)
-__global__ void __launch_bounds__(MAXB) hash_plan_kernel(uint32_t nbt, BinWs ws) {
-    __shared__ uint32_t a[MAXB], c[MAXB];
-    const uint32_t b = threadIdx.x;
-    const uint32_t tot = b < nbt ? ws.tot[b] : 0u;
-    a[b] = tot;
-    c[b] = (tot + CH - 1) / CH;
+// bucket regions + chunk items (one workgroup of MAXB / 2 threads, two buckets each)
+__global__ void __launch_bounds__(MAXB / 2) hash_plan_kernel(uint32_t nbt, BinWs ws) {
+    __shared__ uint32_t a[MAXB / 2], c[MAXB / 2];
+    const uint32_t t = threadIdx.x, b0 = 2 * t, b1 = 2 * t + 1;
+    const uint32_t t0 = b0 < nbt ? ws.tot[b0] : 0u, t1 = b1 < nbt ? ws.tot[b1] : 0u;
+    const uint32_t c0 = (t0 + CH - 1) / CH, c1 = (t1 + CH - 1) / CH;
+    a[t] = t0 + t1;
+    c[t] = c0 + c1;
     __syncthreads();
-    for (uint32_t o = 1; o < MAXB; o <<= 1) {  // Hillis-Steele inclusive scans
-        const uint32_t va = b >= o ? a[b - o] : 0u, vc = b >= o ? c[b - o] : 0u;
+    for (uint32_t o = 1; o < MAXB / 2; o <<= 1) {  // Hillis-Steele inclusive scans over bucket pairs
+        const uint32_t va = t >= o ? a[t - o] : 0u, vc = t >= o ? c[t - o] : 0u;
         __syncthreads();
-        a[b] += va;
-        c[b] += vc;
+        a[t] += va;
+        c[t] += vc;
         __syncthreads();
     }
-    ws.rstart[b + 1] = a[b];
-    ws.items[b + 1] = c[b];
-    if (b == 0) { ws.rstart[0] = 0; ws.items[0] = 0; }
+    ws.rstart[b0 + 1] = a[t] - t1;
+    ws.rstart[b1 + 1] = a[t];
+    ws.items[b0 + 1] = c[t] - c1;
+    ws.items[b1 + 1] = c[t];
+    if (t == 0) { ws.rstart[0] = 0; ws.items[0] = 0; }
 }
 
 // MODE bits: 2 = store each record from registers at its rank (the product
@@ -228,6 +274,7 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
                                                          const int32_t* __restrict__ sidx, GridArgs ga, BinArgs ba,
                                                          const float* __restrict__ denc, float* __restrict__ grad,
                                                          BinWs ws) {
+    static_assert((MODE & 2) || NBL == 64, "MODE 0 (diagnostics) scans one wave of buckets");
     __shared__ LevelLds lv;
     __shared__ uint32_t base[NSLOT];          // this tile's first slot in each bucket region
     // hist is double-buffered by level parity: the MODE-2 path has no barrier
@@ -272,6 +319,56 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
             const uint32_t off = lv.off[l];
             uint4 rec[RPT];
             uint32_t slot[RPT];  // bucket << 16 | rank in the tile's run, or ~0u
+            if ((ba.merge >> l) & 1u) {  // run-merged level (wave-uniform branch)
+#pragma unroll
+                for (int k = 0; k < RPT; ++k) {
+                    const Rec r = make_rec(in[k], gd[k], cy, cz, lv, l);
+                    const RunInfo ri = run_info(valid[k], r.e0, r.e1);
+                    const int lane = t & 63;
+                    // the fp32 products tcnn adds, summed over the run (segmented suffix sums)
+                    float v00 = (1 - r.fx) * r.a0, v01 = (1 - r.fx) * r.a1, v10 = r.fx * r.a0, v11 = r.fx * r.a1;
+                    if (ri.heads != ~0ull) {
+#pragma unroll
+                        for (int o4 = 4; o4 < 64; o4 <<= 1) {
+                            const float d00 = __shfl_down(v00, o4, 64), d01 = __shfl_down(v01, o4, 64);
+                            const float d10 = __shfl_down(v10, o4, 64), d11 = __shfl_down(v11, o4, 64);
+                            const uint64_t span = ((0x1111111111111111ull & ((2ull << o4) - 1ull)) & ~1ull) << lane;
+                            if (lane + o4 < 64 && (ri.heads & span) == 0) {
+                                v00 += d00; v01 += d01; v10 += d10; v11 += d11;
+                            }
+                        }
+                    }
+                    if (!valid[k] || !ri.head) continue;
+                    if (spill) {
+                        atomicAdd(grad + 2 * (size_t)(off + r.e0), v00);
+                        atomicAdd(grad + 2 * (size_t)(off + r.e0) + 1, v01);
+                        atomicAdd(grad + 2 * (size_t)(off + r.e1), v10);
+                        atomicAdd(grad + 2 * (size_t)(off + r.e1) + 1, v11);
+                        continue;
+                    }
+                    const uint32_t b0 = r.e0 >> BSHIFT, b1 = r.e1 >> BSHIFT;
+                    if (ri.longrun) {
+                        const uint4 q0 = make_uint4((r.e0 & (BENT - 1)) | F_SINGLE, __float_as_uint(v00),
+                                                    __float_as_uint(v01), 0u);
+                        const uint4 q1 = make_uint4((r.e1 & (BENT - 1)) | F_SINGLE, __float_as_uint(v10),
+                                                    __float_as_uint(v11), 0u);
+                        ws.rec[base[l * NBL + b0] + atomicAdd(&hist[b0], 1u)] = q0;
+                        ws.rec[base[l * NBL + b1] + atomicAdd(&hist[b1], 1u)] = q1;
+                        continue;
+                    }
+                    uint32_t key = (r.e0 & (BENT - 1)) | ((r.e1 & (BENT - 1)) << BSHIFT);
+                    if (b1 != b0) {  // pair split by a bucket boundary: corner x+1 goes direct
+                        key |= F_C0;
+                        add_pair_direct(grad, off + r.e1, r.fx, r.a0, r.a1);
+                        ws.fb[ba.bbase[l] + b1] = 1u;
+                    }
+                    ws.rec[base[l * NBL + b0] + atomicAdd(&hist[b0], 1u)] =
+                        make_uint4(key, __float_as_uint(r.fx), __float_as_uint(r.a0), __float_as_uint(r.a1));
+                }
+#pragma unroll
+                for (int k = 0; k < RPT; ++k) gd[k] = gn[k];
+                continue;
+            }
 #pragma unroll
             for (int k = 0; k < RPT; ++k) {
                 slot[k] = ~0u;
@@ -303,7 +400,7 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
                 continue;
             }
             __syncthreads();
-            if (t < 64) {  // exclusive scan of the tile's per-bucket counts (NBL = 64 = one wave)
+            if (t < 64) {  // exclusive scan of the tile's per-bucket counts (MODE 0, diagnostics: NBL <= 64)
                 const uint32_t h = hist[t];
                 uint32_t x = h;
 #pragma unroll
@@ -377,9 +474,11 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
                     if (w0 * a0 + fx * a1 == 1234.5f) img[i0 ^ i1] = 1.0;  // keeps the loads live
                     continue;
                 }
-                // the fp32 products tcnn would add, summed in fp64
-                const bool c1 = !(key & F_C0);
-                double p00 = (double)(w0 * a0), p01 = (double)(w0 * a1);
+                // the fp32 products tcnn would add, summed in fp64; a single-entry
+                // record {i0 | F_SINGLE, g0, g1} carries a run's sums for entry i0
+                const bool single = key & F_SINGLE;
+                const bool c1 = !(key & (F_C0 | F_SINGLE));
+                double p00 = single ? (double)fx : (double)(w0 * a0), p01 = single ? (double)a0 : (double)(w0 * a1);
                 double p10 = c1 ? (double)(fx * a0) : 0.0, p11 = c1 ? (double)(fx * a1) : 0.0;
                 // Runs: records 4 apart in a wave are the same y/z corner of
                 // consecutive samples (a ray's), which on coarse levels often
@@ -433,9 +532,11 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
     }
 }
 
-static int bin_args(const ngp_hashgrid_t* grid, int64_t tiles_cap, int lo, BinArgs& ba, uint32_t& nbt) {
-    if (lo < 0 || lo >= L) return NGP_EINVAL;
+static int bin_args(const ngp_hashgrid_t* grid, int64_t tiles_cap, int lo, int merge_hi, BinArgs& ba,
+                    uint32_t& nbt) {
+    if (lo < 0 || lo >= L || merge_hi < 0 || merge_hi > L) return NGP_EINVAL;
     ba.lo = lo;
+    ba.merge = merge_hi >= 32 ? 0xffffffffu : ((1u << merge_hi) - 1u);
     uint32_t b = 0;
     for (int l = 0; l < L; ++l) {
         ba.bbase[l] = b;
@@ -465,7 +566,7 @@ size_t ngp_hash_backward_binned_workspace(int64_t max_samples) {
 // accumulate (needs denc and the plan of the same inputs).
 static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                        const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                       int64_t max_samples, int level_lo, int phase, void* stream) {
+                       int64_t max_samples, int level_lo, int merge_hi, int phase, void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
@@ -479,7 +580,7 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
     NGP_CHECK_ARG(tiles_cap * TILE * 4 * L < (int64_t)0xffffffffLL);
     BinArgs ba;
     uint32_t nbt;
-    st = bin_args(grid, tiles_cap, level_lo, ba, nbt);
+    st = bin_args(grid, tiles_cap, level_lo, merge_hi, ba, nbt);
     if (st) return st;
     BinWs ws;
     bin_ws_bytes(tiles_cap, &ws, workspace);
@@ -488,7 +589,7 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
         static const unsigned capC = resident_blocks(hash_count_kernel, 256, 0);
         NGP_TIMED(NGP_K_HASH_COUNT, s, hash_count_kernel<<<persistent_blocks(n, TILE, capC), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba, ws));
         NGP_TIMED(NGP_K_HASH_SCAN, s, hash_scan_kernel<<<NSLOT, 256, 0, s>>>(n_dev, n, ba, ws));
-        NGP_TIMED(NGP_K_HASH_PLAN, s, hash_plan_kernel<<<1, MAXB, 0, s>>>(nbt, ws));
+        NGP_TIMED(NGP_K_HASH_PLAN, s, hash_plan_kernel<<<1, MAXB / 2, 0, s>>>(nbt, ws));
     }
     if (phase & 2) {
         static const unsigned capW = resident_blocks(hash_write_kernel<2>, 256, 0);
@@ -510,23 +611,23 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
 
 int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                             int64_t max_samples, int level_lo, void* stream) {
-    return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo, 3,
-                       stream);
+                             int64_t max_samples, int level_lo, int merge_hi, void* stream) {
+    return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo,
+                       merge_hi, 3, stream);
 }
 
 int ngp_hash_binned_plan(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                          const ngp_hashgrid_t* grid, void* workspace, int64_t max_samples, int level_lo,
-                         void* stream) {
-    return hash_binned(xyzs, n, n_dev, sample_idx, grid, nullptr, nullptr, workspace, max_samples, level_lo, 1,
-                       stream);
+                         int merge_hi, void* stream) {
+    return hash_binned(xyzs, n, n_dev, sample_idx, grid, nullptr, nullptr, workspace, max_samples, level_lo,
+                       merge_hi, 1, stream);
 }
 
 int ngp_hash_binned_apply(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                           const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                          int64_t max_samples, int level_lo, void* stream) {
-    return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo, 2,
-                       stream);
+                          int64_t max_samples, int level_lo, int merge_hi, void* stream) {
+    return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo,
+                       merge_hi, 2, stream);
 }
 
 }  // extern "C"

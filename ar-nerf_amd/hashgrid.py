@@ -49,10 +49,10 @@ def _lib():
         L.ngp_field_forward_indexed.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp]
         L.ngp_field_mlp_forward.argtypes = [vp, vp, c_int64, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_hash_backward.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
-        L.ngp_hash_backward_binned.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, vp]
+        L.ngp_hash_backward_binned.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, c_int, vp]
         L.ngp_hash_backward_levels.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp]
-        L.ngp_hash_binned_plan.argtypes = [vp, c_int64, vp, vp, P, vp, c_int64, c_int, vp]
-        L.ngp_hash_binned_apply.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, vp]
+        L.ngp_hash_binned_plan.argtypes = [vp, c_int64, vp, vp, P, vp, c_int64, c_int, c_int, vp]
+        L.ngp_hash_binned_apply.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, c_int, vp]
         L.ngp_hash_backward_binned_workspace.argtypes = [c_int64]
         L.ngp_hash_backward_binned_workspace.restype = ctypes.c_size_t
         for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_density_input_grad, L.ngp_field_backward, L.ngp_field_backward_mlp,

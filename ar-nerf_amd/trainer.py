@@ -46,7 +46,7 @@ class NGPTrainer:
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
                  device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=None, bin_level_lo=None,
-                 chunk_first=64, erode=False, lambda_distortion=0.0):
+                 chunk_first=64, erode=False, lambda_distortion=0.0, bin_merge_hi=None):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
@@ -189,6 +189,10 @@ class NGPTrainer:
             bin_samples_per_ray = 512 if big else 128
         self.hash_backward = hash_backward
         self.bin_level_lo = 0 if hash_backward == "binned" else bin_level_lo
+        # binned levels [bin_level_lo, bin_merge_hi) merge runs of equal corner pairs along a ray
+        if bin_merge_hi is None:
+            bin_merge_hi = int(os.environ.get("NGP_BIN_MERGE_HI", "0"))
+        self.bin_merge_hi = bin_merge_hi
         if hash_backward != "atomic":
             self.bin_max_samples = R * bin_samples_per_ray
             nbytes = HG._lib().ngp_hash_backward_binned_workspace(self.bin_max_samples)
@@ -714,7 +718,7 @@ class NGPTrainer:
                 vren._ok(HGL.ngp_hash_binned_plan(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
                                                   _p(self.bin_ws), self.bin_max_samples, self.bin_level_lo,
-                                                  vren._stream()), "hash_binned_plan")
+                                                  self.bin_merge_hi, vren._stream()), "hash_binned_plan")
                 planned = torch.cuda.Event()
                 planned.record(bs)
         self._ev("mlp_bwd", 0)
@@ -748,8 +752,8 @@ class NGPTrainer:
                 vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                    _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
                                                    _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws),
-                                                   self.bin_max_samples, self.bin_level_lo, vren._stream()),
-                         "hash_binned_apply")
+                                                   self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi,
+                                                   vren._stream()), "hash_binned_apply")
                 self._ev("hash_binned_apply", 1)
                 if adam_split:
                     self._adam(split, self.params.numel(), vren._stream())

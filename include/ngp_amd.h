@@ -359,22 +359,25 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
  * (pair it with ngp_hash_backward_levels for the others).  max_samples =
  * samples the workspace holds (1 KiB each; samples beyond it take the atomic
  * path, still exact); workspace = ngp_hash_backward_binned_workspace(
- * max_samples) bytes, 256-byte aligned device memory.  Replaces the same tcnn
- * grid backward. */
+ * max_samples) bytes, 256-byte aligned device memory.  Levels [level_lo,
+ * merge_hi) merge runs of consecutive samples (sample_idx order: along rays)
+ * that share a corner pair into one summed record per corner (the coarse
+ * levels, where a ray stays in a cell for many samples); merge_hi <= level_lo
+ * disables it.  Replaces the same tcnn grid backward. */
 size_t ngp_hash_backward_binned_workspace(int64_t max_samples);
 int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                             int64_t max_samples, int level_lo, void* stream);
+                             int64_t max_samples, int level_lo, int merge_hi, void* stream);
 /* ngp_hash_backward_binned in two phases on the same workspace and inputs:
  * _plan (record counts, bucket regions: reads xyzs / sample_idx only, so it
  * can run beside the MLP backward that produces denc) then _apply (records,
  * LDS range sums, gradient). */
 int ngp_hash_binned_plan(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                          const ngp_hashgrid_t* grid, void* workspace, int64_t max_samples, int level_lo,
-                         void* stream);
+                         int merge_hi, void* stream);
 int ngp_hash_binned_apply(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                           const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                          int64_t max_samples, int level_lo, void* stream);
+                          int64_t max_samples, int level_lo, int merge_hi, void* stream);
 /* ngp_hash_backward restricted to levels [level_lo, level_hi). */
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,

@@ -69,7 +69,7 @@ def main():
         assert L.ngp_hash_backward_levels(*args(), p(grad), lo, hi, vp(stream.cuda_stream)) == 0
 
     def binned(lo, stream):
-        assert L.ngp_hash_backward_binned(*args(), p(grad), p(ws), cap, lo, vp(stream.cuda_stream)) == 0
+        assert L.ngp_hash_backward_binned(*args(), p(grad), p(ws), cap, lo, 0, vp(stream.cuda_stream)) == 0
 
     def timed(fn, reps=30):
         for _ in range(3):

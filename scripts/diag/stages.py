@@ -91,7 +91,7 @@ def main():
         p(tr.drgb), p(tr.denc), p(tr.grad), vren._stream()), "mb"))
     st["hash_bwd_binned_fine"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_binned(
         p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
-        p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, tr.bin_level_lo, vren._stream()), "hb"))
+        p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, tr.bin_level_lo, 0, vren._stream()), "hb"))
     st["hash_bwd_atomic_coarse"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_levels(
         p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
         p(tr.grad[HG.MLP_PARAMS:]), 0, tr.bin_level_lo, vren._stream()), "ha"))
@@ -102,7 +102,7 @@ def main():
     for lo in (4, 6, 10, 12):
         st[f"hash_binned_from_L{lo}"] = timed(lambda: vren._ok(HGL.ngp_hash_backward_binned(
             p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
-            p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, lo, vren._stream()), "hb"))
+            p(tr.grad[HG.MLP_PARAMS:]), p(tr.bin_ws), tr.bin_max_samples, lo, 0, vren._stream()), "hb"))
     st["hash_bwd_atomic_all"] = timed(lambda: vren._ok(HGL.ngp_hash_backward(
         p(tr.xyzs), tr.cap, p(tr.n_active_total), p(tr.sample_idx), HG.ctypes.byref(tr.grid.desc), p(tr.denc),
         p(tr.grad[HG.MLP_PARAMS:]), vren._stream()), "hall"))

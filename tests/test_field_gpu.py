@@ -174,15 +174,31 @@ def test_field_autograd_function():
     assert params.grad[:HG.MLP_PARAMS].abs().sum() > 0
 
 
+def _ray_points(n_rays, per_ray, scale, seed):
+    """samples along rays, consecutive per ray (a march's layout): runs of
+    equal corner pairs on the coarse levels"""
+    g = torch.Generator().manual_seed(seed)
+    o = (torch.rand(n_rays, 3, generator=g) * 2 - 1) * scale * 0.9
+    d = torch.randn(n_rays, 3, generator=g)
+    d = d / d.norm(dim=1, keepdim=True)
+    t = torch.arange(per_ray).float() * (3 ** 0.5 / 1024) * scale * 2
+    x = (o[:, None] + t[None, :, None] * d[:, None]).clamp(-scale, scale).reshape(-1, 3)
+    return x.contiguous()
+
+
 @pytest.mark.parametrize("scale", [0.5, 16.0])
-@pytest.mark.parametrize("level_cap,level_lo", [(1 << 20, 0), (3000, 0), (1 << 20, 8)])  # workspace max_samples
-def test_hash_backward_binned_matches_atomic(scale, level_cap, level_lo):
+@pytest.mark.parametrize("level_cap,level_lo,merge_hi,rays", [(1 << 20, 0, 0, False), (3000, 0, 0, False),
+                                                             (1 << 20, 8, 8, False), (1 << 20, 0, 12, True),
+                                                             (3000, 0, 16, True), (1 << 20, 4, 12, True)])
+def test_hash_backward_binned_matches_atomic(scale, level_cap, level_lo, merge_hi, rays):
     """ngp_hash_backward_binned (records + LDS range sums) == ngp_hash_backward
     (per-sample atomics) up to fp32 summation order, through a sample_idx
     subset, onto a non-zero gradient (+= contract).  max_samples=3000 sends
     most tiles through the overflow path (direct atomics); level_lo=8 bins the
-    fine levels only, the coarse ones going through ngp_hash_backward_levels."""
-    x, _ = _points(40000, scale, seed=3)
+    fine levels only, the coarse ones going through ngp_hash_backward_levels;
+    merge_hi > level_lo merges runs of equal corner pairs on samples laid out
+    along rays (rays=True, where runs exist)."""
+    x = _ray_points(400, 100, scale, seed=3) if rays else _points(40000, scale, seed=3)[0]
     n = x.shape[0]
     grid = HG.HashGrid(scale)
     g = torch.Generator().manual_seed(5)
@@ -203,7 +219,7 @@ def test_hash_backward_binned_matches_atomic(scale, level_cap, level_lo):
     for _ in range(2):  # the workspace is reusable: counters reset per call
         out.copy_(base)
         vren._ok(L.ngp_hash_backward_binned(p(x), n, p(n_dev), p(sidx), HG.ctypes.byref(grid.desc), p(denc), p(out),
-                                            p(ws), level_cap, level_lo, vren._stream()), "hash_backward_binned")
+                                            p(ws), level_cap, level_lo, merge_hi, vren._stream()), "hash_backward_binned")
         vren._ok(L.ngp_hash_backward_levels(p(x), n, p(n_dev), p(sidx), HG.ctypes.byref(grid.desc), p(denc), p(out),
                                             0, level_lo, vren._stream()), "hash_backward_levels")
     torch.cuda.synchronize()
