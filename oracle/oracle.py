@@ -353,7 +353,7 @@ def mlp_forward_bound(x16, Ws):
 
 
 # density net 32->64->16, color net 32->64->64->16(pad; 3 used)
-DENSITY_DIMS = (32, 64, 16)
+DENSITY_DIMS = (32, 64, 16)  # the reference's (networks.py:51-57, 68-78)
 COLOR_DIMS = (32, 64, 64, 16)
 
 
@@ -381,28 +381,37 @@ class _HashEncodeFn(torch.autograd.Function):
 class OracleNGPField(torch.nn.Module):
     """CPU oracle of NGP.density / NGP.forward (models/networks.py:95-165) with
     tcnn semantics; flat params like the tcnn torch modules:
-      xyz_params = [W1 (64x32), W2 (16x64), hash table (entries x 2)]
-      rgb_params = [W3 (64x32), W4 (64x64), W5 (16x64)]"""
+      xyz_params = [W1 (w x in), W2 (16 x w), hash table (entries x 2)]
+      rgb_params = [W3 (w x 32), W4 (w x w), W5 (16 x w)]
+    w = width (64 in the reference, networks.py:54,75), in = 2 L padded to a
+    multiple of 16 (tcnn's FullyFusedMLP input granularity; the padded
+    encoding dims hold 1.0, tcnn's padding value -- parity unpinned: only
+    BASELINE config 1, L = 4, w = 32, pads: 8 -> 16)."""
 
     def __init__(self, scale=0.5, n_levels=16, log2_T=19, base_resolution=16, seed=4,
-                 table_init=1e-4):
+                 table_init=1e-4, width=64):
         super().__init__()
-        self.scale = scale
+        self.scale, self.width = scale, width
         self.spec = HashGridSpec(n_levels, log2_T, base_resolution, scale=scale)
+        self.n_in = (2 * n_levels + 15) // 16 * 16
+        self.dens_dims = (self.n_in, width, 16)
+        self.color_dims = (32, width, width, 16)
         self.register_buffer("xyz_min", -torch.ones(1, 3) * scale)
         self.register_buffer("xyz_max", torch.ones(1, 3) * scale)
         gen = torch.Generator().manual_seed(seed)
-        dens = xavier_mlp((2 * n_levels, 64, 16), gen)
+        dens = xavier_mlp(self.dens_dims, gen)
         table = (torch.rand(self.spec.n_entries * 2, generator=gen) * 2 - 1) * table_init
-        col = xavier_mlp(COLOR_DIMS, gen)
+        col = xavier_mlp(self.color_dims, gen)
         self.xyz_params = torch.nn.Parameter(torch.cat([dens, table]))
         self.rgb_params = torch.nn.Parameter(col)
         self.n_dens = dens.numel()
 
     def density_feat(self, x):
-        Ws, _ = mlp_layers(self.xyz_params[:self.n_dens], (2 * self.spec.L, 64, 16))
+        Ws, _ = mlp_layers(self.xyz_params[:self.n_dens], self.dens_dims)
         table = self.xyz_params[self.n_dens:]
         enc = _HashEncodeFn.apply(table, x, self.spec, self.xyz_min, self.xyz_max)
+        if enc.shape[1] < self.n_in:  # tcnn pads the encoding to the MLP's input width with ones
+            enc = torch.cat([enc, torch.ones(enc.shape[0], self.n_in - enc.shape[1], dtype=enc.dtype)], 1)
         h = mlp_forward(enc, Ws)
         return h
 
@@ -414,7 +423,7 @@ class OracleNGPField(torch.nn.Module):
     def forward(self, x, d):
         sig, h = self.density(x, return_feat=True)
         sh = sh4(d).float()
-        Ws, _ = mlp_layers(self.rgb_params, COLOR_DIMS)
+        Ws, _ = mlp_layers(self.rgb_params, self.color_dims)
         out = mlp_forward(torch.cat([sh, h], 1), Ws)
         rgb = rh(torch.sigmoid(out[:, :3]))
         return sig, rgb
@@ -554,13 +563,19 @@ class OracleTrainer:
     oracle: march (C), field (torch MLP with fp16 storage points + C hash),
     VolumeRenderer fw/bw (C), NeRFLoss (torch), autograd, Adam (C)."""
 
-    def __init__(self, flat_params, scale, bitfield, cascades, grid_size=128, lr=1e-2):
-        self.field = OracleNGPField(scale=scale, table_init=0.0)
+    def __init__(self, flat_params, scale, bitfield, cascades, grid_size=128, lr=1e-2, n_levels=16, width=64,
+                 seed=4, table_init=0.0):
+        """flat_params: the product's flat layout [W1 W2 | W3 W4 W5 | table],
+        or None to train the oracle field's own initialisation (any L / width:
+        BASELINE config 1 runs L = 4, width 32 on the CPU only)."""
+        self.field = OracleNGPField(scale=scale, table_init=table_init, n_levels=n_levels, width=width, seed=seed)
         nd = self.field.n_dens
-        flat = flat_params.detach().float().cpu()
-        with torch.no_grad():
-            self.field.xyz_params.copy_(torch.cat([flat[:nd], flat[10240:]]))
-            self.field.rgb_params.copy_(flat[nd:10240])
+        self.n_mlp = nd + self.field.rgb_params.numel()
+        if flat_params is not None:
+            flat = flat_params.detach().float().cpu()
+            with torch.no_grad():
+                self.field.xyz_params.copy_(torch.cat([flat[:nd], flat[self.n_mlp:]]))
+                self.field.rgb_params.copy_(flat[nd:self.n_mlp])
         self.scale, self.cascades, self.G, self.lr = scale, cascades, grid_size, lr
         self.bitfield = bitfield.cpu().contiguous()
         self.state = {p: (torch.zeros_like(p), torch.zeros_like(p)) for p in (self.field.xyz_params,
