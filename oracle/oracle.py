@@ -326,7 +326,7 @@ def ulp16(v):
     return torch.exp2(torch.floor(torch.log2(a)) - 10)
 
 
-def mlp_forward_bound(x16, Ws):
+def mlp_forward_bound(x16, Ws, d_in=None):
     """mlp_forward (ReLU hidden, no output activation) plus, per output, a
     bound on |out - out'| for ANY implementation with the same fp16 storage
     points (fp16 weights and layer outputs) that accumulates each dot
@@ -335,9 +335,10 @@ def mlp_forward_bound(x16, Ws):
     by at most gamma_n * sum|terms| (gamma_n = n u / (1 - n u)); an error d
     in a layer's inputs moves its outputs by at most |W| d; rounding to fp16
     then adds at most one fp16 ulp (the two values may straddle a rounding
-    boundary); ReLU is 1-Lipschitz.  Returns (out, bound), both fp32."""
+    boundary); ReLU is 1-Lipschitz.  d_in: a bound on the inputs' own error
+    (default exact).  Returns (out, bound), both fp32."""
     h = x16.float()
-    d = torch.zeros_like(h)
+    d = torch.zeros_like(h) if d_in is None else d_in.float()
     for i, W in enumerate(Ws):
         W16 = rh(W.detach()).float()
         n = W16.shape[1]

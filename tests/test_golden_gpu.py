@@ -51,6 +51,10 @@ def test_product_train_step_matches_reference_glue(case):
     assert int(res["rm_samples"]) == int(fx["rm_samples"])
     for k in ("rgb", "opacity", "depth", "ws"):
         torch.testing.assert_close(res[k].detach().cpu(), torch.from_numpy(fx[k]), atol=2e-3, rtol=0)
+    # composited count: the field's sigma differs from the oracle's within the
+    # fp16 MLP bound (test_field_forward_parity), so a ray whose transmittance
+    # sits on T_thr within that bound may end one sample apart
+    # (test_composite_train_fw_bw pins the per-ray form of this); 2 of the batch
     assert abs(int(res["vr_samples"]) - int(fx["vr_samples"])) <= 2
     loss_d = NeRFLoss(30, "raw", float(fx["scale"]), 0.0, lambda_distortion=0.0)(res, {"rgb": gt})
     loss = sum(v.mean() for v in loss_d.values())

@@ -148,3 +148,59 @@ def test_adam_matches_torch():
         p_ref.grad = gr.clone()
         opt.step()
     torch.testing.assert_close(p, p_ref.detach(), atol=1e-6, rtol=1e-5)
+
+
+def test_grid_encode_fp32_vs_half_fma_accumulation():
+    """Deviation of the encoding's corner sum accumulated in fp32 (this oracle
+    and the product, bit-exact with each other) from tcnn's kernel_grid, which
+    accumulates result = fma((T)weight, val, result) in T = __half (every
+    corner's fma rounded to fp16).  Measured on ray samples with tcnn-scale
+    table values: the features agree exactly or within 2 fp16 ulps of the
+    half-accumulated value (documented in DESIGN.md §4)."""
+    import synthetic as S
+    spec = O.HashGridSpec(16, 19, 16, scale=0.5)
+    g = torch.Generator().manual_seed(0)
+    x = (torch.rand(20000, 3, generator=g) - 0.5)
+    table = (torch.rand(spec.n_entries * 2, generator=g) * 2 - 1) * 1.0
+    mn, mx = -torch.ones(1, 3) * 0.5, torch.ones(1, 3) * 0.5
+    enc32 = O.hash_encode_fwd(spec, x, mn, mx, table).float()  # (N, 32)
+    idx, w = O.hash_corners(spec, x, mn, mx)  # (N, L, 8) entry index per corner, fp32 weight
+    tab = table.half().double().view(-1, 2)
+    wh = w.half().double()  # (T)weight
+    r = torch.zeros(x.shape[0], spec.L, 2, dtype=torch.float64)
+    for c in range(8):  # fma in half: exact product + sum, one rounding to fp16
+        v = tab[idx[:, :, c].long()]
+        r = (wh[:, :, c:c + 1] * v + r).half().double()
+    enc16 = r.reshape(x.shape[0], 2 * spec.L).float()
+    # scale of the accumulation: sum_c |w_c v_c| (fp16 ulps of the partial sums)
+    mag = (wh.unsqueeze(-1) * tab[idx.long()].abs()).sum(2).reshape(x.shape[0], 2 * spec.L).float()
+    ulps = (enc32 - enc16).abs() / O.ulp16(mag)
+    same = float((enc32 == enc16).float().mean())
+    print(f"grid encode, fp32 vs __half fma accumulation: {same:.2%} identical, "
+          f"{float((ulps <= 1).float().mean()):.2%} within 1 fp16 ulp of sum|w v|, max {float(ulps.max()):.2f} ulps, "
+          f"max abs {float((enc32 - enc16).abs().max()):.2e}")
+    # 8 fma roundings of partial sums <= sum|w v|, each <= half an ulp
+    assert float(ulps.max()) <= 4
+
+
+def test_mlp_weight_gradient_operand_rounding():
+    """The MLP weight gradients dW = sum_s G[o][s] H[i][s] take bf16 operands
+    on the GPU (field.hip field_bwd_mlp_kernel; tcnn: fp16).  Operand
+    rounding alone, over a step's ~150k samples of activation / gradient
+    magnitudes like the training step's: relative L2 vs fp32 operands,
+    bf16 vs fp16 (both accumulating in fp32) -- the figure documented next to
+    the bench's dtype."""
+    g = torch.Generator().manual_seed(1)
+    n = 150000
+    H = torch.relu(torch.randn(64, n, generator=g)).half().float()  # fp16 activations
+    G = torch.randn(16, n, generator=g) * 1e-4 * torch.exp(torch.randn(1, n, generator=g))
+    ref = G.double() @ H.double().t()
+
+    def rel(a):
+        return float((a.double() - ref).norm() / ref.norm())
+
+    bf = G.bfloat16().float() @ H.bfloat16().float().t()
+    hf = (G * 2 ** 14 / G.abs().max()).half().float() @ H.half().float().t() * (G.abs().max() / 2 ** 14)
+    e_bf, e_hf = rel(bf), rel(hf)
+    print(f"dW operand rounding, relative L2 vs fp32 operands: bf16 {e_bf:.2e}, fp16 (scaled) {e_hf:.2e}")
+    assert e_bf < 5e-3 and e_hf < 1e-3
