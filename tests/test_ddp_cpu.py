@@ -51,7 +51,9 @@ def _worker(rank, world, port, q):
         thr = torch.tensor([1.0 + rank, 2.0])
         ddp.sync_threshold_(thr)
         out["thr"] = thr
-        q.put((rank, out))
+        # numpy, not torch tensors: torch's queue shares tensor storage through
+        # file descriptors that vanish when this process exits first
+        q.put((rank, {k: v.numpy() for k, v in out.items()}))
     finally:
         dist.destroy_process_group()
 
@@ -63,7 +65,7 @@ def test_ddp_pieces_world2():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
+    res = {r: {k: torch.from_numpy(v) for k, v in o.items()} for r, o in (q.get(timeout=120) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

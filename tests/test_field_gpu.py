@@ -181,6 +181,47 @@ def test_field_backward_parity(table_init):
     assert torch.equal(gc[HG.MLP_PARAMS:] == 0, ref[HG.MLP_PARAMS:] == 0)
 
 
+def test_field_backward_per_sample_scales():
+    """dL/denc per sample when the per-sample gradient magnitudes span nine
+    decades (composited weights of a batch do): the MLP backward scales each
+    sample's gradient column by its own power of two before the fp16 cast,
+    so small-gradient samples keep full precision beside large ones.  Oracle:
+    fp32 autograd through the oracle's MLP from the same fp16 encoding."""
+    f, flat = _oracle_and_params(0.5)
+    x, d = _points(20000, 0.5, seed=3)
+    g = torch.Generator().manual_seed(11)
+    mag = 10.0 ** (torch.rand(x.shape[0], generator=g) * 9 - 7)  # 1e-7 .. 1e2 per sample
+    dsig = torch.randn(x.shape[0], generator=g) * mag * 1e-2
+    drgb = torch.randn(x.shape[0], 3, generator=g) * mag[:, None]
+    grid = HG.HashGrid(0.5)
+    p16 = flat.to(DEV).half()
+    _, _, enc, _ = HG.field_forward(x.to(DEV), d.to(DEV), grid, p16)
+    grad = torch.zeros(grid.n_params, device=DEV)
+    denc = torch.empty(x.shape[0], 32, device=DEV)
+    HG.field_backward(x.to(DEV), d.to(DEV), grid, p16, enc, dsig.to(DEV), drgb.to(DEV), grad, denc_ws=denc)
+    e = enc.cpu().float().requires_grad_()
+    nd = f.n_dens
+    Wd, _ = O.mlp_layers(f.xyz_params.detach()[:nd], f.dens_dims)
+    Wc, _ = O.mlp_layers(f.rgb_params.detach(), f.color_dims)
+    h = O.mlp_forward(e, Wd)
+    sig = O.TruncExpCPU.apply(h[:, 0])
+    out = O.mlp_forward(torch.cat([O.sh4(d).float(), h], 1), Wc)
+    rgb = O.rh(torch.sigmoid(out[:, :3]))
+    ((sig * dsig).sum() + (rgb * drgb).sum()).backward()
+    ref, got = e.grad, denc.cpu()
+    assert bool(torch.isfinite(got).all())
+    rn = ref.norm(dim=1)
+    rel = (got - ref).norm(dim=1) / rn.clamp_min(1e-38)
+    live = rn > 0
+    frac = float((rel[live] <= 2e-2).float().mean())
+    print(f"dL/denc per sample: {frac:.2%} of {int(live.sum())} samples within 2e-2 relative, "
+          f"median {float(rel[live].median()):.1e}")
+    assert frac >= 0.99
+    # the smallest-gradient decade as well as the largest
+    lo, hi = live & (mag < 1e-6), live & (mag > 10)
+    assert float((rel[lo] <= 2e-2).float().mean()) >= 0.99 and float((rel[hi] <= 2e-2).float().mean()) >= 0.99
+
+
 def test_field_autograd_function():
     f, flat = _oracle_and_params(0.5)
     x, d = _points(5000, 0.5, seed=2)
