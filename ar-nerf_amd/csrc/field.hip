@@ -208,6 +208,38 @@ __device__ __forceinline__ void load_fwd_weights(const _Float16* __restrict__ ml
     for (int i = t; i < 16 * 64; i += nt) sw[SW5 + (i >> 6) * R64 + (i & 63)] = mlp[OW5 + (i >> 6) * 64 + P64(i & 63)];
 }
 
+// Inverses of P64 / P32: weight column i -> its position in the permuted row.
+__device__ __forceinline__ int P64inv(int i) {
+    const int q = i >> 5, r = i & 31;
+    return 32 * q + (r < 16 ? 8 * (r >> 2) + (r & 3) : 8 * ((r - 16) >> 2) + 4 + (r & 3));
+}
+__device__ __forceinline__ int P32inv(int i) { return i < 16 ? 8 * (i >> 2) + (i & 3) : 8 * ((i - 16) >> 2) + 4 + (i & 3); }
+
+// The forward weight image built straight from global memory: coalesced
+// 16-byte loads of the row-major buffer, each half scattered to its permuted
+// LDS position (8 consecutive halfs share one row) -- no 20 KB raw staging
+// buffer, so the MLP-only forward fits more blocks per CU.
+__device__ __forceinline__ void load_fwd_weights_direct(const _Float16* __restrict__ mlp, _Float16* sw, bool color) {
+    const h8* src = reinterpret_cast<const h8*>(mlp);
+    const int nv = (color ? NGP_MLP_PARAMS : OW3) / 8;
+    for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+        const h8 v = src[c];
+        const int i0 = 8 * c;
+        int row, col0;  // destination row start, and the first column
+        bool p64 = false, p32 = false;
+        if (i0 < OW2) { row = SW1 + (i0 >> 5) * R32; col0 = i0 & 31; }
+        else if (i0 < OW3) { row = SW2 + ((i0 - OW2) >> 6) * R64; col0 = (i0 - OW2) & 63; p64 = true; }
+        else if (i0 < OW4) { row = SW3 + ((i0 - OW3) >> 5) * R32; col0 = (i0 - OW3) & 31; p32 = true; }
+        else if (i0 < OW5) { row = SW4 + ((i0 - OW4) >> 6) * R64; col0 = (i0 - OW4) & 63; p64 = true; }
+        else { row = SW5 + ((i0 - OW5) >> 6) * R64; col0 = (i0 - OW5) & 63; p64 = true; }
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const int col = col0 + jj;
+            sw[row + (p64 ? P64inv(col) : p32 ? P32inv(col) : col)] = v[jj];
+        }
+    }
+}
+
 // Density net on one column block: returns h (rows 4g+r of sample s) and
 // the four relu'd hidden tiles.
 __device__ __forceinline__ h4 density_net(h8 e, const _Float16* sw, int s, int g, h4 h1[4]) {
@@ -255,12 +287,9 @@ __global__ void __launch_bounds__(256) field_fwd_kernel(const float* __restrict_
                                                         int64_t enc_stride = 0,
                                                         const int32_t* __restrict__ sidx = nullptr) {
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
-    __shared__ __attribute__((aligned(16))) _Float16 raw[NGP_MLP_PARAMS];
     __shared__ LevelLds lv;
-    stage_raw_weights(mlp, raw);
+    load_fwd_weights_direct(mlp, sw, COLOR);
     if constexpr (!ENC_IN) load_levels(ga, lv);
-    __syncthreads();
-    load_fwd_weights(raw, sw, COLOR);
     __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
@@ -493,6 +522,14 @@ __device__ __forceinline__ float pow2_scale(float maxabs) {
     e = min(max(14 - e, -100), 100);
     return ldexpf(1.0f, e);
 }
+// the same scale and its exact reciprocal (both powers of two: no division)
+__device__ __forceinline__ void pow2_scales(float maxabs, float& sc, float& is) {
+    int e;
+    frexpf(maxabs, &e);
+    e = min(max(14 - e, -100), 100);
+    sc = ldexpf(1.0f, e);
+    is = ldexpf(1.0f, -e);
+}
 __device__ __forceinline__ h4 scaled_h(f4 v, float sc) {
     return h4{(_Float16)(v[0] * sc), (_Float16)(v[1] * sc), (_Float16)(v[2] * sc), (_Float16)(v[3] * sc)};
 }
@@ -551,6 +588,9 @@ __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& 
     ow = OW1; in_dim = 32; o0 = 16 * (k >> 1); i0 = 16 * (k & 1);
 }
 
+// MODE (diagnostics only, scripts/diag/mlp_split.py): bit 0 skips the weight
+// gradients, bit 1 the block reduction
+template <int MODE>
 __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
     const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
     const _Float16* __restrict__ enc,
@@ -683,6 +723,7 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
         // ---- weight gradients dW = sum_s G[o][s] H[i][s]: bf16 operands (true,
         // unscaled gradients), transposed through LDS, K = 16 samples,
         // accumulated in the MFMA C operand
+        if (MODE & 1) { cur = nxt; continue; }
         wave_sync_lds();  // previous iteration's reads are done
         put_tile(scr + T_DO * TTILE, bf16x4(dout), s, g);
 #pragma unroll
@@ -734,6 +775,13 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
     // Plain LDS stores of each wave's tiles + a 4-way sum, CHK tiles at a
     // time (ds_add_f32 costs ~3 cycles per lane on gfx950: 160 per thread
     // were ~50 us per launch).
+    if (MODE & 2) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < NACC; ++k) t += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+        if (t == 1234.5f) grad_mlp[threadIdx.x] = t;
+        return;
+    }
     constexpr int CHK = 10;
     static_assert(NACC % CHK == 0 && 4 * CHK * 256 * 4 <= 4 * SCRW * 2, "reduction chunk exceeds the scratch");
     float* red = reinterpret_cast<float*>(smem + SCR);
@@ -754,6 +802,276 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
         }
     }
 }
+
+// Kernel A (product path): the same MLP backward, block-cooperative.  Eight
+// waves per block (two per SIMD -- the per-wave kernel above holds its 40
+// weight-gradient tiles in registers and runs one wave per SIMD, latency-bound
+// on its dependent MFMA / LDS chain).  Each wave back-propagates its own
+// 16-sample column block as above; the weight gradients are then summed by
+// the block: every wave puts its operand tiles into its LDS region and wave w
+// accumulates output tiles {k} over all eight regions (K = 128 samples per
+// block iteration), 5 of the 40 tiles per wave.  Operands go through LDS in
+// two phases (layers 5-3: 19 tiles, then layers 2-1: 11 tiles) so eight
+// regions fit beside the weight images.  Gradient operands of the data
+// chain are scaled per SAMPLE (column of the B operand; the four lanes of a
+// sample exchange their maxima with v_permlane16/32_swap) by a power of two
+// before the fp16 cast and unscaled exactly in fp32.
+constexpr int CW = 8, NT1 = 19, NT2 = 11, CSCRW = NT1 * TTILE;
+constexpr int COOP_LDS_HALFS = SCR + CW * CSCRW;
+static_assert(NGP_MLP_PARAMS <= CW * CSCRW && NT2 <= NT1, "raw weight staging / phase-2 tiles exceed the scratch");
+static_assert(COOP_LDS_HALFS * 2 <= 160 * 1024, "cooperative MLP backward exceeds the LDS");
+// phase-1 / phase-2 tile ids inside a wave's region
+constexpr int P_DO = 0, P_DA4 = 1, P_DA3 = 5, P_H4 = 9, P_H3 = 13, P_C = 17;
+constexpr int Q_DH = 0, Q_DA1 = 1, Q_H1 = 5, Q_E = 9;
+
+// max over the four lanes of one sample (lanes s, s+16, s+32, s+48)
+__device__ __forceinline__ float sample_max(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+
+// output tile k (acc_tile_info order) -> operand tile ids (G, H) in its phase's region
+__device__ __forceinline__ void coop_tile_ops(int k, int& gid, int& hid) {
+    if (k < 4) { gid = P_DO; hid = P_H4 + k; return; }
+    if (k < 20) { gid = P_DA4 + ((k - 4) >> 2); hid = P_H3 + ((k - 4) & 3); return; }
+    if (k < 28) { gid = P_DA3 + ((k - 20) >> 1); hid = P_C + ((k - 20) & 1); return; }
+    if (k < 32) { gid = Q_DH; hid = Q_H1 + (k - 28); return; }
+    gid = Q_DA1 + ((k - 32) >> 1);
+    hid = Q_E + ((k - 32) & 1);
+}
+
+// phase 1: waves 0-3 own tiles 4w..4w+3, waves 4-7 own 16+3(w-4)..+2;
+// phase 2: waves 0-3 own 28+w, waves 4-7 own 32+2(w-4), +1
+__device__ __forceinline__ int coop_k1(int w, int t) { return w < 4 ? 4 * w + t : 16 + 3 * (w - 4) + t; }
+__device__ __forceinline__ int coop_n1(int w) { return w < 4 ? 4 : 3; }
+__device__ __forceinline__ int coop_k2(int w, int t) { return w < 4 ? 28 + w : 32 + 2 * (w - 4) + t; }
+__device__ __forceinline__ int coop_n2(int w) { return w < 4 ? 1 : 2; }
+
+// v_mfma_f32_16x16x32_bf16 over two source regions at a time: the K order
+// (lane group g, element j) <- sample 4g + (j & 3) of region src + (j >> 2) is
+// the same for the A and the B operand, so the sum over K is the sum over the
+// 32 samples
+typedef short s8v __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f4 mfma32bf(h4 a0, h4 a1, h4 b0, h4 b1, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(__bf16 __attribute__((ext_vector_type(8))), pack(a0, a1)),
+                                                  __builtin_bit_cast(__bf16 __attribute__((ext_vector_type(8))), pack(b0, b1)),
+                                                  c, 0, 0, 0);
+}
+
+template <int NTL>
+__device__ __forceinline__ void coop_dw(const _Float16* scr, int w, int s, int g, int n, int (*kf)(int, int), f4* acc) {
+    int gid[NTL], hid[NTL];
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) coop_tile_ops(kf(w, t < n ? t : 0), gid[t], hid[t]);
+#pragma unroll 2
+    for (int src = 0; src < CW; src += 2) {
+        const _Float16* R0 = scr + src * CSCRW;
+        const _Float16* R1 = R0 + CSCRW;
+        h4 G0 = get_tile(R0 + gid[0] * TTILE, s, g), G1 = get_tile(R1 + gid[0] * TTILE, s, g);
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) {
+            if (t >= n) break;
+            if (t > 0 && gid[t] != gid[t - 1]) {
+                G0 = get_tile(R0 + gid[t] * TTILE, s, g);
+                G1 = get_tile(R1 + gid[t] * TTILE, s, g);
+            }
+            acc[t] = mfma32bf(G0, G1, get_tile(R0 + hid[t] * TTILE, s, g), get_tile(R1 + hid[t] * TTILE, s, g), acc[t]);
+        }
+    }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
+    const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
+    const _Float16* __restrict__ enc, const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig,
+    const float* __restrict__ dL_drgb, float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride) {
+    extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+    _Float16* sw = smem;
+    _Float16* scr = smem + SCR;
+    stage_raw_weights(mlp, scr);  // (the scratch is free until the loop)
+    __syncthreads();
+    load_fwd_weights(scr, sw, true);
+    load_bwd_weights(scr, sw);
+    __syncthreads();
+    const int64_t N = n_dev ? *n_dev : n;
+    const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    _Float16* mine = scr + wid * CSCRW;
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    f4 acc1[4] = {z, z, z, z}, acc2[2] = {z, z};
+    struct In {
+        h8 e;
+        float dx, dy, dz, dsig, gr[3];
+    };
+    auto load_in = [&](int64_t b, In& x) {
+        const int64_t jj = b + s;
+        x.e = h8{0, 0, 0, 0, 0, 0, 0, 0};
+        x.dx = 0.f; x.dy = 0.f; x.dz = 1.f; x.dsig = 0.f; x.gr[0] = x.gr[1] = x.gr[2] = 0.f;
+        if (jj < N) {
+            const int64_t ii = sidx ? (int64_t)sidx[jj] : jj;
+            if (enc_pm_stride > 0)  // pair-major (ngp_hash_encode): pairs 2g, 2g+1
+                x.e = pack(*reinterpret_cast<const h4*>(enc + ((2 * g) * enc_pm_stride + ii) * 4),
+                           *reinterpret_cast<const h4*>(enc + ((2 * g + 1) * enc_pm_stride + ii) * 4));
+            else
+                x.e = *reinterpret_cast<const h8*>(enc + ii * 32 + 8 * g);
+            x.dx = dirs[3 * ii]; x.dy = dirs[3 * ii + 1]; x.dz = dirs[3 * ii + 2];
+            x.dsig = dL_dsig[ii];
+            x.gr[0] = dL_drgb[3 * ii]; x.gr[1] = dL_drgb[3 * ii + 1]; x.gr[2] = dL_drgb[3 * ii + 2];
+        }
+    };
+    const int64_t stride = (int64_t)gridDim.x * CW * 16;
+    In cur;
+    load_in((int64_t)blockIdx.x * CW * 16 + 16 * wid, cur);
+    // block-uniform trip count: every wave reaches every barrier
+    for (int64_t bb = (int64_t)blockIdx.x * CW * 16; bb < N; bb += stride) {
+        const int64_t base = bb + 16 * wid;
+        In nxt;
+        load_in(base + stride, nxt);
+        const int64_t j = base + s;
+        const bool valid = j < N;
+        const h8 e = cur.e;
+        // ---- forward recompute
+        h4 h1[4];
+        const h4 hh = density_net(e, sw, s, g, h1);
+        float sh[4];
+        sh4_select(cur.dx, cur.dy, cur.dz, g, sh);
+        const h4 shh = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3]};
+        h4 h3[4], h4v[4];
+        const h4 o = color_net(pack(shh, hh), sw, s, g, h3, h4v);
+        // ---- output layer: sigmoid backward on rows 0..2
+        f4 dout = z;
+        if (g == 0) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const float y = 1.0f / (1.0f + expf(-(float)o[r]));
+                dout[r] = cur.gr[r] * (y * (1.0f - y));
+            }
+        }
+        float sc_o, is_o;
+        pow2_scales(sample_max(max4(dout)), sc_o, is_o);
+        const h4 do_h = scaled_h(dout, sc_o);
+        // ---- dh4 = W5^T do
+        f4 da4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da4[t] = mask_relu(mfma16(lds4(sw + BT5 + (16 * t + s) * RT16 + 4 * g), do_h, z) * is_o, h4v[t]);
+        float m = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da4[t]));
+        float sc_4, is_4;
+        pow2_scales(sample_max(m), sc_4, is_4);
+        h4 da4h[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da4h[t] = scaled_h(da4[t], sc_4);
+        // ---- dh3 = W4^T da4
+        f4 da3[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            f4 c = z;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT4 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da4h[kt], c);
+            da3[t] = mask_relu(c * is_4, h3[t]);
+        }
+        m = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da3[t]));
+        float sc_3, is_3;
+        pow2_scales(sample_max(m), sc_3, is_3);
+        h4 da3h[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da3h[t] = scaled_h(da3[t], sc_3);
+        // ---- d h (colour-net input, h part) = W3h^T da3, + TruncExp backward
+        f4 dh = z;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) dh = mfma16(lds4(sw + BT3 + s * RT64 + 16 * kt + 4 * g), da3h[kt], dh);
+        dh = dh * is_3;
+        if (g == 0) dh[0] += cur.dsig * expf(fminf(fmaxf((float)hh[0], -15.f), 15.f));  // custom_functions.py:169-173
+        float sc_h, is_h;
+        pow2_scales(sample_max(max4(dh)), sc_h, is_h);
+        const h4 dhh = scaled_h(dh, sc_h);
+        // ---- dh1 = W2^T dh
+        f4 da1[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da1[t] = mask_relu(mfma16(lds4(sw + BT2 + (16 * t + s) * RT16 + 4 * g), dhh, z) * is_h, h1[t]);
+        m = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da1[t]));
+        float sc_1, is_1;
+        pow2_scales(sample_max(m), sc_1, is_1);
+        h4 da1h[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) da1h[t] = scaled_h(da1[t], sc_1);
+        // ---- dL/denc = W1^T da1 (rows 16t + 4g + r of sample s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            f4 c = z;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT1 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da1h[kt], c);
+            c = c * is_1;
+            if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
+        }
+        cur = nxt;
+        if (MODE & 1) continue;
+        // ---- weight gradients, phase 1 (layers 5, 4, 3): bf16 operand tiles
+        __syncthreads();  // every wave's phase-2 reads of the previous iteration are done
+        put_tile(mine + P_DO * TTILE, bf16x4(dout), s, g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            put_tile(mine + (P_DA4 + t) * TTILE, bf16x4(da4[t]), s, g);
+            put_tile(mine + (P_DA3 + t) * TTILE, bf16x4(da3[t]), s, g);
+            put_tile(mine + (P_H4 + t) * TTILE, bf16x4(h4v[t]), s, g);
+            put_tile(mine + (P_H3 + t) * TTILE, bf16x4(h3[t]), s, g);
+        }
+        put_tile(mine + P_C * TTILE, bf16x4(shh), s, g);
+        put_tile(mine + (P_C + 1) * TTILE, bf16x4(hh), s, g);
+        __syncthreads();
+        coop_dw<4>(scr, wid, s, g, coop_n1(wid), coop_k1, acc1);
+        __syncthreads();  // phase-1 reads done: the regions take the phase-2 tiles
+        // ---- phase 2 (layers 2, 1)
+        put_tile(mine + Q_DH * TTILE, bf16x4(dh), s, g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            put_tile(mine + (Q_DA1 + t) * TTILE, bf16x4(da1[t]), s, g);
+            put_tile(mine + (Q_H1 + t) * TTILE, bf16x4(h1[t]), s, g);
+        }
+        {   // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
+            const h4 e0 = bf16x4(h4{e[0], e[1], e[2], e[3]}), e1 = bf16x4(h4{e[4], e[5], e[6], e[7]});
+            *reinterpret_cast<h8*>(mine + (Q_E + (g >> 1)) * TTILE + s * TROW + 8 * (g & 1)) = pack(e0, e1);
+        }
+        __syncthreads();
+        coop_dw<2>(scr, wid, s, g, coop_n2(wid), coop_k2, acc2);
+    }
+    if (MODE & 2) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t += acc1[k][0] + acc1[k][1] + acc1[k][2] + acc1[k][3];
+        t += acc2[0][0] + acc2[1][0];
+        if (t == 1234.5f) grad_mlp[threadIdx.x] = t;
+        return;
+    }
+    // each output tile lives in exactly one wave of the block: one global add
+    // per weight.  Wave w of every block owns the same tiles, so the adds of a
+    // lane start at a block-dependent rotation (same-address adds serialise at
+    // the memory-side atomic unit: 12 -> 7 us per launch; per-block partial
+    // rows + a reduction launch measured slower).
+    const int n1 = coop_n1(wid), nadd = 4 * (n1 + coop_n2(wid));
+    const int rot = (int)(blockIdx.x % (unsigned)nadd);
+#pragma unroll 1
+    for (int q0 = 0; q0 < nadd; ++q0) {
+        const int q = (q0 + rot) % nadd, t = q >> 2, r = q & 3;
+        const int t2 = t - n1;  // tiles t < n1: phase 1, else phase 2
+        const f4 a = t2 >= 0 ? (t2 == 0 ? acc2[0] : acc2[1])
+                             : (t == 0 ? acc1[0] : t == 1 ? acc1[1] : t == 2 ? acc1[2] : acc1[3]);
+        const float v = r == 0 ? a[0] : r == 1 ? a[1] : r == 2 ? a[2] : a[3];
+        const int k = t2 < 0 ? coop_k1(wid, t) : coop_k2(wid, t2);
+        int ow, in_dim, o0, i0;
+        acc_tile_info(k, ow, in_dim, o0, i0);
+        const int w = ow + (o0 + 4 * g + r) * in_dim + i0 + s;
+        atomicAdd(&grad_mlp[w], v);
+    }
+}
+
 
 // Kernel B: hash-table gradient scatter, dL/dtable[e][f] += w_c * dL/denc[2l+f].
 // Lane map: 16 consecutive samples per wave, 4 lanes per sample:
@@ -977,26 +1295,58 @@ int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, cons
 }
 
 int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
-                           const void* enc_f16, int64_t enc_pm_stride,
-                           const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws,
-                           float* grad_mlp, void* stream) {
+                           const void* enc_f16, int64_t enc_pm_stride, const void* mlp_f16, const float* dL_dsigmas,
+                           const float* dL_drgbs, float* denc_ws, float* grad_mlp, void* stream) {
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(dirs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp);
     NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
     static bool attr_set = false;
-    const size_t lds = (size_t)BWD_LDS_HALFS * sizeof(_Float16);
+    const size_t lds = (size_t)BWD_LDS_HALFS * sizeof(_Float16), clds = (size_t)COOP_LDS_HALFS * sizeof(_Float16);
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)field_bwd_mlp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds) != hipSuccess)
-            return NGP_ERANGE;
+        for (const void* k : {(const void*)field_bwd_mlp_kernel<0>, (const void*)field_bwd_mlp_kernel<1>,
+                              (const void*)field_bwd_mlp_kernel<2>, (const void*)field_bwd_mlp_kernel<3>})
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return NGP_ERANGE;
+        for (const void* k : {(const void*)field_bwd_mlp_coop_kernel<0>, (const void*)field_bwd_mlp_coop_kernel<1>,
+                              (const void*)field_bwd_mlp_coop_kernel<2>, (const void*)field_bwd_mlp_coop_kernel<3>})
+            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds) != hipSuccess)
+                return NGP_ERANGE;
         attr_set = true;
     }
-    NGP_TIMED(NGP_K_MLP_BWD, as_stream(stream), field_bwd_mlp_kernel<<<persistent_blocks(n, 64, 256), 256, lds, as_stream(stream)>>>(
-        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
-        grad_mlp, enc_pm_stride));
+    // diagnostics (scripts/diag/mlp_split.py): NGP_MLP_BWD_DIAG = mode bits,
+    // NGP_MLP_BWD_WAVE=1 the per-wave kernel
+    const char* dm = getenv("NGP_MLP_BWD_DIAG");
+    const int mode = dm ? atoi(dm) & 3 : 0;
+    const char* pw = getenv("NGP_MLP_BWD_WAVE");
+    hipStream_t s = as_stream(stream);
+    if (pw && pw[0] == '1') {
+        const unsigned nb = persistent_blocks(n, 64, 256);
+#define NGP_MLPB(M)                                                                                                   \
+    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_kernel<M><<<nb, 256, lds, s>>>(                                         \
+        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, \
+        grad_mlp, enc_pm_stride))
+        if (mode == 1) NGP_MLPB(1);
+        else if (mode == 2) NGP_MLPB(2);
+        else if (mode == 3) NGP_MLPB(3);
+        else NGP_MLPB(0);
+#undef NGP_MLPB
+        return ngp_launch_status();
+    }
+    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel<0>, 512, clds);
+    const unsigned cb = persistent_blocks(n, CW * 16, ccap);
+#define NGP_MLPB(M)                                                                                                   \
+    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<M><<<cb, 512, clds, s>>>(                                   \
+        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, \
+        grad_mlp, enc_pm_stride))
+    if (mode == 1) NGP_MLPB(1);
+    else if (mode == 2) NGP_MLPB(2);
+    else if (mode == 3) NGP_MLPB(3);
+    else NGP_MLPB(0);
+#undef NGP_MLPB
     return ngp_launch_status();
 }
+
 
 int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                       const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* stream) {
