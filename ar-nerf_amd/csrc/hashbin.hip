@@ -573,8 +573,9 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
     NGP_CHECK_ARG(n >= 0 && max_samples > 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && workspace && ((uintptr_t)workspace & 255) == 0);
-    if (phase & 2)
-        NGP_CHECK_ARG(denc && grad_table && ((uintptr_t)denc & 7) == 0 && ((uintptr_t)grad_table & 15) == 0);
+    if (phase & 6)
+        NGP_CHECK_ARG(grad_table && ((uintptr_t)grad_table & 15) == 0);
+    if (phase & 2) NGP_CHECK_ARG(denc && ((uintptr_t)denc & 7) == 0);
     const int64_t tiles_cap = (max_samples + TILE - 1) / TILE;
     // record slots are uint32-indexed
     NGP_CHECK_ARG(tiles_cap * TILE * 4 * L < (int64_t)0xffffffffLL);
@@ -595,6 +596,8 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
         static const unsigned capW = resident_blocks(hash_write_kernel<2>, 256, 0);
         NGP_TIMED(NGP_K_HASH_WRITE, s, hash_write_kernel<2><<<persistent_blocks(n, TILE, capW), 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, ba,
                                                                            denc, grad_table, ws));
+    }
+    if (phase & 4) {
         static bool attr = false;
         const size_t lds = (size_t)BENT * 2 * sizeof(double);
         if (!attr) {
@@ -613,7 +616,7 @@ int ngp_hash_backward_binned(const float* xyzs, int64_t n, const int64_t* n_dev,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
                              int64_t max_samples, int level_lo, int merge_hi, void* stream) {
     return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo,
-                       merge_hi, 3, stream);
+                       merge_hi, 7, stream);
 }
 
 int ngp_hash_binned_plan(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
@@ -627,7 +630,22 @@ int ngp_hash_binned_apply(const float* xyzs, int64_t n, const int64_t* n_dev, co
                           const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
                           int64_t max_samples, int level_lo, int merge_hi, void* stream) {
     return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo,
+                       merge_hi, 6, stream);
+}
+
+int ngp_hash_binned_write(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                          const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                          int64_t max_samples, int level_lo, int merge_hi, void* stream) {
+    return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo,
                        merge_hi, 2, stream);
+}
+
+int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
+                          int level_lo, int merge_hi, void* stream) {
+    // (xyzs / n only gate the argument checks here; the accumulation reads the workspace)
+    static const float dummy[1] = {0.f};
+    return hash_binned(dummy, 1, nullptr, nullptr, grid, nullptr, grad_table, workspace, max_samples, level_lo,
+                       merge_hi, 4, stream);
 }
 
 }  // extern "C"

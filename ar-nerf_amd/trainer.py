@@ -148,6 +148,10 @@ class NGPTrainer:
         # NGP_ADAM_SPLIT=1: Adam of the MLP + coarse levels beside the binned
         # levels (measured slower: it takes HBM bandwidth from the apply)
         self.adam_split = os.environ.get("NGP_ADAM_SPLIT", "0") == "1"
+        # NGP_COARSE_AFTER_WRITE=1: the coarse atomic levels start after the binned record write
+        # (measured slower: the accumulation then slows as much as the write speeds up,
+        # profiles/r02/ab/coarse_overlap.txt)
+        self.coarse_after_write = os.environ.get("NGP_COARSE_AFTER_WRITE", "0") == "1"
         self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "1") == "1"
         self.enc = torch.empty(8 * cap * 4, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
@@ -758,11 +762,29 @@ class NGPTrainer:
                 if adam_split:
                     self._adam(split, self.params.numel(), vren._stream())
 
-            bs.wait_stream(cs)
-            with torch.cuda.stream(bs):
-                coarse()
-            cs.wait_event(planned)
-            apply()
+            if self.coarse_after_write:
+                # coarse atomics beside the accumulation only (the record write
+                # runs alone: it slowed ~4x beside the memory-side atomics)
+                cs.wait_event(planned)
+                self._ev("hash_binned_apply", 0)
+                args = (HG.ctypes.byref(self.grid.desc), _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws),
+                        self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi)
+                vren._ok(HGL.ngp_hash_binned_write(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                   _p(self.sample_idx), args[0], _p(self.denc), *args[1:],
+                                                   vren._stream()), "hash_binned_write")
+                bs.wait_stream(cs)
+                with torch.cuda.stream(bs):
+                    coarse()
+                vren._ok(HGL.ngp_hash_binned_accum(*args, vren._stream()), "hash_binned_accum")
+                self._ev("hash_binned_apply", 1)
+                if adam_split:
+                    self._adam(split, self.params.numel(), vren._stream())
+            else:
+                bs.wait_stream(cs)
+                with torch.cuda.stream(bs):
+                    coarse()
+                cs.wait_event(planned)
+                apply()
             cs.wait_stream(bs)
             if adam_split:
                 self._ev("hash_bwd", 1)

@@ -378,6 +378,15 @@ int ngp_hash_binned_plan(const float* xyzs, int64_t n, const int64_t* n_dev, con
 int ngp_hash_binned_apply(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                           const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
                           int64_t max_samples, int level_lo, int merge_hi, void* stream);
+/* The two launches of ngp_hash_binned_apply separately (write the records,
+ * then sum them per bucket into grad_table), so a caller can order other
+ * work between them (the trainer runs the coarse levels' atomic scatter
+ * beside the accumulation instead of beside the record write). */
+int ngp_hash_binned_write(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                          const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                          int64_t max_samples, int level_lo, int merge_hi, void* stream);
+int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
+                          int level_lo, int merge_hi, void* stream);
 /* ngp_hash_backward restricted to levels [level_lo, level_hi). */
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
