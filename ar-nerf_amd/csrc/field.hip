@@ -375,8 +375,11 @@ __device__ __forceinline__ uint32_t reduce_idx(uint32_t idx, const LevelU& u) {
     return idx % u.size;
 }
 
-__device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& u, const uint32_t* __restrict__ table,
-                                               float& a0, float& a1) {
+// encode_level_u in two halves, so a caller can issue the gathers of several
+// levels before it consumes any: corner weights + the level's loads, then the
+// fp32 corner sum (the same fmaf order)
+__device__ __forceinline__ void gather_level_u(const float in[3], const LevelU& u, const uint32_t* __restrict__ table,
+                                               float w[8], uint32_t v[8]) {
     float pos[3];
     uint32_t pg[3];
 #pragma unroll
@@ -386,7 +389,6 @@ __device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& 
         pg[d] = (uint32_t)(int)fl;
         pos[d] = p - fl;
     }
-    float w[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
         float wt = 1.0f;
@@ -410,10 +412,12 @@ __device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& 
         i0[yz] = reduce_idx(r0, u);
         i1[yz] = reduce_idx(r1, u);
     }
-    uint32_t v[8];
     const uint32_t* tl = table + u.off;
 #pragma unroll
     for (int yz = 0; yz < 4; ++yz) fetch_pair(tl, i0[yz], i1[yz], u.dense || !u.pow2, v[2 * yz], v[2 * yz + 1]);
+}
+
+__device__ __forceinline__ void sum_level(const float w[8], const uint32_t v[8], float& a0, float& a1) {
     a0 = 0.f;
     a1 = 0.f;
 #pragma unroll
@@ -425,6 +429,14 @@ __device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& 
     }
 }
 
+__device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& u, const uint32_t* __restrict__ table,
+                                               float& a0, float& a1) {
+    float w[8];
+    uint32_t v[8];
+    gather_level_u(in, u, table, w, v);
+    sum_level(w, v, a0, a1);
+}
+
 // ALL = true (the product path): each lane encodes every level of one
 // sample, so a wave instruction gathers ONE level for 64 consecutive samples
 // (a ray's neighbours: shared lines on the coarse levels) -- measured 1.55x
@@ -432,7 +444,7 @@ __device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& 
 // NGP_ENCODE_XCD=1) and 1.8x the fused kernel's lane (sample, level group)
 // layout (scripts/diag/encode_split.py).  sidx (nullable): rows j < N encode
 // sample sidx[j] (rows of enc_pm are samples).
-template <bool ALL>
+template <bool ALL, int PGT = 1>
 __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restrict__ xyzs, int64_t n,
                                                           const int64_t* __restrict__ n_dev,
                                                           const int32_t* __restrict__ sidx, GridArgs ga,
@@ -449,14 +461,24 @@ __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restric
         const int64_t i = sidx ? (int64_t)sidx[j] : j;
         float in[3];
         load_x01(xyzs, i, true, ga, in);
+        // PG level pairs per iteration, their gathers issued together: a lane
+        // encodes about one sample per launch (the grid covers the batch), so
+        // the launch time is the lane's chain of dependent gather rounds
+        constexpr int PG = ALL ? PGT : 1;
 #pragma unroll 1
-        for (int pr = p0; pr < (ALL ? 8 : p0 + 1); ++pr) {
-            const LevelU u0 = level_u(lv, 2 * pr), u1 = level_u(lv, 2 * pr + 1);
-            float a0, a1, b0, b1;
-            encode_level_u(in, u0, table, a0, a1);
-            encode_level_u(in, u1, table, b0, b1);
-            *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) =
-                h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
+        for (int pr0 = p0; pr0 < (ALL ? 8 : p0 + 1); pr0 += PG) {
+            float w[2 * PG][8];
+            uint32_t v[2 * PG][8];
+#pragma unroll
+            for (int q = 0; q < 2 * PG; ++q) gather_level_u(in, level_u(lv, 2 * pr0 + q), table, w[q], v[q]);
+#pragma unroll
+            for (int q = 0; q < PG; ++q) {
+                float a0, a1, b0, b1;
+                sum_level(w[2 * q], v[2 * q], a0, a1);
+                sum_level(w[2 * q + 1], v[2 * q + 1], b0, b1);
+                *reinterpret_cast<h4*>(enc_pm + ((int64_t)(pr0 + q) * n + i) * 4) =
+                    h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
+            }
         }
     }
 }
@@ -1256,10 +1278,22 @@ int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const in
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0);  // 16-byte group gathers
     static const bool xcd = getenv("NGP_ENCODE_XCD") && getenv("NGP_ENCODE_XCD")[0] == '1';  // diagnostic
     if (!xcd) {
-        static const unsigned cap = resident_blocks(hash_encode_kernel<true>, 256, 0);
-        NGP_TIMED(NGP_K_HASH_ENCODE, as_stream(stream), hash_encode_kernel<true><<<std::max(1u, std::min(cap, (unsigned)((n + 255) / 256))), 256, 0,
-                                   as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16,
-                                                        (_Float16*)enc_pm));
+        // level pairs per gather round (diagnostic NGP_ENCODE_PG = 2, 4: more
+        // gathers in flight per lane at fewer waves per SIMD -- measured no
+        // faster (2) and 1.4x slower (4): the encode is bound by the L2/MALL
+        // request rate, not by a lane's chain of gather rounds)
+        static const int pg = getenv("NGP_ENCODE_PG") ? atoi(getenv("NGP_ENCODE_PG")) : 1;
+        hipStream_t s = as_stream(stream);
+#define NGP_ENC(PGV)                                                                                                   \
+    do {                                                                                                               \
+        static const unsigned cap = resident_blocks(hash_encode_kernel<true, PGV>, 256, 0);                            \
+        NGP_TIMED(NGP_K_HASH_ENCODE, s, hash_encode_kernel<true, PGV><<<std::max(1u, std::min(cap, (unsigned)((n + 255) / 256))), 256, 0, s>>>( \
+            xyzs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (_Float16*)enc_pm));                           \
+    } while (0)
+        if (pg == 1) NGP_ENC(1);
+        else if (pg == 4) NGP_ENC(4);
+        else NGP_ENC(2);
+#undef NGP_ENC
         return ngp_launch_status();
     }
     static const unsigned cap = resident_blocks(hash_encode_kernel<false>, 256, 0);

@@ -847,14 +847,14 @@ __global__ void __launch_bounds__(256) chunk_first_kernel(const int64_t* __restr
     counts[r] = (int32_t)min(rays_a[3 * r + 2], (int64_t)first);
 }
 
-// Round-2 counts: one wave per row computes the transmittance of its first
-// min(N_r, first) samples exactly as composite_loss_ray's forward does (same
-// expressions, chunk_transmittance); a row that has not terminated there and
-// has more samples needs N_r - first more.
+// Later-round counts: one wave per row computes the transmittance of its
+// first min(N_r, first) samples exactly as composite_loss_ray's forward does
+// (same expressions, chunk_transmittance); a row that has not terminated there
+// and has more samples needs min(N_r, last) - first more (last <= 0: N_r).
 __global__ void __launch_bounds__(256) chunk_rest_kernel(const float* __restrict__ sigmas,
                                                          const float* __restrict__ deltas,
                                                          const int64_t* __restrict__ rays_a, int64_t n_rows, int first,
-                                                         float T_thr, int32_t* __restrict__ counts) {
+                                                         int last, float T_thr, int32_t* __restrict__ counts) {
     const int64_t n = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (n >= n_rows) return;
     const int lane = threadIdx.x & 63;
@@ -871,7 +871,8 @@ __global__ void __launch_bounds__(256) chunk_rest_kernel(const float* __restrict
         done = ct.hit;
         T = __shfl(ct.Tn, ct.stop - 1, 64);
     }
-    if (lane == 0) counts[n] = (!done && N > first) ? (int32_t)(N - first) : 0;
+    const int64_t end = last > 0 ? min(N, (int64_t)last) : N;
+    if (lane == 0) counts[n] = (!done && N > first) ? (int32_t)(end - first) : 0;
 }
 
 }  // namespace ngp
@@ -903,7 +904,12 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
 
 int ngp_chunk_counts(const int64_t* rays_a, int64_t n_rows, int first, const float* sigmas, const float* deltas,
                      float T_threshold, int32_t* counts, void* stream) {
-    NGP_CHECK_ARG(n_rows >= 0 && first >= 1 && counts && rays_a);
+    return ngp_chunk_counts_range(rays_a, n_rows, first, 0, sigmas, deltas, T_threshold, counts, stream);
+}
+
+int ngp_chunk_counts_range(const int64_t* rays_a, int64_t n_rows, int first, int last, const float* sigmas,
+                           const float* deltas, float T_threshold, int32_t* counts, void* stream) {
+    NGP_CHECK_ARG(n_rows >= 0 && first >= 1 && counts && rays_a && (last <= 0 || last > first));
     if (n_rows == 0) return NGP_OK;
     if (!sigmas) {
         NGP_TIMED(NGP_K_CHUNK, as_stream(stream), chunk_first_kernel<<<(unsigned)((n_rows + 255) / 256), 256, 0, as_stream(stream)>>>(rays_a, n_rows, first,
@@ -911,7 +917,7 @@ int ngp_chunk_counts(const int64_t* rays_a, int64_t n_rows, int first, const flo
     } else {
         NGP_CHECK_ARG(deltas != nullptr);
         NGP_TIMED(NGP_K_CHUNK, as_stream(stream), chunk_rest_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, as_stream(stream)>>>(sigmas, deltas, rays_a, n_rows,
-                                                                                      first, T_threshold, counts));
+                                                                                      first, last, T_threshold, counts));
     }
     return ngp_launch_status();
 }

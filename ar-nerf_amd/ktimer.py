@@ -24,7 +24,7 @@ NAMES = ["sample_batch", "bitfield_summary", "march", "scan_rays", "march_compac
          "field_mlp", "chunk_rest", "composite_loss", "hash_count", "hash_scan", "hash_plan", "mlp_bwd",
          "hash_bwd_coarse", "hash_write", "hash_accum", "adam"]  # include/ngp_amd.h NGP_K_* order
 _UID = itertools.count(1)
-PER_ID = 4  # launches per kernel id per step (segments runs 3x, encode / MLP 2x, +1 in occupancy updates)
+PER_ID = 8  # launches per kernel id per step (segments: one per evaluation round + 1, encode / MLP: one per round, +1 in occupancy updates)
 
 
 def _lib():
@@ -87,6 +87,29 @@ class KernelTimer:
         b = st[:, NAMES.index(self.span[1]), 0, 1]
         ok = (a > 0) & (b >= a)
         return ((b - a)[ok].double() * self.tick_ns * 1e-6).tolist()
+
+    def timeline(self):
+        """{"kernel#slot": (avg start us, avg end us)} relative to the first
+        stamp of each step row -- the in-step schedule of every launch (all
+        streams), over the rows where that launch was stamped"""
+        st = self.stamps.cpu().view(self.rows, len(NAMES), PER_ID, 2).to(torch.int64)
+        valid = (st > 0).view(self.rows, -1)
+        rows = valid.any(1)
+        st, valid = st[rows], valid[rows]
+        if st.shape[0] == 0:
+            return {}
+        big = torch.iinfo(torch.int64).max
+        t0 = torch.where(valid, st.view(st.shape[0], -1), torch.full_like(st.view(st.shape[0], -1), big)).min(1).values
+        out = {}
+        for k, n in enumerate(NAMES):
+            for i in range(PER_ID):
+                a, b = st[:, k, i, 0], st[:, k, i, 1]
+                ok = (a > 0) & (b >= a)
+                if ok.any():
+                    sa = ((a - t0)[ok].double() * self.tick_ns * 1e-3).mean().item()
+                    sb = ((b - t0)[ok].double() * self.tick_ns * 1e-3).mean().item()
+                    out[f"{n}#{i}"] = (round(sa, 1), round(sb, 1))
+        return dict(sorted(out.items(), key=lambda kv: kv[1][0]))
 
     def steps(self):
         st = self.stamps.view(self.rows, -1)

@@ -166,6 +166,10 @@ class NGPTrainer:
         # chunked field evaluation (ngp_chunk_counts): first `chunk_first` samples of
         # every row, then the rest of the rows not yet terminated (0 = every sample)
         self.chunk_first = int(os.environ.get("NGP_CHUNK_FIRST", chunk_first))
+        # further round bounds after chunk_first (NGP_CHUNK_ROUNDS="128" -> rounds [0,64) [64,128) [128,N)):
+        # 22 % fewer evaluated samples, but each extra round's encode launch costs more than it saves
+        # (profiles/r02/ab/chunk_rounds.txt)
+        self.chunk_rounds = [int(x) for x in os.environ.get("NGP_CHUNK_ROUNDS", "").split(",") if x.strip()]
         self.eval_counts = torch.empty(R, dtype=torch.int32, device=dev)
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -674,11 +678,16 @@ class NGPTrainer:
                 vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, 0, _p(self.act_start),
                                             _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
             self._field_indexed(s)
-            vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, _p(self.sigmas), _p(self.deltas), ctypes_float(1e-4),
-                                        _p(self.eval_counts), s), "chunk_counts")
-            vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, K, _p(self.act_start),
-                                        _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
-            self._field_indexed(s)
+            # later rounds [c_i, c_{i+1}) of rows still transparent, the last one open-ended
+            bounds = [b for b in self.chunk_rounds if b > K] + [0]
+            lo = K
+            for hi in bounds:
+                vren._ok(L.ngp_chunk_counts_range(_p(self.rays_a), R, lo, hi, _p(self.sigmas), _p(self.deltas),
+                                                  ctypes_float(1e-4), _p(self.eval_counts), s), "chunk_counts")
+                vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, lo, _p(self.act_start),
+                                            _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
+                self._field_indexed(s)
+                lo = hi
         elif self.split_forward:  # encode (pair-major self.enc), then the MLPs, over every marched sample
             vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.n_samples), None,
                                          HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),

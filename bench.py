@@ -299,7 +299,7 @@ def main():
     torch.cuda.synchronize()
     t_bd = (time.perf_counter() - t_bd) / n_bd
     trainer.timer = None
-    bd_summary, bd_steps = full.summary(), full.steps()
+    bd_summary, bd_steps, bd_timeline = full.summary(), full.steps(), full.timeline()
     marched_bd, composited_bd, active_bd, evaluated_bd = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         evaluated_bd = marched_bd
@@ -419,11 +419,13 @@ def main():
             "roofline": roof,
             "ops": ops,
             "kernels": kernels,
+            "timeline_us": bd_timeline,
             "step_bound": step_bound,
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "breakdown_note": (f"ops / kernels: wall-clock stamps around every kernel inside the captured graphs "
-                               f"over {bd_steps} replayed steps ({t_bd * 1e3:.3f} ms/step with all stamps); roofline: "
-                               f"see roofline.measured"),
+                               f"over {bd_steps} replayed steps ({t_bd * 1e3:.3f} ms/step with all stamps); timeline_us: "
+                               f"average [start, end] of each launch (kernel#slot) from the step's first stamp, all "
+                               f"streams; roofline: see roofline.measured"),
             "cpu_baseline": cpu,
             "quality": quality,
             "inference": infer,

@@ -441,6 +441,12 @@ int ngp_active_samples(const int32_t* n_active, const int64_t* rays_a, int64_t n
  * T_threshold and N_r > first, else 0 (round 2). */
 int ngp_chunk_counts(const int64_t* rays_a, int64_t n_rows, int first, const float* sigmas,
                      const float* deltas, float T_threshold, int32_t* counts, void* stream);
+/* ngp_chunk_counts of a later round with a cap: a row still transparent after
+ * its first min(N_r, first) samples gets min(N_r, last) - first (last <= 0:
+ * N_r - first, the round-2 form above); evaluation rounds over [first, last)
+ * let rows that terminate there skip the rest of their samples. */
+int ngp_chunk_counts_range(const int64_t* rays_a, int64_t n_rows, int first, int last, const float* sigmas,
+                           const float* deltas, float T_threshold, int32_t* counts, void* stream);
 /* Sample list of per-row segments: sample_idx[start_r + k] = rays_a[r].start +
  * first + k for k < counts[r] (start = exclusive prefix of counts, in
  * start_ws (n_rows) i64); *total = the list length, *total_acc += it
