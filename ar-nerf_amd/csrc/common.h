@@ -43,6 +43,37 @@ static unsigned resident_blocks(K kernel, int threads, size_t dyn_lds) {
 
 namespace ngp {
 
+// apex FusedAdam's per-element update (ADAM_MODE_0, no weight decay;
+// train.py:146-152), shared by adam_kernel and the binned accumulation's fused
+// Adam so the two paths are bit-identical.  g = gradient x grad_scale.
+__device__ __forceinline__ void adam_bias(const float* lr_dev, const int64_t* step_dev, float b1, float b2,
+                                          float& lr, float& bc1, float& bc2) {
+    if (lr_dev) lr = *lr_dev;
+    if (step_dev) {
+        const float st = (float)(*step_dev + 1);
+        bc1 = 1.0f - powf(b1, st);
+        bc2 = 1.0f - powf(b2, st);
+    }
+}
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float lr, float b1, float b2,
+                                          float eps, float bc1, float bc2) {
+    m = b1 * m + (1 - b1) * g;
+    v = b2 * v + (1 - b2) * g * g;
+    const float denom = sqrtf(v / bc2) + eps;
+    p = p - lr * ((m / bc1) / denom);
+}
+
+// Adam state of one parameter range (same layout as the gradient it steps)
+struct AdamArgs {
+    float* p;
+    float* m;
+    float* v;
+    _Float16* p16;
+    const float* lr_dev;
+    const int64_t* step_dev;
+    float b1, b2, eps, grad_scale;
+};
+
 // helper_math.h:280-283 clamp(f,a,b) = fmaxf(a, fminf(f,b)) -- keeps the
 // NaN behaviour of fminf/fmaxf that the marcher relies on.
 __device__ __forceinline__ float clampf(float f, float a, float b) { return fmaxf(a, fminf(f, b)); }

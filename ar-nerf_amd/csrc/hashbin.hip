@@ -432,15 +432,50 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
     }
 }
 
+// A bucket whose summed gradient one workgroup owns: a single chunk, no
+// direct adds into its range, no workspace overflow.  With FUSED the
+// accumulation applies Adam to such a bucket straight from its LDS image
+// (its gradient never goes through memory) and hash_adam_residual_kernel
+// steps every other bucket from the gradient in memory.
+__device__ __forceinline__ bool fused_bucket(const BinWs& ws, uint32_t b, bool overflow) {
+    return !overflow && ws.fb[b] == 0 && ws.items[b + 1] - ws.items[b] <= 1u;
+}
+
+__device__ __forceinline__ uint32_t bucket_level(const BinArgs& ba, uint32_t b) {
+    int l = 0;
+    while (l < L - 1 && b >= ba.bbase[l + 1]) ++l;
+    return (uint32_t)l;
+}
+
+// Adam over params [4e, 4e+4) of a bucket range (entries 2e, 2e+1 x 2 features)
+// with gradient g (already x grad_scale); same arithmetic as adam_kernel.
+__device__ __forceinline__ void adam4(const AdamArgs& a, size_t base, uint32_t e, float4 g, float lr, float bc1,
+                                      float bc2) {
+    float4 P = reinterpret_cast<const float4*>(a.p + base)[e];
+    float4 M = reinterpret_cast<const float4*>(a.m + base)[e];
+    float4 V = reinterpret_cast<const float4*>(a.v + base)[e];
+    adam_elem(P.x, M.x, V.x, g.x, lr, a.b1, a.b2, a.eps, bc1, bc2);
+    adam_elem(P.y, M.y, V.y, g.y, lr, a.b1, a.b2, a.eps, bc1, bc2);
+    adam_elem(P.z, M.z, V.z, g.z, lr, a.b1, a.b2, a.eps, bc1, bc2);
+    adam_elem(P.w, M.w, V.w, g.w, lr, a.b1, a.b2, a.eps, bc1, bc2);
+    reinterpret_cast<float4*>(a.p + base)[e] = P;
+    reinterpret_cast<float4*>(a.m + base)[e] = M;
+    reinterpret_cast<float4*>(a.v + base)[e] = V;
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    reinterpret_cast<h4*>(a.p16 + base)[e] = h4{(_Float16)P.x, (_Float16)P.y, (_Float16)P.z, (_Float16)P.w};
+}
+
 // MODE != 0: diagnostic variants for scripts/diag (1: no LDS adds, 2: no
 // flush, 3: neither)
-template <int MODE>
+template <int MODE, bool FUSED = false>
 __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
-                                                          float* __restrict__ grad, BinWs ws) {
+                                                          float* __restrict__ grad, BinWs ws, AdamArgs adam) {
     extern __shared__ __attribute__((aligned(16))) double img[];  // [2][BENT]: feature-major, 8-byte stride
     const uint32_t total = ws.items[nbt];
     const int t = threadIdx.x, lane = t & 63;
     const bool overflow = ws.fb[MAXB] != 0;
+    float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
+    if (FUSED) adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
     for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
         uint32_t lo = 0, hi = nbt;  // bucket b: items[b] <= it < items[b + 1]
         while (hi - lo > 1) {
@@ -510,14 +545,18 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
             }
         }
         __syncthreads();
-        float* g = grad + 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
+        const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
+        float* g = grad + gbase;
         const bool own = nch == 1 && !overflow && ws.fb[b] == 0;
         for (uint32_t e = t; e < ((MODE & 2) ? 0u : 2 * ne / 4); e += blockDim.x) {
             // entries 2e, 2e+1 x features 0, 1 -> grad[4e .. 4e+3]
             const double2 f0 = reinterpret_cast<const double2*>(img)[e];
             const double2 f1 = reinterpret_cast<const double2*>(img + BENT)[e];
             const float4 v = make_float4((float)f0.x, (float)f1.x, (float)f0.y, (float)f1.y);
-            if (own) {  // sole writer of this range: read-add-store keeps the += contract
+            if (FUSED && own) {  // the range's whole gradient is this image (the memory copy is zero)
+                const float sc = adam.grad_scale;
+                adam4(adam, gbase, e, make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc), lr, bc1, bc2);
+            } else if (own) {  // sole writer of this range: read-add-store keeps the += contract
                 float4 o = reinterpret_cast<const float4*>(g)[e];
                 o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
                 reinterpret_cast<float4*>(g)[e] = o;
@@ -529,6 +568,36 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
             }
         }
         __syncthreads();
+    }
+    if (FUSED) {  // buckets without records: Adam with a zero gradient (moments still decay)
+        for (uint32_t b = blockIdx.x; b < nbt; b += gridDim.x) {
+            if (ws.tot[b] != 0u || !fused_bucket(ws, b, overflow)) continue;
+            const uint32_t l = bucket_level(ba, b), lb = b - ba.bbase[l];
+            const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
+            const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
+            for (uint32_t e = t; e < 2 * ne / 4; e += blockDim.x)
+                adam4(adam, gbase, e, make_float4(0.f, 0.f, 0.f, 0.f), lr, bc1, bc2);
+        }
+    }
+}
+
+// Adam (+ gradient zeroing) of the binned buckets the fused accumulation did
+// not step: one workgroup per bucket, from the gradient in memory.
+__global__ void __launch_bounds__(256) hash_adam_residual_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
+                                                                  float* __restrict__ grad, BinWs ws, AdamArgs adam) {
+    const uint32_t b = blockIdx.x;
+    if (b >= nbt || fused_bucket(ws, b, ws.fb[MAXB] != 0)) return;
+    float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
+    adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
+    const uint32_t l = bucket_level(ba, b), lb = b - ba.bbase[l];
+    const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
+    const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
+    float4* g4 = reinterpret_cast<float4*>(grad + gbase);
+    const float sc = adam.grad_scale;
+    for (uint32_t e = threadIdx.x; e < 2 * ne / 4; e += blockDim.x) {
+        const float4 gv = g4[e];
+        adam4(adam, gbase, e, make_float4(gv.x * sc, gv.y * sc, gv.z * sc, gv.w * sc), lr, bc1, bc2);
+        g4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
@@ -566,7 +635,8 @@ size_t ngp_hash_backward_binned_workspace(int64_t max_samples) {
 // accumulate (needs denc and the plan of the same inputs).
 static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                        const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
-                       int64_t max_samples, int level_lo, int merge_hi, int phase, void* stream) {
+                       int64_t max_samples, int level_lo, int merge_hi, int phase, void* stream,
+                       const AdamArgs* adam = nullptr) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
@@ -602,12 +672,19 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
         const size_t lds = (size_t)BENT * 2 * sizeof(double);
         if (!attr) {
             if (hipFuncSetAttribute((const void*)hash_accum_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds) != hipSuccess)
+                                    (int)lds) != hipSuccess ||
+                hipFuncSetAttribute((const void*)hash_accum_kernel<0, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
                 return NGP_ERANGE;
             attr = true;
         }
         static const unsigned capB = resident_blocks(hash_accum_kernel<0>, 1024, lds);
-        NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws));
+        if (adam) {
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0, true><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam));
+            NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<nbt, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam));
+        } else {
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}));
+        }
     }
     return ngp_launch_status();
 }
@@ -638,6 +715,20 @@ int ngp_hash_binned_write(const float* xyzs, int64_t n, const int64_t* n_dev, co
                           int64_t max_samples, int level_lo, int merge_hi, void* stream) {
     return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo,
                        merge_hi, 2, stream);
+}
+
+int ngp_hash_binned_apply_adam(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                               const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                               int64_t max_samples, int level_lo, int merge_hi, float* params, float* exp_avg,
+                               float* exp_avg_sq, void* params_f16, const float* lr_dev, float beta1, float beta2,
+                               float eps, const int64_t* step_dev, float grad_scale, void* stream) {
+    NGP_CHECK_ARG(params && exp_avg && exp_avg_sq && params_f16 && lr_dev && step_dev);
+    NGP_CHECK_ARG(((uintptr_t)params & 15) == 0 && ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0 &&
+                  ((uintptr_t)params_f16 & 7) == 0);
+    const AdamArgs a{params, exp_avg, exp_avg_sq, (_Float16*)params_f16, lr_dev, step_dev, beta1, beta2, eps,
+                     grad_scale};
+    return hash_binned(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, workspace, max_samples, level_lo,
+                       merge_hi, 6, stream, &a);
 }
 
 int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,

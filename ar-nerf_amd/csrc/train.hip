@@ -364,12 +364,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2,
                                                    float grad_scale, int zero_grad, const float* __restrict__ lr_dev,
                                                    const int64_t* __restrict__ step_dev) {
-    if (lr_dev) lr = *lr_dev;
-    if (step_dev) {
-        const float st = (float)(*step_dev + 1);
-        bc1 = 1.0f - powf(b1, st);
-        bc2 = 1.0f - powf(b2, st);
-    }
+    adam_bias(lr_dev, step_dev, b1, b2, lr, bc1, bc2);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         float4 P = reinterpret_cast<float4*>(p)[i], Gd = reinterpret_cast<float4*>(grad)[i];
@@ -379,11 +374,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         h4 out;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float gk = gp[k] * grad_scale;
-            mp[k] = b1 * mp[k] + (1 - b1) * gk;
-            vp[k] = b2 * vp[k] + (1 - b2) * gk * gk;
-            const float denom = sqrtf(vp[k] / bc2) + eps;
-            pp[k] = pp[k] - lr * ((mp[k] / bc1) / denom);
+            adam_elem(pp[k], mp[k], vp[k], gp[k] * grad_scale, lr, b1, b2, eps, bc1, bc2);
             out[k] = (_Float16)pp[k];
         }
         reinterpret_cast<float4*>(p)[i] = P;

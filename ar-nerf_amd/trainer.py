@@ -145,13 +145,19 @@ class NGPTrainer:
         # memory-side atomics vs LDS-bound passes overlap)
         self.bwd_stream = torch.cuda.Stream(device=dev)
         self.overlap_hash_bwd = os.environ.get("NGP_BWD_OVERLAP", "1") == "1"
-        # NGP_ADAM_SPLIT=1: Adam of the MLP + coarse levels beside the binned
-        # levels (measured slower: it takes HBM bandwidth from the apply)
-        self.adam_split = os.environ.get("NGP_ADAM_SPLIT", "0") == "1"
+        # Adam of the MLP + coarse levels on the side stream right after the coarse
+        # levels' backward, beside the binned levels' accumulation (single process;
+        # with the binned levels' Adam fused into their accumulation: +5 %,
+        # profiles/r02/ab/fused_adam.txt; NGP_ADAM_SPLIT=0 turns it off)
+        self.adam_split = os.environ.get("NGP_ADAM_SPLIT", "1") == "1"
         # NGP_COARSE_AFTER_WRITE=1: the coarse atomic levels start after the binned record write
         # (measured slower: the accumulation then slows as much as the write speeds up,
         # profiles/r02/ab/coarse_overlap.txt)
         self.coarse_after_write = os.environ.get("NGP_COARSE_AFTER_WRITE", "0") == "1"
+        # NGP_FUSED_ADAM=0: one FusedAdam launch over all params after the backward
+        # (else the binned levels are stepped inside their accumulation, bit-identical)
+        self.fused_adam = os.environ.get("NGP_FUSED_ADAM", "1") == "1"
+        self._adam_hi = None
         self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "1") == "1"
         self.enc = torch.empty(8 * cap * 4, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
@@ -747,6 +753,9 @@ class NGPTrainer:
             # (after the plan) here, side by side: disjoint gradient ranges
             split = HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
             adam_split = self.adam_split and apply_adam and self.world == 1 and bs is not cs
+            # single process: the binned levels' Adam runs inside their accumulation
+            fused = self.fused_adam and apply_adam and self.world == 1 and not self.coarse_after_write
+            self._adam_hi = split if fused else self.n_params
 
             def coarse():
                 self._ev("hash_bwd_coarse", 0)
@@ -762,13 +771,23 @@ class NGPTrainer:
 
             def apply():
                 self._ev("hash_binned_apply", 0)
-                vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
-                                                   _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws),
-                                                   self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi,
-                                                   vren._stream()), "hash_binned_apply")
+                if fused:  # + FusedAdam of the binned levels inside the accumulation
+                    t = HG.MLP_PARAMS
+                    vren._ok(HGL.ngp_hash_binned_apply_adam(
+                        _p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                        HG.ctypes.byref(self.grid.desc), _p(self.denc), _p(self.grad[t:]), _p(self.bin_ws),
+                        self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi, _p(self.params[t:]),
+                        _p(self.exp_avg[t:]), _p(self.exp_avg_sq[t:]), _p(self.params16[t:]), _p(self.lr_dev),
+                        ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                        ctypes_float(1.0 / self.world), vren._stream()), "hash_binned_apply_adam")
+                else:
+                    vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                       _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
+                                                       _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws),
+                                                       self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi,
+                                                       vren._stream()), "hash_binned_apply")
                 self._ev("hash_binned_apply", 1)
-                if adam_split:
+                if adam_split and not fused:
                     self._adam(split, self.params.numel(), vren._stream())
 
             if self.coarse_after_write:
@@ -807,7 +826,7 @@ class NGPTrainer:
         self._ev("hash_bwd", 1)
         if self.world == 1 and apply_adam:
             self._ev("adam", 0)
-            self._adam(0, self.n_params, s)
+            self._adam(0, self._adam_hi if hybrid else self.n_params, s)
             self._ev("adam", 1)
         elif self.world > 1 and not self._segmented:
             self._reduce_grads()
@@ -850,6 +869,13 @@ class NGPTrainer:
             for (a, b), (lo, hi) in zip(self.buckets, self.shards):
                 ddp.all_gather_(self._pbuf[a:b], self._pbuf[lo:hi].clone(), self.pg)
         return self.params
+
+    def fused_params(self):
+        """Parameters whose Adam runs inside the binned accumulation (the binned
+        hash levels; single process, hybrid/binned backward), 0 otherwise."""
+        if not (self.fused_adam and self.world == 1 and self.hash_backward != "atomic" and not self.coarse_after_write):
+            return 0
+        return self.n_params - (HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo])
 
     def _adam(self, lo, hi, s):
         """FusedAdam over params[lo:hi] (16-byte aligned bounds).  lr and the

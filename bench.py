@@ -63,15 +63,19 @@ _MLP_FWD = 2 * (32 * 64 + 64 * 16) + 2 * (32 * 64 + 64 * 64 + 64 * 16)
 _MLP_BWD = (2 * (32 * 64 + 64 * 16 + 32 * 64 + 64 * 64 + 64 * 16)
             + 2 * (16 * 64 + 64 * 64 + 64 * 16 + 16 * 64 + 64 * 32)
             + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32))
-KERNEL_WORK = {  # name: (bound, work per unit, unit basis, member kernels)
-    "hash_encode": ("hbm", 16 * 8 * 4 + 12 + 4 + 64, "evaluated", ["hash_encode"]),
-    "field_mlp": ("mfma", _MLP_FWD, "evaluated", ["field_mlp"]),
-    "mlp_bwd": ("mfma", _MLP_BWD, "active", ["mlp_bwd"]),
-    "hash_bwd_coarse": ("atomic", 8 * 8 * 2 * 4, "active", ["hash_bwd_coarse"]),
-    "hash_bwd_fine": ("hbm", 16 + 64 + 2 * 8 * 8 * 2 * 4, "active", ["hash_write", "hash_accum"]),
-    "march": ("hbm", 32, "marched", ["march", "march_compact"]),
-    "composite_loss": ("hbm", 76, "composited", ["composite_loss"]),
-    "adam": ("hbm", 34, "params", ["adam"]),
+KERNEL_WORK = {  # name: (bound, [(work per unit, unit basis), ...], member kernels)
+    "hash_encode": ("hbm", [(16 * 8 * 4 + 12 + 4 + 64, "evaluated")], ["hash_encode"]),
+    "field_mlp": ("mfma", [(_MLP_FWD, "evaluated")], ["field_mlp"]),
+    "mlp_bwd": ("mfma", [(_MLP_BWD, "active")], ["mlp_bwd"]),
+    "hash_bwd_coarse": ("atomic", [(8 * 8 * 2 * 4, "active")], ["hash_bwd_coarse"]),
+    # records written + read (1104 B / active sample) and, when the binned
+    # levels' Adam is fused into the accumulation, their Adam state: p, m, v
+    # read and written + the fp16 shadow (26 B / param; no gradient traffic)
+    "hash_bwd_fine": ("hbm", [(16 + 64 + 2 * 8 * 8 * 2 * 4, "active"), (26, "fused_params")],
+                      ["hash_write", "hash_accum"]),
+    "march": ("hbm", [(32, "marched")], ["march", "march_compact"]),
+    "composite_loss": ("hbm", [(76, "composited")], ["composite_loss"]),
+    "adam": ("hbm", [(34, "adam_params")], ["adam"]),  # params the Adam launches step
 }
 PEAK = {"hbm": (8000.0, "GB/s"), "mfma": (2500.0, "TFLOP/s"), "atomic": (1300.0, "GB/s")}
 
@@ -303,20 +307,22 @@ def main():
     marched_bd, composited_bd, active_bd, evaluated_bd = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         evaluated_bd = marched_bd
+    fused_p = trainer.fused_params()
+    pw = {"params": trainer.params.numel(), "fused_params": fused_p, "adam_params": trainer.params.numel() - fused_p}
     units_bd = {"marched": marched_bd / n_bd, "evaluated": evaluated_bd / n_bd, "composited": composited_bd / n_bd,
-                "active": active_bd / n_bd, "params": trainer.params.numel()}
+                "active": active_bd / n_bd, **pw}
 
     def op_row(name, summary, units):
-        bound, per_unit, basis, members = KERNEL_WORK[name]
+        bound, terms, members = KERNEL_WORK[name]
         ms = sum(summary[m][0] * summary[m][1] for m in members if m in summary)  # per step
         if ms <= 0:
             return None
-        work = units[basis] * per_unit  # per step
+        work = sum(units[basis] * per_unit for per_unit, basis in terms)  # per step
         peak, unit = PEAK[bound]
         achieved = work / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
         return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 4), "ms_per_step": round(ms, 4),
-                "work_per_unit": per_unit, "units_per_step": round(units[basis], 1), "unit_basis": basis,
+                "work_per_step": round(work), "work_terms": [[pu, b, round(units[b], 1)] for pu, b in terms if units[b]],
                 "kernels": members}
 
     ops = {k: r for k in KERNEL_WORK if (r := op_row(k, bd_summary, units_bd)) is not None}
@@ -341,7 +347,7 @@ def main():
     # ---- roofline region: the same number of graph-replayed steps again, with
     # one stamp before the dominant op's first kernel and one after its last
     # (consecutive on the main stream)
-    members = KERNEL_WORK[dominant][3]
+    members = KERNEL_WORK[dominant][2]
     dom = KT.KernelTimer(trainer.dctr, rows=max(4096, 2 * args.steps), span=(members[0], members[-1]))
     trainer.timer = dom
     run(64)  # capture this timer's graph variants
@@ -359,7 +365,7 @@ def main():
     if trainer.chunk_first <= 0:
         e_rf = m_rf
     units_rf = {"marched": m_rf / args.steps, "evaluated": e_rf / args.steps, "composited": c_rf / args.steps,
-                "active": a_rf / args.steps, "params": trainer.params.numel()}
+                "active": a_rf / args.steps, **pw}
     t_max = torch.tensor([t_el], device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -369,7 +375,7 @@ def main():
     if trainer.chunk_first <= 0:
         evaluated = marched
     units = {"marched": marched / args.steps, "evaluated": evaluated / args.steps,
-             "composited": composited / args.steps, "active": active / args.steps, "params": trainer.params.numel()}
+             "composited": composited / args.steps, "active": active / args.steps, **pw}
     rm_s, vr_s, ev_s = units["marched"] / R, units["composited"] / R, units["evaluated"] / R
     roof = op_row(dominant, dom_summary, units_rf)
     roof = dict(op=dominant, traffic=pmc_traffic(members, bd_summary), traffic_unit="bytes per step", **roof,
@@ -377,8 +383,10 @@ def main():
                          f"{args.steps} graph-replayed steps run right after the timed ones "
                          f"({t_rf * 1e3:.4f} ms/step with the 2 stamps; ktimer)")
     # step-level bound: every op's algorithmic bytes at HBM peak + MLP FLOPs at MFMA peak
-    hbm_bytes = sum(units[KERNEL_WORK[k][2]] * KERNEL_WORK[k][1] for k in KERNEL_WORK if KERNEL_WORK[k][0] != "mfma")
-    flops = sum(units[KERNEL_WORK[k][2]] * KERNEL_WORK[k][1] for k in KERNEL_WORK if KERNEL_WORK[k][0] == "mfma")
+    def op_work(k):
+        return sum(units[b] * pu for pu, b in KERNEL_WORK[k][1])
+    hbm_bytes = sum(op_work(k) for k in KERNEL_WORK if KERNEL_WORK[k][0] != "mfma")
+    flops = sum(op_work(k) for k in KERNEL_WORK if KERNEL_WORK[k][0] == "mfma")
     bound_ms = hbm_bytes / 8000e9 * 1e3 + flops / 2500e12 * 1e3
     adam_ms = units["params"] * 34 / 8000e9 * 1e3
     step_bound = {"hbm_bytes_per_step": round(hbm_bytes), "mlp_flops_per_step": round(flops),

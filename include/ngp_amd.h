@@ -387,6 +387,22 @@ int ngp_hash_binned_write(const float* xyzs, int64_t n, const int64_t* n_dev, co
                           int64_t max_samples, int level_lo, int merge_hi, void* stream);
 int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
                           int level_lo, int merge_hi, void* stream);
+/* ngp_hash_binned_apply with FusedAdam of the binned levels' parameters
+ * (apex FusedAdam, train.py:146-152, as ngp_adam_step_dev): a bucket whose
+ * whole gradient one workgroup sums (one chunk, no direct adds, no overflow)
+ * is stepped straight from its LDS image -- its gradient never goes through
+ * memory -- and every other bucket of levels [level_lo, 16) from grad_table
+ * (which those entries leave zeroed).  params / exp_avg / exp_avg_sq (fp32)
+ * and params_f16 have grad_table's layout (the table part of the flat
+ * vector); the caller steps the rest (MLP, levels < level_lo) with
+ * ngp_adam_step_dev.  Requires the binned levels' gradient to be zero on
+ * entry apart from this call's own direct adds (the trainer's invariant:
+ * Adam zeroes it).  Results are bit-identical to apply + ngp_adam_step_dev. */
+int ngp_hash_binned_apply_adam(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                               const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
+                               int64_t max_samples, int level_lo, int merge_hi, float* params, float* exp_avg,
+                               float* exp_avg_sq, void* params_f16, const float* lr_dev, float beta1, float beta2,
+                               float eps, const int64_t* step_dev, float grad_scale, void* stream);
 /* ngp_hash_backward restricted to levels [level_lo, level_hi). */
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
