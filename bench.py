@@ -326,6 +326,19 @@ def main():
                 "kernels": members}
 
     ops = {k: r for k in KERNEL_WORK if (r := op_row(k, bd_summary, units_bd)) is not None}
+    if "hash_encode" in ops:
+        # the encode's real limit is the lane-gather issue rate: 4 loads per level on dense levels,
+        # 4 + 1/4 on hashed ones; scripts/diag/gather_diag.py measured 265 G lane-gathers/s for
+        # random 4-16 B gathers from an L2-resident table, 72 G/s from a 24 MB one
+        # (profiles/r02/gather_microbench.json)
+        sizes = list(trainer.grid.desc.sizes)[:trainer.grid.n_levels]
+        n_hashed = sum(1 for z in sizes if z == 1 << trainer.grid.log2_T)
+        per_sample = 4 * (len(sizes) - n_hashed) + 5 * n_hashed
+        ge = units_bd["evaluated"] * per_sample / (ops["hash_encode"]["ms_per_step"] * 1e-3)
+        ops["hash_encode"]["lane_gathers_per_sample"] = per_sample
+        ops["hash_encode"]["G_lane_gathers_per_s"] = round(ge / 1e9, 1)
+        ops["hash_encode"]["gather_peak_note"] = ("random-gather rate 265 G/s L2-resident, 72 G/s from a 24 MB "
+                                                  "table (profiles/r02/gather_microbench.json)")
     dominant = max(ops, key=lambda k: ops[k]["ms_per_step"])
     kernels = {k: {"avg_launch_ms": round(v[0], 4), "launches_per_step": round(v[1], 2),
                    "ms_per_step": round(v[0] * v[1], 4)} for k, v in sorted(bd_summary.items(), key=lambda kv: -kv[1][0] * kv[1][1])}
