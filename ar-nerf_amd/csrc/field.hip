@@ -483,6 +483,88 @@ __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restric
     }
 }
 
+// ------------------------------------------- fused encode + MLP forward
+// hash_encode_kernel's lane-per-sample gathers (same arithmetic) and the
+// field MLPs in one launch: a wave encodes 64 consecutive samples (one per
+// lane), writes the pair-major encoding for the backward, parks it in its LDS
+// rows and runs the MLPs on four 16-sample column blocks read back in the
+// MFMA B layout -- the separate MLP launch (its fixed cost, the encoding's
+// re-read) disappears and the MLP math overlaps other waves' gathers.
+constexpr int XROW = 40;  // halfs per parked encoding row (32 + pad: conflict-free 16-B reads)
+constexpr int FEM_WAVES = 8;  // 512-thread blocks: the 24 KB weight image shared by 8 waves (4 waves/SIMD)
+template <bool COLOR>
+__global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const float* __restrict__ xyzs,
+                                                               const float* __restrict__ dirs, int64_t n,
+                                                               const int64_t* __restrict__ n_dev,
+                                                               const int32_t* __restrict__ sidx, GridArgs ga,
+                                                               const uint32_t* __restrict__ table,
+                                                               const _Float16* __restrict__ mlp,
+                                                               _Float16* __restrict__ enc_pm,
+                                                               float* __restrict__ sigmas, float* __restrict__ rgbs,
+                                                               _Float16* __restrict__ h_out) {
+    __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
+    __shared__ __attribute__((aligned(16))) _Float16 xs[FEM_WAVES][64 * XROW];
+    __shared__ int32_t xi[FEM_WAVES][64];
+    __shared__ LevelLds lv;
+    load_fwd_weights_direct(mlp, sw, COLOR);
+    load_levels(ga, lv);
+    __syncthreads();
+    const int64_t N = n_dev ? *n_dev : n;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, s = lane & 15, g = lane >> 4;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    // wave-uniform trip count (the MFMAs need every lane)
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + wv * 64; base < N; base += stride) {
+        const int64_t j = base + lane;
+        const bool valid = j < N;
+        const int64_t i = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
+        float in[3];
+        load_x01(xyzs, i, valid, ga, in);
+        _Float16* row = &xs[wv][lane * XROW];
+#pragma unroll 1
+        for (int pr = 0; pr < 8; ++pr) {
+            const LevelU u0 = level_u(lv, 2 * pr), u1 = level_u(lv, 2 * pr + 1);
+            float a0, a1, b0, b1;
+            encode_level_u(in, u0, table, a0, a1);
+            encode_level_u(in, u1, table, b0, b1);
+            const h4 e4 = h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
+            if (valid) *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) = e4;
+            *reinterpret_cast<h4*>(row + 4 * pr) = e4;
+        }
+        xi[wv][lane] = valid ? (int32_t)i : -1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+        for (int c = 0; c < 4; ++c) {
+            const int src = 16 * c + s;
+            const int32_t ic = xi[wv][src];
+            const bool ok = ic >= 0;
+            const h8 e = *reinterpret_cast<const h8*>(&xs[wv][src * XROW + 8 * g]);
+            h4 h1[4];
+            const h4 hh = density_net(e, sw, s, g, h1);
+            if (ok) {
+                if (h_out) *reinterpret_cast<h4*>(h_out + (int64_t)ic * 16 + 4 * g) = hh;
+                if (g == 0) sigmas[ic] = expf((float)hh[0]);  // TruncExp forward (custom_functions.py:165-167)
+            }
+            if constexpr (COLOR) {
+                const float dx = ok ? dirs[3 * (int64_t)ic] : 0.f, dy = ok ? dirs[3 * (int64_t)ic + 1] : 0.f,
+                            dz = ok ? dirs[3 * (int64_t)ic + 2] : 1.f;
+                float sh[4];
+                sh4_select(dx, dy, dz, g, sh);
+                const h8 cin = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3], hh[0], hh[1], hh[2], hh[3]};
+                h4 h3[4], h4v[4];
+                const h4 o = color_net(cin, sw, s, g, h3, h4v);
+                if (ok && g == 0) {
+                    rgbs[3 * (int64_t)ic] = sigmoid_h(o[0]);
+                    rgbs[3 * (int64_t)ic + 1] = sigmoid_h(o[1]);
+                    rgbs[3 * (int64_t)ic + 2] = sigmoid_h(o[2]);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // this iteration's LDS reads before the next one's writes (in order per wave)
+    }
+}
+
 // ------------------------------------------------------------------ backward
 // Kernel A: MLP backward.  Recomputes the forward from the saved encoding
 // (MFMA, cheap), back-propagates with v_mfma_f32_16x16x16_f16 (whose B
@@ -1301,6 +1383,31 @@ int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const in
     NGP_TIMED(NGP_K_HASH_ENCODE, as_stream(stream), hash_encode_kernel<false><<<8 * per_pair, 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga,
                                                                            (const uint32_t*)table_f16,
                                                                            (_Float16*)enc_pm));
+    return ngp_launch_status();
+}
+
+int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
+                         const int32_t* sample_idx, const ngp_hashgrid_t* grid, const void* table_f16,
+                         const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs, void* h_f16, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && table_f16 && mlp_f16 && enc_pm && sigmas && (dirs != nullptr) == (rgbs != nullptr));
+    NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0);
+    hipStream_t s = as_stream(stream);
+    if (!dirs) {
+        static const unsigned capd = resident_blocks(field_encode_mlp_kernel<false>, 64 * FEM_WAVES, 0);
+        NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_kernel<false><<<std::max(1u, std::min(capd, (unsigned)((n + 511) / 512))), 64 * FEM_WAVES, 0, s>>>(
+            xyzs, nullptr, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16,
+            (_Float16*)enc_pm, sigmas, nullptr, (_Float16*)h_f16));
+        return ngp_launch_status();
+    }
+    static const unsigned cap = resident_blocks(field_encode_mlp_kernel<true>, 64 * FEM_WAVES, 0);
+    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_kernel<true><<<std::max(1u, std::min(cap, (unsigned)((n + 511) / 512))), 64 * FEM_WAVES, 0, s>>>(
+        xyzs, dirs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16,
+        (_Float16*)enc_pm, sigmas, rgbs, (_Float16*)h_f16));
     return ngp_launch_status();
 }
 

@@ -48,6 +48,7 @@ def _lib():
         L.ngp_hash_encode.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
         L.ngp_field_forward_indexed.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp]
         L.ngp_field_mlp_forward.argtypes = [vp, vp, c_int64, vp, vp, vp, vp, vp, vp, vp]
+        L.ngp_field_encode_mlp.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_hash_backward.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
         L.ngp_hash_backward_binned.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, c_int, vp]
         L.ngp_hash_backward_levels.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp]
@@ -60,7 +61,7 @@ def _lib():
         L.ngp_hash_backward_binned_workspace.argtypes = [c_int64]
         L.ngp_hash_backward_binned_workspace.restype = ctypes.c_size_t
         for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_density_input_grad, L.ngp_field_backward, L.ngp_field_backward_mlp,
-                  L.ngp_hash_encode, L.ngp_field_mlp_forward, L.ngp_field_forward_indexed,
+                  L.ngp_hash_encode, L.ngp_field_mlp_forward, L.ngp_field_forward_indexed, L.ngp_field_encode_mlp,
                   L.ngp_hash_backward, L.ngp_hash_backward_binned, L.ngp_hash_backward_levels,
                   L.ngp_hash_binned_plan, L.ngp_hash_binned_apply, L.ngp_hash_binned_write,
                   L.ngp_hash_binned_accum, L.ngp_hash_binned_apply_adam):

@@ -135,8 +135,10 @@ class NGPTrainer:
         self._pending = None  # (set index, event) of a batch marched ahead
         self.n_prefetched = 0
         self.no_prefetch = os.environ.get("NGP_NO_PREFETCH", "0") == "1"  # march every batch inline (diagnostics)
-        # where in the step the next batch's march is launched on the side stream
-        self.prefetch_at = os.environ.get("NGP_PREFETCH_AT", "after_fwd")
+        # where in the step the next batch's march is launched on the side stream: at
+        # the start (beside the gather-bound encode rather than the VALU-bound MLP
+        # backward: +1.5 %, profiles/r02/ab/prefetch_at.txt)
+        self.prefetch_at = os.environ.get("NGP_PREFETCH_AT", "start")
         self._bind(self.msets[0])
         self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         # saved encoding: pair-major (8, cap, 4) for the split forward, else row-major (cap, 32)
@@ -159,6 +161,9 @@ class NGPTrainer:
         self.fused_adam = os.environ.get("NGP_FUSED_ADAM", "1") == "1"
         self._adam_hi = None
         self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "1") == "1"
+        # the training forward's encode and MLPs in one launch (pair-major enc as split_forward;
+        # +1.8 % over 4 interleaved runs, profiles/r02/ab/fused_field.txt; NGP_FUSED_FIELD=0: two launches)
+        self.fused_field = self.split_forward and os.environ.get("NGP_FUSED_FIELD", "1") == "1"
         self.enc = torch.empty(8 * cap * 4, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         self.denc = torch.empty(cap, 32, **f)
@@ -890,6 +895,14 @@ class NGPTrainer:
     def _field_indexed(self, s):
         """Field forward over the listed samples eval_idx[:eval_total]."""
         HGL = HG._lib()
+        if self.fused_field:  # encode + MLPs in one launch
+            self._ev("hash_encode", 0)
+            vren._ok(HGL.ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.eval_total),
+                                              _p(self.eval_idx), HG.ctypes.byref(self.grid.desc),
+                                              _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc),
+                                              _p(self.sigmas), _p(self.rgbs), None, s), "field_encode_mlp")
+            self._ev("hash_encode", 1)
+            return
         if self.split_forward:
             self._ev("hash_encode", 0)
             vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.eval_total), _p(self.eval_idx),

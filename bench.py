@@ -77,6 +77,18 @@ KERNEL_WORK = {  # name: (bound, [(work per unit, unit basis), ...], member kern
     "composite_loss": ("hbm", [(76, "composited")], ["composite_loss"]),
     "adam": ("hbm", [(34, "adam_params")], ["adam"]),  # params the Adam launches step
 }
+
+
+def active_work(trainer):
+    """KERNEL_WORK for the trainer's configuration: with the fused forward
+    (ngp_field_encode_mlp) the MLP forward runs inside the encode launches, so
+    it has no op of its own (its FLOPs are noted on hash_encode)."""
+    kw = dict(KERNEL_WORK)
+    if getattr(trainer, "fused_field", False):
+        kw.pop("field_mlp")
+    return kw
+
+
 PEAK = {"hbm": (8000.0, "GB/s"), "mfma": (2500.0, "TFLOP/s"), "atomic": (1300.0, "GB/s")}
 
 
@@ -273,6 +285,7 @@ def main():
     trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward,
                          bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray, erode=erode)
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
+    WORK = active_work(trainer)
     R = args.batch
 
     def run(n):
@@ -313,7 +326,7 @@ def main():
                 "active": active_bd / n_bd, **pw}
 
     def op_row(name, summary, units):
-        bound, terms, members = KERNEL_WORK[name]
+        bound, terms, members = WORK[name]
         ms = sum(summary[m][0] * summary[m][1] for m in members if m in summary)  # per step
         if ms <= 0:
             return None
@@ -325,7 +338,7 @@ def main():
                 "work_per_step": round(work), "work_terms": [[pu, b, round(units[b], 1)] for pu, b in terms if units[b]],
                 "kernels": members}
 
-    ops = {k: r for k in KERNEL_WORK if (r := op_row(k, bd_summary, units_bd)) is not None}
+    ops = {k: r for k in WORK if (r := op_row(k, bd_summary, units_bd)) is not None}
     if "hash_encode" in ops:
         # the encode's real limit is the lane-gather issue rate: 4 loads per level on dense levels,
         # 4 + 1/4 on hashed ones; scripts/diag/gather_diag.py measured 265 G lane-gathers/s for
@@ -339,6 +352,8 @@ def main():
         ops["hash_encode"]["G_lane_gathers_per_s"] = round(ge / 1e9, 1)
         ops["hash_encode"]["gather_peak_note"] = ("random-gather rate 265 G/s L2-resident, 72 G/s from a 24 MB "
                                                   "table (profiles/r02/gather_microbench.json)")
+        if "field_mlp" not in WORK:
+            ops["hash_encode"]["fused_mlp_forward_flop_per_sample"] = _MLP_FWD
     dominant = max(ops, key=lambda k: ops[k]["ms_per_step"])
     kernels = {k: {"avg_launch_ms": round(v[0], 4), "launches_per_step": round(v[1], 2),
                    "ms_per_step": round(v[0] * v[1], 4)} for k, v in sorted(bd_summary.items(), key=lambda kv: -kv[1][0] * kv[1][1])}
@@ -360,7 +375,7 @@ def main():
     # ---- roofline region: the same number of graph-replayed steps again, with
     # one stamp before the dominant op's first kernel and one after its last
     # (consecutive on the main stream)
-    members = KERNEL_WORK[dominant][2]
+    members = WORK[dominant][2]
     dom = KT.KernelTimer(trainer.dctr, rows=max(4096, 2 * args.steps), span=(members[0], members[-1]))
     trainer.timer = dom
     run(64)  # capture this timer's graph variants
@@ -398,6 +413,7 @@ def main():
     # step-level bound: every op's algorithmic bytes at HBM peak + MLP FLOPs at MFMA peak
     def op_work(k):
         return sum(units[b] * pu for pu, b in KERNEL_WORK[k][1])
+    # (all ops' work, the fused MLP forward's FLOPs included)
     hbm_bytes = sum(op_work(k) for k in KERNEL_WORK if KERNEL_WORK[k][0] != "mfma")
     flops = sum(op_work(k) for k in KERNEL_WORK if KERNEL_WORK[k][0] == "mfma")
     bound_ms = hbm_bytes / 8000e9 * 1e3 + flops / 2500e12 * 1e3

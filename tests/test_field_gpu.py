@@ -109,6 +109,22 @@ def test_split_encode_mlp_equals_fused(scale):
     rest = torch.ones(n, dtype=torch.bool, device=DEV)
     rest[ix] = False
     assert bool((sig2[rest] == -1.0).all()) and bool((rows[rest] == 7.0).all())
+    # encode + MLPs in one launch (ngp_field_encode_mlp, the trainer's forward): same values, listed rows only
+    enc_pm.fill_(7.0); sig2.fill_(-1.0); rgb2.fill_(-1.0)
+    vren._ok(L.ngp_field_encode_mlp(vp(x.data_ptr()), vp(d.data_ptr()), n, vp(m.data_ptr()), vp(sidx.data_ptr()),
+                                    ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:].data_ptr()), vp(p16.data_ptr()),
+                                    vp(enc_pm.data_ptr()), vp(sig2.data_ptr()), vp(rgb2.data_ptr()), None,
+                                    vren._stream()), "encode_mlp_ix")
+    rows = enc_pm.permute(1, 0, 2).reshape(n, 32)
+    assert torch.equal(rows[ix].view(torch.int16), enc[ix].view(torch.int16))
+    assert torch.equal(sig2[ix], sig[ix]) and torch.equal(rgb2[ix], rgb[ix])
+    assert bool((sig2[rest] == -1.0).all()) and bool((rows[rest] == 7.0).all())
+    # all rows, density net only
+    sig3.fill_(-1.0)
+    vren._ok(L.ngp_field_encode_mlp(vp(x.data_ptr()), None, n, None, None, ctypes.byref(grid.desc),
+                                    vp(p16[HG.MLP_PARAMS:].data_ptr()), vp(p16.data_ptr()), vp(enc_pm.data_ptr()),
+                                    vp(sig3.data_ptr()), None, None, vren._stream()), "encode_density")
+    assert torch.equal(sig3, HG.density_forward(x, grid, p16)[0])
 
 
 @pytest.mark.parametrize("scale", [0.5, 16.0])
