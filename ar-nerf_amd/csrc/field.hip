@@ -527,7 +527,7 @@ __global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const 
             encode_level_u(in, u0, table, a0, a1);
             encode_level_u(in, u1, table, b0, b1);
             const h4 e4 = h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
-            if (valid) *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) = e4;
+            if (valid && enc_pm) *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) = e4;
             *reinterpret_cast<h4*>(row + 4 * pr) = e4;
         }
         xi[wv][lane] = valid ? (int32_t)i : -1;
@@ -1394,7 +1394,7 @@ int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const 
     if (st) return st;
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && table_f16 && mlp_f16 && enc_pm && sigmas && (dirs != nullptr) == (rgbs != nullptr));
+    NGP_CHECK_ARG(xyzs && table_f16 && mlp_f16 && sigmas && (dirs != nullptr) == (rgbs != nullptr));
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0);
     hipStream_t s = as_stream(stream);
     if (!dirs) {

@@ -9,7 +9,7 @@ a host sync and ~10 launches per iteration, ~20-40 iterations per frame.
 TestRenderer runs the same loop with every decision in device memory
 (include/ngp_amd.h "device-resident test-time render"): one iteration is
   ngp_render_test_march   (loop test, N_samples, march, valid-sample list)
-  ngp_hash_encode + ngp_field_mlp_forward over the list (NGP.forward)
+  ngp_field_encode_mlp over the list (NGP.forward: encode + MLPs in one launch)
   ngp_render_test_composite (composite_test_fw + survivor compaction)
 and the iterations are captured in HIP graphs: a frame is graph A (begin +
 summary + `iters_per_graph` iterations), then graph B (`iters_tail` more)
@@ -100,12 +100,11 @@ class TestRenderer:
                                          _p(self.dirs), _p(self.deltas), _p(self.ts), _p(self.n_eff),
                                          _p(self.sample_idx), s), "render_test_march")
         # model(xyzs[valid], dirs[valid]) (rendering.py:204-218): NGP.forward over the list
-        vren._ok(L.ngp_hash_encode(_p(self.xyzs), self.cap, self.n_valid_ptr, _p(self.sample_idx),
-                                   ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc), s),
-                 "hash_encode")
-        vren._ok(L.ngp_field_mlp_forward(_p(self.enc), _p(self.dirs), self.cap, self.n_valid_ptr, _p(self.sample_idx),
-                                         _p(self.params16), _p(self.sigmas), _p(self.rgbs), None, s),
-                 "field_mlp_forward")
+        # (encode + MLPs in one launch; no encoding kept: nothing goes backward)
+        vren._ok(L.ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, self.n_valid_ptr, _p(self.sample_idx),
+                                        ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
+                                        _p(self.params16), None, _p(self.sigmas), _p(self.rgbs), None, s),
+                 "field_encode_mlp")
         vren._ok(L.ngp_render_test_composite(_p(self.sigmas), _p(self.rgbs), _p(self.deltas), _p(self.ts),
                                              _p(self.n_eff), self.n_rays, par, _p(self.state), _p(self.alive[par]),
                                              _p(self.alive[par ^ 1]), c_float(self.T_threshold), _p(self.opacity),

@@ -354,7 +354,12 @@ class NGPTrainer:
                     vren._ok(L.ngp_occupancy_samples(*args, _p(self._occ_xyz), _p(self._occ_flat), s),
                              "occupancy_samples")
                 HGL = HG._lib()
-                if self.split_forward and 32 * n <= self.enc.numel():  # encode into the step's (free) enc buffer
+                if self.fused_field:  # encode + density net in one launch (no encoding kept)
+                    vren._ok(HGL.ngp_field_encode_mlp(_p(self._occ_xyz), None, n, None, None,
+                                                      HG.ctypes.byref(self.grid.desc),
+                                                      _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), None,
+                                                      _p(self._occ_sig), None, None, s), "density_encode_mlp")
+                elif self.split_forward and 32 * n <= self.enc.numel():  # encode into the step's (free) enc buffer
                     vren._ok(HGL.ngp_hash_encode(_p(self._occ_xyz), n, None, None, HG.ctypes.byref(self.grid.desc),
                                                  _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc), s), "hash_encode")
                     vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), None, n, None, None, _p(self.params16),

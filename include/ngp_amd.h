@@ -328,8 +328,9 @@ int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const in
 int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                     const ngp_hashgrid_t* grid, const void* table_f16, void* enc_pm, void* stream);
 /* ngp_hash_encode + ngp_field_mlp_forward in one launch (same values): the
- * pair-major encoding enc_pm (plane stride n) of the listed samples, their
- * sigmas / rgbs (dirs == NULL: density net only, rgbs NULL) and h (nullable).
+ * pair-major encoding enc_pm (plane stride n; nullable: not stored) of the
+ * listed samples, their sigmas / rgbs (dirs == NULL: density net only, rgbs
+ * NULL) and h (nullable).
  * Replaces NGP.forward / NGP.density (models/networks.py:95-146). */
 int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
                          const int32_t* sample_idx, const ngp_hashgrid_t* grid, const void* table_f16,
