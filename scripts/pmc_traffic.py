@@ -12,6 +12,8 @@ import os
 import sys
 
 NAMES = {"hash_bwd_kernel": "hash_bwd_coarse", "field_bwd_mlp_kernel": "mlp_bwd", "hash_encode_kernel": "hash_encode",
+         "field_bwd_mlp_coop_kernel": "mlp_bwd", "field_encode_mlp_kernel": "hash_encode",
+         "hash_adam_residual_kernel": "adam",
          "adam_kernel": "adam", "field_fwd_kernel": "field_mlp", "hash_write_kernel": "hash_write",
          "hash_accum_kernel": "hash_accum", "hash_count_kernel": "hash_count", "march_slots_wave_kernel": "march",
          "march_compact_kernel": "march_compact", "composite_loss_wave_kernel": "composite_loss"}  # ktimer names
@@ -47,9 +49,16 @@ def main():
         if k is None or "FETCH_SIZE" not in c or "WRITE_SIZE" not in w:
             continue
         rd, wr = 2 * c["FETCH_SIZE"] * 1024, w["WRITE_SIZE"] * 1024
-        res[k] = {"bytes_per_launch": round(rd + wr), "read_bytes": round(rd), "write_bytes": round(wr),
-                  "FETCH_SIZE_KB": c["FETCH_SIZE"], "WRITE_SIZE_KB": w["WRITE_SIZE"], "rocprof_kernel": kname,
-                  "dur_us_fetch_pass": c.get("dur_us"), "dur_us_write_pass": w.get("dur_us")}
+        row = {"bytes_per_launch": round(rd + wr), "read_bytes": round(rd), "write_bytes": round(wr),
+               "FETCH_SIZE_KB": c["FETCH_SIZE"], "WRITE_SIZE_KB": w["WRITE_SIZE"], "rocprof_kernel": kname,
+               "dur_us_fetch_pass": c.get("dur_us"), "dur_us_write_pass": w.get("dur_us")}
+        if k == "adam" and k in res:  # two launches per step under one timer name (MLP + coarse, residual):
+            a = res[k]                # bytes_per_launch = their mean, so x launches/step = their sum
+            for f in ("bytes_per_launch", "read_bytes", "write_bytes"):
+                a[f] = round((a[f] + row[f]) / 2)
+            a["rocprof_kernel"] += " + " + kname
+        elif k not in res or "ILb0E" in res[k]["rocprof_kernel"]:
+            res[k] = row  # template variants: not the density-only forward of the occupancy update (1 in 16 steps)
     res["_note"] = ("read = 2 x FETCH_SIZE (gfx950 128-B requests tallied at 64 B); write = WRITE_SIZE; gathers of "
                     "4-16 B lanes and partial-line atomics are uncalibrated widths (MI355X_MICROARCH.md HBM); "
                     "source: " + os.path.basename(os.path.normpath(d)))
