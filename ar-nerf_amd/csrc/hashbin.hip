@@ -731,6 +731,20 @@ int ngp_hash_binned_apply_adam(const float* xyzs, int64_t n, const int64_t* n_de
                        merge_hi, 6, stream, &a);
 }
 
+int ngp_hash_binned_accum_adam(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
+                               int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
+                               void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
+                               const int64_t* step_dev, float grad_scale, void* stream) {
+    NGP_CHECK_ARG(params && exp_avg && exp_avg_sq && params_f16 && lr_dev && step_dev);
+    NGP_CHECK_ARG(((uintptr_t)params & 15) == 0 && ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0 &&
+                  ((uintptr_t)params_f16 & 7) == 0);
+    const AdamArgs a{params, exp_avg, exp_avg_sq, (_Float16*)params_f16, lr_dev, step_dev, beta1, beta2, eps,
+                     grad_scale};
+    static const float dummy[1] = {0.f};
+    return hash_binned(dummy, 1, nullptr, nullptr, grid, nullptr, grad_table, workspace, max_samples, level_lo,
+                       merge_hi, 4, stream, &a);
+}
+
 int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
                           int level_lo, int merge_hi, void* stream) {
     // (xyzs / n only gate the argument checks here; the accumulation reads the workspace)

@@ -58,13 +58,15 @@ def _lib():
         L.ngp_hash_binned_accum.argtypes = [P, vp, vp, c_int64, c_int, c_int, vp]
         L.ngp_hash_binned_apply_adam.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, c_int, vp, vp, vp,
                                                  vp, vp, c_float, c_float, c_float, vp, c_float, vp]
+        L.ngp_hash_binned_accum_adam.argtypes = [P, vp, vp, c_int64, c_int, c_int, vp, vp, vp, vp, vp, c_float, c_float,
+                                                 c_float, vp, c_float, vp]
         L.ngp_hash_backward_binned_workspace.argtypes = [c_int64]
         L.ngp_hash_backward_binned_workspace.restype = ctypes.c_size_t
         for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_density_input_grad, L.ngp_field_backward, L.ngp_field_backward_mlp,
                   L.ngp_hash_encode, L.ngp_field_mlp_forward, L.ngp_field_forward_indexed, L.ngp_field_encode_mlp,
                   L.ngp_hash_backward, L.ngp_hash_backward_binned, L.ngp_hash_backward_levels,
                   L.ngp_hash_binned_plan, L.ngp_hash_binned_apply, L.ngp_hash_binned_write,
-                  L.ngp_hash_binned_accum, L.ngp_hash_binned_apply_adam):
+                  L.ngp_hash_binned_accum, L.ngp_hash_binned_apply_adam, L.ngp_hash_binned_accum_adam):
             f.restype = c_int
         _declared = True
     return L

@@ -764,7 +764,7 @@ class NGPTrainer:
             split = HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
             adam_split = self.adam_split and apply_adam and self.world == 1 and bs is not cs
             # single process: the binned levels' Adam runs inside their accumulation
-            fused = self.fused_adam and apply_adam and self.world == 1 and not self.coarse_after_write
+            fused = self.fused_adam and apply_adam and self.world == 1
             self._adam_hi = split if fused else self.n_params
 
             def coarse():
@@ -813,9 +813,17 @@ class NGPTrainer:
                 bs.wait_stream(cs)
                 with torch.cuda.stream(bs):
                     coarse()
-                vren._ok(HGL.ngp_hash_binned_accum(*args, vren._stream()), "hash_binned_accum")
+                if fused:
+                    t = HG.MLP_PARAMS
+                    vren._ok(HGL.ngp_hash_binned_accum_adam(
+                        *args, _p(self.params[t:]), _p(self.exp_avg[t:]), _p(self.exp_avg_sq[t:]),
+                        _p(self.params16[t:]), _p(self.lr_dev), ctypes_float(0.9), ctypes_float(0.999),
+                        ctypes_float(1e-15), _p(self.dctr), ctypes_float(1.0 / self.world), vren._stream()),
+                        "hash_binned_accum_adam")
+                else:
+                    vren._ok(HGL.ngp_hash_binned_accum(*args, vren._stream()), "hash_binned_accum")
                 self._ev("hash_binned_apply", 1)
-                if adam_split:
+                if adam_split and not fused:
                     self._adam(split, self.params.numel(), vren._stream())
             else:
                 bs.wait_stream(cs)
@@ -883,7 +891,7 @@ class NGPTrainer:
     def fused_params(self):
         """Parameters whose Adam runs inside the binned accumulation (the binned
         hash levels; single process, hybrid/binned backward), 0 otherwise."""
-        if not (self.fused_adam and self.world == 1 and self.hash_backward != "atomic" and not self.coarse_after_write):
+        if not (self.fused_adam and self.world == 1 and self.hash_backward != "atomic"):
             return 0
         return self.n_params - (HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo])
 

@@ -411,6 +411,12 @@ int ngp_hash_binned_apply_adam(const float* xyzs, int64_t n, const int64_t* n_de
                                int64_t max_samples, int level_lo, int merge_hi, float* params, float* exp_avg,
                                float* exp_avg_sq, void* params_f16, const float* lr_dev, float beta1, float beta2,
                                float eps, const int64_t* step_dev, float grad_scale, void* stream);
+/* The accumulation launch of ngp_hash_binned_apply_adam alone (after
+ * ngp_hash_binned_write), so other work can be ordered between the two. */
+int ngp_hash_binned_accum_adam(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
+                               int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
+                               void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
+                               const int64_t* step_dev, float grad_scale, void* stream);
 /* ngp_hash_backward restricted to levels [level_lo, level_hi). */
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
