@@ -249,3 +249,34 @@ def test_fused_adam_matches_separate_adam(spr, monkeypatch):
             assert float((fa - fb).abs().max()) <= 2e-6 * max(1.0, float(fb.abs().max()))
         ca, cb = a[:split].float(), b[:split].float()
         assert float((ca - cb).abs().max()) <= 1e-5 * max(1.0, float(cb.abs().max()))
+
+
+def test_fused_adam_matches_separate_adam_cascaded(monkeypatch):
+    """The garden-shaped configuration (scale 16: 6 cascades, every hash level
+    binned, the MLP's Adam alone outside the accumulation): fused vs separate
+    FusedAdam from the same state and batch."""
+    import hashgrid as HG
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("NGP_FUSED_ADAM", fused)
+        sc = S.AnalyticScene(W=200, H=200, n_images=10)
+        tr = NGPTrainer(scale=16.0, batch_size=2048, device=DEV, seed=3)
+        with torch.no_grad():
+            g = torch.Generator().manual_seed(11)
+            tr.params[10240:] = ((torch.rand(tr.params.numel() - 10240, generator=g) * 2 - 1) * 2.0).to(DEV)
+            tr.params16.copy_(tr.params.half())
+        tr.global_step = 1
+        gen = torch.Generator().manual_seed(3)
+        img, pix = sc.sample_batch(2048, gen)
+        noise = torch.rand(2048, generator=gen)
+        o, d = sc.rays(img, pix)
+        tr.step(img.to(DEV), pix.to(DEV), sc.gt_rgb_rays(o, d).to(DEV), sc.directions.to(DEV), sc.poses.to(DEV),
+                noise=noise.to(DEV), apply_adam=True)
+        torch.cuda.synchronize()
+        assert tr.bin_level_lo == 0 and float(tr.grad.abs().max()) == 0.0
+        outs.append([t.clone() for t in (tr.params, tr.exp_avg, tr.exp_avg_sq)])
+    for a, b in zip(outs[0], outs[1]):
+        fa, fb = a[HG.MLP_PARAMS:], b[HG.MLP_PARAMS:]
+        assert float((fa == fb).float().mean()) > 0.999
+        assert float((fa - fb).abs().max()) <= 2e-6 * max(1.0, float(fb.abs().max()))
+        assert float((a[:HG.MLP_PARAMS] - b[:HG.MLP_PARAMS]).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
