@@ -442,8 +442,9 @@ def main():
             "dtype": "fp16 field (MLP weight gradients on bf16 MFMA operands) / fp32 march, composite, Adam",
             "data": "synthetic (analytic sphere+box scene, 100 views 800x800, Lego intrinsics; random-init weights "
                     f"trained {args.pretrain} setup steps)",
-            "config": {"workload": "lego-shaped training step: 8192 rays/rank, scale 0.5, 128^3 grid, L=16 F=2 "
-                                   "T=2^19 hash, 64-wide MLPs, raw loss, Adam lr 1e-2",
+            "config": {"workload": (f"{'lego' if args.scale <= 0.5 else 'garden'}-shaped training step: {R} rays/rank, "
+                                    f"scale {args.scale:g}, {trainer.cascades} x 128^3 grid, L=16 F=2 T=2^19 hash, "
+                                    f"64-wide MLPs, raw loss, Adam lr 1e-2"),
                        "batch_rays_per_gpu": R, "global_batch_rays": R * world, "pretrain_steps": args.pretrain,
                        "rm_samples_per_ray": round(rm_s, 2), "vr_samples_per_ray": round(vr_s, 2),
                        "field_evaluated_per_ray": round(ev_s, 2),
