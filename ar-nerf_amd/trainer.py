@@ -245,6 +245,10 @@ class NGPTrainer:
         self.timer = None
         # world > 1 graph replays run as segments with the collectives between them
         self._segmented = False
+        # world > 1: the hash backward as separate graph segments, the first bucket's
+        # reduce-scatter overlapping the binned levels (NGP_RS_OVERLAP=0: one segment, then both)
+        self._seg_split = os.environ.get("NGP_RS_OVERLAP", "1") == "1"
+        self.comm_stream = torch.cuda.Stream(device=dev) if torch.cuda.is_available() else None
         self._throttle_q = []  # events of every THROTTLE_EVERY-th step (train_step)
 
     @staticmethod
@@ -564,7 +568,15 @@ class NGPTrainer:
             self._run_graph(key, lambda: self._graph_body(k, gt, directions, poses, update_after))
         else:  # collectives between graph segments (no RCCL inside captures)
             self._run_graph(key + ("compute",), lambda: self._segment_compute(k, gt, directions, poses, update_after))
-            self._reduce_grads()
+            if self._seg_split and self.hash_backward != "atomic":
+                cs = torch.cuda.current_stream()
+                self.bwd_stream.wait_stream(cs)
+                with torch.cuda.stream(self.bwd_stream):
+                    self._run_graph(key + ("coarse",), self._segment_coarse)
+                self._run_graph(key + ("apply",), self._segment_apply)
+                self._reduce_grads_overlapped(self.bwd_stream)
+            else:
+                self._reduce_grads()
             self._run_graph(key + ("adam",), self._segment_adam)
             self._gather_params16()
             if update_after:  # (every 16 steps) eager: the update has its own collectives
@@ -618,6 +630,37 @@ class NGPTrainer:
             self._segmented = False
         if fork is not None:
             cs.wait_stream(self.march_stream)
+
+    def _segment_coarse(self):
+        """world > 1 graph segment (side stream): the atomic coarse hash levels."""
+        HGL = HG._lib()
+        vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                                              HG.ctypes.byref(self.grid.desc), _p(self.denc),
+                                              _p(self.grad[HG.MLP_PARAMS:]), 0, self.bin_level_lo, vren._stream()),
+                 "hash_backward_levels")
+
+    def _segment_apply(self):
+        """world > 1 graph segment (main stream): the binned hash levels."""
+        HGL = HG._lib()
+        vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                                           HG.ctypes.byref(self.grid.desc), _p(self.denc),
+                                           _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
+                                           self.bin_level_lo, self.bin_merge_hi, vren._stream()), "hash_binned_apply")
+
+    def _reduce_grads_overlapped(self, coarse_stream):
+        """Reduce-scatter of bucket 0 ([MLP | coarse levels], complete once the
+        coarse segment on `coarse_stream` is) on the comm stream while the
+        binned levels run on the main stream, then bucket 1 after them; the
+        main stream waits for both and zeroes the local gradient."""
+        cs, comm = torch.cuda.current_stream(), self.comm_stream
+        comm.wait_stream(coarse_stream)
+        for i, ((a, b), gs) in enumerate(zip(self.buckets, self._gshard)):
+            if i == 1 or len(self.buckets) == 1:
+                comm.wait_stream(cs)
+            with torch.cuda.stream(comm):
+                ddp.reduce_scatter_(self._gbuf[a:b], gs, self.pg)
+        cs.wait_stream(comm)
+        self._gbuf.zero_()
 
     def _segment_adam(self):
         self._adam_shards()
@@ -757,6 +800,13 @@ class NGPTrainer:
                                             _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
         at("after_mlp_bwd")
+        if self._segmented and self._seg_split and hybrid:
+            # (world > 1 graph segments: the hash backward runs as two more
+            # graphs -- coarse levels on the side stream, binned levels here --
+            # so the reduce-scatter of the [MLP | coarse] bucket overlaps the
+            # binned levels; _replay / _segment_coarse / _segment_apply)
+            cs.wait_stream(bs)
+            return self.out_loss
         self._ev("hash_bwd", 0)
         if hybrid:
             # atomic coarse levels on the side stream and binned fine levels
