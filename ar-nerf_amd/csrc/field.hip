@@ -1195,8 +1195,14 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
                                                        const int64_t* __restrict__ n_dev,
                                                        const int32_t* __restrict__ sidx, GridArgs ga,
                                                        const float* __restrict__ denc, float* __restrict__ grad,
-                                                       int lo, int hi) {
+                                                       int lo, int hi, float* __restrict__ rep = nullptr,
+                                                       int rep_hi = 0, uint32_t rep_stride = 0, int nrep = 1) {
     float sink = 0.f;
+    // levels below rep_hi add into this block's replica of their gradient
+    // range (ngp_hash_backward_levels_rep): the coarsest levels are a few
+    // hundred KB that every sample touches, so their memory-side atomics
+    // queue on few lines; nrep copies spread them (summed afterwards)
+    float* const grep = rep ? rep + (size_t)(blockIdx.x % nrep) * rep_stride : grad;
     __shared__ LevelLds lv;
     // the wave's 16 denc rows, staged once per iteration with coalesced 16-B
     // loads (one global round trip instead of one per level)
@@ -1230,6 +1236,7 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
 #pragma unroll 1
         for (int l = lo; l < hi; ++l) {
             const float gd = drow[wv][s][2 * l + f];
+            float* const dst = l < rep_hi ? grep : grad;
             const float sc = lv.scale[l];
             const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
             const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
@@ -1282,12 +1289,35 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
             for (int yz = 0; yz < 4; ++yz) {
                 const bool head = (heads[yz] >> lane) & 1ull;
                 if (MODE == 1 || MODE == 4) sink += head && valid ? v[yz] : 0.f;
-                else if (MODE == 2) { if (head && valid) grad[2 * (size_t)idx[yz] + f] = v[yz]; }
-                else if ((head || MODE == 3) && valid) atomicAdd(&grad[2 * (size_t)idx[yz] + f], v[yz]);
+                else if (MODE == 2) { if (head && valid) dst[2 * (size_t)idx[yz] + f] = v[yz]; }
+                else if ((head || MODE == 3) && valid) atomicAdd(&dst[2 * (size_t)idx[yz] + f], v[yz]);
             }
         }
     }
     if ((MODE == 1 || MODE == 4) && sink == 1234.5f) grad[threadIdx.x] = sink;
+}
+
+// grad[i] += sum_r rep[r][i]; rep[r][i] = 0 (i < n4 float4 groups), replicas
+// summed in order r = 0..nrep-1; all of a lane's loads are issued first
+template <int MAXR>
+__global__ void __launch_bounds__(256) rep_reduce_kernel(float* __restrict__ grad, float* __restrict__ rep,
+                                                         uint32_t n4, uint32_t stride4, int nrep) {
+    float4* g4 = reinterpret_cast<float4*>(grad);
+    float4* r4 = reinterpret_cast<float4*>(rep);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+        float4 b[MAXR];
+#pragma unroll
+        for (int r = 0; r < MAXR; ++r)
+            if (r < nrep) b[r] = r4[(size_t)r * stride4 + i];
+        float4 a = g4[i];
+#pragma unroll
+        for (int r = 0; r < MAXR; ++r)
+            if (r < nrep) {
+                a.x += b[r].x; a.y += b[r].y; a.z += b[r].z; a.w += b[r].w;
+                r4[(size_t)r * stride4 + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        g4[i] = a;
+    }
 }
 
 }  // namespace ngp
@@ -1528,6 +1558,45 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
     else
         NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<0><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
     return ngp_launch_status();
+}
+
+int ngp_hash_backward_levels_rep(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                                 const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
+                                 int level_hi, float* rep, int rep_levels, int n_rep, int fold, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0 && 0 <= level_lo && level_lo <= level_hi && level_hi <= L);
+    NGP_CHECK_ARG(0 <= rep_levels && rep_levels <= level_hi && n_rep >= 1 && n_rep <= 64);
+    if (rep_levels == 0 || !rep)
+        return ngp_hash_backward_levels(xyzs, n, n_dev, sample_idx, grid, denc, grad_table, level_lo, level_hi,
+                                        stream);
+    if (n == 0 || level_lo == level_hi) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && denc && grad_table && ((uintptr_t)denc & 15) == 0);
+    NGP_CHECK_ARG(((uintptr_t)grad_table & 15) == 0 && ((uintptr_t)rep & 15) == 0);
+    // replicas cover table entries [0, offsets[rep_levels]) (x 2 features)
+    const uint32_t nfl = 2u * grid->offsets[rep_levels];
+    NGP_CHECK_ARG(nfl % 4 == 0);
+    static const unsigned cap = (unsigned)std::max(1, getenv("NGP_HASH_BWD_BLOCKS") ? atoi(getenv("NGP_HASH_BWD_BLOCKS"))
+                                                                                    : 8192);
+    const unsigned blocks = persistent_blocks(n, 64, cap);
+    hipStream_t s = as_stream(stream);
+    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<0><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi, rep, rep_levels, nfl, n_rep));
+    if (!fold) return ngp_launch_status();  // the caller folds them (ngp_hash_binned_accum_adam_dense)
+    const uint32_t n4 = nfl / 4;
+    const unsigned rb = std::min(2048u, (n4 + 255) / 256);
+    if (n_rep <= 8)
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, rep_reduce_kernel<8><<<rb, 256, 0, s>>>(grad_table, rep, n4, n4, n_rep));
+    else if (n_rep <= 16)
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, rep_reduce_kernel<16><<<rb, 256, 0, s>>>(grad_table, rep, n4, n4, n_rep));
+    else
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, rep_reduce_kernel<64><<<rb, 256, 0, s>>>(grad_table, rep, n4, n4, n_rep));
+    return ngp_launch_status();
+}
+
+size_t ngp_hash_backward_rep_floats(const ngp_hashgrid_t* grid, int rep_levels, int n_rep) {
+    if (!grid || rep_levels < 0 || rep_levels > L || n_rep < 1) return 0;
+    return (size_t)n_rep * 2u * grid->offsets[rep_levels];
 }
 
 int ngp_field_backward(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,

@@ -448,12 +448,10 @@ __device__ __forceinline__ uint32_t bucket_level(const BinArgs& ba, uint32_t b) 
 }
 
 // Adam over params [4e, 4e+4) of a bucket range (entries 2e, 2e+1 x 2 features)
-// with gradient g (already x grad_scale); same arithmetic as adam_kernel.
-__device__ __forceinline__ void adam4(const AdamArgs& a, size_t base, uint32_t e, float4 g, float lr, float bc1,
-                                      float bc2) {
-    float4 P = reinterpret_cast<const float4*>(a.p + base)[e];
-    float4 M = reinterpret_cast<const float4*>(a.m + base)[e];
-    float4 V = reinterpret_cast<const float4*>(a.v + base)[e];
+// with gradient g (already x grad_scale) and the state P, M, V already loaded;
+// same arithmetic as adam_kernel.
+__device__ __forceinline__ void adam4_regs(const AdamArgs& a, size_t base, uint32_t e, float4 g, float4 P, float4 M,
+                                           float4 V, float lr, float bc1, float bc2) {
     adam_elem(P.x, M.x, V.x, g.x, lr, a.b1, a.b2, a.eps, bc1, bc2);
     adam_elem(P.y, M.y, V.y, g.y, lr, a.b1, a.b2, a.eps, bc1, bc2);
     adam_elem(P.z, M.z, V.z, g.z, lr, a.b1, a.b2, a.eps, bc1, bc2);
@@ -465,11 +463,32 @@ __device__ __forceinline__ void adam4(const AdamArgs& a, size_t base, uint32_t e
     reinterpret_cast<h4*>(a.p16 + base)[e] = h4{(_Float16)P.x, (_Float16)P.y, (_Float16)P.z, (_Float16)P.w};
 }
 
+__device__ __forceinline__ void adam4(const AdamArgs& a, size_t base, uint32_t e, float4 g, float lr, float bc1,
+                                      float bc2) {
+    adam4_regs(a, base, e, g, reinterpret_cast<const float4*>(a.p + base)[e],
+               reinterpret_cast<const float4*>(a.m + base)[e], reinterpret_cast<const float4*>(a.v + base)[e], lr, bc1,
+               bc2);
+}
+
+// A dense FusedAdam range stepped by the accumulation's tail (float4 units):
+// [0, n4) of p/m/v/p16/grad, replicas rep[r][j] of groups [rep_off4, rep_off4 + rep4)
+struct DenseAdam {
+    float* p;
+    float* m;
+    float* v;
+    _Float16* p16;
+    float* grad;
+    float* rep;
+    uint32_t n4, rep_off4, rep4;
+    int nrep;
+};
+
 // MODE != 0: diagnostic variants for scripts/diag (1: no LDS adds, 2: no
 // flush, 3: neither)
 template <int MODE, bool FUSED = false>
 __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
-                                                          float* __restrict__ grad, BinWs ws, AdamArgs adam) {
+                                                          float* __restrict__ grad, BinWs ws, AdamArgs adam,
+                                                          DenseAdam da = DenseAdam{}) {
     extern __shared__ __attribute__((aligned(16))) double img[];  // [2][BENT]: feature-major, 8-byte stride
     const uint32_t total = ws.items[nbt];
     const int t = threadIdx.x, lane = t & 63;
@@ -487,11 +506,31 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
         while (l < L - 1 && b >= ba.bbase[l + 1]) ++l;
         const uint32_t lb = b - ba.bbase[l];
         const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
+        const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
+        const bool own = nch == 1 && !overflow && ws.fb[b] == 0;
+        // A fused bucket's Adam state (p, m, v of the range) is loaded before
+        // the records are summed, so its HBM latency hides behind the LDS
+        // accumulation instead of following it (the flush then only computes
+        // and stores).  PF x blockDim.x covers a whole bucket at 1024 threads.
+        constexpr int PF = 4;
+        const uint32_t ng = (MODE & 2) ? 0u : 2 * ne / 4;  // float4 groups of the range
+        float4 pP[PF], pM[PF], pV[PF];
+        if (FUSED && own) {
+#pragma unroll
+            for (int k = 0; k < PF; ++k) {
+                const uint32_t e = t + k * blockDim.x;
+                if (e < ng) {
+                    pP[k] = reinterpret_cast<const float4*>(adam.p + gbase)[e];
+                    pM[k] = reinterpret_cast<const float4*>(adam.m + gbase)[e];
+                    pV[k] = reinterpret_cast<const float4*>(adam.v + gbase)[e];
+                }
+            }
+        }
         for (uint32_t e = t; e < 2 * BENT / 2; e += blockDim.x)
             reinterpret_cast<double2*>(img)[e] = make_double2(0.0, 0.0);
         __syncthreads();
         const uint32_t r0 = ws.rstart[b] + c * CH, r1 = min(ws.rstart[b + 1], r0 + CH);
-        constexpr int U = 4;  // records in flight per thread
+        constexpr int U = FUSED ? 2 : 4;  // records in flight per thread (FUSED: registers hold the Adam state)
         for (uint32_t q0 = r0 + t; q0 < r1; q0 += U * blockDim.x) {
             uint4 v[U];
 #pragma unroll
@@ -545,15 +584,27 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
             }
         }
         __syncthreads();
-        const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
         float* g = grad + gbase;
-        const bool own = nch == 1 && !overflow && ws.fb[b] == 0;
-        for (uint32_t e = t; e < ((MODE & 2) ? 0u : 2 * ne / 4); e += blockDim.x) {
-            // entries 2e, 2e+1 x features 0, 1 -> grad[4e .. 4e+3]
+        // entries 2e, 2e+1 x features 0, 1 -> grad[4e .. 4e+3]
+        auto image4 = [&](uint32_t e) {
             const double2 f0 = reinterpret_cast<const double2*>(img)[e];
             const double2 f1 = reinterpret_cast<const double2*>(img + BENT)[e];
-            const float4 v = make_float4((float)f0.x, (float)f1.x, (float)f0.y, (float)f1.y);
-            if (FUSED && own) {  // the range's whole gradient is this image (the memory copy is zero)
+            return make_float4((float)f0.x, (float)f1.x, (float)f0.y, (float)f1.y);
+        };
+        uint32_t e0 = t;
+        if (FUSED && own) {  // the range's whole gradient is this image (the memory copy is zero)
+            const float sc = adam.grad_scale;
+#pragma unroll
+            for (int k = 0; k < PF; ++k, e0 += blockDim.x) {
+                if (e0 >= ng) break;
+                const float4 v = image4(e0);
+                adam4_regs(adam, gbase, e0, make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc), pP[k], pM[k], pV[k],
+                           lr, bc1, bc2);
+            }
+        }
+        for (uint32_t e = e0; e < ng; e += blockDim.x) {
+            const float4 v = image4(e);
+            if (FUSED && own) {  // (blocks narrower than PF x the range: the rest from memory)
                 const float sc = adam.grad_scale;
                 adam4(adam, gbase, e, make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc), lr, bc1, bc2);
             } else if (own) {  // sole writer of this range: read-add-store keeps the += contract
@@ -577,6 +628,28 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
             const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
             for (uint32_t e = t; e < 2 * ne / 4; e += blockDim.x)
                 adam4(adam, gbase, e, make_float4(0.f, 0.f, 0.f, 0.f), lr, bc1, bc2);
+        }
+        if (da.n4) {  // the dense range (MLP + atomic coarse levels), replicas folded in order
+            const AdamArgs dargs{da.p, da.m, da.v, da.p16, nullptr, nullptr, adam.b1, adam.b2, adam.eps, 0.f};
+            float4* g4 = reinterpret_cast<float4*>(da.grad);
+            float4* r4 = reinterpret_cast<float4*>(da.rep);
+            const float sc = adam.grad_scale;
+            for (uint32_t i = blockIdx.x * blockDim.x + t; i < da.n4; i += gridDim.x * blockDim.x) {
+                const float4 P = reinterpret_cast<const float4*>(da.p)[i];
+                const float4 M = reinterpret_cast<const float4*>(da.m)[i];
+                const float4 V = reinterpret_cast<const float4*>(da.v)[i];
+                float4 G = g4[i];
+                const uint32_t j = i - da.rep_off4;
+                if (i >= da.rep_off4 && j < da.rep4) {
+                    for (int r = 0; r < da.nrep; ++r) {
+                        const float4 b = r4[(size_t)r * da.rep4 + j];
+                        G.x += b.x; G.y += b.y; G.z += b.z; G.w += b.w;
+                        r4[(size_t)r * da.rep4 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+                adam4_regs(dargs, 0, i, make_float4(G.x * sc, G.y * sc, G.z * sc, G.w * sc), P, M, V, lr, bc1, bc2);
+                g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
     }
 }
@@ -636,7 +709,7 @@ size_t ngp_hash_backward_binned_workspace(int64_t max_samples) {
 static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                        const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
                        int64_t max_samples, int level_lo, int merge_hi, int phase, void* stream,
-                       const AdamArgs* adam = nullptr) {
+                       const AdamArgs* adam = nullptr, const DenseAdam& da = DenseAdam{}) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
@@ -680,7 +753,7 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
         }
         static const unsigned capB = resident_blocks(hash_accum_kernel<0>, 1024, lds);
         if (adam) {
-            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0, true><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam));
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0, true><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam, da));
             NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<nbt, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam));
         } else {
             NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}));
@@ -743,6 +816,30 @@ int ngp_hash_binned_accum_adam(const ngp_hashgrid_t* grid, float* grad_table, vo
     static const float dummy[1] = {0.f};
     return hash_binned(dummy, 1, nullptr, nullptr, grid, nullptr, grad_table, workspace, max_samples, level_lo,
                        merge_hi, 4, stream, &a);
+}
+
+int ngp_hash_binned_accum_adam_dense(const ngp_hashgrid_t* grid, float* grad, void* workspace, int64_t max_samples,
+                                     int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
+                                     void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
+                                     const int64_t* step_dev, float grad_scale, int64_t table_offset, int64_t dense_n,
+                                     float* rep, int64_t rep_n, int n_rep, void* stream) {
+    NGP_CHECK_ARG(grid && grad && params && exp_avg && exp_avg_sq && params_f16 && lr_dev && step_dev);
+    NGP_CHECK_ARG(((uintptr_t)params & 15) == 0 && ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0 &&
+                  ((uintptr_t)params_f16 & 7) == 0 && ((uintptr_t)grad & 15) == 0);
+    NGP_CHECK_ARG(table_offset >= 0 && table_offset % 4 == 0 && dense_n >= 0 && dense_n % 4 == 0);
+    NGP_CHECK_ARG(dense_n <= 0x7fffffffLL && rep_n >= 0 && rep_n % 4 == 0 && table_offset + rep_n <= dense_n);
+    NGP_CHECK_ARG(rep_n == 0 || (rep && ((uintptr_t)rep & 15) == 0 && n_rep >= 1 && n_rep <= 64));
+    // the binned levels start at table offset 2 * offsets[level_lo]: the dense range must end there
+    NGP_CHECK_ARG(level_lo >= 0 && level_lo < L && dense_n == table_offset + 2 * (int64_t)grid->offsets[level_lo]);
+    const int64_t t = table_offset;
+    const AdamArgs a{params + t, exp_avg + t, exp_avg_sq + t, (_Float16*)params_f16 + t, lr_dev, step_dev, beta1,
+                     beta2, eps, grad_scale};
+    DenseAdam da{params, exp_avg, exp_avg_sq, (_Float16*)params_f16, grad, rep, (uint32_t)(dense_n / 4),
+                 (uint32_t)(table_offset / 4), (uint32_t)(rep_n / 4), n_rep};
+    if (rep_n == 0) da.rep4 = 0;
+    static const float dummy[1] = {0.f};
+    return hash_binned(dummy, 1, nullptr, nullptr, grid, nullptr, grad + t, workspace, max_samples, level_lo,
+                       merge_hi, 4, stream, &a, da);
 }
 
 int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,

@@ -159,6 +159,12 @@ class NGPTrainer:
         # NGP_FUSED_ADAM=0: one FusedAdam launch over all params after the backward
         # (else the binned levels are stepped inside their accumulation, bit-identical)
         self.fused_adam = os.environ.get("NGP_FUSED_ADAM", "1") == "1"
+        # NGP_DENSE_IN_ACCUM=1 (with fused_adam + adam_split): the MLP + coarse levels' Adam
+        # (and the coarse replica fold) in the binned accumulation's tail instead of two
+        # launches on the side stream -- measured slower (the accumulation then waits for
+        # the coarse stream, ~10 us join, and grows by the dense Adam's 23 us;
+        # profiles/r02/ab/dense_in_accum.txt), so off by default
+        self.dense_in_accum = os.environ.get("NGP_DENSE_IN_ACCUM", "0") == "1"
         self._adam_hi = None
         self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "1") == "1"
         # the training forward's encode and MLPs in one launch (pair-major enc as split_forward;
@@ -216,6 +222,17 @@ class NGPTrainer:
             self.bin_max_samples = R * bin_samples_per_ray
             nbytes = HG._lib().ngp_hash_backward_binned_workspace(self.bin_max_samples)
             self.bin_ws = torch.empty((nbytes + 255) // 256, 64, dtype=torch.int32, device=dev)
+        # coarse atomic levels [0, coarse_rep_levels) add into coarse_rep replicas of their
+        # gradient range, folded afterwards (ngp_hash_backward_levels_rep): the coarsest
+        # levels are a few hundred KB every sample touches (NGP_COARSE_REP=0: off)
+        self.coarse_rep = int(os.environ.get("NGP_COARSE_REP", "8"))
+        self.coarse_rep_levels = min(int(os.environ.get("NGP_COARSE_REP_LEVELS", "4")), self.bin_level_lo) \
+            if hash_backward != "atomic" else 0
+        self.rep_buf = None
+        if self.coarse_rep > 0 and self.coarse_rep_levels > 0:
+            nrep = HG._lib().ngp_hash_backward_rep_floats(HG.ctypes.byref(self.grid.desc), self.coarse_rep_levels,
+                                                          self.coarse_rep)
+            self.rep_buf = torch.zeros(nrep, **f)
         self.bg = torch.ones(3, **f) if self.esf == 0 else torch.zeros(3, **f)  # models/rendering.py:287-296
         self._bg_rand = torch.zeros(3, **f)
         self.gen = torch.Generator(device=dev)
@@ -631,13 +648,19 @@ class NGPTrainer:
         if fork is not None:
             cs.wait_stream(self.march_stream)
 
+    def _coarse_levels(self, fold=True):
+        """The atomic coarse hash levels [0, bin_level_lo) on the current stream
+        (fold=False: their replicated part stays in rep_buf for the accumulation)."""
+        vren._ok(HG._lib().ngp_hash_backward_levels_rep(
+            _p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
+            _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), 0, self.bin_level_lo,
+            _p(self.rep_buf) if self.rep_buf is not None else None,
+            self.coarse_rep_levels if self.rep_buf is not None else 0, max(1, self.coarse_rep), int(fold),
+            vren._stream()), "hash_backward_levels")
+
     def _segment_coarse(self):
         """world > 1 graph segment (side stream): the atomic coarse hash levels."""
-        HGL = HG._lib()
-        vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                                              HG.ctypes.byref(self.grid.desc), _p(self.denc),
-                                              _p(self.grad[HG.MLP_PARAMS:]), 0, self.bin_level_lo, vren._stream()),
-                 "hash_backward_levels")
+        self._coarse_levels()
 
     def _segment_apply(self):
         """world > 1 graph segment (main stream): the binned hash levels."""
@@ -819,10 +842,7 @@ class NGPTrainer:
 
             def coarse():
                 self._ev("hash_bwd_coarse", 0)
-                vren._ok(HGL.ngp_hash_backward_levels(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                      _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
-                                                      _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), 0,
-                                                      self.bin_level_lo, vren._stream()), "hash_backward_levels")
+                self._coarse_levels()
                 self._ev("hash_bwd_coarse", 1)
                 # single process: Adam of the MLP + coarse levels right after them
                 # (no all-reduce orders it after the whole gradient)
@@ -850,7 +870,35 @@ class NGPTrainer:
                 if adam_split and not fused:
                     self._adam(split, self.params.numel(), vren._stream())
 
-            if self.coarse_after_write:
+            if fused and adam_split and self.dense_in_accum:
+                # coarse levels (replicas unfolded) on the side stream beside the
+                # record write; then one accumulation launch sums the binned levels
+                # with their FusedAdam and, in its tail, folds the replicas and
+                # steps the dense range [MLP | coarse levels] (no separate Adam)
+                bs.wait_stream(cs)
+                with torch.cuda.stream(bs):
+                    self._ev("hash_bwd_coarse", 0)
+                    self._coarse_levels(fold=False)
+                    self._ev("hash_bwd_coarse", 1)
+                cs.wait_event(planned)
+                self._ev("hash_binned_apply", 0)
+                desc = HG.ctypes.byref(self.grid.desc)
+                t = HG.MLP_PARAMS
+                vren._ok(HGL.ngp_hash_binned_write(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                   _p(self.sample_idx), desc, _p(self.denc), _p(self.grad[t:]),
+                                                   _p(self.bin_ws), self.bin_max_samples, self.bin_level_lo,
+                                                   self.bin_merge_hi, vren._stream()), "hash_binned_write")
+                cs.wait_stream(bs)
+                rep = self.rep_buf is not None
+                vren._ok(HGL.ngp_hash_binned_accum_adam_dense(
+                    desc, _p(self.grad), _p(self.bin_ws), self.bin_max_samples, self.bin_level_lo,
+                    self.bin_merge_hi, _p(self.params), _p(self.exp_avg), _p(self.exp_avg_sq), _p(self.params16),
+                    _p(self.lr_dev), ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                    ctypes_float(1.0 / self.world), t, split, _p(self.rep_buf) if rep else None,
+                    2 * self.grid.offsets[self.coarse_rep_levels] if rep else 0, max(1, self.coarse_rep),
+                    vren._stream()), "hash_binned_accum_adam_dense")
+                self._ev("hash_binned_apply", 1)
+            elif self.coarse_after_write:
                 # coarse atomics beside the accumulation only (the record write
                 # runs alone: it slowed ~4x beside the memory-side atomics)
                 cs.wait_event(planned)
@@ -944,6 +992,13 @@ class NGPTrainer:
         if not (self.fused_adam and self.world == 1 and self.hash_backward != "atomic"):
             return 0
         return self.n_params - (HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo])
+
+    def dense_accum_params(self):
+        """Parameters of the dense range [MLP | atomic coarse levels] whose Adam
+        runs in the binned accumulation's tail (dense_in_accum), 0 otherwise."""
+        if not (self.fused_params() and self.dense_in_accum and self.adam_split and self.overlap_hash_bwd):
+            return 0
+        return HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
 
     def _adam(self, lo, hi, s):
         """FusedAdam over params[lo:hi] (16-byte aligned bounds).  lr and the

@@ -417,10 +417,37 @@ int ngp_hash_binned_accum_adam(const ngp_hashgrid_t* grid, float* grad_table, vo
                                int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
                                void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
                                const int64_t* step_dev, float grad_scale, void* stream);
+/* ngp_hash_binned_accum_adam plus, in the same launch after the buckets,
+ * FusedAdam of the dense range [0, dense_n) of the FULL parameter vector
+ * (MLP + the atomic coarse levels; params / exp_avg / exp_avg_sq / params_f16
+ * / grad here point at element 0 of the vector, the table at table_offset)
+ * from grad + the n_rep replicas of ngp_hash_backward_levels_rep(fold = 0)
+ * covering table floats [0, rep_n) (folded in replica order, then zeroed,
+ * grad zeroed): bit-identical to folding the replicas and running
+ * ngp_adam_step_dev over [0, dense_n).  dense_n, table_offset, rep_n:
+ * multiples of 4.  The coarse levels' gradient must be complete on entry. */
+int ngp_hash_binned_accum_adam_dense(const ngp_hashgrid_t* grid, float* grad, void* workspace, int64_t max_samples,
+                                     int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
+                                     void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
+                                     const int64_t* step_dev, float grad_scale, int64_t table_offset, int64_t dense_n,
+                                     float* rep, int64_t rep_n, int n_rep, void* stream);
 /* ngp_hash_backward restricted to levels [level_lo, level_hi). */
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
                              int level_hi, void* stream);
+/* ngp_hash_backward_levels whose levels < rep_levels add into n_rep
+ * replicas of their gradient range (workgroup w into replica w % n_rep), then
+ * one launch folds the replicas into grad_table and zeroes them.  The
+ * coarsest levels are a few hundred KB that every sample touches: their
+ * memory-side atomics queue on few lines, replicas spread them.  rep holds
+ * ngp_hash_backward_rep_floats(grid, rep_levels, n_rep) floats, 16-byte
+ * aligned, zero on the first call (each call leaves it zero).  Same sums as
+ * ngp_hash_backward_levels up to fp32 summation order.  fold = 0 leaves the
+ * sums in the replicas for ngp_hash_binned_accum_adam_dense to fold. */
+int ngp_hash_backward_levels_rep(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                                 const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
+                                 int level_hi, float* rep, int rep_levels, int n_rep, int fold, void* stream);
+size_t ngp_hash_backward_rep_floats(const ngp_hashgrid_t* grid, int rep_levels, int n_rep);
 
 /* ------------------------------------------------------ training step */
 /* Fused compositing + NeRFLoss + compositing backward for one training batch:

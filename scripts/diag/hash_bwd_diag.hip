@@ -3,6 +3,7 @@
 // its time into compute, scatter-shape and atomic cost.  scripts/diag/hash_bwd.py
 #include "../../ar-nerf_amd/csrc/field.hip"
 #include "../../ar-nerf_amd/csrc/hashbin.hip"
+#include "../../ar-nerf_amd/csrc/host.hip"
 
 extern "C" int ngp_diag_hash_bwd(int mode, int lo, int hi, int blocks_cap, const float* xyzs, int64_t n,
                                  const int64_t* n_dev, const int32_t* sidx, const ngp_hashgrid_t* grid,
@@ -31,7 +32,7 @@ extern "C" int ngp_diag_hash_accum(int mode, int threads, const ngp_hashgrid_t* 
     const int64_t tiles_cap = (max_samples + TILE - 1) / TILE;
     BinArgs ba;
     uint32_t nbt;
-    st = bin_args(grid, tiles_cap, lo, ba, nbt);
+    st = bin_args(grid, tiles_cap, lo, 0, ba, nbt);
     if (st) return st;
     BinWs ws;
     bin_ws_bytes(tiles_cap, &ws, workspace);
@@ -45,10 +46,10 @@ extern "C" int ngp_diag_hash_accum(int mode, int threads, const ngp_hashgrid_t* 
         attr[mode] = true;
     }
     switch (mode) {
-        case 0: hash_accum_kernel<0><<<256, threads, lds, s>>>(ga, ba, nbt, grad, ws); break;
-        case 1: hash_accum_kernel<1><<<256, threads, lds, s>>>(ga, ba, nbt, grad, ws); break;
-        case 2: hash_accum_kernel<2><<<256, threads, lds, s>>>(ga, ba, nbt, grad, ws); break;
-        case 3: hash_accum_kernel<3><<<256, threads, lds, s>>>(ga, ba, nbt, grad, ws); break;
+        case 0: hash_accum_kernel<0><<<256, threads, lds, s>>>(ga, ba, nbt, grad, ws, AdamArgs{}); break;
+        case 1: hash_accum_kernel<1><<<256, threads, lds, s>>>(ga, ba, nbt, grad, ws, AdamArgs{}); break;
+        case 2: hash_accum_kernel<2><<<256, threads, lds, s>>>(ga, ba, nbt, grad, ws, AdamArgs{}); break;
+        case 3: hash_accum_kernel<3><<<256, threads, lds, s>>>(ga, ba, nbt, grad, ws, AdamArgs{}); break;
         default: return NGP_EINVAL;
     }
     return ngp_launch_status();
@@ -109,7 +110,7 @@ extern "C" int ngp_diag_hash_write(int mode, const float* xyzs, int64_t n, const
     const int64_t tiles_cap = (max_samples + TILE - 1) / TILE;
     BinArgs ba;
     uint32_t nbt;
-    st = bin_args(grid, tiles_cap, lo, ba, nbt);
+    st = bin_args(grid, tiles_cap, lo, 0, ba, nbt);
     if (st) return st;
     BinWs ws;
     bin_ws_bytes(tiles_cap, &ws, workspace);

@@ -304,3 +304,44 @@ def test_hash_backward_binned_matches_atomic(scale, level_cap, level_lo, merge_h
     assert _rel(d_out, d_ref) < 5e-5  # product order (1-fx)*((wy*wz)*g) vs ((wx*wy)*wz)*g + sum order
     # rtol: a coarse entry sums thousands of terms in another order
     torch.testing.assert_close(out.cpu(), ref.cpu(), rtol=1e-4, atol=1e-6 * float(d_ref.abs().max()))
+
+
+@pytest.mark.parametrize("rep_levels,n_rep", [(4, 8), (8, 16), (2, 1)])
+def test_hash_backward_levels_replicated(rep_levels, n_rep):
+    """ngp_hash_backward_levels_rep (levels < rep_levels into n_rep replicas,
+    folded afterwards) == ngp_hash_backward_levels up to fp32 summation order,
+    onto a non-zero gradient (+= contract); the replicas are left zero, so a
+    second call gives the same result."""
+    x = _ray_points(400, 100, 0.5, seed=7)
+    n = x.shape[0]
+    grid = HG.HashGrid(0.5)
+    g = torch.Generator().manual_seed(9)
+    sidx = torch.randperm(n, generator=g)[: n * 3 // 4].sort().values.to(torch.int32)
+    m = sidx.numel()
+    denc = (torch.randn(m, 32, generator=g) * 1e-2).to(DEV)
+    x, sidx = x.to(DEV), sidx.to(DEV)
+    n_dev = torch.tensor([m], dtype=torch.int64, device=DEV)
+    base = torch.randn(grid.n_entries * 2, generator=g).to(DEV)
+    L = HG._lib()
+    p = lambda t: vren.c_void_p(t.data_ptr())  # noqa: E731
+    desc = HG.ctypes.byref(grid.desc)
+    ref = base.clone()
+    vren._ok(L.ngp_hash_backward_levels(p(x), n, p(n_dev), p(sidx), desc, p(denc), p(ref), 0, 8, vren._stream()),
+             "hash_backward_levels")
+    rep = torch.zeros(L.ngp_hash_backward_rep_floats(desc, rep_levels, n_rep), device=DEV)
+    assert rep.numel() == n_rep * 2 * grid.offsets[rep_levels]
+    for _ in range(2):
+        out = base.clone()
+        vren._ok(L.ngp_hash_backward_levels_rep(p(x), n, p(n_dev), p(sidx), desc, p(denc), p(out), 0, 8, p(rep),
+                                                rep_levels, n_rep, 1, vren._stream()), "hash_backward_levels_rep")
+        torch.cuda.synchronize()
+        assert float(rep.abs().max()) == 0.0
+        d_ref, d_out = (ref - base).cpu().double(), (out - base).cpu().double()
+        assert float(d_ref[: 2 * grid.offsets[rep_levels]].abs().max()) > 0
+        assert _rel(d_out, d_ref) < 1e-5
+        torch.testing.assert_close(out.cpu(), ref.cpu(), rtol=1e-4, atol=1e-6 * float(d_ref.abs().max()))
+    # argument checks: replicas beyond the atomic levels, replica count bounds
+    assert L.ngp_hash_backward_levels_rep(p(x), n, p(n_dev), p(sidx), desc, p(denc), p(out), 0, 8, p(rep), 9, 8, 1,
+                                          vren._stream()) < 0
+    assert L.ngp_hash_backward_levels_rep(p(x), n, p(n_dev), p(sidx), desc, p(denc), p(out), 0, 8, p(rep), 4, 0, 1,
+                                          vren._stream()) < 0
