@@ -54,8 +54,15 @@ namespace ngp {
 
 // entries per bucket (fp64 LDS image: 2 x BENT x 8 B = 128 KB, one accumulating workgroup per CU;
 // 4096-entry buckets at two per CU measured the same accumulation time and a slower count pass)
-constexpr int BSHIFT = 13, BENT = 1 << BSHIFT;
-constexpr int NBL = 64;                          // bucket slots per level (2^19 / BENT)
+#ifndef NGP_BSHIFT
+#define NGP_BSHIFT 13
+#endif
+constexpr int BSHIFT = NGP_BSHIFT, BENT = 1 << BSHIFT;
+constexpr int NBL = (1 << 19) / BENT;            // bucket slots per level (2^19 / BENT)
+// accumulation workgroup: 8192-entry buckets (128 KB LDS, one per CU) take
+// 1024 threads, 4096-entry buckets (64 KB, two per CU) 512, so that a
+// thread covers 4 float4 groups of its bucket either way (PF below)
+constexpr int ACC_T = BENT / 8;
 constexpr int NSLOT = L * NBL;                   // (level, bucket) slots per tile row
 constexpr int MAXB = 2048;                       // buckets over all levels
 constexpr int TILE = 256;                        // samples per count/write tile
@@ -486,7 +493,7 @@ struct DenseAdam {
 // MODE != 0: diagnostic variants for scripts/diag (1: no LDS adds, 2: no
 // flush, 3: neither)
 template <int MODE, bool FUSED = false>
-__global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
+__global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
                                                           float* __restrict__ grad, BinWs ws, AdamArgs adam,
                                                           DenseAdam da = DenseAdam{}) {
     extern __shared__ __attribute__((aligned(16))) double img[];  // [2][BENT]: feature-major, 8-byte stride
@@ -511,7 +518,7 @@ __global__ void __launch_bounds__(1024) hash_accum_kernel(GridArgs ga, BinArgs b
         // A fused bucket's Adam state (p, m, v of the range) is loaded before
         // the records are summed, so its HBM latency hides behind the LDS
         // accumulation instead of following it (the flush then only computes
-        // and stores).  PF x blockDim.x covers a whole bucket at 1024 threads.
+        // and stores).  PF x blockDim.x covers a whole bucket at ACC_T threads.
         constexpr int PF = 4;
         const uint32_t ng = (MODE & 2) ? 0u : 2 * ne / 4;  // float4 groups of the range
         float4 pP[PF], pM[PF], pV[PF];
@@ -751,12 +758,12 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
                 return NGP_ERANGE;
             attr = true;
         }
-        static const unsigned capB = resident_blocks(hash_accum_kernel<0>, 1024, lds);
+        static const unsigned capB = resident_blocks(hash_accum_kernel<0>, ACC_T, lds);
         if (adam) {
-            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0, true><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam, da));
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0, true><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam, da));
             NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<nbt, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam));
         } else {
-            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0><<<capB, 1024, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}));
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}));
         }
     }
     return ngp_launch_status();

@@ -363,12 +363,22 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    float* __restrict__ v, _Float16* __restrict__ p16, int64_t n4,
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2,
                                                    float grad_scale, int zero_grad, const float* __restrict__ lr_dev,
-                                                   const int64_t* __restrict__ step_dev) {
+                                                   const int64_t* __restrict__ step_dev, float* __restrict__ rep = nullptr,
+                                                   int64_t rep_lo4 = 0, int64_t rep4 = 0, int nrep = 0) {
     adam_bias(lr_dev, step_dev, b1, b2, lr, bc1, bc2);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         float4 P = reinterpret_cast<float4*>(p)[i], Gd = reinterpret_cast<float4*>(grad)[i];
         float4 M = reinterpret_cast<float4*>(m)[i], V = reinterpret_cast<float4*>(v)[i];
+        const int64_t j = i - rep_lo4;
+        if (rep && j >= 0 && j < rep4) {  // gradient replicas (ngp_hash_backward_levels_rep), folded in order
+            float4* r4 = reinterpret_cast<float4*>(rep);
+            for (int r = 0; r < nrep; ++r) {
+                const float4 b = r4[r * rep4 + j];
+                Gd.x += b.x; Gd.y += b.y; Gd.z += b.z; Gd.w += b.w;
+                r4[r * rep4 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
         float* pp = &P.x; float* gp = &Gd.x; float* mp = &M.x; float* vp = &V.x;
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         h4 out;
@@ -975,6 +985,27 @@ int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_av
     NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
                                                                  1.f, grad_scale, zero_grad, lr_dev, step_dev));
+    return ngp_launch_status();
+}
+
+int ngp_adam_step_dev_rep(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16, int64_t n,
+                          const float* lr_dev, float beta1, float beta2, float eps, const int64_t* step_dev,
+                          float grad_scale, int zero_grad, float* rep, int64_t rep_offset, int64_t rep_n, int n_rep,
+                          void* stream) {
+    if (!rep || rep_n == 0)
+        return ngp_adam_step_dev(params, grads, exp_avg, exp_avg_sq, params_f16, n, lr_dev, beta1, beta2, eps,
+                                 step_dev, grad_scale, zero_grad, stream);
+    NGP_CHECK_ARG(n >= 0 && rep_offset >= 0 && rep_n > 0 && rep_offset % 4 == 0 && rep_n % 4 == 0 &&
+                  rep_offset + rep_n <= n && n_rep >= 1 && n_rep <= 64 && ((uintptr_t)rep & 15) == 0);
+    NGP_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && params_f16 && lr_dev && step_dev);
+    if (n % 4 != 0) return NGP_ERANGE;
+    const int64_t n4 = n / 4;
+    int64_t blocks = (n4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
+                                                                 (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
+                                                                 1.f, grad_scale, zero_grad, lr_dev, step_dev, rep,
+                                                                 rep_offset / 4, rep_n / 4, n_rep));
     return ngp_launch_status();
 }
 

@@ -229,6 +229,9 @@ class NGPTrainer:
         self.coarse_rep_levels = min(int(os.environ.get("NGP_COARSE_REP_LEVELS", "4")), self.bin_level_lo) \
             if hash_backward != "atomic" else 0
         self.rep_buf = None
+        # single process: the replicas are folded by the MLP + coarse levels' Adam launch
+        # (NGP_ADAM_REP=0: by a launch of their own before it)
+        self.adam_rep = os.environ.get("NGP_ADAM_REP", "1") == "1"
         if self.coarse_rep > 0 and self.coarse_rep_levels > 0:
             nrep = HG._lib().ngp_hash_backward_rep_floats(HG.ctypes.byref(self.grid.desc), self.coarse_rep_levels,
                                                           self.coarse_rep)
@@ -841,13 +844,15 @@ class NGPTrainer:
             self._adam_hi = split if fused else self.n_params
 
             def coarse():
-                self._ev("hash_bwd_coarse", 0)
-                self._coarse_levels()
-                self._ev("hash_bwd_coarse", 1)
                 # single process: Adam of the MLP + coarse levels right after them
-                # (no all-reduce orders it after the whole gradient)
+                # (no all-reduce orders it after the whole gradient), folding the
+                # coarse gradient replicas itself (one launch less)
+                fold_in_adam = adam_split and self.rep_buf is not None and self.adam_rep
+                self._ev("hash_bwd_coarse", 0)
+                self._coarse_levels(fold=not fold_in_adam)
+                self._ev("hash_bwd_coarse", 1)
                 if adam_split:
-                    self._adam(0, split, vren._stream())
+                    self._adam(0, split, vren._stream(), rep=fold_in_adam)
 
             def apply():
                 self._ev("hash_binned_apply", 0)
@@ -1000,11 +1005,20 @@ class NGPTrainer:
             return 0
         return HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
 
-    def _adam(self, lo, hi, s):
+    def _adam(self, lo, hi, s, rep=False):
         """FusedAdam over params[lo:hi] (16-byte aligned bounds).  lr and the
         step count from device memory (graph replays); dctr[0] = steps taken
-        so far, advanced after the step by ngp_counters_inc."""
+        so far, advanced after the step by ngp_counters_inc.  rep: the coarse
+        levels' gradient replicas (unfolded, fold=False) are folded here
+        (lo <= MLP_PARAMS, hi past the replicated levels)."""
         q = lambda t: _p(t[lo:hi])  # noqa: E731
+        if rep:
+            vren._ok(self.L.ngp_adam_step_dev_rep(
+                q(self.params), q(self.grad), q(self.exp_avg), q(self.exp_avg_sq), q(self.params16), hi - lo,
+                _p(self.lr_dev), ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                ctypes_float(1.0 / self.world), 1, _p(self.rep_buf), HG.MLP_PARAMS - lo,
+                2 * self.grid.offsets[self.coarse_rep_levels], self.coarse_rep, s), "adam")
+            return
         vren._ok(self.L.ngp_adam_step_dev(q(self.params), q(self.grad), q(self.exp_avg), q(self.exp_avg_sq),
                                           q(self.params16), hi - lo, _p(self.lr_dev), ctypes_float(0.9),
                                           ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),

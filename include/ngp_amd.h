@@ -530,6 +530,14 @@ int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
 int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16,
                       int64_t n, const float* lr_dev, float beta1, float beta2, float eps,
                       const int64_t* step_dev, float grad_scale, int zero_grad, void* stream);
+/* ngp_adam_step_dev whose gradient over [rep_offset, rep_offset + rep_n) of
+ * this range is grads + the n_rep replicas of ngp_hash_backward_levels_rep
+ * (fold = 0; replica r at rep + r * rep_n), folded in replica order and
+ * zeroed: bit-identical to folding them first (fold = 1) and stepping. */
+int ngp_adam_step_dev_rep(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16, int64_t n,
+                          const float* lr_dev, float beta1, float beta2, float eps, const int64_t* step_dev,
+                          float grad_scale, int zero_grad, float* rep, int64_t rep_offset, int64_t rep_n, int n_rep,
+                          void* stream);
 /* counters[i] += 1, i < n (n <= 64): advances the device step counters. */
 int ngp_counters_inc(int64_t* counters, int n, void* stream);
 
