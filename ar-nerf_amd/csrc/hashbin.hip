@@ -440,12 +440,13 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
 }
 
 // A bucket whose summed gradient one workgroup owns: a single chunk, no
-// direct adds into its range, no workspace overflow.  With FUSED the
-// accumulation applies Adam to such a bucket straight from its LDS image
-// (its gradient never goes through memory) and hash_adam_residual_kernel
-// steps every other bucket from the gradient in memory.
+// workspace overflow.  With FUSED the accumulation applies Adam to such a
+// bucket straight from its LDS image (plus, for a bucket flagged in fb[], the
+// direct adds the record write made into its range, read back from memory:
+// the same fp32 sum the flush's atomic would form) and
+// hash_adam_residual_kernel steps every other bucket from memory.
 __device__ __forceinline__ bool fused_bucket(const BinWs& ws, uint32_t b, bool overflow) {
-    return !overflow && ws.fb[b] == 0 && ws.items[b + 1] - ws.items[b] <= 1u;
+    return !overflow && ws.items[b + 1] - ws.items[b] <= 1u;
 }
 
 __device__ __forceinline__ uint32_t bucket_level(const BinArgs& ba, uint32_t b) {
@@ -515,6 +516,8 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
         const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
         const bool own = nch == 1 && !overflow && ws.fb[b] == 0;
+        const bool fz = FUSED && nch == 1 && !overflow;  // fused_bucket
+        const bool flagged = ws.fb[b] != 0;               // direct adds in the range
         // A fused bucket's Adam state (p, m, v of the range) is loaded before
         // the records are summed, so its HBM latency hides behind the LDS
         // accumulation instead of following it (the flush then only computes
@@ -522,7 +525,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         constexpr int PF = 4;
         const uint32_t ng = (MODE & 2) ? 0u : 2 * ne / 4;  // float4 groups of the range
         float4 pP[PF], pM[PF], pV[PF];
-        if (FUSED && own) {
+        if (fz) {
 #pragma unroll
             for (int k = 0; k < PF; ++k) {
                 const uint32_t e = t + k * blockDim.x;
@@ -538,12 +541,20 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         __syncthreads();
         const uint32_t r0 = ws.rstart[b] + c * CH, r1 = min(ws.rstart[b + 1], r0 + CH);
         constexpr int U = FUSED ? 2 : 4;  // records in flight per thread (FUSED: registers hold the Adam state)
+        // software-pipelined: the next iteration's records are loaded before
+        // this iteration's are summed (one load latency per item, not per pass)
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t q = r0 + t + u * blockDim.x;
+            v[u] = q < r1 ? ws.rec[q] : make_uint4(0u, 0u, 0u, 0u);
+        }
         for (uint32_t q0 = r0 + t; q0 < r1; q0 += U * blockDim.x) {
-            uint4 v[U];
+            uint4 vn[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t q = q0 + u * blockDim.x;
-                v[u] = q < r1 ? ws.rec[q] : make_uint4(0u, 0u, 0u, 0u);
+                const uint32_t q = q0 + (U + u) * blockDim.x;
+                vn[u] = q < r1 ? ws.rec[q] : make_uint4(0u, 0u, 0u, 0u);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -589,6 +600,8 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
                     atomicAdd(&img[BENT + i1], p11);
                 }
             }
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = vn[u];
         }
         __syncthreads();
         float* g = grad + gbase;
@@ -598,23 +611,33 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
             const double2 f1 = reinterpret_cast<const double2*>(img + BENT)[e];
             return make_float4((float)f0.x, (float)f1.x, (float)f0.y, (float)f1.y);
         };
-        uint32_t e0 = t;
-        if (FUSED && own) {  // the range's whole gradient is this image (the memory copy is zero)
+        // the range's whole gradient: this image (+ the direct adds of a flagged bucket, zeroed after)
+        auto fused_grad = [&](uint32_t e) {
+            float4 v = image4(e);
+            if (flagged) {
+                float4* g4 = reinterpret_cast<float4*>(g) + e;
+                const float4 m = *g4;
+                v.x = m.x + v.x; v.y = m.y + v.y; v.z = m.z + v.z; v.w = m.w + v.w;
+                *g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             const float sc = adam.grad_scale;
+            return make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+        };
+        uint32_t e0 = t;
+        if (fz) {
 #pragma unroll
             for (int k = 0; k < PF; ++k, e0 += blockDim.x) {
                 if (e0 >= ng) break;
-                const float4 v = image4(e0);
-                adam4_regs(adam, gbase, e0, make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc), pP[k], pM[k], pV[k],
-                           lr, bc1, bc2);
+                adam4_regs(adam, gbase, e0, fused_grad(e0), pP[k], pM[k], pV[k], lr, bc1, bc2);
             }
         }
         for (uint32_t e = e0; e < ng; e += blockDim.x) {
+            if (fz) {  // (blocks narrower than PF x the range: the rest from memory)
+                adam4(adam, gbase, e, fused_grad(e), lr, bc1, bc2);
+                continue;
+            }
             const float4 v = image4(e);
-            if (FUSED && own) {  // (blocks narrower than PF x the range: the rest from memory)
-                const float sc = adam.grad_scale;
-                adam4(adam, gbase, e, make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc), lr, bc1, bc2);
-            } else if (own) {  // sole writer of this range: read-add-store keeps the += contract
+            if (own) {  // sole writer of this range: read-add-store keeps the += contract
                 float4 o = reinterpret_cast<const float4*>(g)[e];
                 o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
                 reinterpret_cast<float4*>(g)[e] = o;
@@ -633,8 +656,18 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
             const uint32_t l = bucket_level(ba, b), lb = b - ba.bbase[l];
             const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
             const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
-            for (uint32_t e = t; e < 2 * ne / 4; e += blockDim.x)
-                adam4(adam, gbase, e, make_float4(0.f, 0.f, 0.f, 0.f), lr, bc1, bc2);
+            const bool flagged = ws.fb[b] != 0;  // direct adds only
+            float4* g4 = reinterpret_cast<float4*>(grad + gbase);
+            for (uint32_t e = t; e < 2 * ne / 4; e += blockDim.x) {
+                float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (flagged) {
+                    const float sc = adam.grad_scale;
+                    const float4 m = g4[e];
+                    gv = make_float4(m.x * sc, m.y * sc, m.z * sc, m.w * sc);
+                    g4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                adam4(adam, gbase, e, gv, lr, bc1, bc2);
+            }
         }
         if (da.n4) {  // the dense range (MLP + atomic coarse levels), replicas folded in order
             const AdamArgs dargs{da.p, da.m, da.v, da.p16, nullptr, nullptr, adam.b1, adam.b2, adam.eps, 0.f};
