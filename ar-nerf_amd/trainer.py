@@ -757,6 +757,7 @@ class NGPTrainer:
             if R <= 65536:  # counts min(N_r, K) + scan + list in one launch
                 vren._ok(L.ngp_ray_segments_capped(_p(self.rays_a), R, K, _p(self.act_start), _p(self.eval_total),
                                                    _p(self.stats[3:]), _p(self.eval_idx), s), "segments_capped")
+                at("after_seg0")
             else:
                 vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, None, None, ctypes_float(1e-4),
                                             _p(self.eval_counts), s), "chunk_counts")
