@@ -774,6 +774,13 @@ class NGPTrainer:
                                             _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
                 self._field_indexed(s)
                 lo = hi
+        elif self.fused_field:  # encode + MLPs in one launch over every marched sample
+            self._ev("hash_encode", 0)
+            vren._ok(HGL.ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples), None,
+                                              HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
+                                              _p(self.params16), _p(self.enc), _p(self.sigmas), _p(self.rgbs), None,
+                                              s), "field_encode_mlp")
+            self._ev("hash_encode", 1)
         elif self.split_forward:  # encode (pair-major self.enc), then the MLPs, over every marched sample
             vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.n_samples), None,
                                          HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
