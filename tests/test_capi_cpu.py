@@ -89,3 +89,34 @@ def test_new_entry_points_reject_bad_arguments_without_launching():
     assert L.ngp_distortion_loss_fw(None, None, None, None, 0, None, None, None, None) == 0  # empty: no-op
     g = HG.HashGrid(0.5)
     assert L.ngp_density_input_grad(None, 5, C.byref(g.desc), None, None, None, None, None) == -1
+
+
+def test_gradient_replica_entry_points_check_arguments_without_launching():
+    """ngp_hash_backward_levels_rep / ngp_hash_backward_rep_floats /
+    ngp_adam_step_dev_rep / ngp_hash_binned_accum_adam_dense: sizes and
+    argument checks on the host, before any launch (NGP_EINVAL = -1)."""
+    import ctypes as C
+    L = HG._lib()
+    g = HG.HashGrid(0.5)
+    d = C.byref(g.desc)
+    assert L.ngp_hash_backward_rep_floats(d, 4, 8) == 8 * 2 * g.offsets[4]
+    assert L.ngp_hash_backward_rep_floats(d, 0, 8) == 0
+    assert L.ngp_hash_backward_rep_floats(d, 17, 8) == 0 and L.ngp_hash_backward_rep_floats(d, 4, 0) == 0
+    p = C.c_void_p(16)  # never dereferenced: every call below fails its checks first
+    # replicas beyond the atomic levels, replica count 0 / > 64, negative n
+    assert L.ngp_hash_backward_levels_rep(p, 10, None, None, d, p, p, 0, 8, p, 9, 8, 1, None) == -1
+    assert L.ngp_hash_backward_levels_rep(p, 10, None, None, d, p, p, 0, 8, p, 4, 0, 1, None) == -1
+    assert L.ngp_hash_backward_levels_rep(p, 10, None, None, d, p, p, 0, 8, p, 4, 65, 1, None) == -1
+    assert L.ngp_hash_backward_levels_rep(p, -1, None, None, d, p, p, 0, 8, p, 4, 8, 1, None) == -1
+    f = C.c_float
+    # replica range not a multiple of 4, past the Adam range, misaligned replicas
+    assert L.ngp_adam_step_dev_rep(p, p, p, p, p, 64, p, f(0.9), f(0.999), f(1e-15), p, f(1.0), 1, p, 2, 8, 8,
+                                   None) == -1
+    assert L.ngp_adam_step_dev_rep(p, p, p, p, p, 64, p, f(0.9), f(0.999), f(1e-15), p, f(1.0), 1, p, 0, 68, 8,
+                                   None) == -1
+    assert L.ngp_adam_step_dev_rep(p, p, p, p, p, 64, p, f(0.9), f(0.999), f(1e-15), p, f(1.0), 1, C.c_void_p(20),
+                                   0, 8, 8, None) == -1
+    # dense range that does not end where the binned levels start
+    dense = HG.MLP_PARAMS + 2 * g.offsets[8]
+    assert L.ngp_hash_binned_accum_adam_dense(d, p, p, 1024, 8, 0, p, p, p, p, p, f(0.9), f(0.999), f(1e-15), p,
+                                              f(1.0), HG.MLP_PARAMS, dense + 4, None, 0, 1, None) == -1
