@@ -1,4 +1,6 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-bash scripts/gpu_abn.sh ab_rep3 2 "NGP_COARSE_REP=8" "NGP_COARSE_REP_LEVELS=5" "NGP_COARSE_REP_LEVELS=6" "NGP_COARSE_REP=16"
+mkdir -p gpurun_out/wf
+NGP_WRITE_FIRST=1 timeout -k 10 300 python -u -m pytest tests/test_trainer_gpu.py -x -v --timeout 120 --timeout-method thread -k "fused_adam or step" > gpurun_out/wf/pytest.log 2>&1
+bash scripts/gpu_abn.sh ab_wf 3 "NGP_WRITE_FIRST=0" "NGP_WRITE_FIRST=1"
