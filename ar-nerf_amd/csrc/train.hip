@@ -780,9 +780,18 @@ __global__ void __launch_bounds__(SEG_THREADS) segments_kernel(const int32_t* __
     auto count = [&](int64_t r) -> int64_t {
         return CAPPED ? min(rays_a[3 * r + 2], (int64_t)cap) : (int64_t)counts[r];
     };
-    // 1) prefix of the rows before this block
+    // 1) prefix of the rows before this block: 8 independent loads in flight
+    // per thread (the L2 round trips overlap instead of chaining)
     int64_t acc = 0;
-    for (int64_t r = t; r < r0; r += SEG_THREADS) acc += count(r);
+    int64_t r = t;
+    for (; r + 7 * SEG_THREADS < r0; r += 8 * SEG_THREADS) {
+        int64_t c[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = count(r + k * SEG_THREADS);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += c[k];
+    }
+    for (; r < r0; r += SEG_THREADS) acc += count(r);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if (lane == 0) red[w] = acc;
