@@ -1,6 +1,5 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-mkdir -p gpurun_out/items
-timeout -k 10 300 python -u -m pytest tests/test_trainer_gpu.py tests/test_field_gpu.py -x -v --timeout 120 --timeout-method thread -k "fused_adam or binned" > gpurun_out/items/pytest.log 2>&1
-bash scripts/gpu_abn.sh ab_items 3 "NGP_AMD_LIB=build_ab/base.so" "NGP_X=1"
+mkdir -p gpurun_out/dense2
+timeout -k 10 300 python -u -m pytest tests/test_trainer_gpu.py -x -v --timeout 120 --timeout-method thread -k "dense or fused_adam" > gpurun_out/dense2/pytest.log 2>&1

@@ -280,3 +280,36 @@ def test_fused_adam_matches_separate_adam_cascaded(monkeypatch):
         assert float((fa == fb).float().mean()) > 0.999
         assert float((fa - fb).abs().max()) <= 2e-6 * max(1.0, float(fb.abs().max()))
         assert float((a[:HG.MLP_PARAMS] - b[:HG.MLP_PARAMS]).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
+
+
+def test_dense_adam_in_accumulation_matches_separate_launches(monkeypatch):
+    """NGP_DENSE_IN_ACCUM=1 (ngp_hash_binned_accum_adam_dense: the MLP + coarse
+    levels' FusedAdam and the coarse replica fold in the accumulation's tail)
+    vs the default separate launches, from the same state and batch: the
+    dense range agrees to atomic-order noise, the binned range as in
+    test_fused_adam_matches_separate_adam; gradient and replicas left zero."""
+    import hashgrid as HG
+    outs = []
+    for dense in ("1", "0"):
+        monkeypatch.setenv("NGP_DENSE_IN_ACCUM", dense)
+        sc, tr, img, pix, noise = _setup(table_init=2.0)
+        assert tr.dense_in_accum == (dense == "1")
+        o, d = sc.rays(img, pix)
+        tr.step(img.to(DEV), pix.to(DEV), sc.gt_rgb_rays(o, d).to(DEV), sc.directions.to(DEV), sc.poses.to(DEV),
+                noise=noise.to(DEV), apply_adam=True)
+        torch.cuda.synchronize()
+        assert float(tr.grad.abs().max()) == 0.0
+        if tr.rep_buf is not None:
+            assert float(tr.rep_buf.abs().max()) == 0.0
+        outs.append([t.clone() for t in (tr.params, tr.exp_avg, tr.exp_avg_sq, tr.params16)])
+        split = HG.MLP_PARAMS + 2 * tr.grid.offsets[tr.bin_level_lo]
+    for j, (a, b) in enumerate(zip(outs[0], outs[1])):
+        fa, fb = a[split:].float(), b[split:].float()
+        assert float((fa == fb).float().mean()) > 0.999
+        if j == 3:
+            assert bool(((fa - fb).abs() <= O.ulp16(fb)).all())
+        else:
+            assert float((fa - fb).abs().max()) <= 2e-6 * max(1.0, float(fb.abs().max()))
+        ca, cb = a[:split].float(), b[:split].float()
+        assert float((ca - cb).abs().max()) <= 1e-5 * max(1.0, float(cb.abs().max()))
+        assert float((ca != cb).float().mean()) < 0.5  # mostly bit-identical (same fold order, same Adam)
