@@ -139,6 +139,9 @@ class NGPTrainer:
         # the start (beside the gather-bound encode rather than the VALU-bound MLP
         # backward: +1.5 %, profiles/r02/ab/prefetch_at.txt)
         self.prefetch_at = os.environ.get("NGP_PREFETCH_AT", "start")
+        # NGP_PAIR_STEPS=1: two consecutive steady-state steps per graph replay (_replay_pair)
+        self.pair_steps = os.environ.get("NGP_PAIR_STEPS", "0") == "1"
+        self._ran_ahead = False
         self._bind(self.msets[0])
         self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         # saved encoding: pair-major (8, cap, 4) for the split forward, else row-major (cap, 32)
@@ -543,8 +546,15 @@ class NGPTrainer:
         (NGP_GRAPHS=0: always eager)."""
         gs, ui = self.global_step, self.update_interval
         self._throttle()
+        if self._ran_ahead:  # this step was the second half of the previous call's two-step graph
+            self._ran_ahead = False
+            self.global_step += 1
+            return self.out_loss
         if (self.use_graphs and self._pending is not None and (gs % ui != 0 or self._updated_for == gs)
                 and gs >= self.warmup_steps and self.kernel_events is None and not self.no_prefetch):
+            if (self.pair_steps and self.world == 1 and self.timer is None and (gs + 1) % ui != 0
+                    and (gs + 2) % ui != 0 and gs // self.steps_per_epoch == (gs + 1) // self.steps_per_epoch):
+                return self._replay_pair(gt, directions, poses)
             return self._replay(gt, directions, poses, (gs + 1) % ui == 0)
         return self._on_exec_stream(self._step, ("sample", 0, gt), None, directions, poses, True,
                                     ("sample", 1, gt))
@@ -609,6 +619,31 @@ class NGPTrainer:
         self.global_step += 1
         if update_after:
             self._updated_for = self.global_step
+        return self.out_loss
+
+    def _replay_pair(self, gt, directions, poses):
+        """Two consecutive steady-state steps (no occupancy update at, between
+        or right after them; one epoch, so one learning rate) as ONE graph
+        replay: the replay boundary (the GPU finishing one graph before it
+        starts the next) is paid once per two steps.  The second step's
+        train_step call then only advances the host step count
+        (self._ran_ahead); out_loss holds the second step's losses."""
+        k, ev = self._pending
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+        self._set_lr()
+        key = ("pair", k, gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype)
+
+        def body():
+            self._graph_body(k, gt, directions, poses, False)
+            self._graph_body(1 - k, gt, directions, poses, False)
+        self._run_graph(key, body)
+        self.cur = 1 - k
+        self._bind(self.msets[1 - k])
+        self._pending = (k, None)  # the batch after both, marched inside the graph
+        self.n_prefetched += 2
+        self.global_step += 1
+        self._ran_ahead = True
         return self.out_loss
 
     def _run_graph(self, key, body):
