@@ -1,7 +1,6 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-mkdir -p gpurun_out/final
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/final/pytest_gpu.log 2>&1
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final/smoke.log 2>&1
-timeout -k 10 300 python -u bench.py --steps 200 --warmup 10 --no-cpu-baseline --quality-steps 0 --psnr-views 0 --infer-frames 0 > gpurun_out/final/bench.json 2> gpurun_out/final/bench.err
+mkdir -p gpurun_out/rt
+timeout -k 10 300 python -u -m pytest tests/test_field_gpu.py tests/test_trainer_gpu.py tests/test_golden_gpu.py -x -v --timeout 120 --timeout-method thread > gpurun_out/rt/pytest.log 2>&1
+bash scripts/gpu_abn.sh ab_rt 3 "NGP_AMD_LIB=build_ab/base.so" "NGP_X=1"
