@@ -642,15 +642,25 @@ __device__ __forceinline__ f4 mask_relu(f4 g, h4 act) {
               act[3] > (_Float16)0 ? g[3] : 0.f};
 }
 // Accumulator tile X[4g + r][s] (lane (s, g)) -> image row s, units 4g..4g+3.
+// The four 8-byte chunks of row s sit XOR-swizzled, chunk c at c ^ ((s >> 2) & 3):
+// a ds_write_b64 group (16 lanes, banks mod 32) then covers 32 distinct banks
+// (unswizzled, rows 8 dwords apart hit 4 banks 4 ways), and get_tile's reads
+// stay conflict-free.
 __device__ __forceinline__ void put_tile(_Float16* T, h4 v, int s, int g) {
-    *reinterpret_cast<h4*>(T + s * TROW + 4 * g) = v;
+    *reinterpret_cast<h4*>(T + s * TROW + 4 * (g ^ ((s >> 2) & 3))) = v;
+}
+// units 8h..8h+7 of row s (chunks 2h, 2h+1; e0 = units 8h..8h+3) under the same swizzle
+__device__ __forceinline__ void put_tile_pair(_Float16* T, h4 e0, h4 e1, int s, int h) {
+    const int sw = (s >> 2) & 3;
+    *reinterpret_cast<h8*>(T + s * TROW + 4 * ((2 * h) ^ (sw & 2))) = (sw & 1) ? pack(e1, e0) : pack(e0, e1);
 }
 // Transposed read: lane (u = s, g) receives X[u][4g + q], q = 0..3, i.e. the
 // K = sample fragment of the 16x16x16 operand.  Lane 4q+p of each 16-lane
 // group addresses image row 4g+q, units 4p..4p+3 (= T + 4*lane).
 typedef __fp16 hp4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
 __device__ __forceinline__ h4 get_tile(const _Float16* T, int s, int g) {
-    const _Float16* a = T + 64 * g + 4 * s;
+    // row 4g + (s >> 2), chunk s & 3 -> stored at chunk (s & 3) ^ g (put_tile's swizzle)
+    const _Float16* a = T + 64 * g + 4 * ((s & 12) | ((s & 3) ^ g));
     return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
                                       (__attribute__((address_space(3))) hp4*)(const_cast<_Float16*>(a))));
 }
@@ -845,7 +855,7 @@ __global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
         // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
         {
             const h4 e0 = bf16x4(h4{e[0], e[1], e[2], e[3]}), e1 = bf16x4(h4{e[4], e[5], e[6], e[7]});
-            *reinterpret_cast<h8*>(scr + (T_E + (g >> 1)) * TTILE + s * TROW + 8 * (g & 1)) = pack(e0, e1);
+            put_tile_pair(scr + (T_E + (g >> 1)) * TTILE, e0, e1, s, g & 1);
         }
         wave_sync_lds();
         int k = 0;
@@ -1141,7 +1151,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         }
         {   // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
             const h4 e0 = bf16x4(h4{e[0], e[1], e[2], e[3]}), e1 = bf16x4(h4{e[4], e[5], e[6], e[7]});
-            *reinterpret_cast<h8*>(mine + (Q_E + (g >> 1)) * TTILE + s * TROW + 8 * (g & 1)) = pack(e0, e1);
+            put_tile_pair(mine + (Q_E + (g >> 1)) * TTILE, e0, e1, s, g & 1);
         }
         __syncthreads();
         coop_dw<2>(scr, wid, s, g, coop_n2(wid), coop_k2, acc2);
