@@ -333,17 +333,7 @@ __global__ void __launch_bounds__(256) field_fwd_kernel(const float* __restrict_
     }
 }
 
-// ------------------------------------------------ level-pair-per-XCD encode
-// Multires hash encoding alone (the gathers of field_fwd_kernel, same
-// arithmetic, bit-identical values), written pair-major:
-//   enc_pm[p][i][0..3] = enc[i][4p .. 4p+3]  (levels 2p, 2p+1; p = 0..7).
-// Block b encodes level pair b % 8 for its share of the samples.  Blocks b
-// and b + 8 land on the same XCD (round-robin dealing; a placement-only
-// assumption: any placement gives the same result), so each XCD's L2 serves
-// ONE level pair (<= 2 x 2 MB of fp16 table) instead of all 23 MB --
-// the fused kernel's gathers mostly missed L2 and queued on the Infinity
-// Cache.  One lane per sample: 8 independent pair-gathers in flight, ~40
-// VGPRs, full occupancy (the fused kernel ran 2 waves per SIMD).
+// ------------------------------------------------------ hash encode alone
 // One level's parameters as wave-uniform (scalar) values, so the per-level
 // index variant is chosen by scalar branches, not computed for every lane.
 struct LevelU {
@@ -437,14 +427,15 @@ __device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& 
     sum_level(w, v, a0, a1);
 }
 
-// ALL = true (the product path): each lane encodes every level of one
-// sample, so a wave instruction gathers ONE level for 64 consecutive samples
-// (a ray's neighbours: shared lines on the coarse levels) -- measured 1.55x
-// the rate of one level pair per XCD (ALL = false, kept for diagnostics:
-// NGP_ENCODE_XCD=1) and 1.8x the fused kernel's lane (sample, level group)
-// layout (scripts/diag/encode_split.py).  sidx (nullable): rows j < N encode
-// sample sidx[j] (rows of enc_pm are samples).
-template <bool ALL, int PGT = 1>
+// Multires hash encoding alone (the gathers of field_fwd_kernel, same
+// arithmetic, bit-identical values), written pair-major:
+//   enc_pm[p][i][0..3] = enc[i][4p .. 4p+3]  (levels 2p, 2p+1; p = 0..7).
+// Each lane encodes every level of one sample, so a wave instruction gathers
+// ONE level for 64 consecutive samples (a ray's neighbours: shared lines on
+// the coarse levels) -- 1.55x the rate of one level pair per XCD and 1.8x
+// field_fwd_kernel's lane (sample, level group) layout
+// (scripts/diag/encode_split.py).  sidx (nullable): rows j < N encode sample
+// sidx[j] (rows of enc_pm are samples).
 __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restrict__ xyzs, int64_t n,
                                                           const int64_t* __restrict__ n_dev,
                                                           const int32_t* __restrict__ sidx, GridArgs ga,
@@ -454,31 +445,21 @@ __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restric
     load_levels(ga, lv);
     __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
-    const int p0 = ALL ? 0 : blockIdx.x & 7;
-    const int64_t nb = ALL ? gridDim.x : gridDim.x >> 3;
-    const int64_t b = ALL ? blockIdx.x : blockIdx.x >> 3;
-    for (int64_t j = b * blockDim.x + threadIdx.x; j < N; j += nb * blockDim.x) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < N; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = sidx ? (int64_t)sidx[j] : j;
         float in[3];
         load_x01(xyzs, i, true, ga, in);
-        // PG level pairs per iteration, their gathers issued together: a lane
-        // encodes about one sample per launch (the grid covers the batch), so
-        // the launch time is the lane's chain of dependent gather rounds
-        constexpr int PG = ALL ? PGT : 1;
 #pragma unroll 1
-        for (int pr0 = p0; pr0 < (ALL ? 8 : p0 + 1); pr0 += PG) {
-            float w[2 * PG][8];
-            uint32_t v[2 * PG][8];
-#pragma unroll
-            for (int q = 0; q < 2 * PG; ++q) gather_level_u(in, level_u(lv, 2 * pr0 + q), table, w[q], v[q]);
-#pragma unroll
-            for (int q = 0; q < PG; ++q) {
-                float a0, a1, b0, b1;
-                sum_level(w[2 * q], v[2 * q], a0, a1);
-                sum_level(w[2 * q + 1], v[2 * q + 1], b0, b1);
-                *reinterpret_cast<h4*>(enc_pm + ((int64_t)(pr0 + q) * n + i) * 4) =
-                    h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
-            }
+        for (int pr = 0; pr < 8; ++pr) {
+            float w[2][8];
+            uint32_t v[2][8];
+            gather_level_u(in, level_u(lv, 2 * pr), table, w[0], v[0]);
+            gather_level_u(in, level_u(lv, 2 * pr + 1), table, w[1], v[1]);
+            float a0, a1, b0, b1;
+            sum_level(w[0], v[0], a0, a1);
+            sum_level(w[1], v[1], b0, b1);
+            *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) =
+                h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
         }
     }
 }
@@ -582,14 +563,11 @@ __device__ __forceinline__ h4 lds4(const _Float16* p) { return *reinterpret_cast
 constexpr int RT16 = 20, RT64 = 68;  // transposed-weight rows: 16 / 64 halfs + pad
 constexpr int BT5 = SWF, BT4 = BT5 + 64 * RT16, BT3 = BT4 + 64 * RT64, BT2 = BT3 + 16 * RT64, BT1 = BT2 + 64 * RT16,
               BTE = BT1 + 32 * RT64;
-// per-wave transpose scratch: 30 tiles, each a [sample][unit] 16x16 fp16 image
+// operand tiles of the weight-gradient sums: [sample][unit] 16x16 images
 // (32-byte rows: the packed 8-byte stores and the ds_read_b64_tr_b16 reads
-// of a 32-lane half both cover 64 distinct banks)
-constexpr int TROW = 16, TTILE = 16 * TROW, NT = 30;
-constexpr int SCR = (BTE + 7) & ~7, SCRW = NT * TTILE, BWD_LDS_HALFS = SCR + 4 * SCRW;
-// scratch tile ids
-constexpr int T_DO = 0, T_DA4 = 1, T_DA3 = 5, T_DH = 9, T_DA1 = 10, T_H4 = 14, T_H3 = 18, T_C = 22, T_H1 = 24, T_E = 28;
-constexpr int NACC = 40;
+// of a 32-lane half both cover 64 distinct banks), after the weight images
+constexpr int TROW = 16, TTILE = 16 * TROW;
+constexpr int SCR = (BTE + 7) & ~7;
 
 __device__ __forceinline__ void load_bwd_weights(const _Float16* __restrict__ mlp, _Float16* sw) {
     const int t = threadIdx.x, nt = blockDim.x;
@@ -702,226 +680,12 @@ __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& 
     ow = OW1; in_dim = 32; o0 = 16 * (k >> 1); i0 = 16 * (k & 1);
 }
 
-// MODE (diagnostics only, scripts/diag/mlp_split.py): bit 0 skips the weight
-// gradients, bit 1 the block reduction
-template <int MODE>
-__global__ void __launch_bounds__(256) field_bwd_mlp_kernel(
-    const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
-    const _Float16* __restrict__ enc,
-    const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig, const float* __restrict__ dL_drgb,
-    float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride) {
-    extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
-    _Float16* sw = smem;
-    _Float16* raw = smem + SCR;  // the per-wave scratch is free until the loop
-    stage_raw_weights(mlp, raw);
-    __syncthreads();
-    load_fwd_weights(raw, sw, true);
-    load_bwd_weights(raw, sw);
-    __syncthreads();
-    const int64_t N = n_dev ? *n_dev : n;
-    const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4, wid = threadIdx.x >> 6;
-    _Float16* scr = smem + SCR + wid * SCRW;
-    const f4 z = {0.f, 0.f, 0.f, 0.f};
-    f4 acc[NACC];
-#pragma unroll
-    for (int k = 0; k < NACC; ++k) acc[k] = z;
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    // per-sample inputs of the NEXT column block are loaded while this one
-    // computes (one wave per SIMD: nothing else would hide the latency)
-    struct In {
-        h8 e;
-        float dx, dy, dz, dsig, gr[3];
-    };
-    auto load_in = [&](int64_t b, In& x) {
-        const int64_t jj = b + s;
-        x.e = h8{0, 0, 0, 0, 0, 0, 0, 0};
-        x.dx = 0.f; x.dy = 0.f; x.dz = 1.f; x.dsig = 0.f; x.gr[0] = x.gr[1] = x.gr[2] = 0.f;
-        if (jj < N) {
-            const int64_t ii = sidx ? (int64_t)sidx[jj] : jj;
-            if (enc_pm_stride > 0)  // pair-major (ngp_hash_encode): pairs 2g, 2g+1
-                x.e = pack(*reinterpret_cast<const h4*>(enc + ((2 * g) * enc_pm_stride + ii) * 4),
-                           *reinterpret_cast<const h4*>(enc + ((2 * g + 1) * enc_pm_stride + ii) * 4));
-            else
-                x.e = *reinterpret_cast<const h8*>(enc + ii * 32 + 8 * g);
-            x.dx = dirs[3 * ii]; x.dy = dirs[3 * ii + 1]; x.dz = dirs[3 * ii + 2];
-            x.dsig = dL_dsig[ii];
-            x.gr[0] = dL_drgb[3 * ii]; x.gr[1] = dL_drgb[3 * ii + 1]; x.gr[2] = dL_drgb[3 * ii + 2];
-        }
-    };
-    int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wid) * 16;
-    In cur;
-    load_in(base, cur);
-    for (; base < N; base += nw * 16) {
-        In nxt;
-        load_in(base + nw * 16, nxt);
-        const int64_t j = base + s;  // compact position (denc row)
-        const bool valid = j < N;
-        const h8 e = cur.e;
-        const float dx = cur.dx, dy = cur.dy, dz = cur.dz, dsig = cur.dsig;
-        const float gr[3] = {cur.gr[0], cur.gr[1], cur.gr[2]};
-        // ---- forward recompute
-        h4 h1[4];
-        const h4 hh = density_net(e, sw, s, g, h1);
-        float sh[4];
-        sh4_select(dx, dy, dz, g, sh);
-        const h4 shh = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3]};
-        const h8 cin = pack(shh, hh);
-        h4 h3[4], h4v[4];
-        const h4 o = color_net(cin, sw, s, g, h3, h4v);
-        // ---- output layer: sigmoid backward on rows 0..2
-        f4 dout = z;
-        if (g == 0) {
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const float y = 1.0f / (1.0f + expf(-(float)o[r]));
-                dout[r] = gr[r] * (y * (1.0f - y));
-            }
-        }
-        const float sc_o = pow2_scale(wave_max(max4(dout))), is_o = 1.0f / sc_o;
-        const h4 do_h = scaled_h(dout, sc_o);
-        // ---- dh4 = W5^T do
-        f4 da4[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) da4[t] = mask_relu(mfma16(lds4(sw + BT5 + (16 * t + s) * RT16 + 4 * g), do_h, z) * is_o, h4v[t]);
-        float m = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da4[t]));
-        const float sc_4 = pow2_scale(wave_max(m)), is_4 = 1.0f / sc_4;
-        h4 da4h[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) da4h[t] = scaled_h(da4[t], sc_4);
-        // ---- dh3 = W4^T da4
-        f4 da3[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            f4 c = z;
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT4 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da4h[kt], c);
-            da3[t] = mask_relu(c * is_4, h3[t]);
-        }
-        m = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da3[t]));
-        const float sc_3 = pow2_scale(wave_max(m)), is_3 = 1.0f / sc_3;
-        h4 da3h[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) da3h[t] = scaled_h(da3[t], sc_3);
-        // ---- d h (colour-net input, h part) = W3h^T da3, + TruncExp backward
-        f4 dh = z;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) dh = mfma16(lds4(sw + BT3 + s * RT64 + 16 * kt + 4 * g), da3h[kt], dh);
-        dh = dh * is_3;
-        if (g == 0) dh[0] += dsig * expf(fminf(fmaxf((float)hh[0], -15.f), 15.f));  // custom_functions.py:169-173
-        const float sc_h = pow2_scale(wave_max(max4(dh))), is_h = 1.0f / sc_h;
-        const h4 dhh = scaled_h(dh, sc_h);
-        // ---- dh1 = W2^T dh
-        f4 da1[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) da1[t] = mask_relu(mfma16(lds4(sw + BT2 + (16 * t + s) * RT16 + 4 * g), dhh, z) * is_h, h1[t]);
-        m = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da1[t]));
-        const float sc_1 = pow2_scale(wave_max(m)), is_1 = 1.0f / sc_1;
-        h4 da1h[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) da1h[t] = scaled_h(da1[t], sc_1);
-        // ---- dL/denc = W1^T da1 (rows 16t + 4g + r of sample s)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            f4 c = z;
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT1 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da1h[kt], c);
-            c = c * is_1;
-            if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
-        }
-        // ---- weight gradients dW = sum_s G[o][s] H[i][s]: bf16 operands (true,
-        // unscaled gradients), transposed through LDS, K = 16 samples,
-        // accumulated in the MFMA C operand
-        if (MODE & 1) { cur = nxt; continue; }
-        wave_sync_lds();  // previous iteration's reads are done
-        put_tile(scr + T_DO * TTILE, bf16x4(dout), s, g);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            put_tile(scr + (T_DA4 + t) * TTILE, bf16x4(da4[t]), s, g);
-            put_tile(scr + (T_DA3 + t) * TTILE, bf16x4(da3[t]), s, g);
-            put_tile(scr + (T_DA1 + t) * TTILE, bf16x4(da1[t]), s, g);
-            put_tile(scr + (T_H4 + t) * TTILE, bf16x4(h4v[t]), s, g);
-            put_tile(scr + (T_H3 + t) * TTILE, bf16x4(h3[t]), s, g);
-            put_tile(scr + (T_H1 + t) * TTILE, bf16x4(h1[t]), s, g);
-        }
-        put_tile(scr + T_DH * TTILE, bf16x4(dh), s, g);
-        put_tile(scr + T_C * TTILE, bf16x4(shh), s, g);
-        put_tile(scr + (T_C + 1) * TTILE, bf16x4(hh), s, g);
-        // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
-        {
-            const h4 e0 = bf16x4(h4{e[0], e[1], e[2], e[3]}), e1 = bf16x4(h4{e[4], e[5], e[6], e[7]});
-            put_tile_pair(scr + (T_E + (g >> 1)) * TTILE, e0, e1, s, g & 1);
-        }
-        wave_sync_lds();
-        int k = 0;
-        const h4 gdo = get_tile(scr + T_DO * TTILE, s, g);
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt, ++k) acc[k] = mfma16bf(gdo, get_tile(scr + (T_H4 + nt) * TTILE, s, g), acc[k]);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const h4 ga = get_tile(scr + (T_DA4 + mt) * TTILE, s, g);
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt, ++k) acc[k] = mfma16bf(ga, get_tile(scr + (T_H3 + nt) * TTILE, s, g), acc[k]);
-        }
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const h4 ga = get_tile(scr + (T_DA3 + mt) * TTILE, s, g);
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt, ++k) acc[k] = mfma16bf(ga, get_tile(scr + (T_C + nt) * TTILE, s, g), acc[k]);
-        }
-        const h4 gdh = get_tile(scr + T_DH * TTILE, s, g);
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt, ++k) acc[k] = mfma16bf(gdh, get_tile(scr + (T_H1 + nt) * TTILE, s, g), acc[k]);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            const h4 ga = get_tile(scr + (T_DA1 + mt) * TTILE, s, g);
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt, ++k) acc[k] = mfma16bf(ga, get_tile(scr + (T_E + nt) * TTILE, s, g), acc[k]);
-        }
-        cur = nxt;
-    }
-    // ---- block reduction of the 40 tiles, then one global add per weight.
-    // Plain LDS stores of each wave's tiles + a 4-way sum, CHK tiles at a
-    // time (ds_add_f32 costs ~3 cycles per lane on gfx950: 160 per thread
-    // were ~50 us per launch).
-    if (MODE & 2) {
-        float t = 0.f;
-#pragma unroll
-        for (int k = 0; k < NACC; ++k) t += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
-        if (t == 1234.5f) grad_mlp[threadIdx.x] = t;
-        return;
-    }
-    constexpr int CHK = 10;
-    static_assert(NACC % CHK == 0 && 4 * CHK * 256 * 4 <= 4 * SCRW * 2, "reduction chunk exceeds the scratch");
-    float* red = reinterpret_cast<float*>(smem + SCR);
-#pragma unroll
-    for (int c0 = 0; c0 < NACC; c0 += CHK) {
-        __syncthreads();  // previous chunk's reads (or the loop's scratch use) are done
-#pragma unroll
-        for (int k = 0; k < CHK; ++k)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) red[(wid * CHK + k) * 256 + (4 * g + r) * 16 + s] = acc[c0 + k][r];
-        __syncthreads();
-        for (int e = threadIdx.x; e < CHK * 256; e += blockDim.x) {
-            const float v = (red[e] + red[CHK * 256 + e]) + (red[2 * CHK * 256 + e] + red[3 * CHK * 256 + e]);
-            const int k = c0 + (e >> 8), row = (e >> 4) & 15, col = e & 15;
-            int ow, in_dim, o0, i0;
-            acc_tile_info(k, ow, in_dim, o0, i0);
-            atomicAdd(&grad_mlp[ow + (o0 + row) * in_dim + i0 + col], v);
-        }
-    }
-}
-
-// Kernel A (product path): the same MLP backward, block-cooperative.  Eight
-// waves per block (two per SIMD -- the per-wave kernel above holds its 40
-// weight-gradient tiles in registers and runs one wave per SIMD, latency-bound
-// on its dependent MFMA / LDS chain).  Each wave back-propagates its own
-// 16-sample column block as above; the weight gradients are then summed by
+// Kernel A: the MLP backward, block-cooperative.  Eight waves per block (two
+// per SIMD -- a per-wave kernel holding all 40 weight-gradient tiles in
+// registers ran one wave per SIMD, latency-bound on its dependent MFMA / LDS
+// chain: 105.8 vs 78.8 us, profiles/r02/mlp_split_coop.json).  Each wave
+// back-propagates its own 16-sample column block (forward recomputed from the
+// saved fp16 encoding); the weight gradients are then summed by
 // the block: every wave puts its operand tiles into its LDS region and wave w
 // accumulates output tiles {k} over all eight regions (K = 128 samples per
 // block iteration), 5 of the 40 tiles per wave.  Operands go through LDS in
@@ -996,7 +760,6 @@ __device__ __forceinline__ void coop_dw(const _Float16* scr, int w, int s, int g
     }
 }
 
-template <int MODE>
 __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
     const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
     const _Float16* __restrict__ enc, const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig,
@@ -1126,7 +889,6 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
             if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
         }
         cur = nxt;
-        if (MODE & 1) continue;
         // ---- weight gradients, phase 1 (layers 5, 4, 3): bf16 operand tiles
         __syncthreads();  // every wave's phase-2 reads of the previous iteration are done
         put_tile(mine + P_DO * TTILE, bf16x4(dout), s, g);
@@ -1155,14 +917,6 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         }
         __syncthreads();
         coop_dw<2>(scr, wid, s, g, coop_n2(wid), coop_k2, acc2);
-    }
-    if (MODE & 2) {
-        float t = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) t += acc1[k][0] + acc1[k][1] + acc1[k][2] + acc1[k][3];
-        t += acc2[0][0] + acc2[1][0];
-        if (t == 1234.5f) grad_mlp[threadIdx.x] = t;
-        return;
     }
     // each output tile lives in exactly one wave of the block: one global add
     // per weight.  Wave w of every block owns the same tiles, so the adds of a
@@ -1197,17 +951,14 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
 // sample instead of four scattered ones.  Samples of one ray are consecutive,
 // so equal indices of the same (cx, f) at lane stride 4 are first summed by a
 // segmented suffix scan; only each run's head issues its fp32 atomic.
-// MODE != 0 and a level range other than [0, L) are diagnostic variants used
-// only by scripts/diag (1: no atomics, 2: plain stores, 3: no run merge,
-// 4: neither run merge nor atomics).
-template <int MODE>
+// Levels [lo, hi) (the hybrid backward's atomic coarse levels; [0, L) for
+// the all-atomic API path).
 __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__ xyzs, int64_t n,
                                                        const int64_t* __restrict__ n_dev,
                                                        const int32_t* __restrict__ sidx, GridArgs ga,
                                                        const float* __restrict__ denc, float* __restrict__ grad,
                                                        int lo, int hi, float* __restrict__ rep = nullptr,
                                                        int rep_hi = 0, uint32_t rep_stride = 0, int nrep = 1) {
-    float sink = 0.f;
     // levels below rep_hi add into this block's replica of their gradient
     // range (ngp_hash_backward_levels_rep): the coarsest levels are a few
     // hundred KB that every sample touches, so their memory-side atomics
@@ -1281,7 +1032,7 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
             for (int yz = 0; yz < 4; ++yz) prev[yz] = __shfl_up(idx[yz], 4, 64);
 #pragma unroll
             for (int yz = 0; yz < 4; ++yz) heads[yz] = __ballot(lane < 4 || prev[yz] != idx[yz]);
-            if (MODE != 3 && MODE != 4 && (heads[0] & heads[1] & heads[2] & heads[3]) != ~0ull) {
+            if ((heads[0] & heads[1] & heads[2] & heads[3]) != ~0ull) {
                 // some runs: segmented suffix sums at lane stride 4
 #pragma unroll
                 for (int o4 = 4; o4 < 64; o4 <<= 1) {
@@ -1298,14 +1049,13 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
 #pragma unroll
             for (int yz = 0; yz < 4; ++yz) {
                 const bool head = (heads[yz] >> lane) & 1ull;
-                if (MODE == 1 || MODE == 4) sink += head && valid ? v[yz] : 0.f;
-                else if (MODE == 2) { if (head && valid) dst[2 * (size_t)idx[yz] + f] = v[yz]; }
-                else if ((head || MODE == 3) && valid) atomicAdd(&dst[2 * (size_t)idx[yz] + f], v[yz]);
+                if (head && valid) atomicAdd(&dst[2 * (size_t)idx[yz] + f], v[yz]);
             }
         }
     }
-    if ((MODE == 1 || MODE == 4) && sink == 1234.5f) grad[threadIdx.x] = sink;
 }
+
+constexpr unsigned HASH_BWD_BLOCKS = 8192;  // grid cap of hash_bwd_kernel (2048 measured slower)
 
 // grad[i] += sum_r rep[r][i]; rep[r][i] = 0 (i < n4 float4 groups), replicas
 // summed in order r = 0..nrep-1; all of a lane's loads are issued first
@@ -1398,31 +1148,10 @@ int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const in
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && table_f16 && enc_pm && ((uintptr_t)enc_pm & 7) == 0);
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0);  // 16-byte group gathers
-    static const bool xcd = getenv("NGP_ENCODE_XCD") && getenv("NGP_ENCODE_XCD")[0] == '1';  // diagnostic
-    if (!xcd) {
-        // level pairs per gather round (diagnostic NGP_ENCODE_PG = 2, 4: more
-        // gathers in flight per lane at fewer waves per SIMD -- measured no
-        // faster (2) and 1.4x slower (4): the encode is bound by the L2/MALL
-        // request rate, not by a lane's chain of gather rounds)
-        static const int pg = getenv("NGP_ENCODE_PG") ? atoi(getenv("NGP_ENCODE_PG")) : 1;
-        hipStream_t s = as_stream(stream);
-#define NGP_ENC(PGV)                                                                                                   \
-    do {                                                                                                               \
-        static const unsigned cap = resident_blocks(hash_encode_kernel<true, PGV>, 256, 0);                            \
-        NGP_TIMED(NGP_K_HASH_ENCODE, s, hash_encode_kernel<true, PGV><<<std::max(1u, std::min(cap, (unsigned)((n + 255) / 256))), 256, 0, s>>>( \
-            xyzs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (_Float16*)enc_pm));                           \
-    } while (0)
-        if (pg == 1) NGP_ENC(1);
-        else if (pg == 4) NGP_ENC(4);
-        else NGP_ENC(2);
-#undef NGP_ENC
-        return ngp_launch_status();
-    }
-    static const unsigned cap = resident_blocks(hash_encode_kernel<false>, 256, 0);
-    const unsigned per_pair = std::max(1u, std::min(cap / 8, (unsigned)((n + 255) / 256)));
-    NGP_TIMED(NGP_K_HASH_ENCODE, as_stream(stream), hash_encode_kernel<false><<<8 * per_pair, 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx, ga,
-                                                                           (const uint32_t*)table_f16,
-                                                                           (_Float16*)enc_pm));
+    hipStream_t s = as_stream(stream);
+    static const unsigned cap = resident_blocks(hash_encode_kernel, 256, 0);
+    NGP_TIMED(NGP_K_HASH_ENCODE, s, hash_encode_kernel<<<std::max(1u, std::min(cap, (unsigned)((n + 255) / 256))), 256, 0, s>>>(
+        xyzs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (_Float16*)enc_pm));
     return ngp_launch_status();
 }
 
@@ -1483,48 +1212,19 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
     NGP_CHECK_ARG(dirs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp);
     NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
     static bool attr_set = false;
-    const size_t lds = (size_t)BWD_LDS_HALFS * sizeof(_Float16), clds = (size_t)COOP_LDS_HALFS * sizeof(_Float16);
+    const size_t clds = (size_t)COOP_LDS_HALFS * sizeof(_Float16);
     if (!attr_set) {
-        for (const void* k : {(const void*)field_bwd_mlp_kernel<0>, (const void*)field_bwd_mlp_kernel<1>,
-                              (const void*)field_bwd_mlp_kernel<2>, (const void*)field_bwd_mlp_kernel<3>})
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                return NGP_ERANGE;
-        for (const void* k : {(const void*)field_bwd_mlp_coop_kernel<0>, (const void*)field_bwd_mlp_coop_kernel<1>,
-                              (const void*)field_bwd_mlp_coop_kernel<2>, (const void*)field_bwd_mlp_coop_kernel<3>})
-            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds) != hipSuccess)
-                return NGP_ERANGE;
+        if (hipFuncSetAttribute((const void*)field_bwd_mlp_coop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)clds) != hipSuccess)
+            return NGP_ERANGE;
         attr_set = true;
     }
-    // diagnostics (scripts/diag/mlp_split.py): NGP_MLP_BWD_DIAG = mode bits,
-    // NGP_MLP_BWD_WAVE=1 the per-wave kernel
-    const char* dm = getenv("NGP_MLP_BWD_DIAG");
-    const int mode = dm ? atoi(dm) & 3 : 0;
-    const char* pw = getenv("NGP_MLP_BWD_WAVE");
     hipStream_t s = as_stream(stream);
-    if (pw && pw[0] == '1') {
-        const unsigned nb = persistent_blocks(n, 64, 256);
-#define NGP_MLPB(M)                                                                                                   \
-    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_kernel<M><<<nb, 256, lds, s>>>(                                         \
-        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, \
-        grad_mlp, enc_pm_stride))
-        if (mode == 1) NGP_MLPB(1);
-        else if (mode == 2) NGP_MLPB(2);
-        else if (mode == 3) NGP_MLPB(3);
-        else NGP_MLPB(0);
-#undef NGP_MLPB
-        return ngp_launch_status();
-    }
-    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel<0>, 512, clds);
+    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel, 512, clds);
     const unsigned cb = persistent_blocks(n, CW * 16, ccap);
-#define NGP_MLPB(M)                                                                                                   \
-    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<M><<<cb, 512, clds, s>>>(                                   \
-        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws, \
-        grad_mlp, enc_pm_stride))
-    if (mode == 1) NGP_MLPB(1);
-    else if (mode == 2) NGP_MLPB(2);
-    else if (mode == 3) NGP_MLPB(3);
-    else NGP_MLPB(0);
-#undef NGP_MLPB
+    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<<<cb, 512, clds, s>>>(
+        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
+        grad_mlp, enc_pm_stride));
     return ngp_launch_status();
 }
 
@@ -1537,7 +1237,7 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
     NGP_CHECK_ARG(n >= 0);
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(xyzs && denc && grad_table && ((uintptr_t)denc & 15) == 0);
-    NGP_TIMED(NGP_K_HASH_BWD_COARSE, as_stream(stream), hash_bwd_kernel<0><<<persistent_blocks(n, 64, 8192), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx,
+    NGP_TIMED(NGP_K_HASH_BWD_COARSE, as_stream(stream), hash_bwd_kernel<<<persistent_blocks(n, 64, HASH_BWD_BLOCKS), 256, 0, as_stream(stream)>>>(xyzs, n, n_dev, sample_idx,
                                                                                      ga, denc, grad_table, 0, L));
     return ngp_launch_status();
 }
@@ -1551,22 +1251,10 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
     NGP_CHECK_ARG(n >= 0 && 0 <= level_lo && level_lo <= level_hi && level_hi <= L);
     if (n == 0 || level_lo == level_hi) return NGP_OK;
     NGP_CHECK_ARG(xyzs && denc && grad_table && ((uintptr_t)denc & 15) == 0);
-    static const int mode = getenv("NGP_HASH_BWD_MODE") ? atoi(getenv("NGP_HASH_BWD_MODE")) : 0;  // diagnostic
-    // (NGP_HASH_BWD_BLOCKS: diagnostic grid cap; 2048 measured slower)
-    static const unsigned cap = (unsigned)std::max(1, getenv("NGP_HASH_BWD_BLOCKS") ? atoi(getenv("NGP_HASH_BWD_BLOCKS"))
-                                                                                    : 8192);
-    const unsigned blocks = persistent_blocks(n, 64, cap);
+    const unsigned blocks = persistent_blocks(n, 64, HASH_BWD_BLOCKS);
     hipStream_t s = as_stream(stream);
-    if (mode == 1)
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<1><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
-    else if (mode == 2)
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<2><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
-    else if (mode == 4)
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<4><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
-    else if (mode == 3)
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<3><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
-    else
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<0><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi));
+    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc,
+                                                                           grad_table, level_lo, level_hi));
     return ngp_launch_status();
 }
 
@@ -1587,12 +1275,10 @@ int ngp_hash_backward_levels_rep(const float* xyzs, int64_t n, const int64_t* n_
     // replicas cover table entries [0, offsets[rep_levels]) (x 2 features)
     const uint32_t nfl = 2u * grid->offsets[rep_levels];
     NGP_CHECK_ARG(nfl % 4 == 0);
-    static const unsigned cap = (unsigned)std::max(1, getenv("NGP_HASH_BWD_BLOCKS") ? atoi(getenv("NGP_HASH_BWD_BLOCKS"))
-                                                                                    : 8192);
-    const unsigned blocks = persistent_blocks(n, 64, cap);
+    const unsigned blocks = persistent_blocks(n, 64, HASH_BWD_BLOCKS);
     hipStream_t s = as_stream(stream);
-    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<0><<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi, rep, rep_levels, nfl, n_rep));
-    if (!fold) return ngp_launch_status();  // the caller folds them (ngp_hash_binned_accum_adam_dense)
+    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi, rep, rep_levels, nfl, n_rep));
+    if (!fold) return ngp_launch_status();  // the caller folds them (ngp_adam_step_dev_rep)
     const uint32_t n4 = nfl / 4;
     const unsigned rb = std::min(2048u, (n4 + 255) / 256);
     if (n_rep <= 8)

@@ -478,25 +478,9 @@ __device__ __forceinline__ void adam4(const AdamArgs& a, size_t base, uint32_t e
                bc2);
 }
 
-// A dense FusedAdam range stepped by the accumulation's tail (float4 units):
-// [0, n4) of p/m/v/p16/grad, replicas rep[r][j] of groups [rep_off4, rep_off4 + rep4)
-struct DenseAdam {
-    float* p;
-    float* m;
-    float* v;
-    _Float16* p16;
-    float* grad;
-    float* rep;
-    uint32_t n4, rep_off4, rep4;
-    int nrep;
-};
-
-// MODE != 0: diagnostic variants for scripts/diag (1: no LDS adds, 2: no
-// flush, 3: neither)
-template <int MODE, bool FUSED = false>
+template <bool FUSED = false>
 __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
-                                                          float* __restrict__ grad, BinWs ws, AdamArgs adam,
-                                                          DenseAdam da = DenseAdam{}) {
+                                                          float* __restrict__ grad, BinWs ws, AdamArgs adam) {
     extern __shared__ __attribute__((aligned(16))) double img[];  // [2][BENT]: feature-major, 8-byte stride
     const uint32_t total = ws.items[nbt];
     const int t = threadIdx.x, lane = t & 63;
@@ -523,7 +507,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         // accumulation instead of following it (the flush then only computes
         // and stores).  PF x blockDim.x covers a whole bucket at ACC_T threads.
         constexpr int PF = 4;
-        const uint32_t ng = (MODE & 2) ? 0u : 2 * ne / 4;  // float4 groups of the range
+        const uint32_t ng = 2 * ne / 4;  // float4 groups of the range
         float4 pP[PF], pM[PF], pV[PF];
         if (fz) {
 #pragma unroll
@@ -562,10 +546,6 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
                 const uint32_t key = v[u].x, i0 = key & (BENT - 1), i1 = (key >> BSHIFT) & (BENT - 1);
                 const float fx = __uint_as_float(v[u].y), a0 = __uint_as_float(v[u].z), a1 = __uint_as_float(v[u].w);
                 const float w0 = 1 - fx;
-                if (MODE & 1) {
-                    if (w0 * a0 + fx * a1 == 1234.5f) img[i0 ^ i1] = 1.0;  // keeps the loads live
-                    continue;
-                }
                 // the fp32 products tcnn would add, summed in fp64; a single-entry
                 // record {i0 | F_SINGLE, g0, g1} carries a run's sums for entry i0
                 const bool single = key & F_SINGLE;
@@ -669,28 +649,6 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
                 adam4(adam, gbase, e, gv, lr, bc1, bc2);
             }
         }
-        if (da.n4) {  // the dense range (MLP + atomic coarse levels), replicas folded in order
-            const AdamArgs dargs{da.p, da.m, da.v, da.p16, nullptr, nullptr, adam.b1, adam.b2, adam.eps, 0.f};
-            float4* g4 = reinterpret_cast<float4*>(da.grad);
-            float4* r4 = reinterpret_cast<float4*>(da.rep);
-            const float sc = adam.grad_scale;
-            for (uint32_t i = blockIdx.x * blockDim.x + t; i < da.n4; i += gridDim.x * blockDim.x) {
-                const float4 P = reinterpret_cast<const float4*>(da.p)[i];
-                const float4 M = reinterpret_cast<const float4*>(da.m)[i];
-                const float4 V = reinterpret_cast<const float4*>(da.v)[i];
-                float4 G = g4[i];
-                const uint32_t j = i - da.rep_off4;
-                if (i >= da.rep_off4 && j < da.rep4) {
-                    for (int r = 0; r < da.nrep; ++r) {
-                        const float4 b = r4[(size_t)r * da.rep4 + j];
-                        G.x += b.x; G.y += b.y; G.z += b.z; G.w += b.w;
-                        r4[(size_t)r * da.rep4 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
-                }
-                adam4_regs(dargs, 0, i, make_float4(G.x * sc, G.y * sc, G.z * sc, G.w * sc), P, M, V, lr, bc1, bc2);
-                g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
     }
 }
 
@@ -749,7 +707,7 @@ size_t ngp_hash_backward_binned_workspace(int64_t max_samples) {
 static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                        const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
                        int64_t max_samples, int level_lo, int merge_hi, int phase, void* stream,
-                       const AdamArgs* adam = nullptr, const DenseAdam& da = DenseAdam{}) {
+                       const AdamArgs* adam = nullptr) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
@@ -784,19 +742,19 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
         static bool attr = false;
         const size_t lds = (size_t)BENT * 2 * sizeof(double);
         if (!attr) {
-            if (hipFuncSetAttribute((const void*)hash_accum_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+            if (hipFuncSetAttribute((const void*)hash_accum_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds) != hipSuccess ||
-                hipFuncSetAttribute((const void*)hash_accum_kernel<0, true>,
+                hipFuncSetAttribute((const void*)hash_accum_kernel<true>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
                 return NGP_ERANGE;
             attr = true;
         }
-        static const unsigned capB = resident_blocks(hash_accum_kernel<0>, ACC_T, lds);
+        static const unsigned capB = resident_blocks(hash_accum_kernel<false>, ACC_T, lds);
         if (adam) {
-            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0, true><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam, da));
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<true><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam));
             NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<nbt, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam));
         } else {
-            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<0><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}));
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<false><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}));
         }
     }
     return ngp_launch_status();
@@ -856,30 +814,6 @@ int ngp_hash_binned_accum_adam(const ngp_hashgrid_t* grid, float* grad_table, vo
     static const float dummy[1] = {0.f};
     return hash_binned(dummy, 1, nullptr, nullptr, grid, nullptr, grad_table, workspace, max_samples, level_lo,
                        merge_hi, 4, stream, &a);
-}
-
-int ngp_hash_binned_accum_adam_dense(const ngp_hashgrid_t* grid, float* grad, void* workspace, int64_t max_samples,
-                                     int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
-                                     void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
-                                     const int64_t* step_dev, float grad_scale, int64_t table_offset, int64_t dense_n,
-                                     float* rep, int64_t rep_n, int n_rep, void* stream) {
-    NGP_CHECK_ARG(grid && grad && params && exp_avg && exp_avg_sq && params_f16 && lr_dev && step_dev);
-    NGP_CHECK_ARG(((uintptr_t)params & 15) == 0 && ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0 &&
-                  ((uintptr_t)params_f16 & 7) == 0 && ((uintptr_t)grad & 15) == 0);
-    NGP_CHECK_ARG(table_offset >= 0 && table_offset % 4 == 0 && dense_n >= 0 && dense_n % 4 == 0);
-    NGP_CHECK_ARG(dense_n <= 0x7fffffffLL && rep_n >= 0 && rep_n % 4 == 0 && table_offset + rep_n <= dense_n);
-    NGP_CHECK_ARG(rep_n == 0 || (rep && ((uintptr_t)rep & 15) == 0 && n_rep >= 1 && n_rep <= 64));
-    // the binned levels start at table offset 2 * offsets[level_lo]: the dense range must end there
-    NGP_CHECK_ARG(level_lo >= 0 && level_lo < L && dense_n == table_offset + 2 * (int64_t)grid->offsets[level_lo]);
-    const int64_t t = table_offset;
-    const AdamArgs a{params + t, exp_avg + t, exp_avg_sq + t, (_Float16*)params_f16 + t, lr_dev, step_dev, beta1,
-                     beta2, eps, grad_scale};
-    DenseAdam da{params, exp_avg, exp_avg_sq, (_Float16*)params_f16, grad, rep, (uint32_t)(dense_n / 4),
-                 (uint32_t)(table_offset / 4), (uint32_t)(rep_n / 4), n_rep};
-    if (rep_n == 0) da.rep4 = 0;
-    static const float dummy[1] = {0.f};
-    return hash_binned(dummy, 1, nullptr, nullptr, grid, nullptr, grad + t, workspace, max_samples, level_lo,
-                       merge_hi, 4, stream, &a, da);
 }
 
 int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,

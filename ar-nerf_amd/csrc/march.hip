@@ -353,72 +353,39 @@ __global__ void __launch_bounds__(64) march_write_kernel(const float* __restrict
 // [r*max_samples, r*max_samples + n_r).  The reference's second walk
 // (:243-279) re-derives exactly these first n_r samples, so storing them is
 // equivalent and halves the latency-bound marching.
-// The samples are staged in LDS (SB per lane, lane-minor: conflict-free) and
-// written out SB at a time with 16-byte stores: a global store inside the
-// walk would sit in vmcnt in front of the next bitfield-word load, and the
-// s_waitcnt for that load would then wait for the (scattered, slow) store too
-// -- one store round trip per occupied sample.
-constexpr int SB = 32;
-constexpr int MARCH_RPW = 16;  // default rays per wave (NGP_MARCH_RPW overrides)
-template <bool SIMPLE, bool STAGE>
+// The general (cascaded / esf > 0) walk: one lane per ray, MARCH_RPW rays
+// per 64-lane wave (the walk is a serial, latency-bound chain per ray, so
+// fewer rays per wave -- more waves on more SIMDs -- finish sooner).
+constexpr int MARCH_RPW = 16;
+template <bool SIMPLE>
 __global__ void __launch_bounds__(256) march_slots_kernel(const float* __restrict__ rays_o,
                                                           const float* __restrict__ rays_d,
                                                           const float* __restrict__ hits_t, int64_t n_rays,
                                                           const float* __restrict__ noise, MarchParams p,
                                                           int32_t* __restrict__ counts, float* __restrict__ slot_t,
-                                                          float* __restrict__ slot_dt, int rpw) {
+                                                          float* __restrict__ slot_dt) {
     extern __shared__ uint32_t ssum[];
-    __shared__ float bt[STAGE ? SB : 1][256], bd[STAGE ? SB : 1][256];
     WordCache wc;
     wc.sum = load_summary(p, ssum);
     __syncthreads();
-    const int lane = threadIdx.x & 63, tid = threadIdx.x;
-    if (lane >= rpw) return;
-    const int64_t r = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * rpw + lane;
+    const int lane = threadIdx.x & 63;
+    if (lane >= MARCH_RPW) return;
+    const int64_t r = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * MARCH_RPW + lane;
     if (r >= n_rays) return;
     float o[3], d[3], dinv[3];
     load_ray(rays_o, rays_d, r, o, d, dinv);
     const float t2 = hits_t[2 * r + 1];
     float t = start_t(hits_t, noise, r, p);
-    int N = 0, nb = 0;
+    int N = 0;
     float x, y, z, dt;
     float* st = slot_t + r * (int64_t)p.max_samples;
     float* sd = slot_dt + r * (int64_t)p.max_samples;
-    // 16-byte stores need 16-byte aligned ray slot ranges
-    const bool vec = (p.max_samples & 3) == 0 && ((uintptr_t)slot_t & 15) == 0 && ((uintptr_t)slot_dt & 15) == 0;
     while (0 <= t && t < t2 && N < p.max_samples) {
         const float tc = t;
         if (march_step<SIMPLE>(t, o, d, dinv, p, x, y, z, dt, wc)) {
-            if constexpr (!STAGE) {
-                st[N] = tc;
-                sd[N] = dt;
-                N++;
-            } else {
-                bt[nb][tid] = tc;
-                bd[nb][tid] = dt;
-                N++;
-                if (++nb == SB) {
-                    const int b0 = N - SB;
-                    if (vec) {
-#pragma unroll
-                        for (int k = 0; k < SB; k += 4) {
-                            *reinterpret_cast<float4*>(st + b0 + k) =
-                                make_float4(bt[k][tid], bt[k + 1][tid], bt[k + 2][tid], bt[k + 3][tid]);
-                            *reinterpret_cast<float4*>(sd + b0 + k) =
-                                make_float4(bd[k][tid], bd[k + 1][tid], bd[k + 2][tid], bd[k + 3][tid]);
-                        }
-                    } else {
-                        for (int k = 0; k < SB; ++k) { st[b0 + k] = bt[k][tid]; sd[b0 + k] = bd[k][tid]; }
-                    }
-                    nb = 0;
-                }
-            }
-        }
-    }
-    if constexpr (STAGE) {
-        for (int k = 0; k < nb; ++k) {
-            st[N - nb + k] = bt[k][tid];
-            sd[N - nb + k] = bd[k][tid];
+            st[N] = tc;
+            sd[N] = dt;
+            N++;
         }
     }
     counts[r] = N;
@@ -426,7 +393,6 @@ __global__ void __launch_bounds__(256) march_slots_kernel(const float* __restric
 
 // (lattice helpers LatSeg / lat_build / lat_jump: march.h)
 
-template <int DIAG = 0>  // DIAG != 0: timing-only variants for scripts/diag (1: no chase, 2: no jump targets)
 __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __restrict__ rays_o,
                                                                const float* __restrict__ rays_d,
                                                                const float* __restrict__ hits_t, int64_t n_rays,
@@ -517,41 +483,33 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
         if (live) {
             float x, y, z, dts, T;
             occ = march_probe<true>(tk, o, d, dinv, p, x, y, z, dts, wc, T);
-            if constexpr (DIAG == 2) nxt = k + 1 + (T > 1e30f);
-            else nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
+            nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
         }
         const uint64_t occm = __ballot(occ && live);
-        uint64_t vis;
-        int pnt;
-        if constexpr (DIAG == 1) {
-            pnt = c + 64 + (__builtin_amdgcn_readlane(nxt, 63) > 1 << 30);
-            vis = occm;
-        } else {
-            // The walk's chain through the window, in parallel: J_b(i) = the
-            // 2^b-th successor of window point i (64 = out of the window),
-            // built by pointer doubling; every lane then climbs from point 0
-            // with binary lifting to the last chain point <= itself -- it is
-            // on the chain iff that is itself.  (Successors only move forward.)
-            int J[6];
-            J[0] = live ? min(nxt - c, 64) : 64;
+        // The walk's chain through the window, in parallel: J_b(i) = the
+        // 2^b-th successor of window point i (64 = out of the window),
+        // built by pointer doubling; every lane then climbs from point 0
+        // with binary lifting to the last chain point <= itself -- it is
+        // on the chain iff that is itself.  (Successors only move forward.)
+        int J[6];
+        J[0] = live ? min(nxt - c, 64) : 64;
 #pragma unroll
-            for (int b = 1; b < 6; ++b) {
-                const int prev = J[b - 1];
-                const int v = __builtin_amdgcn_ds_bpermute(min(prev, 63) << 2, prev);
-                J[b] = prev >= 64 ? 64 : v;
-            }
-            int cur = 0;
-#pragma unroll
-            for (int b = 5; b >= 0; --b) {
-                const int v = __builtin_amdgcn_ds_bpermute(min(cur, 63) << 2, J[b]);
-                const int to = cur >= 64 ? 64 : v;
-                if (to <= lane) cur = to;
-            }
-            vis = __ballot(cur == lane);
-            const int last = 63 - __builtin_clzll(vis);  // the chain's last point in the window
-            pnt = __builtin_amdgcn_readlane(nxt, last);   // k_end if it ends the walk
-            vis &= occm;
+        for (int b = 1; b < 6; ++b) {
+            const int prev = J[b - 1];
+            const int v = __builtin_amdgcn_ds_bpermute(min(prev, 63) << 2, prev);
+            J[b] = prev >= 64 ? 64 : v;
         }
+        int cur = 0;
+#pragma unroll
+        for (int b = 5; b >= 0; --b) {
+            const int v = __builtin_amdgcn_ds_bpermute(min(cur, 63) << 2, J[b]);
+            const int to = cur >= 64 ? 64 : v;
+            if (to <= lane) cur = to;
+        }
+        uint64_t vis = __ballot(cur == lane);
+        const int last = 63 - __builtin_clzll(vis);  // the chain's last point in the window
+        const int pnt = __builtin_amdgcn_readlane(nxt, last);   // k_end if it ends the walk
+        vis &= occm;
         // emit the chain's occupied points, at most up to max_samples
         const int room = p.max_samples - N;
         const int nv = __builtin_popcountll(vis);
@@ -811,36 +769,13 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
     hipStream_t s = as_stream(stream);
     if (n_rays > 0) {
         NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && slot_t && slot_dt);
-        // Rays per 64-lane wave: the walk is a serial, latency-bound chain
-        // per ray, so fewer rays per wave (more waves on more SIMDs) can
-        // finish sooner (NGP_MARCH_RPW / NGP_MARCH_STAGE: diagnostics).
-        const char* env = getenv("NGP_MARCH_RPW");
-        const int rpw = env ? std::max(1, std::min(64, atoi(env))) : MARCH_RPW;
-        const char* es = getenv("NGP_MARCH_STAGE");
-        const bool stage = es ? atoi(es) != 0 : false;
-        const unsigned blocks = nblk(n_rays, 4 * rpw);
         const size_t lds = march_summary_lds(p);
-        const char* eser = getenv("NGP_MARCH_SERIAL");
-        const bool serial = eser ? atoi(eser) != 0 : false;
-        if (march_simple(p) && !serial) {
-            const char* edg = getenv("NGP_MARCH_DIAG");
-            const int dg = edg ? atoi(edg) : 0;
-            if (dg == 1)
-                NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<1><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
-                                                                            counts, slot_t, slot_dt));
-            else if (dg == 2)
-                NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<2><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
-                                                                            counts, slot_t, slot_dt));
-            else
-                NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<0><<<nblk(n_rays, 4), 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p,
-                                                                            counts, slot_t, slot_dt));
-        } else if (march_simple(p)) {
-            if (stage) NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<true, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw));
-            else NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<true, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw));
-        } else {
-            if (stage) NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false, true><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw));
-            else NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false, false><<<blocks, 256, lds, s>>>(rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, rpw));
-        }
+        if (march_simple(p))  // one cascade, esf 0: the wave-per-ray lattice walk
+            NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<nblk(n_rays, 4), 256, lds, s>>>(
+                                          rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt));
+        else
+            NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false><<<nblk(n_rays, 4 * MARCH_RPW), 256, lds, s>>>(
+                                          rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt));
     }
     NGP_TIMED(NGP_K_SCAN_RAYS, s, scan_rays_kernel<<<1, 1024, 0, s>>>(counts, n_rays, rays_a, total));
     return ngp_launch_status();

@@ -143,7 +143,7 @@ __device__ __forceinline__ void block_append_k(const int (&cnt)[CRPT], int64_t (
 // walk's chain resolved by pointer doubling) -- the same points as the serial
 // walk, bit for bit.  Sample indices are staged in LDS and appended with one
 // global atomic per block flush.
-constexpr int WAVE_NS = 16;  // default threshold (NGP_RENDER_WAVE_NS overrides, for A/B runs)
+constexpr int WAVE_NS = 16;  // N_samples threshold of the wave-per-ray mode (profiles/r01/render/wave_ns_ab.txt)
 constexpr int STAGE = 2048;
 
 struct WaveLds {
@@ -485,7 +485,7 @@ int ngp_render_test_march(const float* rays_o, const float* rays_d, float* hits_
     if (n_rays == 0) return ngp_launch_status();
     NGP_CHECK_ARG(rays_o && rays_d && hits_t && alive && xyzs && dirs && deltas && ts && n_eff && sample_idx);
     const unsigned blocks = std::min(nblk(n_rays, 256), 2048u);
-    static const int wave_ns = getenv("NGP_RENDER_WAVE_NS") ? atoi(getenv("NGP_RENDER_WAVE_NS")) : WAVE_NS;
+    const int wave_ns = WAVE_NS;
     if (march_simple(p))
         render_march_kernel<true><<<blocks, 256, march_summary_lds(p), s>>>(
             rays_o, rays_d, hits_t, p, state, parity, alive, xyzs, dirs, deltas, ts, n_eff, sample_idx, wave_ns);

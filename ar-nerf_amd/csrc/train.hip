@@ -418,26 +418,62 @@ __global__ void scatter_last_kernel(const int64_t* __restrict__ idx, const float
 
 // ---------------------------------------- occupancy cell sampling on device
 // sample_uniform_and_occupied_cells (models/networks.py:181-207) without the
-// host sync of torch.nonzero: occ_list_kernel lists the cells of one cascade
-// with density > threshold (order unspecified; one atomic per workgroup),
+// host sync of torch.nonzero: occ_count_kernel + occ_list_kernel list the
+// cells of one cascade with density > threshold in ascending cell order, as
+// torch.nonzero does (two launches: per-block counts, then each block sums
+// the counts of the blocks before it and writes its run -- deterministic, so
+// every rank of a data-parallel job builds the same list);
 // occ_sample_kernel draws M uniform cells and M cells uniformly from that
 // list (none if it is empty, as the reference's empty nonzero gives none)
 // and their jittered world positions (networks.py:262-266).
-__global__ void __launch_bounds__(1024) occ_list_kernel(const float* __restrict__ grid_c, int64_t n_cells, float thr,
-                                                        int32_t* __restrict__ list,
-                                                        unsigned long long* __restrict__ count) {
-    __shared__ uint32_t wcnt[16];
-    __shared__ unsigned long long base;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    constexpr int PER = 8;
-    const int64_t c0 = ((int64_t)blockIdx.x * 1024 + tid) * PER;
-    bool hit[PER];
+constexpr int OCC_T = 1024, OCC_PER = 8, OCC_CHUNK = OCC_T * OCC_PER;  // cells per block
+
+__device__ __forceinline__ uint32_t occ_hits(const float* __restrict__ grid_c, int64_t n_cells, float thr, int64_t c0,
+                                             bool hit[OCC_PER]) {
     uint32_t mine = 0;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
+    for (int k = 0; k < OCC_PER; ++k) {
         hit[k] = c0 + k < n_cells && grid_c[c0 + k] > thr;
         mine += hit[k];
     }
+    return mine;
+}
+
+__global__ void __launch_bounds__(OCC_T) occ_count_kernel(const float* __restrict__ grid_c, int64_t n_cells, float thr,
+                                                          uint32_t* __restrict__ block_counts) {
+    __shared__ uint32_t wcnt[OCC_T / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    bool hit[OCC_PER];
+    uint32_t v = occ_hits(grid_c, n_cells, thr, ((int64_t)blockIdx.x * OCC_T + tid) * OCC_PER, hit);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) wcnt[wid] = v;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < OCC_T / 64; ++w) tot += wcnt[w];
+        block_counts[blockIdx.x] = tot;
+    }
+}
+
+__global__ void __launch_bounds__(OCC_T) occ_list_kernel(const float* __restrict__ grid_c, int64_t n_cells, float thr,
+                                                         const uint32_t* __restrict__ block_counts,
+                                                         int32_t* __restrict__ list,
+                                                         unsigned long long* __restrict__ count) {
+    __shared__ uint32_t wcnt[OCC_T / 64];
+    __shared__ unsigned long long wbase[OCC_T / 64];
+    __shared__ unsigned long long base;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // this block's base: the counts of the blocks before it, summed by every
+    // wave over a strided share (a few hundred words, L2-resident)
+    unsigned long long before = 0ull;
+    for (int64_t b = tid; b < (int64_t)blockIdx.x; b += OCC_T) before += block_counts[b];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+    if (lane == 0) wbase[wid] = before;
+    bool hit[OCC_PER];
+    const int64_t c0 = ((int64_t)blockIdx.x * OCC_T + tid) * OCC_PER;
+    const uint32_t mine = occ_hits(grid_c, n_cells, thr, c0, hit);
     uint32_t incl = mine;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -447,20 +483,23 @@ __global__ void __launch_bounds__(1024) occ_list_kernel(const float* __restrict_
     if (lane == 63) wcnt[wid] = incl;
     __syncthreads();
     if (tid == 0) {
+        unsigned long long b = 0ull;
+        for (int w = 0; w < OCC_T / 64; ++w) b += wbase[w];
         uint32_t tot = 0;
-        for (int w = 0; w < 16; ++w) { const uint32_t v = wcnt[w]; wcnt[w] = tot; tot += v; }
-        base = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+        for (int w = 0; w < OCC_T / 64; ++w) { const uint32_t v = wcnt[w]; wcnt[w] = tot; tot += v; }
+        base = b;
+        if (blockIdx.x == gridDim.x - 1) *count = b + tot;
     }
     __syncthreads();
-    // (the list holds at most n_cells entries: a reservation past that can
-    // only come from a corrupted count -- dropped instead of written)
+    // (the list holds at most n_cells entries: a base past that can only come
+    // from corrupted counts -- dropped instead of written)
     if (base > (unsigned long long)n_cells) {
         if (tid == 0) atomicAdd(&g_guard_hits, 1ull);
         return;
     }
     int64_t pos = (int64_t)base + wcnt[wid] + incl - mine;
 #pragma unroll
-    for (int k = 0; k < PER; ++k)
+    for (int k = 0; k < OCC_PER; ++k)
         if (hit[k] && pos < n_cells) list[pos++] = (int32_t)(c0 + k);
 }
 
@@ -1046,13 +1085,19 @@ int ngp_density_scatter_last(const int64_t* indices, const float* sigmas, int64_
     return ngp_launch_status();
 }
 
+size_t ngp_occupied_cells_workspace(int64_t n_cells) {
+    return n_cells > 0 ? (size_t)((n_cells + OCC_CHUNK - 1) / OCC_CHUNK) * sizeof(uint32_t) : 0;
+}
+
 int ngp_occupied_cells(const float* grid_cascade, int64_t n_cells, float threshold, int32_t* list, int64_t* count,
-                       void* stream) {
-    NGP_CHECK_ARG(n_cells > 0 && grid_cascade && list && count && ((uintptr_t)count & 7) == 0);
+                       void* workspace, void* stream) {
+    NGP_CHECK_ARG(n_cells > 0 && n_cells < (1ll << 31) && grid_cascade && list && count && workspace &&
+                  ((uintptr_t)count & 7) == 0 && ((uintptr_t)workspace & 3) == 0);
     hipStream_t s = as_stream(stream);
-    zero_words_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(count), 1);
-    occ_list_kernel<<<(unsigned)((n_cells + 8191) / 8192), 1024, 0, s>>>(grid_cascade, n_cells, threshold, list,
-                                                                        (unsigned long long*)count);
+    const unsigned nb = (unsigned)((n_cells + OCC_CHUNK - 1) / OCC_CHUNK);
+    uint32_t* bc = reinterpret_cast<uint32_t*>(workspace);
+    occ_count_kernel<<<nb, OCC_T, 0, s>>>(grid_cascade, n_cells, threshold, bc);
+    occ_list_kernel<<<nb, OCC_T, 0, s>>>(grid_cascade, n_cells, threshold, bc, list, (unsigned long long*)count);
     return ngp_launch_status();
 }
 

@@ -54,9 +54,6 @@ def _lib():
         L.ngp_hash_backward_levels.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp]
         L.ngp_hash_backward_levels_rep.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp, c_int, c_int, c_int,
                                                    vp]
-        L.ngp_hash_binned_accum_adam_dense.argtypes = [P, vp, vp, c_int64, c_int, c_int, vp, vp, vp, vp, vp, c_float,
-                                                       c_float, c_float, vp, c_float, c_int64, c_int64, vp, c_int64,
-                                                       c_int, vp]
         L.ngp_hash_backward_rep_floats.argtypes = [P, c_int, c_int]
         L.ngp_hash_backward_rep_floats.restype = ctypes.c_size_t
         L.ngp_hash_binned_plan.argtypes = [vp, c_int64, vp, vp, P, vp, c_int64, c_int, c_int, vp]
@@ -72,7 +69,7 @@ def _lib():
         for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_density_input_grad, L.ngp_field_backward, L.ngp_field_backward_mlp,
                   L.ngp_hash_encode, L.ngp_field_mlp_forward, L.ngp_field_forward_indexed, L.ngp_field_encode_mlp,
                   L.ngp_hash_backward, L.ngp_hash_backward_binned, L.ngp_hash_backward_levels,
-                  L.ngp_hash_backward_levels_rep, L.ngp_hash_binned_accum_adam_dense,
+                  L.ngp_hash_backward_levels_rep,
                   L.ngp_hash_binned_plan, L.ngp_hash_binned_apply, L.ngp_hash_binned_write,
                   L.ngp_hash_binned_accum, L.ngp_hash_binned_apply_adam, L.ngp_hash_binned_accum_adam):
             f.restype = c_int

@@ -18,7 +18,6 @@ kernels read the live sample count from device memory.
 from __future__ import annotations
 
 import math
-import os
 
 import numpy as np
 import torch
@@ -39,6 +38,7 @@ def _p(t):
 
 STAT_STRIPES, STAT_STRIDE = 32, 16  # include/ngp_amd.h NGP_STAT_*
 THROTTLE_EVERY, THROTTLE_DEPTH = 32, 4  # host run-ahead bound: <= 160 steps enqueued
+COARSE_REP, COARSE_REP_LEVELS = 8, 4  # gradient replicas of the coarsest atomic levels
 
 
 class NGPTrainer:
@@ -46,7 +46,8 @@ class NGPTrainer:
                  lambda_opacity=1e-3, lambda_depth=0.0, random_bg=False, exp_step_factor=None, grid_size=128,
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
                  device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=None, bin_level_lo=None,
-                 chunk_first=64, erode=False, lambda_distortion=0.0, bin_merge_hi=None):
+                 chunk_first=64, erode=False, lambda_distortion=0.0, bin_merge_hi=0, fused_adam=True, use_graphs=True,
+                 pair_steps=False):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
@@ -74,11 +75,27 @@ class NGPTrainer:
         self.grid = HG.HashGrid(scale)
         init = HG.init_params(self.grid, seed=seed, device=dev)
         self.n_params = n = init.numel()
+        # hash backward: "atomic": per-sample fp32 atomics (ngp_hash_backward); "binned": all
+        # levels through the counting-sort path; "hybrid" (default): coarse levels
+        # [0, bin_level_lo) atomic -- their in-wave run merge keeps the requests few --
+        # fine levels binned (DESIGN.md "hash backward").  Defaults by scene size (measured,
+        # DESIGN.md §9): one cascade (object scenes, ~70 samples/ray) 8 atomic levels + 128
+        # binned samples/ray; cascaded (unbounded) scenes have ~2x the gradient-carrying
+        # samples and 4 more hashed levels: all levels binned (+17 % at scale 16) with room
+        # for 512 samples/ray.  Resolved before the ZeRO-1 buckets, which split at it.
+        assert hash_backward in ("atomic", "binned", "hybrid")
+        big = self.cascades > 1
+        if bin_level_lo is None:
+            bin_level_lo = 0 if big else 8
+        if bin_samples_per_ray is None:
+            bin_samples_per_ray = 512 if big else 128
+        self.hash_backward = hash_backward
+        self.bin_level_lo = 0 if hash_backward == "binned" else min(max(int(bin_level_lo), 0), self.grid.n_levels)
         # ZeRO-1 layout (ddp.zero_buckets): buffers padded to n_pad, two
         # buckets [MLP | coarse levels] [fine levels] split where the coarse
-        # gradient is complete; rank r owns shard r of each bucket
-        lo_level = 8 if bin_level_lo is None else bin_level_lo
-        split = HG.MLP_PARAMS + 2 * int(self.grid.offsets[min(max(lo_level, 0), len(self.grid.offsets) - 1)])
+        # (atomic) gradient is complete; rank r owns shard r of each bucket.
+        # All levels binned (bin_level_lo 0): bucket 0 is the MLP alone.
+        split = HG.MLP_PARAMS + 2 * int(self.grid.offsets[self.bin_level_lo])
         self.n_pad, self.buckets = ddp.zero_buckets(n, split, self.world)
         pb = torch.zeros(self.n_pad, device=dev)
         pb[:n] = init
@@ -109,11 +126,11 @@ class NGPTrainer:
         self._occ_key = torch.zeros(self.density_grid.shape, dtype=torch.int64, device=dev)
         self._occ_list = torch.empty(self.G ** 3, dtype=torch.int32, device=dev)
         self._occ_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._occ_list_ws = torch.empty((vren.lib().ngp_occupied_cells_workspace(self.G ** 3) + 3) // 4,
+                                        dtype=torch.int32, device=dev)
         self._occ_xyz = torch.empty(M2, 3, device=dev)
         self._occ_flat = torch.empty(M2, dtype=torch.int64, device=dev)
         self._occ_sig = torch.empty(M2, device=dev)
-        # NGP_OCC_SORTED=0: cells in draw order (ngp_occupancy_samples)
-        self.occ_sorted = os.environ.get("NGP_OCC_SORTED", "1") == "1"
         self._occ_ws = torch.empty((vren.lib().ngp_occupancy_sorted_workspace(M2 // 2) + 7) // 8, dtype=torch.float64,
                                    device=dev)
         self.threshold = torch.zeros(2, device=dev)
@@ -129,50 +146,29 @@ class NGPTrainer:
         self.msets = [self._march_buffers(R, cap, f, self.density_bitfield.numel()) for _ in range(2)]
         self.cur = 0
         self.march_stream = torch.cuda.Stream(device=dev)
-        # NGP_EXEC_PRIORITY=1: steps run on a high-priority stream (measured: no gain)
-        self.exec_stream = (torch.cuda.Stream(device=dev, priority=-1)
-                            if os.environ.get("NGP_EXEC_PRIORITY", "0") == "1" else None)
         self._pending = None  # (set index, event) of a batch marched ahead
         self.n_prefetched = 0
-        self.no_prefetch = os.environ.get("NGP_NO_PREFETCH", "0") == "1"  # march every batch inline (diagnostics)
-        # where in the step the next batch's march is launched on the side stream: at
-        # the start (beside the gather-bound encode rather than the VALU-bound MLP
-        # backward: +1.5 %, profiles/r02/ab/prefetch_at.txt)
-        self.prefetch_at = os.environ.get("NGP_PREFETCH_AT", "start")
-        # NGP_PAIR_STEPS=1: two consecutive steady-state steps per graph replay (_replay_pair)
-        self.pair_steps = os.environ.get("NGP_PAIR_STEPS", "0") == "1"
+        self.no_prefetch = False  # (diagnostics) march every batch inline
+        # pair_steps: two consecutive steady-state steps per graph replay (_replay_pair)
+        self.pair_steps = bool(pair_steps)
         self._ran_ahead = False
+        self._pair_key = None
         self._bind(self.msets[0])
         self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         # saved encoding: pair-major (8, cap, 4) for the split forward, else row-major (cap, 32)
         # hybrid hash backward: the atomic coarse levels run on their own
         # stream beside the binned fine levels (disjoint gradient ranges;
         # memory-side atomics vs LDS-bound passes overlap)
+        # (Single process) the Adam of the MLP + coarse levels runs on that side stream
+        # right after the coarse levels' backward, beside the binned levels'
+        # accumulation, whose own FusedAdam is fused into it (+5 %,
+        # profiles/r02/ab/fused_adam.txt; bit-identical to one FusedAdam launch after the
+        # backward, which fused_adam=False restores).
         self.bwd_stream = torch.cuda.Stream(device=dev)
-        self.overlap_hash_bwd = os.environ.get("NGP_BWD_OVERLAP", "1") == "1"
-        # Adam of the MLP + coarse levels on the side stream right after the coarse
-        # levels' backward, beside the binned levels' accumulation (single process;
-        # with the binned levels' Adam fused into their accumulation: +5 %,
-        # profiles/r02/ab/fused_adam.txt; NGP_ADAM_SPLIT=0 turns it off)
-        self.adam_split = os.environ.get("NGP_ADAM_SPLIT", "1") == "1"
-        # NGP_COARSE_AFTER_WRITE=1: the coarse atomic levels start after the binned record write
-        # (measured slower: the accumulation then slows as much as the write speeds up,
-        # profiles/r02/ab/coarse_overlap.txt)
-        self.coarse_after_write = os.environ.get("NGP_COARSE_AFTER_WRITE", "0") == "1"
-        # NGP_FUSED_ADAM=0: one FusedAdam launch over all params after the backward
-        # (else the binned levels are stepped inside their accumulation, bit-identical)
-        self.fused_adam = os.environ.get("NGP_FUSED_ADAM", "1") == "1"
-        # NGP_DENSE_IN_ACCUM=1 (with fused_adam + adam_split): the MLP + coarse levels' Adam
-        # (and the coarse replica fold) in the binned accumulation's tail instead of two
-        # launches on the side stream -- measured slower (the accumulation then waits for
-        # the coarse stream, ~10 us join, and grows by the dense Adam's 23 us;
-        # profiles/r02/ab/dense_in_accum.txt), so off by default
-        self.dense_in_accum = os.environ.get("NGP_DENSE_IN_ACCUM", "0") == "1"
+        self.fused_adam = bool(fused_adam)
         self._adam_hi = None
-        self.split_forward = os.environ.get("NGP_SPLIT_FORWARD", "1") == "1"
-        # the training forward's encode and MLPs in one launch (pair-major enc as split_forward;
-        # +1.8 % over 4 interleaved runs, profiles/r02/ab/fused_field.txt; NGP_FUSED_FIELD=0: two launches)
-        self.fused_field = self.split_forward and os.environ.get("NGP_FUSED_FIELD", "1") == "1"
+        # the training forward: encode + MLPs in one launch (ngp_field_encode_mlp), the
+        # pair-major encoding kept for the backward (+1.8 %, profiles/r02/ab/fused_field.txt)
         self.enc = torch.empty(8 * cap * 4, dtype=torch.float16, device=dev)
         self.dsig, self.drgb = torch.empty(cap, **f), torch.empty(cap, 3, **f)
         self.denc = torch.empty(cap, 32, **f)
@@ -184,12 +180,10 @@ class NGPTrainer:
         # [0, 3] = field-evaluated samples (ngp_ray_segments total_acc)
         self.stats = torch.zeros(STAT_STRIPES * STAT_STRIDE, dtype=torch.int64, device=dev)
         # chunked field evaluation (ngp_chunk_counts): first `chunk_first` samples of
-        # every row, then the rest of the rows not yet terminated (0 = every sample)
-        self.chunk_first = int(os.environ.get("NGP_CHUNK_FIRST", chunk_first))
-        # further round bounds after chunk_first (NGP_CHUNK_ROUNDS="128" -> rounds [0,64) [64,128) [128,N)):
-        # 22 % fewer evaluated samples, but each extra round's encode launch costs more than it saves
-        # (profiles/r02/ab/chunk_rounds.txt)
-        self.chunk_rounds = [int(x) for x in os.environ.get("NGP_CHUNK_ROUNDS", "").split(",") if x.strip()]
+        # every row, then the rest of the rows not yet terminated (0 = every sample).
+        # (More rounds evaluate 22 % fewer samples, but each extra encode launch costs
+        # more than it saves: profiles/r02/ab/chunk_rounds.txt)
+        self.chunk_first = int(chunk_first)
         self.eval_counts = torch.empty(R, dtype=torch.int32, device=dev)
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -201,40 +195,20 @@ class NGPTrainer:
         # binned hash backward: workspace for bin_samples_per_ray gradient-
         # carrying samples per ray on average (1 KiB each; the rest take the
         # atomic path, still exact)
-        # "atomic": per-sample fp32 atomics (ngp_hash_backward); "binned": all
-        # levels through the counting-sort path; "hybrid" (default): coarse
-        # levels [0, bin_level_lo) atomic -- their in-wave run merge keeps the
-        # requests few -- fine levels binned (DESIGN.md "hash backward").
-        assert hash_backward in ("atomic", "binned", "hybrid")
-        # defaults by scene size (measured): one cascade (object scenes, ~70
-        # samples/ray) 8 atomic levels + 128 binned samples/ray; cascaded (unbounded) scenes
-        # have ~2x the gradient-carrying samples and 4 more hashed levels: all levels binned
-        # (+17 % at scale 16) with room for 512 samples/ray
-        big = self.cascades > 1
-        if bin_level_lo is None:
-            bin_level_lo = 0 if big else 8
-        if bin_samples_per_ray is None:
-            bin_samples_per_ray = 512 if big else 128
-        self.hash_backward = hash_backward
-        self.bin_level_lo = 0 if hash_backward == "binned" else bin_level_lo
         # binned levels [bin_level_lo, bin_merge_hi) merge runs of equal corner pairs along a ray
-        if bin_merge_hi is None:
-            bin_merge_hi = int(os.environ.get("NGP_BIN_MERGE_HI", "0"))
-        self.bin_merge_hi = bin_merge_hi
+        self.bin_merge_hi = int(bin_merge_hi)
         if hash_backward != "atomic":
             self.bin_max_samples = R * bin_samples_per_ray
             nbytes = HG._lib().ngp_hash_backward_binned_workspace(self.bin_max_samples)
             self.bin_ws = torch.empty((nbytes + 255) // 256, 64, dtype=torch.int32, device=dev)
         # coarse atomic levels [0, coarse_rep_levels) add into coarse_rep replicas of their
         # gradient range, folded afterwards (ngp_hash_backward_levels_rep): the coarsest
-        # levels are a few hundred KB every sample touches (NGP_COARSE_REP=0: off)
-        self.coarse_rep = int(os.environ.get("NGP_COARSE_REP", "8"))
-        self.coarse_rep_levels = min(int(os.environ.get("NGP_COARSE_REP_LEVELS", "4")), self.bin_level_lo) \
-            if hash_backward != "atomic" else 0
+        # levels are a few hundred KB every sample touches (levels 0-3 x 8 measured best,
+        # profiles/r02/ab/coarse_replicas.txt); single process: folded by the MLP + coarse
+        # levels' Adam launch
+        self.coarse_rep = COARSE_REP
+        self.coarse_rep_levels = min(COARSE_REP_LEVELS, self.bin_level_lo) if hash_backward != "atomic" else 0
         self.rep_buf = None
-        # single process: the replicas are folded by the MLP + coarse levels' Adam launch
-        # (NGP_ADAM_REP=0: by a launch of their own before it)
-        self.adam_rep = os.environ.get("NGP_ADAM_REP", "1") == "1"
         if self.coarse_rep > 0 and self.coarse_rep_levels > 0:
             nrep = HG._lib().ngp_hash_backward_rep_floats(HG.ctypes.byref(self.grid.desc), self.coarse_rep_levels,
                                                           self.coarse_rep)
@@ -258,7 +232,7 @@ class NGPTrainer:
         self.lr_dev = torch.full((1,), float(lr), device=dev)
         self._lr_set = float(lr)
         # HIP graphs of the steady-state step, one per buffer set (see train_step)
-        self.use_graphs = os.environ.get("NGP_GRAPHS", "1") == "1"
+        self.use_graphs = bool(use_graphs)
         self._graphs = {}
         self.L = vren.lib()
         HG._lib()
@@ -268,9 +242,6 @@ class NGPTrainer:
         self.timer = None
         # world > 1 graph replays run as segments with the collectives between them
         self._segmented = False
-        # world > 1: the hash backward as separate graph segments, the first bucket's
-        # reduce-scatter overlapping the binned levels (NGP_RS_OVERLAP=0: one segment, then both)
-        self._seg_split = os.environ.get("NGP_RS_OVERLAP", "1") == "1"
         self.comm_stream = torch.cuda.Stream(device=dev) if torch.cuda.is_available() else None
         self._throttle_q = []  # events of every THROTTLE_EVERY-th step (train_step)
 
@@ -369,32 +340,21 @@ class NGPTrainer:
             else:  # sample_uniform_and_occupied_cells (networks.py:181-207), on device
                 M = G ** 3 // 4
                 vren._ok(L.ngp_occupied_cells(_p(self.density_grid[c]), G ** 3, ctypes_float(density_threshold),
-                                              _p(self._occ_list), _p(self._occ_count), s), "occupied_cells")
+                                              _p(self._occ_list), _p(self._occ_count), _p(self._occ_list_ws), s),
+                         "occupied_cells")
                 lo, hi = ddp.shard_range(2 * M, self.rank, self.world)
                 n = hi - lo
                 args = (self.occ_seed, _p(self.dctr[2:]), c, G, M, ctypes_float(sc - half_grid_size),
                         ctypes_float(half_grid_size), _p(self._occ_list), _p(self._occ_count), lo, hi)
-                if self.occ_sorted:  # ascending cells: the density forward's waves stay cache-local
-                    vren._ok(L.ngp_occupancy_samples_sorted(*args, _p(self._occ_ws), _p(self._occ_xyz),
-                                                            _p(self._occ_flat), s), "occupancy_samples_sorted")
-                else:
-                    vren._ok(L.ngp_occupancy_samples(*args, _p(self._occ_xyz), _p(self._occ_flat), s),
-                             "occupancy_samples")
-                HGL = HG._lib()
-                if self.fused_field:  # encode + density net in one launch (no encoding kept)
-                    vren._ok(HGL.ngp_field_encode_mlp(_p(self._occ_xyz), None, n, None, None,
-                                                      HG.ctypes.byref(self.grid.desc),
-                                                      _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), None,
-                                                      _p(self._occ_sig), None, None, s), "density_encode_mlp")
-                elif self.split_forward and 32 * n <= self.enc.numel():  # encode into the step's (free) enc buffer
-                    vren._ok(HGL.ngp_hash_encode(_p(self._occ_xyz), n, None, None, HG.ctypes.byref(self.grid.desc),
-                                                 _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc), s), "hash_encode")
-                    vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), None, n, None, None, _p(self.params16),
-                                                       _p(self._occ_sig), None, None, s), "density_mlp")
-                else:
-                    vren._ok(HGL.ngp_density_forward(_p(self._occ_xyz), n, None, HG.ctypes.byref(self.grid.desc),
-                                                     _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16),
-                                                     _p(self._occ_sig), None, s), "density_forward")
+                # each half's cells drawn in ascending order: the density forward's waves
+                # stay cache-local (1.8x faster than draw order, scripts/diag/density_order.py)
+                vren._ok(L.ngp_occupancy_samples_sorted(*args, _p(self._occ_ws), _p(self._occ_xyz),
+                                                        _p(self._occ_flat), s), "occupancy_samples_sorted")
+                # encode + density net in one launch (no encoding kept)
+                vren._ok(HG._lib().ngp_field_encode_mlp(_p(self._occ_xyz), None, n, None, None,
+                                                        HG.ctypes.byref(self.grid.desc),
+                                                        _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), None,
+                                                        _p(self._occ_sig), None, None, s), "density_encode_mlp")
                 sig, flat = self._occ_sig, self._occ_flat
             # density_grid_tmp[c, indices] = sigma, list positions lo + i (rank shards)
             vren._ok(L.ngp_density_scatter_last(_p(flat), _p(sig), n, lo, _p(key), s), "density_scatter_last")
@@ -507,20 +467,6 @@ class NGPTrainer:
             ev[name][-1][1].record(st)
 
     # ---------------------------------------------------------------- step
-    def _on_exec_stream(self, fn, *args):
-        """Run one step on the trainer's high-priority stream (ordered after
-        and before the caller's current stream): the batch marched ahead on
-        the normal-priority side stream then only takes CU slots the step's
-        kernels leave free."""
-        if self.exec_stream is None:
-            return fn(*args)
-        caller = torch.cuda.current_stream()
-        self.exec_stream.wait_stream(caller)
-        with torch.cuda.stream(self.exec_stream):
-            out = fn(*args)
-        caller.wait_stream(self.exec_stream)
-        return out
-
     def stat_totals(self):
         """(marched, composited, active, evaluated) samples accumulated since
         stats was last zeroed (sum over the stripes)."""
@@ -532,8 +478,7 @@ class NGPTrainer:
         next_batch = (img, pix) of the following step: marched ahead on the
         side stream."""
         nxt = None if next_batch is None else ("idx", next_batch[0], next_batch[1], None)
-        return self._on_exec_stream(self._step, ("idx", img_idxs, pix_idxs, noise), rgb_gt, directions, poses,
-                                    apply_adam, nxt)
+        return self._step(("idx", img_idxs, pix_idxs, noise), rgb_gt, directions, poses, apply_adam, nxt)
 
     def train_step(self, gt, directions, poses):
         """One training step on a batch drawn on device from the training set
@@ -547,6 +492,9 @@ class NGPTrainer:
         gs, ui = self.global_step, self.update_interval
         self._throttle()
         if self._ran_ahead:  # this step was the second half of the previous call's two-step graph
+            if self._pair_key != (gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype):
+                raise RuntimeError("pair_steps: the second step of a two-step graph replay must be given the same "
+                                   "gt / directions / poses as the first (it already ran on them)")
             self._ran_ahead = False
             self.global_step += 1
             return self.out_loss
@@ -556,17 +504,22 @@ class NGPTrainer:
                     and (gs + 2) % ui != 0 and gs // self.steps_per_epoch == (gs + 1) // self.steps_per_epoch):
                 return self._replay_pair(gt, directions, poses)
             return self._replay(gt, directions, poses, (gs + 1) % ui == 0)
-        return self._on_exec_stream(self._step, ("sample", 0, gt), None, directions, poses, True,
-                                    ("sample", 1, gt))
+        return self._step(("sample", 0, gt), None, directions, poses, True, ("sample", 1, gt))
 
     def _throttle(self):
-        """Bound how far the host runs ahead of the GPU: an event every
-        THROTTLE_EVERY steps, and before enqueueing more the host waits for
-        the one THROTTLE_DEPTH events back (that step finished long ago when
-        the GPU is the bottleneck, so the queue never drains).  Thousands of
-        enqueued graph replays outstanding at once were followed by memory
-        faults in long runs (30k steps without a host sync); with the host
-        kept within a few hundred steps they ran clean."""
+        """Back-pressure on the host: an event every THROTTLE_EVERY steps, and
+        before enqueueing more the host waits for the one THROTTLE_DEPTH events
+        back, so at most ~160 steps are ever enqueued ahead of the GPU (that
+        step finished long ago when the GPU is the bottleneck: the queue never
+        drains, measured no slower).  It bounds the host's lead -- a caller
+        that stops, reads out_loss or edits the scene waits for at most that
+        many steps, and the runtime's command queue stays bounded -- and is not
+        a fault fix.  (The memory faults once seen in long graph-replayed runs
+        had another cause, found and fixed in d87e59d: a captured
+        hipMemsetAsync of the occupancy-list counter was not ordered before the
+        list kernel, which then read stale counts and wrote past the list;
+        counters are now zeroed by a kernel node, and the list is built from
+        per-block counts with no counter to zero at all.)"""
         if self.global_step % THROTTLE_EVERY:
             return
         ev = torch.cuda.Event()
@@ -598,7 +551,7 @@ class NGPTrainer:
             self._run_graph(key, lambda: self._graph_body(k, gt, directions, poses, update_after))
         else:  # collectives between graph segments (no RCCL inside captures)
             self._run_graph(key + ("compute",), lambda: self._segment_compute(k, gt, directions, poses, update_after))
-            if self._seg_split and self.hash_backward != "atomic":
+            if self.hash_backward != "atomic":
                 cs = torch.cuda.current_stream()
                 self.bwd_stream.wait_stream(cs)
                 with torch.cuda.stream(self.bwd_stream):
@@ -644,6 +597,7 @@ class NGPTrainer:
         self.n_prefetched += 2
         self.global_step += 1
         self._ran_ahead = True
+        self._pair_key = key[2:]
         return self.out_loss
 
     def _run_graph(self, key, body):
@@ -777,59 +731,38 @@ class NGPTrainer:
     def _compute(self, rgb_gt, apply_adam, fork):
         """Field forward (chunked), compositing + loss + its backward, field
         backward, [all-reduce], Adam -- on the current stream, no host sync.
-        fork() (nullable) launches the next batch's march on the side stream at
-        the step point self.prefetch_at."""
+        fork() (nullable) launches the next batch's march on the side stream;
+        it runs at the step's start, beside the gather-bound encode rather
+        than the VALU-bound MLP backward (+1.5 %, profiles/r02/ab/prefetch_at.txt)."""
         L, s, HGL, R = self.L, vren._stream(), HG._lib(), self.batch_size
-
-        def at(point):
-            if fork is not None and self.prefetch_at == point:
-                fork()
-
-        at("start")
+        if fork is not None:
+            fork()
         self._ev("field_fwd", 0)
         if self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
             if R <= 65536:  # counts min(N_r, K) + scan + list in one launch
                 vren._ok(L.ngp_ray_segments_capped(_p(self.rays_a), R, K, _p(self.act_start), _p(self.eval_total),
                                                    _p(self.stats[3:]), _p(self.eval_idx), s), "segments_capped")
-                at("after_seg0")
             else:
                 vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, None, None, ctypes_float(1e-4),
                                             _p(self.eval_counts), s), "chunk_counts")
                 vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, 0, _p(self.act_start),
                                             _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
             self._field_indexed(s)
-            # later rounds [c_i, c_{i+1}) of rows still transparent, the last one open-ended
-            bounds = [b for b in self.chunk_rounds if b > K] + [0]
-            lo = K
-            for hi in bounds:
-                vren._ok(L.ngp_chunk_counts_range(_p(self.rays_a), R, lo, hi, _p(self.sigmas), _p(self.deltas),
-                                                  ctypes_float(1e-4), _p(self.eval_counts), s), "chunk_counts")
-                vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, lo, _p(self.act_start),
-                                            _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
-                self._field_indexed(s)
-                lo = hi
-        elif self.fused_field:  # encode + MLPs in one launch over every marched sample
+            # second round [K, N_r) of the rows still transparent after K samples
+            vren._ok(L.ngp_chunk_counts_range(_p(self.rays_a), R, K, 0, _p(self.sigmas), _p(self.deltas),
+                                              ctypes_float(1e-4), _p(self.eval_counts), s), "chunk_counts")
+            vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, K, _p(self.act_start),
+                                        _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
+            self._field_indexed(s)
+        else:  # encode + MLPs in one launch over every marched sample
             self._ev("hash_encode", 0)
             vren._ok(HGL.ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples), None,
                                               HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
                                               _p(self.params16), _p(self.enc), _p(self.sigmas), _p(self.rgbs), None,
                                               s), "field_encode_mlp")
             self._ev("hash_encode", 1)
-        elif self.split_forward:  # encode (pair-major self.enc), then the MLPs, over every marched sample
-            vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.n_samples), None,
-                                         HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
-                                         _p(self.enc), s), "hash_encode")
-            vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), _p(self.dirs), self.cap, _p(self.n_samples), None,
-                                               _p(self.params16), _p(self.sigmas), _p(self.rgbs), None, s),
-                     "field_mlp_forward")
-        else:  # fused gathers + MLPs over every marched sample (row-major self.enc)
-            vren._ok(HGL.ngp_field_forward(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples),
-                                           HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
-                                           _p(self.params16), _p(self.sigmas), _p(self.rgbs), _p(self.enc), None, s),
-                     "field_forward")
         self._ev("field_fwd", 1)
-        at("after_fwd")
         bg = self.bg
         if self.random_bg:  # rendering.py:287-288, one colour per batch, drawn on device (graph-safe)
             bg = self._bg_rand
@@ -849,10 +782,9 @@ class NGPTrainer:
         vren._ok(L.ngp_active_samples(_p(self.n_active), _p(self.rays_a), R, _p(self.act_start),
                                       _p(self.n_active_total), _p(self.sample_idx), s), "active_samples")
         self._ev("composite_loss", 1)
-        at("after_composite")
         cs = torch.cuda.current_stream()
         hybrid = self.hash_backward != "atomic"
-        bs = self.bwd_stream if self.overlap_hash_bwd else cs
+        bs = self.bwd_stream
         if hybrid:  # bucket plan of the binned fine levels (xyzs / sample_idx only) beside the MLP backward
             bs.wait_stream(cs)
             with torch.cuda.stream(bs):
@@ -864,12 +796,10 @@ class NGPTrainer:
                 planned.record(bs)
         self._ev("mlp_bwd", 0)
         vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                                            _p(self.enc), self.cap if self.split_forward else 0,
-                                            _p(self.params16), _p(self.dsig), _p(self.drgb), _p(self.denc),
-                                            _p(self.grad), s), "field_backward_mlp")
+                                            _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
+                                            _p(self.denc), _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
-        at("after_mlp_bwd")
-        if self._segmented and self._seg_split and hybrid:
+        if self._segmented and hybrid:
             # (world > 1 graph segments: the hash backward runs as two more
             # graphs -- coarse levels on the side stream, binned levels here --
             # so the reduce-scatter of the [MLP | coarse] bucket overlaps the
@@ -881,107 +811,43 @@ class NGPTrainer:
             # atomic coarse levels on the side stream and binned fine levels
             # (after the plan) here, side by side: disjoint gradient ranges
             split = HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
-            adam_split = self.adam_split and apply_adam and self.world == 1 and bs is not cs
-            # single process: the binned levels' Adam runs inside their accumulation
-            fused = self.fused_adam and apply_adam and self.world == 1
+            # single process: the MLP + coarse levels' Adam right after them on the side stream
+            # (no all-reduce orders it after the whole gradient), folding the coarse gradient
+            # replicas itself; the binned levels' Adam inside their accumulation (fused_adam)
+            adam_split = apply_adam and self.world == 1
+            fused = self.fused_adam and adam_split
             self._adam_hi = split if fused else self.n_params
-
-            def coarse():
-                # single process: Adam of the MLP + coarse levels right after them
-                # (no all-reduce orders it after the whole gradient), folding the
-                # coarse gradient replicas itself (one launch less)
-                fold_in_adam = adam_split and self.rep_buf is not None and self.adam_rep
+            fold_in_adam = adam_split and self.rep_buf is not None
+            bs.wait_stream(cs)
+            with torch.cuda.stream(bs):
                 self._ev("hash_bwd_coarse", 0)
                 self._coarse_levels(fold=not fold_in_adam)
                 self._ev("hash_bwd_coarse", 1)
                 if adam_split:
                     self._adam(0, split, vren._stream(), rep=fold_in_adam)
-
-            def apply():
-                self._ev("hash_binned_apply", 0)
-                if fused:  # + FusedAdam of the binned levels inside the accumulation
-                    t = HG.MLP_PARAMS
-                    vren._ok(HGL.ngp_hash_binned_apply_adam(
-                        _p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                        HG.ctypes.byref(self.grid.desc), _p(self.denc), _p(self.grad[t:]), _p(self.bin_ws),
-                        self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi, _p(self.params[t:]),
-                        _p(self.exp_avg[t:]), _p(self.exp_avg_sq[t:]), _p(self.params16[t:]), _p(self.lr_dev),
-                        ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
-                        ctypes_float(1.0 / self.world), vren._stream()), "hash_binned_apply_adam")
-                else:
-                    vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                       _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
-                                                       _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws),
-                                                       self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi,
-                                                       vren._stream()), "hash_binned_apply")
-                self._ev("hash_binned_apply", 1)
-                if adam_split and not fused:
-                    self._adam(split, self.params.numel(), vren._stream())
-
-            if fused and adam_split and self.dense_in_accum:
-                # coarse levels (replicas unfolded) on the side stream beside the
-                # record write; then one accumulation launch sums the binned levels
-                # with their FusedAdam and, in its tail, folds the replicas and
-                # steps the dense range [MLP | coarse levels] (no separate Adam)
-                bs.wait_stream(cs)
-                with torch.cuda.stream(bs):
-                    self._ev("hash_bwd_coarse", 0)
-                    self._coarse_levels(fold=False)
-                    self._ev("hash_bwd_coarse", 1)
-                cs.wait_event(planned)
-                self._ev("hash_binned_apply", 0)
-                desc = HG.ctypes.byref(self.grid.desc)
-                t = HG.MLP_PARAMS
-                vren._ok(HGL.ngp_hash_binned_write(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                   _p(self.sample_idx), desc, _p(self.denc), _p(self.grad[t:]),
-                                                   _p(self.bin_ws), self.bin_max_samples, self.bin_level_lo,
-                                                   self.bin_merge_hi, vren._stream()), "hash_binned_write")
-                cs.wait_stream(bs)
-                rep = self.rep_buf is not None
-                vren._ok(HGL.ngp_hash_binned_accum_adam_dense(
-                    desc, _p(self.grad), _p(self.bin_ws), self.bin_max_samples, self.bin_level_lo,
-                    self.bin_merge_hi, _p(self.params), _p(self.exp_avg), _p(self.exp_avg_sq), _p(self.params16),
-                    _p(self.lr_dev), ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
-                    ctypes_float(1.0 / self.world), t, split, _p(self.rep_buf) if rep else None,
-                    2 * self.grid.offsets[self.coarse_rep_levels] if rep else 0, max(1, self.coarse_rep),
-                    vren._stream()), "hash_binned_accum_adam_dense")
-                self._ev("hash_binned_apply", 1)
-            elif self.coarse_after_write:
-                # coarse atomics beside the accumulation only (the record write
-                # runs alone: it slowed ~4x beside the memory-side atomics)
-                cs.wait_event(planned)
-                self._ev("hash_binned_apply", 0)
-                args = (HG.ctypes.byref(self.grid.desc), _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws),
-                        self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi)
-                vren._ok(HGL.ngp_hash_binned_write(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                   _p(self.sample_idx), args[0], _p(self.denc), *args[1:],
-                                                   vren._stream()), "hash_binned_write")
-                bs.wait_stream(cs)
-                with torch.cuda.stream(bs):
-                    coarse()
-                if fused:
-                    t = HG.MLP_PARAMS
-                    vren._ok(HGL.ngp_hash_binned_accum_adam(
-                        *args, _p(self.params[t:]), _p(self.exp_avg[t:]), _p(self.exp_avg_sq[t:]),
-                        _p(self.params16[t:]), _p(self.lr_dev), ctypes_float(0.9), ctypes_float(0.999),
-                        ctypes_float(1e-15), _p(self.dctr), ctypes_float(1.0 / self.world), vren._stream()),
-                        "hash_binned_accum_adam")
-                else:
-                    vren._ok(HGL.ngp_hash_binned_accum(*args, vren._stream()), "hash_binned_accum")
-                self._ev("hash_binned_apply", 1)
-                if adam_split and not fused:
-                    self._adam(split, self.params.numel(), vren._stream())
+            cs.wait_event(planned)
+            self._ev("hash_binned_apply", 0)
+            t = HG.MLP_PARAMS
+            if fused:  # + FusedAdam of the binned levels inside the accumulation
+                vren._ok(HGL.ngp_hash_binned_apply_adam(
+                    _p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                    HG.ctypes.byref(self.grid.desc), _p(self.denc), _p(self.grad[t:]), _p(self.bin_ws),
+                    self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi, _p(self.params[t:]),
+                    _p(self.exp_avg[t:]), _p(self.exp_avg_sq[t:]), _p(self.params16[t:]), _p(self.lr_dev),
+                    ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                    ctypes_float(1.0 / self.world), s), "hash_binned_apply_adam")
             else:
-                bs.wait_stream(cs)
-                with torch.cuda.stream(bs):
-                    coarse()
-                cs.wait_event(planned)
-                apply()
+                vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
+                                                   _p(self.denc), _p(self.grad[t:]), _p(self.bin_ws),
+                                                   self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi, s),
+                         "hash_binned_apply")
+                if adam_split:
+                    self._adam(split, self.n_params, s)
+            self._ev("hash_binned_apply", 1)
             cs.wait_stream(bs)
             if adam_split:
                 self._ev("hash_bwd", 1)
-                self._ev("allreduce", 0)  # (no all-reduce: one process)
-                self._ev("allreduce", 1)
                 return self.out_loss
         else:
             vren._ok(HGL.ngp_hash_backward(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
@@ -990,7 +856,7 @@ class NGPTrainer:
         self._ev("hash_bwd", 1)
         if self.world == 1 and apply_adam:
             self._ev("adam", 0)
-            self._adam(0, self._adam_hi if hybrid else self.n_params, s)
+            self._adam(0, self.n_params, s)
             self._ev("adam", 1)
         elif self.world > 1 and not self._segmented:
             self._reduce_grads()
@@ -1041,13 +907,6 @@ class NGPTrainer:
             return 0
         return self.n_params - (HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo])
 
-    def dense_accum_params(self):
-        """Parameters of the dense range [MLP | atomic coarse levels] whose Adam
-        runs in the binned accumulation's tail (dense_in_accum), 0 otherwise."""
-        if not (self.fused_params() and self.dense_in_accum and self.adam_split and self.overlap_hash_bwd):
-            return 0
-        return HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo]
-
     def _adam(self, lo, hi, s, rep=False):
         """FusedAdam over params[lo:hi] (16-byte aligned bounds).  lr and the
         step count from device memory (graph replays); dctr[0] = steps taken
@@ -1068,32 +927,14 @@ class NGPTrainer:
                                           ctypes_float(1.0 / self.world), 1, s), "adam")
 
     def _field_indexed(self, s):
-        """Field forward over the listed samples eval_idx[:eval_total]."""
-        HGL = HG._lib()
-        if self.fused_field:  # encode + MLPs in one launch
-            self._ev("hash_encode", 0)
-            vren._ok(HGL.ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.eval_total),
-                                              _p(self.eval_idx), HG.ctypes.byref(self.grid.desc),
-                                              _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc),
-                                              _p(self.sigmas), _p(self.rgbs), None, s), "field_encode_mlp")
-            self._ev("hash_encode", 1)
-            return
-        if self.split_forward:
-            self._ev("hash_encode", 0)
-            vren._ok(HGL.ngp_hash_encode(_p(self.xyzs), self.cap, _p(self.eval_total), _p(self.eval_idx),
-                                         HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
-                                         _p(self.enc), s), "hash_encode")
-            self._ev("hash_encode", 1)
-            self._ev("field_mlp", 0)
-            vren._ok(HGL.ngp_field_mlp_forward(_p(self.enc), _p(self.dirs), self.cap, _p(self.eval_total),
-                                               _p(self.eval_idx), _p(self.params16), _p(self.sigmas), _p(self.rgbs),
-                                               None, s), "field_mlp_forward")
-            self._ev("field_mlp", 1)
-            return
-        vren._ok(HGL.ngp_field_forward_indexed(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.eval_total),
-                                               _p(self.eval_idx), HG.ctypes.byref(self.grid.desc),
-                                               _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.sigmas),
-                                               _p(self.rgbs), _p(self.enc), s), "field_forward_indexed")
+        """Field forward (encode + MLPs in one launch) over the listed samples
+        eval_idx[:eval_total]; the pair-major encoding kept for the backward."""
+        self._ev("hash_encode", 0)
+        vren._ok(HG._lib().ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.eval_total),
+                                                _p(self.eval_idx), HG.ctypes.byref(self.grid.desc),
+                                                _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc),
+                                                _p(self.sigmas), _p(self.rgbs), None, s), "field_encode_mlp")
+        self._ev("hash_encode", 1)
 
     # ---------------------------------------------------- test-time render
     @torch.no_grad()

@@ -48,7 +48,7 @@ def _declare(L):
                                   c_int64, c_int64, c_int, vp],
         "ngp_counters_inc": [vp, c_int, vp],
         "ngp_random_bg": [ctypes.c_uint64, vp, c_int64, vp, vp],
-        "ngp_occupied_cells": [vp, c_int64, c_float, vp, vp, vp],
+        "ngp_occupied_cells": [vp, c_int64, c_float, vp, vp, vp, vp],
         "ngp_occupancy_samples": [ctypes.c_uint64, vp, c_int, c_int, c_int64, c_float, c_float, vp, vp, c_int64,
                                   c_int64, vp, vp, vp],
         "ngp_occupancy_samples_sorted": [ctypes.c_uint64, vp, c_int, c_int, c_int64, c_float, c_float, vp, vp,
@@ -97,6 +97,8 @@ def _declare(L):
     L.ngp_hashgrid_levels.restype = ctypes.c_uint32
     L.ngp_occupancy_sorted_workspace.argtypes = [c_int64]
     L.ngp_occupancy_sorted_workspace.restype = ctypes.c_size_t
+    L.ngp_occupied_cells_workspace.argtypes = [c_int64]
+    L.ngp_occupied_cells_workspace.restype = ctypes.c_size_t
     L.ngp_render_test_capacity.argtypes = [c_int64, c_int]
     L.ngp_render_test_capacity.restype = c_int64
     L.ngp_guard_hits.argtypes = []

@@ -71,10 +71,7 @@ KERNEL_WORK = {  # name: (bound, [(work per unit, unit basis), ...], member kern
     # records written + read (1104 B / active sample) and, when the binned
     # levels' Adam is fused into the accumulation, their Adam state: p, m, v
     # read and written + the fp16 shadow (26 B / param; no gradient traffic)
-    # (+ 34 B / param of the dense [MLP | coarse levels] range when its Adam
-    # runs in the accumulation's tail, dense_accum_params)
-    "hash_bwd_fine": ("hbm", [(16 + 64 + 2 * 8 * 8 * 2 * 4, "active"), (26, "fused_params"),
-                              (34, "dense_accum_params")],
+    "hash_bwd_fine": ("hbm", [(16 + 64 + 2 * 8 * 8 * 2 * 4, "active"), (26, "fused_params")],
                       ["hash_write", "hash_accum"]),
     "march": ("hbm", [(32, "marched")], ["march", "march_compact"]),
     "composite_loss": ("hbm", [(76, "composited")], ["composite_loss"]),
@@ -83,12 +80,11 @@ KERNEL_WORK = {  # name: (bound, [(work per unit, unit basis), ...], member kern
 
 
 def active_work(trainer):
-    """KERNEL_WORK for the trainer's configuration: with the fused forward
-    (ngp_field_encode_mlp) the MLP forward runs inside the encode launches, so
-    it has no op of its own (its FLOPs are noted on hash_encode)."""
+    """KERNEL_WORK for the trainer's configuration: the training forward is
+    fused (ngp_field_encode_mlp), so the MLP forward runs inside the encode
+    launches and has no op of its own (its FLOPs are noted on hash_encode)."""
     kw = dict(KERNEL_WORK)
-    if getattr(trainer, "fused_field", False):
-        kw.pop("field_mlp")
+    kw.pop("field_mlp")
     return kw
 
 
@@ -323,9 +319,8 @@ def main():
     marched_bd, composited_bd, active_bd, evaluated_bd = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         evaluated_bd = marched_bd
-    fused_p, dense_p = trainer.fused_params(), trainer.dense_accum_params()
-    pw = {"params": trainer.params.numel(), "fused_params": fused_p, "dense_accum_params": dense_p,
-          "adam_params": trainer.params.numel() - fused_p - dense_p}
+    fused_p = trainer.fused_params()
+    pw = {"params": trainer.params.numel(), "fused_params": fused_p, "adam_params": trainer.params.numel() - fused_p}
     units_bd = {"marched": marched_bd / n_bd, "evaluated": evaluated_bd / n_bd, "composited": composited_bd / n_bd,
                 "active": active_bd / n_bd, **pw}
 

@@ -417,20 +417,6 @@ int ngp_hash_binned_accum_adam(const ngp_hashgrid_t* grid, float* grad_table, vo
                                int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
                                void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
                                const int64_t* step_dev, float grad_scale, void* stream);
-/* ngp_hash_binned_accum_adam plus, in the same launch after the buckets,
- * FusedAdam of the dense range [0, dense_n) of the FULL parameter vector
- * (MLP + the atomic coarse levels; params / exp_avg / exp_avg_sq / params_f16
- * / grad here point at element 0 of the vector, the table at table_offset)
- * from grad + the n_rep replicas of ngp_hash_backward_levels_rep(fold = 0)
- * covering table floats [0, rep_n) (folded in replica order, then zeroed,
- * grad zeroed): bit-identical to folding the replicas and running
- * ngp_adam_step_dev over [0, dense_n).  dense_n, table_offset, rep_n:
- * multiples of 4.  The coarse levels' gradient must be complete on entry. */
-int ngp_hash_binned_accum_adam_dense(const ngp_hashgrid_t* grid, float* grad, void* workspace, int64_t max_samples,
-                                     int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
-                                     void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
-                                     const int64_t* step_dev, float grad_scale, int64_t table_offset, int64_t dense_n,
-                                     float* rep, int64_t rep_n, int n_rep, void* stream);
 /* ngp_hash_backward restricted to levels [level_lo, level_hi). */
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
@@ -443,7 +429,7 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
  * ngp_hash_backward_rep_floats(grid, rep_levels, n_rep) floats, 16-byte
  * aligned, zero on the first call (each call leaves it zero).  Same sums as
  * ngp_hash_backward_levels up to fp32 summation order.  fold = 0 leaves the
- * sums in the replicas for ngp_hash_binned_accum_adam_dense to fold. */
+ * sums in the replicas for ngp_adam_step_dev_rep to fold. */
 int ngp_hash_backward_levels_rep(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                                  const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
                                  int level_hi, float* rep, int rep_levels, int n_rep, int fold, void* stream);
@@ -556,9 +542,10 @@ int ngp_counters_inc(int64_t* counters, int n, void* stream);
  * Python), threshold_out[1] = the mean; feed threshold_out to ngp_packbits'
  * threshold_dev.  sum_cnt_ws: 16 bytes of scratch (two fp64 accumulators, 8-byte
  * aligned; the mean is taken in fp64). */
-/* Number of times an occupancy-list kernel found its cell count past the
- * list's capacity and dropped the batch instead of writing out of bounds
- * (diagnostic: nonzero means a corrupted count; synchronises the device). */
+/* Number of times the occupancy-list kernel found a block's list position
+ * past the list's capacity and dropped the block instead of writing out of
+ * bounds (nonzero only after memory corruption: tests assert 0;
+ * synchronises the device). */
 unsigned long long ngp_guard_hits(void);
 int ngp_density_scatter_last(const int64_t* indices, const float* sigmas, int64_t n, int64_t pos_base,
                              uint64_t* grid_key, void* stream);
@@ -567,8 +554,10 @@ int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, flo
                          void* stream);
 /* sample_uniform_and_occupied_cells (models/networks.py:181-207) on device,
  * no host sync: ngp_occupied_cells lists the cells of one cascade (n_cells
- * f32, Morton order) with density > threshold into list (capacity n_cells,
- * order unspecified), *count = their number (8-byte aligned).
+ * f32, Morton order) with density > threshold into list (capacity n_cells)
+ * in ascending cell order -- torch.nonzero's list, deterministic --
+ * *count = their number (8-byte aligned); workspace:
+ * ngp_occupied_cells_workspace(n_cells) bytes (4-byte aligned).
  * ngp_occupancy_samples writes samples [lo, hi) of the 2*M list: sample i <
  * M a uniform cell, i >= M a cell drawn uniformly from the occupied list
  * (flat_idx = -1, skipped by ngp_density_scatter_last, when it is empty);
@@ -577,8 +566,9 @@ int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, flo
  * Morton index.  Randoms from Philox keyed by (seed, *counter_dev, cascade,
  * i): every rank of a data-parallel job draws the same list and can
  * evaluate a disjoint [lo, hi). */
+size_t ngp_occupied_cells_workspace(int64_t n_cells);
 int ngp_occupied_cells(const float* grid_cascade, int64_t n_cells, float threshold, int32_t* list,
-                       int64_t* count, void* stream);
+                       int64_t* count, void* workspace, void* stream);
 int ngp_occupancy_samples(uint64_t seed, const int64_t* counter_dev, int cascade, int grid_size, int64_t M,
                           float s_minus_hgs, float hgs, const int32_t* occ_list, const int64_t* occ_count,
                           int64_t lo, int64_t hi, float* xyzs, int64_t* flat_idx, void* stream);

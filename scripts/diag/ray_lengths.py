@@ -16,9 +16,9 @@ dev = torch.device("cuda")
 scene = S.AnalyticScene(W=800, H=800, n_images=100, scale=0.5)
 gt = scene.gt_images(device=dev)
 dirs, poses = scene.directions.to(dev), scene.poses.to(dev)
-tr = NGPTrainer(scale=0.5, batch_size=8192, device=dev)
+tr = NGPTrainer(scale=0.5, batch_size=8192, device=dev, use_graphs=False)
 tr.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
-os.environ["NGP_GRAPHS"] = "0"
+# (eager steps: the trainer is built with use_graphs=False below)
 for _ in range(2000):
     tr.train_step(gt, dirs, poses)
 tr.drain()

@@ -93,7 +93,7 @@ def test_new_entry_points_reject_bad_arguments_without_launching():
 
 def test_gradient_replica_entry_points_check_arguments_without_launching():
     """ngp_hash_backward_levels_rep / ngp_hash_backward_rep_floats /
-    ngp_adam_step_dev_rep / ngp_hash_binned_accum_adam_dense: sizes and
+    ngp_adam_step_dev_rep: sizes and
     argument checks on the host, before any launch (NGP_EINVAL = -1)."""
     import ctypes as C
     L = HG._lib()
@@ -116,7 +116,4 @@ def test_gradient_replica_entry_points_check_arguments_without_launching():
                                    None) == -1
     assert L.ngp_adam_step_dev_rep(p, p, p, p, p, 64, p, f(0.9), f(0.999), f(1e-15), p, f(1.0), 1, C.c_void_p(20),
                                    0, 8, 8, None) == -1
-    # dense range that does not end where the binned levels start
-    dense = HG.MLP_PARAMS + 2 * g.offsets[8]
-    assert L.ngp_hash_binned_accum_adam_dense(d, p, p, 1024, 8, 0, p, p, p, p, p, f(0.9), f(0.999), f(1e-15), p,
-                                              f(1.0), HG.MLP_PARAMS, dense + 4, None, 0, 1, None) == -1
+

@@ -159,3 +159,106 @@ def test_two_ranks_match_one_process_on_the_concatenated_batch():
         flips = int(np.unpackbits(torch.bitwise_xor(a, b).numpy()).sum())
         print(f"bitfield: {flips} of {a.numel() * 8} cells differ from the one-process run")
         assert flips <= 1e-2 * a.numel() * 8
+
+
+def _seg_worker(rank, world, port, q):
+    """world-2 rank: step 0 eager, step 1 a segmented graph replay (the ZeRO-1
+    reduce-scatter between compute segments); lr 0 keeps the parameters at
+    their initial values, so both runs see the same field.  The reduced
+    gradient shards of step 1 are copied out inside the captured Adam
+    segment."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "ar-nerf_amd")]
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr, sc = _seg_trainer(R)
+        got = []
+        orig = tr._adam_shards
+
+        def spy():  # (recorded into the captured Adam segment: replays refresh the copies)
+            got[:] = [g.clone() for g in tr._gshard]
+            orig()
+        tr._adam_shards = spy
+        gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
+        for _ in range(2):
+            tr.train_step(gt, dirs, poses)
+        tr.drain()
+        torch.cuda.synchronize()
+        assert len(tr._graphs) >= 1 and tr.n_prefetched >= 1  # step 1 was a graph replay
+        q.put((rank, {"shards": [g.cpu().numpy() for g in got], "buckets": tr.buckets, "bin_lo": tr.bin_level_lo}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _seg_trainer(batch):
+    import synthetic as S
+    from trainer import NGPTrainer
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    tr = NGPTrainer(scale=0.5, batch_size=batch, device=torch.device("cuda", 0), seed=3, lr=0.0, warmup_steps=0,
+                    hash_backward="binned", fused_adam=False)
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(11)
+        tr.params[10240:] = ((torch.rand(tr.n_params - 10240, generator=g) * 2 - 1) * 0.5).to(tr.dev)
+        tr.params16.copy_(tr.params.half())
+    tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
+    return tr, sc
+
+
+def test_segmented_replay_reduces_the_whole_gradient_when_every_level_is_binned():
+    """with every hash level binned (bin_level_lo 0: cascaded
+    scenes, hash_backward='binned') the ZeRO-1 bucket split must follow the
+    resolved level split -- bucket 0 = the MLP alone -- or bucket 0's
+    reduce-scatter, started once the (empty) coarse segment is done, reads
+    levels 0-7 before the binned segment has written them.  The world-2
+    segmented replay's reduced gradient of step 1 equals the one-process
+    gradient of the concatenated batch (every parameter group, relative L2)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    import hashgrid as HG
+    r0, r1 = res[0], res[1]
+    assert r0["bin_lo"] == 0 and r0["buckets"][0][1] <= HG.MLP_PARAMS
+    # one process, 2R rays (rank r drew rays [r R, (r+1) R) of the same global batch); its
+    # gradient is copied where the Adam launches read it (inside the captured step)
+    tr, sc = _seg_trainer(2 * R)
+    parts = {}
+    orig = tr._adam
+
+    def spy(lo, hi, s, rep=False):
+        parts[lo] = (hi, tr.grad[lo:hi].clone())
+        orig(lo, hi, s, rep)
+    tr._adam = spy
+    gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
+    for _ in range(2):
+        tr.train_step(gt, dirs, poses)
+    tr.drain()
+    torch.cuda.synchronize()
+    g1 = torch.zeros(tr.n_params)
+    for lo, (hi, g) in parts.items():
+        g1[lo:hi] = g.cpu()
+    full = torch.zeros(max(b for _, b in r0["buckets"]))
+    for i, (a, b) in enumerate(r0["buckets"]):
+        h = (b - a) // 2
+        full[a:a + h] = torch.from_numpy(r0["shards"][i])
+        full[a + h:b] = torch.from_numpy(r1["shards"][i])
+    g2 = full[:tr.n_params] / 2
+    offs = [0, 3072, HG.MLP_PARAMS] + [HG.MLP_PARAMS + 2 * int(o) for o in tr.grid.offsets[1:]]
+    worst = 0.0
+    for a, b in zip(offs[:-1], offs[1:]):
+        ref = g1[a:b].double()
+        if float(ref.norm()) == 0:
+            continue
+        worst = max(worst, float((g2[a:b].double() - ref).norm() / ref.norm()))
+    print(f"segmented replay, all levels binned: worst group relative L2 {worst:.2e}")
+    assert worst < 1e-3

@@ -218,7 +218,7 @@ def test_exact_mode_graph_replays_keep_the_occupancy_counters():
 
 
 @pytest.mark.parametrize("spr", [None, 1])
-def test_fused_adam_matches_separate_adam(spr, monkeypatch):
+def test_fused_adam_matches_separate_adam(spr):
     """FusedAdam of the binned hash levels inside their accumulation
     (ngp_hash_binned_apply_adam) vs one FusedAdam launch after the backward,
     from the same state and batch: the binned levels' parameters and moments
@@ -228,9 +228,8 @@ def test_fused_adam_matches_separate_adam(spr, monkeypatch):
     batch (overflow) -- every bucket takes the residual path."""
     import hashgrid as HG
     outs = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("NGP_FUSED_ADAM", fused)
-        sc, tr, img, pix, noise = _setup(table_init=2.0, bin_samples_per_ray=spr)
+    for fused in (True, False):
+        sc, tr, img, pix, noise = _setup(table_init=2.0, bin_samples_per_ray=spr, fused_adam=fused)
         o, d = sc.rays(img, pix)
         tr.step(img.to(DEV), pix.to(DEV), sc.gt_rgb_rays(o, d).to(DEV), sc.directions.to(DEV), sc.poses.to(DEV),
                 noise=noise.to(DEV), apply_adam=True)
@@ -251,16 +250,15 @@ def test_fused_adam_matches_separate_adam(spr, monkeypatch):
         assert float((ca - cb).abs().max()) <= 1e-5 * max(1.0, float(cb.abs().max()))
 
 
-def test_fused_adam_matches_separate_adam_cascaded(monkeypatch):
+def test_fused_adam_matches_separate_adam_cascaded():
     """The garden-shaped configuration (scale 16: 6 cascades, every hash level
     binned, the MLP's Adam alone outside the accumulation): fused vs separate
     FusedAdam from the same state and batch."""
     import hashgrid as HG
     outs = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("NGP_FUSED_ADAM", fused)
+    for fused in (True, False):
         sc = S.AnalyticScene(W=200, H=200, n_images=10)
-        tr = NGPTrainer(scale=16.0, batch_size=2048, device=DEV, seed=3)
+        tr = NGPTrainer(scale=16.0, batch_size=2048, device=DEV, seed=3, fused_adam=fused)
         with torch.no_grad():
             g = torch.Generator().manual_seed(11)
             tr.params[10240:] = ((torch.rand(tr.params.numel() - 10240, generator=g) * 2 - 1) * 2.0).to(DEV)
@@ -280,36 +278,3 @@ def test_fused_adam_matches_separate_adam_cascaded(monkeypatch):
         assert float((fa == fb).float().mean()) > 0.999
         assert float((fa - fb).abs().max()) <= 2e-6 * max(1.0, float(fb.abs().max()))
         assert float((a[:HG.MLP_PARAMS] - b[:HG.MLP_PARAMS]).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
-
-
-def test_dense_adam_in_accumulation_matches_separate_launches(monkeypatch):
-    """NGP_DENSE_IN_ACCUM=1 (ngp_hash_binned_accum_adam_dense: the MLP + coarse
-    levels' FusedAdam and the coarse replica fold in the accumulation's tail)
-    vs the default separate launches, from the same state and batch: the
-    dense range agrees to atomic-order noise, the binned range as in
-    test_fused_adam_matches_separate_adam; gradient and replicas left zero."""
-    import hashgrid as HG
-    outs = []
-    for dense in ("1", "0"):
-        monkeypatch.setenv("NGP_DENSE_IN_ACCUM", dense)
-        sc, tr, img, pix, noise = _setup(table_init=2.0)
-        assert tr.dense_in_accum == (dense == "1")
-        o, d = sc.rays(img, pix)
-        tr.step(img.to(DEV), pix.to(DEV), sc.gt_rgb_rays(o, d).to(DEV), sc.directions.to(DEV), sc.poses.to(DEV),
-                noise=noise.to(DEV), apply_adam=True)
-        torch.cuda.synchronize()
-        assert float(tr.grad.abs().max()) == 0.0
-        if tr.rep_buf is not None:
-            assert float(tr.rep_buf.abs().max()) == 0.0
-        outs.append([t.clone() for t in (tr.params, tr.exp_avg, tr.exp_avg_sq, tr.params16)])
-        split = HG.MLP_PARAMS + 2 * tr.grid.offsets[tr.bin_level_lo]
-    for j, (a, b) in enumerate(zip(outs[0], outs[1])):
-        fa, fb = a[split:].float(), b[split:].float()
-        assert float((fa == fb).float().mean()) > 0.999
-        if j == 3:
-            assert bool(((fa - fb).abs() <= O.ulp16(fb)).all())
-        else:
-            assert float((fa - fb).abs().max()) <= 2e-6 * max(1.0, float(fb.abs().max()))
-        ca, cb = a[:split].float(), b[:split].float()
-        assert float((ca - cb).abs().max()) <= 1e-5 * max(1.0, float(cb.abs().max()))
-        assert float((ca != cb).float().mean()) < 0.5  # mostly bit-identical (same fold order, same Adam)
