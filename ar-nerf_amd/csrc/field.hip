@@ -180,9 +180,21 @@ __device__ __forceinline__ void sh4_select(float dx, float dy, float dz, int g, 
 }
 
 __device__ __forceinline__ h8 pack(h4 a, h4 b) { return h8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
+// ReLU of an fp32 accumulator tile, rounded to fp16: round first (v_cvt_pk),
+// then clear every half whose sign is set (round(c) <= 0 exactly when c <= 0,
+// so the result equals round(max(c, 0)) bit for bit, +0 included) -- two
+// packed integer ops per pair instead of a canonicalize + max per element.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t relu_bits(uint32_t x) {
+    const uint32_t neg = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, x) >> (s16x2){15, 15});
+    return x & ~neg;
+}
 __device__ __forceinline__ h4 relu_h(f4 c) {
-    return h4{(_Float16)fmaxf(c[0], 0.f), (_Float16)fmaxf(c[1], 0.f), (_Float16)fmaxf(c[2], 0.f),
-              (_Float16)fmaxf(c[3], 0.f)};
+    const uint2 u = __builtin_bit_cast(uint2, h4{(_Float16)c[0], (_Float16)c[1], (_Float16)c[2], (_Float16)c[3]});
+    uint32_t x = u.x, y = u.y;
+    asm volatile("" : "+v"(x), "+v"(y));  // (opaque: one v_cvt_pk per pair, not re-derived per use)
+    return __builtin_bit_cast(h4, make_uint2(relu_bits(x), relu_bits(y)));
 }
 __device__ __forceinline__ h4 to_h(f4 c) { return h4{(_Float16)c[0], (_Float16)c[1], (_Float16)c[2], (_Float16)c[3]}; }
 __device__ __forceinline__ h8 lds8(const _Float16* p) { return *reinterpret_cast<const h8*>(p); }
@@ -547,15 +559,9 @@ __global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const 
 }
 
 // ------------------------------------------------------------------ backward
-// Kernel A: MLP backward.  Recomputes the forward from the saved encoding
-// (MFMA, cheap), back-propagates with v_mfma_f32_16x16x16_f16 (whose B
-// operand layout B[k = 4g + j][n = s] IS the accumulator layout, so every
-// gradient tile chains in registers), writes dL/denc (n,32) f32, and sums
-// the weight gradients dW = sum_s G[o][s] H[i][s] in 40 register tiles over
-// the persistent wave loop (operands transposed through a per-wave LDS
-// scratch).  Gradient operands are scaled per stage by a power of two chosen
-// from the wave's max |g| before the fp16 cast and unscaled exactly in fp32
-// (tcnn's role of a loss scale, without a global scale to tune).
+// MLP backward helpers: v_mfma_f32_16x16x16_f16, whose B operand layout
+// B[k = 4g + j][n = s] IS the accumulator layout, so every gradient tile of
+// the data chain re-enters the next MFMA from registers.
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f4 mfma16(h4 a, h4 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
 __device__ __forceinline__ h4 lds4(const _Float16* p) { return *reinterpret_cast<const h4*>(p); }
@@ -580,44 +586,58 @@ __device__ __forceinline__ void load_bwd_weights(const _Float16* __restrict__ ml
     for (int e = t; e < 32 * 64; e += nt) { const int i = e >> 6, o = e & 63; sw[BT1 + i * RT64 + o] = mlp[OW1 + o * 32 + i]; }
 }
 
-// max over the wave: DPP row rotates inside each 16-lane row, then the four
-// row maxima through scalar readlanes (no LDS round trips)
-#define NGP_DPP_ROR(v, n) \
-    __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + (n), 0xf, 0xf, false))
-__device__ __forceinline__ float wave_max(float v) {
-    v = fmaxf(v, NGP_DPP_ROR(v, 1));
-    v = fmaxf(v, NGP_DPP_ROR(v, 2));
-    v = fmaxf(v, NGP_DPP_ROR(v, 4));
-    v = fmaxf(v, NGP_DPP_ROR(v, 8));
-    const int iv = __builtin_bit_cast(int, v);
-    const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 0));
-    const float b = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 16));
-    const float c = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 32));
-    const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(iv, 48));
-    return fmaxf(fmaxf(a, b), fmaxf(c, d));
-}
 __device__ __forceinline__ float max4(f4 v) { return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))); }
-// power of two s.t. maxabs * s < 2^14 (fp16-safe, full mantissa for the max)
-__device__ __forceinline__ float pow2_scale(float maxabs) {
+// Per-sample power-of-two scales of the data chain: a gradient tile travels in
+// fp16 as value x 2^E, E per sample (the same in its four lanes), chosen from
+// the sample's largest |value| so that it lands in [2^13, 2^14): a full 11-bit
+// mantissa for everything within 2^27 of it.  A layer's MFMA output is in
+// units of the previous E; the next E follows from its max, and one
+// power-of-two factor 2^(E_new - E_prev) re-scales it (exact).
+constexpr int E_MIN = -100, E_MAX = 100;
+__device__ __forceinline__ int fexp(float m) {  // m = f 2^e, f in [0.5, 1) (0 -> 0)
     int e;
-    frexpf(maxabs, &e);
-    e = min(max(14 - e, -100), 100);
-    return ldexpf(1.0f, e);
+    frexpf(m, &e);
+    return e;
 }
-// the same scale and its exact reciprocal (both powers of two: no division)
-__device__ __forceinline__ void pow2_scales(float maxabs, float& sc, float& is) {
-    int e;
-    frexpf(maxabs, &e);
-    e = min(max(14 - e, -100), 100);
-    sc = ldexpf(1.0f, e);
-    is = ldexpf(1.0f, -e);
+__device__ __forceinline__ int next_exp(float m_scaled, int e_prev) {
+    return min(max(e_prev + 14 - fexp(m_scaled), E_MIN), E_MAX);
 }
-__device__ __forceinline__ h4 scaled_h(f4 v, float sc) {
-    return h4{(_Float16)(v[0] * sc), (_Float16)(v[1] * sc), (_Float16)(v[2] * sc), (_Float16)(v[3] * sc)};
+__device__ __forceinline__ h4 cvt4(f4 v, float r) {
+    return h4{(_Float16)(v[0] * r), (_Float16)(v[1] * r), (_Float16)(v[2] * r), (_Float16)(v[3] * r)};
 }
-__device__ __forceinline__ f4 mask_relu(f4 g, h4 act) {
-    return f4{act[0] > (_Float16)0 ? g[0] : 0.f, act[1] > (_Float16)0 ? g[1] : 0.f, act[2] > (_Float16)0 ? g[2] : 0.f,
-              act[3] > (_Float16)0 ? g[3] : 0.f};
+// ReLU' of an fp16 gradient tile by its layer's activation tile (relu_h's
+// output: sign clear): keep a half where act > 0, i.e. its bits are nonzero --
+// (act + 0x7fff) has bit 15 set exactly then, an arithmetic shift spreads it.
+__device__ __forceinline__ uint32_t mask_h2(uint32_t gv, uint32_t av) {
+    const s16x2 t = __builtin_bit_cast(s16x2, __builtin_bit_cast(u16x2, av) + (u16x2){0x7fff, 0x7fff});
+    return gv & __builtin_bit_cast(uint32_t, t >> (s16x2){15, 15});
+}
+__device__ __forceinline__ h4 relu_mask(h4 gr, h4 act) {
+    const uint2 gv = __builtin_bit_cast(uint2, gr), av = __builtin_bit_cast(uint2, act);
+    return __builtin_bit_cast(h4, make_uint2(mask_h2(gv.x, av.x), mask_h2(gv.y, av.y)));
+}
+// 2^k (k <= 0) as a pair of fp16 (subnormal down to 2^-24, 0 below)
+__device__ __forceinline__ uint32_t f16_pow2_x2(int k) {
+    const uint32_t b = k >= -14 ? (uint32_t)(k + 15) << 10 : k >= -24 ? 1u << (k + 24) : 0u;
+    return b | (b << 16);
+}
+// an fp16 tile times a per-lane fp16 factor pair (v_pk_mul_f16; exact for powers of two)
+typedef _Float16 hx2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h4 mul_h4(h4 v, uint32_t f2) {
+    const uint2 u = __builtin_bit_cast(uint2, v);
+    const hx2 f = __builtin_bit_cast(hx2, f2);
+    return __builtin_bit_cast(h4, make_uint2(__builtin_bit_cast(uint32_t, __builtin_bit_cast(hx2, u.x) * f),
+                                             __builtin_bit_cast(uint32_t, __builtin_bit_cast(hx2, u.y) * f)));
+}
+// min over the wave's 16 samples of a per-sample int (lanes 0-15 hold samples 0-15)
+__device__ __forceinline__ int samples_min(int v) {
+#define NGP_DPP_ROR_I(x, n) __builtin_amdgcn_update_dpp(0, (x), 0x120 + (n), 0xf, 0xf, false)
+    v = min(v, NGP_DPP_ROR_I(v, 1));
+    v = min(v, NGP_DPP_ROR_I(v, 2));
+    v = min(v, NGP_DPP_ROR_I(v, 4));
+    v = min(v, NGP_DPP_ROR_I(v, 8));
+#undef NGP_DPP_ROR_I
+    return __builtin_amdgcn_readfirstlane(v);
 }
 // Accumulator tile X[4g + r][s] (lane (s, g)) -> image row s, units 4g..4g+3.
 // The four 8-byte chunks of row s sit XOR-swizzled, chunk c at c ^ ((s >> 2) & 3):
@@ -642,31 +662,6 @@ __device__ __forceinline__ h4 get_tile(const _Float16* T, int s, int g) {
     return __builtin_bit_cast(h4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
                                       (__attribute__((address_space(3))) hp4*)(const_cast<_Float16*>(a))));
 }
-// bf16 operands of the weight-gradient MFMAs (v_mfma_f32_16x16x16_bf16: the
-// same fragment layout as the f16 form).  bf16 keeps fp32's exponent, so the
-// true gradients go in unscaled and every iteration accumulates straight into
-// the MFMA C operand (no per-iteration unscale-and-add in VALU).
-typedef short s4v __attribute__((ext_vector_type(4)));
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef __bf16 b2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, b2v));
-}
-__device__ __forceinline__ h4 bf16x4(f4 v) {  // (bf16 bits carried in an h4 for the LDS tile helpers)
-    const uint2 u = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
-    return __builtin_bit_cast(h4, u);
-}
-__device__ __forceinline__ h4 bf16x4(h4 v) { return bf16x4(f4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]}); }
-__device__ __forceinline__ f4 mfma16bf(h4 a, h4 b, f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4v, a), __builtin_bit_cast(s4v, b), c, 0, 0,
-                                                     0);
-}
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-}
-
 // accumulator tile k -> (matrix offset, in_dim, o0, i0)
 __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& o0, int& i0) {
     if (k < 4) { ow = OW5; in_dim = 64; o0 = 0; i0 = 16 * k; return; }
@@ -691,9 +686,12 @@ __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& 
 // block iteration), 5 of the 40 tiles per wave.  Operands go through LDS in
 // two phases (layers 5-3: 19 tiles, then layers 2-1: 11 tiles) so eight
 // regions fit beside the weight images.  Gradient operands of the data
-// chain are scaled per SAMPLE (column of the B operand; the four lanes of a
-// sample exchange their maxima with v_permlane16/32_swap) by a power of two
-// before the fp16 cast and unscaled exactly in fp32.
+// chain are fp16 scaled per SAMPLE (column of the B operand; the four lanes
+// of a sample exchange their maxima with v_permlane16/32_swap) by a power of
+// two, unscaled exactly in fp32 for dL/denc; the weight gradients take the
+// same fp16 values re-scaled to one power of two per layer and block
+// (tcnn's fp16 operands with the role of its loss scale, no global scale to
+// tune).
 constexpr int CW = 8, NT1 = 19, NT2 = 11, CSCRW = NT1 * TTILE;
 constexpr int COOP_LDS_HALFS = SCR + CW * CSCRW;
 static_assert(NGP_MLP_PARAMS <= CW * CSCRW && NT2 <= NT1, "raw weight staging / phase-2 tiles exceed the scratch");
@@ -727,23 +725,29 @@ __device__ __forceinline__ int coop_n1(int w) { return w < 4 ? 4 : 3; }
 __device__ __forceinline__ int coop_k2(int w, int t) { return w < 4 ? 28 + w : 32 + 2 * (w - 4) + t; }
 __device__ __forceinline__ int coop_n2(int w) { return w < 4 ? 1 : 2; }
 
-// v_mfma_f32_16x16x32_bf16 over two source regions at a time: the K order
+// layer of output tile k: 0 = W5 (G = dL/dout), 1 = W4 (dL/da4), 2 = W3 (dL/da3),
+// 3 = W2 (dL/dh), 4 = W1 (dL/da1)
+__device__ __forceinline__ int tile_layer(int k) { return k < 4 ? 0 : k < 20 ? 1 : k < 28 ? 2 : k < 32 ? 3 : 4; }
+
+// v_mfma_f32_16x16x32_f16 over two source regions at a time: the K order
 // (lane group g, element j) <- sample 4g + (j & 3) of region src + (j >> 2) is
 // the same for the A and the B operand, so the sum over K is the sum over the
-// 32 samples
-typedef short s8v __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ f4 mfma32bf(h4 a0, h4 a1, h4 b0, h4 b1, f4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(__bf16 __attribute__((ext_vector_type(8))), pack(a0, a1)),
-                                                  __builtin_bit_cast(__bf16 __attribute__((ext_vector_type(8))), pack(b0, b1)),
-                                                  c, 0, 0, 0);
-}
-
+// 32 samples.  The G tiles of one layer carry the block's common scale 2^B, so
+// each tile's block sum is added to its accumulator times 2^-B (Bl[layer]).
 template <int NTL>
-__device__ __forceinline__ void coop_dw(const _Float16* scr, int w, int s, int g, int n, int (*kf)(int, int), f4* acc) {
+__device__ __forceinline__ void coop_dw(const _Float16* scr, int w, int s, int g, int n, int (*kf)(int, int), f4* acc,
+                                        const int* Bl) {
     int gid[NTL], hid[NTL];
+    float sc[NTL];
+    f4 part[NTL];
 #pragma unroll
-    for (int t = 0; t < NTL; ++t) coop_tile_ops(kf(w, t < n ? t : 0), gid[t], hid[t]);
-#pragma unroll 2
+    for (int t = 0; t < NTL; ++t) {
+        const int k = kf(w, t < n ? t : 0);
+        coop_tile_ops(k, gid[t], hid[t]);
+        const int l = tile_layer(k);  // (wave-uniform: the select stays scalar)
+        sc[t] = ldexpf(1.0f, -(l == 0 ? Bl[0] : l == 1 ? Bl[1] : l == 2 ? Bl[2] : l == 3 ? Bl[3] : Bl[4]));
+    }
+#pragma unroll
     for (int src = 0; src < CW; src += 2) {
         const _Float16* R0 = scr + src * CSCRW;
         const _Float16* R1 = R0 + CSCRW;
@@ -755,9 +759,13 @@ __device__ __forceinline__ void coop_dw(const _Float16* scr, int w, int s, int g
                 G0 = get_tile(R0 + gid[t] * TTILE, s, g);
                 G1 = get_tile(R1 + gid[t] * TTILE, s, g);
             }
-            acc[t] = mfma32bf(G0, G1, get_tile(R0 + hid[t] * TTILE, s, g), get_tile(R1 + hid[t] * TTILE, s, g), acc[t]);
+            const h8 H = pack(get_tile(R0 + hid[t] * TTILE, s, g), get_tile(R1 + hid[t] * TTILE, s, g));
+            part[t] = mfma32(pack(G0, G1), H, src == 0 ? f4{0.f, 0.f, 0.f, 0.f} : part[t]);
         }
     }
+#pragma unroll
+    for (int t = 0; t < NTL; ++t)
+        if (t < n) acc[t] = part[t] * sc[t] + acc[t];
 }
 
 __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
@@ -765,6 +773,8 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
     const _Float16* __restrict__ enc, const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig,
     const float* __restrict__ dL_drgb, float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride) {
     extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
+    // per-wave minima of the layers' per-sample exponents (double-buffered by iteration parity)
+    __shared__ int emin[2][5][CW];
     _Float16* sw = smem;
     _Float16* scr = smem + SCR;
     stage_raw_weights(mlp, scr);  // (the scratch is free until the loop)
@@ -782,30 +792,39 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         h8 e;
         float dx, dy, dz, dsig, gr[3];
     };
-    auto load_in = [&](int64_t b, In& x) {
-        const int64_t jj = b + s;
+    // the sample of row jj (-1 past the end): listed rows' indices are loaded
+    // two iterations ahead, so the dependent loads of the next iteration's
+    // inputs never wait on an index load
+    auto row_index = [&](int64_t jj) -> int32_t {
+        return jj < N ? (sidx ? sidx[jj] : (int32_t)jj) : -1;
+    };
+    auto load_in = [&](int32_t ii, In& x) {
         x.e = h8{0, 0, 0, 0, 0, 0, 0, 0};
         x.dx = 0.f; x.dy = 0.f; x.dz = 1.f; x.dsig = 0.f; x.gr[0] = x.gr[1] = x.gr[2] = 0.f;
-        if (jj < N) {
-            const int64_t ii = sidx ? (int64_t)sidx[jj] : jj;
+        if (ii >= 0) {
             if (enc_pm_stride > 0)  // pair-major (ngp_hash_encode): pairs 2g, 2g+1
                 x.e = pack(*reinterpret_cast<const h4*>(enc + ((2 * g) * enc_pm_stride + ii) * 4),
                            *reinterpret_cast<const h4*>(enc + ((2 * g + 1) * enc_pm_stride + ii) * 4));
             else
-                x.e = *reinterpret_cast<const h8*>(enc + ii * 32 + 8 * g);
-            x.dx = dirs[3 * ii]; x.dy = dirs[3 * ii + 1]; x.dz = dirs[3 * ii + 2];
+                x.e = *reinterpret_cast<const h8*>(enc + (int64_t)ii * 32 + 8 * g);
+            x.dx = dirs[3 * (int64_t)ii]; x.dy = dirs[3 * (int64_t)ii + 1]; x.dz = dirs[3 * (int64_t)ii + 2];
             x.dsig = dL_dsig[ii];
-            x.gr[0] = dL_drgb[3 * ii]; x.gr[1] = dL_drgb[3 * ii + 1]; x.gr[2] = dL_drgb[3 * ii + 2];
+            x.gr[0] = dL_drgb[3 * (int64_t)ii]; x.gr[1] = dL_drgb[3 * (int64_t)ii + 1];
+            x.gr[2] = dL_drgb[3 * (int64_t)ii + 2];
         }
     };
     const int64_t stride = (int64_t)gridDim.x * CW * 16;
+    const int64_t j0 = (int64_t)blockIdx.x * CW * 16 + 16 * wid + s;
     In cur;
-    load_in((int64_t)blockIdx.x * CW * 16 + 16 * wid, cur);
+    load_in(row_index(j0), cur);
+    int32_t i_next = row_index(j0 + stride);
+    int par = 0;
     // block-uniform trip count: every wave reaches every barrier
-    for (int64_t bb = (int64_t)blockIdx.x * CW * 16; bb < N; bb += stride) {
+    for (int64_t bb = (int64_t)blockIdx.x * CW * 16; bb < N; bb += stride, par ^= 1) {
         const int64_t base = bb + 16 * wid;
         In nxt;
-        load_in(base + stride, nxt);
+        load_in(i_next, nxt);
+        i_next = row_index(base + s + 2 * stride);
         const int64_t j = base + s;
         const bool valid = j < N;
         const h8 e = cur.e;
@@ -826,97 +845,125 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
                 dout[r] = cur.gr[r] * (y * (1.0f - y));
             }
         }
-        float sc_o, is_o;
-        pow2_scales(sample_max(max4(dout)), sc_o, is_o);
-        const h4 do_h = scaled_h(dout, sc_o);
-        // ---- dh4 = W5^T do
-        f4 da4[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) da4[t] = mask_relu(mfma16(lds4(sw + BT5 + (16 * t + s) * RT16 + 4 * g), do_h, z) * is_o, h4v[t]);
+        const int Eo = next_exp(sample_max(max4(dout)), 0);
+        const h4 do_h = cvt4(dout, ldexpf(1.0f, Eo));
+        // ---- dL/da4 = ReLU'(W5^T do)   (MFMA output in units of 2^Eo)
+        f4 c4[4];
         float m = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da4[t]));
-        float sc_4, is_4;
-        pow2_scales(sample_max(m), sc_4, is_4);
+        for (int t = 0; t < 4; ++t) {
+            c4[t] = mfma16(lds4(sw + BT5 + (16 * t + s) * RT16 + 4 * g), do_h, z);
+            m = fmaxf(m, max4(c4[t]));
+        }
+        const int E4 = next_exp(sample_max(m), Eo);
         h4 da4h[4];
+        {
+            const float r = ldexpf(1.0f, E4 - Eo);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) da4h[t] = scaled_h(da4[t], sc_4);
-        // ---- dh3 = W4^T da4
-        f4 da3[4];
+            for (int t = 0; t < 4; ++t) da4h[t] = relu_mask(cvt4(c4[t], r), h4v[t]);
+        }
+        // ---- dL/da3 = ReLU'(W4^T da4)
+        f4 c3[4];
+        m = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             f4 c = z;
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT4 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da4h[kt], c);
-            da3[t] = mask_relu(c * is_4, h3[t]);
+            c3[t] = c;
+            m = fmaxf(m, max4(c));
         }
-        m = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da3[t]));
-        float sc_3, is_3;
-        pow2_scales(sample_max(m), sc_3, is_3);
+        const int E3 = next_exp(sample_max(m), E4);
         h4 da3h[4];
+        {
+            const float r = ldexpf(1.0f, E3 - E4);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) da3h[t] = scaled_h(da3[t], sc_3);
-        // ---- d h (colour-net input, h part) = W3h^T da3, + TruncExp backward
+            for (int t = 0; t < 4; ++t) da3h[t] = relu_mask(cvt4(c3[t], r), h3[t]);
+        }
+        // ---- dL/dh (colour-net input, h part) = W3h^T da3, + TruncExp backward (true units)
         f4 dh = z;
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt) dh = mfma16(lds4(sw + BT3 + s * RT64 + 16 * kt + 4 * g), da3h[kt], dh);
-        dh = dh * is_3;
+        dh = dh * ldexpf(1.0f, -E3);
         if (g == 0) dh[0] += cur.dsig * expf(fminf(fmaxf((float)hh[0], -15.f), 15.f));  // custom_functions.py:169-173
-        float sc_h, is_h;
-        pow2_scales(sample_max(max4(dh)), sc_h, is_h);
-        const h4 dhh = scaled_h(dh, sc_h);
-        // ---- dh1 = W2^T dh
-        f4 da1[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) da1[t] = mask_relu(mfma16(lds4(sw + BT2 + (16 * t + s) * RT16 + 4 * g), dhh, z) * is_h, h1[t]);
+        const int Eh = next_exp(sample_max(max4(dh)), 0);
+        const h4 dhh = cvt4(dh, ldexpf(1.0f, Eh));
+        // ---- dL/da1 = ReLU'(W2^T dh)
+        f4 c1[4];
         m = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) m = fmaxf(m, max4(da1[t]));
-        float sc_1, is_1;
-        pow2_scales(sample_max(m), sc_1, is_1);
+        for (int t = 0; t < 4; ++t) {
+            c1[t] = mfma16(lds4(sw + BT2 + (16 * t + s) * RT16 + 4 * g), dhh, z);
+            m = fmaxf(m, max4(c1[t]));
+        }
+        const int E1 = next_exp(sample_max(m), Eh);
         h4 da1h[4];
+        {
+            const float r = ldexpf(1.0f, E1 - Eh);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) da1h[t] = scaled_h(da1[t], sc_1);
-        // ---- dL/denc = W1^T da1 (rows 16t + 4g + r of sample s)
+            for (int t = 0; t < 4; ++t) da1h[t] = relu_mask(cvt4(c1[t], r), h1[t]);
+        }
+        // ---- dL/denc = W1^T da1 (rows 16t + 4g + r of sample s), true units
+        {
+            const float r = ldexpf(1.0f, -E1);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            f4 c = z;
+            for (int t = 0; t < 2; ++t) {
+                f4 c = z;
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT1 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da1h[kt], c);
-            c = c * is_1;
-            if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
+                for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT1 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da1h[kt], c);
+                c = c * r;
+                if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
+            }
         }
         cur = nxt;
-        // ---- weight gradients, phase 1 (layers 5, 4, 3): bf16 operand tiles
-        __syncthreads();  // every wave's phase-2 reads of the previous iteration are done
-        put_tile(mine + P_DO * TTILE, bf16x4(dout), s, g);
+        // ---- weight gradients: fp16 operands (tcnn's precision), K = samples.  The G
+        // (gradient) tiles of a layer are re-scaled from their per-sample exponent E_s
+        // to the block's common one B = min_s E_s (the block's largest gradient at
+        // [2^13, 2^14); factors <= 1, exact down to fp16 subnormals), the H tiles are
+        // the fp16 activations / encoding as they are.
+        const int Es[5] = {Eo, E4, E3, Eh, E1};
+        int wmin[5];
+#pragma unroll
+        for (int l = 0; l < 5; ++l) wmin[l] = samples_min(Es[l]);  // (uniform: the DPP reads every lane of the row)
+        if (lane == 0) {
+#pragma unroll
+            for (int l = 0; l < 5; ++l) emin[par][l][wid] = wmin[l];
+        }
+        __syncthreads();  // every wave's phase-2 reads of the previous iteration are done; emin[par] complete
+        uint32_t fac[5];
+        int Bl[5];
+#pragma unroll
+        for (int l = 0; l < 5; ++l) {
+            const int4 a = *reinterpret_cast<const int4*>(&emin[par][l][0]);
+            const int4 b = *reinterpret_cast<const int4*>(&emin[par][l][4]);
+            Bl[l] = __builtin_amdgcn_readfirstlane(min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w))));
+            fac[l] = f16_pow2_x2(Bl[l] - Es[l]);
+        }
+        // phase 1 (layers 5, 4, 3)
+        put_tile(mine + P_DO * TTILE, mul_h4(do_h, fac[0]), s, g);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            put_tile(mine + (P_DA4 + t) * TTILE, bf16x4(da4[t]), s, g);
-            put_tile(mine + (P_DA3 + t) * TTILE, bf16x4(da3[t]), s, g);
-            put_tile(mine + (P_H4 + t) * TTILE, bf16x4(h4v[t]), s, g);
-            put_tile(mine + (P_H3 + t) * TTILE, bf16x4(h3[t]), s, g);
+            put_tile(mine + (P_DA4 + t) * TTILE, mul_h4(da4h[t], fac[1]), s, g);
+            put_tile(mine + (P_DA3 + t) * TTILE, mul_h4(da3h[t], fac[2]), s, g);
+            put_tile(mine + (P_H4 + t) * TTILE, h4v[t], s, g);
+            put_tile(mine + (P_H3 + t) * TTILE, h3[t], s, g);
         }
-        put_tile(mine + P_C * TTILE, bf16x4(shh), s, g);
-        put_tile(mine + (P_C + 1) * TTILE, bf16x4(hh), s, g);
+        put_tile(mine + P_C * TTILE, shh, s, g);
+        put_tile(mine + (P_C + 1) * TTILE, hh, s, g);
         __syncthreads();
-        coop_dw<4>(scr, wid, s, g, coop_n1(wid), coop_k1, acc1);
+        coop_dw<4>(scr, wid, s, g, coop_n1(wid), coop_k1, acc1, Bl);
         __syncthreads();  // phase-1 reads done: the regions take the phase-2 tiles
         // ---- phase 2 (layers 2, 1)
-        put_tile(mine + Q_DH * TTILE, bf16x4(dh), s, g);
+        put_tile(mine + Q_DH * TTILE, mul_h4(dhh, fac[3]), s, g);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            put_tile(mine + (Q_DA1 + t) * TTILE, bf16x4(da1[t]), s, g);
-            put_tile(mine + (Q_H1 + t) * TTILE, bf16x4(h1[t]), s, g);
+            put_tile(mine + (Q_DA1 + t) * TTILE, mul_h4(da1h[t], fac[4]), s, g);
+            put_tile(mine + (Q_H1 + t) * TTILE, h1[t], s, g);
         }
-        {   // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
-            const h4 e0 = bf16x4(h4{e[0], e[1], e[2], e[3]}), e1 = bf16x4(h4{e[4], e[5], e[6], e[7]});
-            put_tile_pair(mine + (Q_E + (g >> 1)) * TTILE, e0, e1, s, g & 1);
-        }
+        // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
+        put_tile_pair(mine + (Q_E + (g >> 1)) * TTILE, h4{e[0], e[1], e[2], e[3]}, h4{e[4], e[5], e[6], e[7]}, s, g & 1);
         __syncthreads();
-        coop_dw<2>(scr, wid, s, g, coop_n2(wid), coop_k2, acc2);
+        coop_dw<2>(scr, wid, s, g, coop_n2(wid), coop_k2, acc2, Bl);
     }
     // each output tile lives in exactly one wave of the block: one global add
     // per weight.  Wave w of every block owns the same tiles, so the adds of a
