@@ -1,7 +1,9 @@
 """datasets/__init__.py of the reference.  Implemented: 'nerf' (NeRF-synthetic
-/ Blender) 'nsvf' (Synthetic_NeRF & co.) and 'colmap' (mip-NeRF 360).  The other loaders of the reference (nsvf, colmap, colmap_exr,
-colmap_real_exr, myblender, nerfpp, rtmv) are SURVEY.md §8f rank-2 work not
-done yet; asking for one raises."""
+/ Blender), 'nsvf' (Synthetic_NeRF & co.) and 'colmap' (mip-NeRF 360); the
+first two are pinned to fixtures from the reference's own loaders
+(tests/test_loaders_golden_cpu.py).  The other loaders of the reference
+(colmap_exr, colmap_real_exr, myblender, nerfpp, rtmv: EXR / HDR variants)
+are out of scope; asking for one raises."""
 from .nerf import NeRFDataset
 from .nsvf import NSVFDataset
 from .colmap import ColmapDataset

@@ -110,6 +110,8 @@ def parse():
     ap.add_argument("--hash-backward", default="hybrid", choices=["hybrid", "binned", "atomic"])
     ap.add_argument("--bin-level-lo", type=int, default=None,
                     help="hybrid hash backward: first binned level (default: trainer's, 8 / 0 for cascaded scenes)")
+    ap.add_argument("--pair-steps", action="store_true",
+                    help="two consecutive steady-state steps per graph replay (trainer pair_steps)")
     ap.add_argument("--bin-merge-hi", type=int, default=0,
                     help="binned levels below this merge runs of equal corner pairs along a ray")
     ap.add_argument("--bin-samples-per-ray", type=int, default=None,
@@ -285,7 +287,7 @@ def main():
     erode = args.erode == "on" or (args.erode == "auto" and args.scale > 0.5)
     trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward,
                          bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray, erode=erode,
-                         bin_merge_hi=args.bin_merge_hi)
+                         bin_merge_hi=args.bin_merge_hi, pair_steps=args.pair_steps)
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
     WORK = active_work(trainer)
     R = args.batch

@@ -1,0 +1,162 @@
+"""Generate tests/golden/loaders.npz: the REFERENCE's own dataset loaders
+(datasets/nsvf.py NSVFDataset, datasets/nerf.py NeRFDataset, with their
+ray_utils.get_ray_directions and color_utils.read_image; read from
+/root/reference, never copied) run on small synthetic scenes written by
+write_scenes() below -- the fixture tests/test_loaders_golden_cpu.py holds
+this repo's loaders (ar-nerf_amd/datasets) to.
+
+The scenes: the analytic sphere+box (synthetic.AnalyticScene) at 100x100,
+(a) in NSVF layout under a 'Synthetic_NeRF' directory (rgb/{0,2}_*.png,
+pose/*.txt, intrinsics.txt, bbox.txt) with RGBA frames whose alpha varies,
+so read_image's alpha blend onto white runs, and a bbox whose centre is off
+the origin (the pose shift / scale path); (b) in Blender layout
+(transforms_{train,test}.json with camera_angle_x and [right up back]
+transform matrices, RGBA PNGs).  Downsample 100/800 so the loaders' frame
+size equals the PNGs': no cv2.resize (cv2 is not in this container).
+
+Modules the reference imports but this container lacks are stubbed with
+their documented behaviour for this use: imageio.imread (PNG via Pillow,
+uint8 HxWxC), cv2.resize (identity at equal size; anything else raises),
+kornia.create_meshgrid(H, W, normalized=False) ((1, H, W, 2) pixel
+coordinates (x, y)), matplotlib, tqdm pass-through.
+
+Run:  python tests/golden/make_loaders.py   (needs /root/reference; seconds)
+"""
+import hashlib
+import json
+import os
+import sys
+import tempfile
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("AR_NERF_REFERENCE", "/root/reference")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+RES, N_TRAIN, N_TEST = 100, 3, 2
+CAMERA_ANGLE_X = 0.6911112070083618  # the Blender scenes' value
+
+
+def _rgba(sc, i):
+    """uint8 (RES, RES, 4): the analytic frame i with a radial alpha ramp"""
+    P = sc.poses[i]
+    d = sc.directions @ P[:, :3].t()
+    o = P[:, 3].expand_as(d)
+    rgb = sc.gt_rgb_rays(o.contiguous(), d.contiguous()).reshape(RES, RES, 3)
+    yy, xx = torch.meshgrid(torch.arange(RES), torch.arange(RES), indexing="ij")
+    a = ((xx + 2 * yy + 17 * i) % 256).to(torch.uint8)
+    return torch.cat([(rgb.clamp(0, 1) * 255 + 0.5).to(torch.uint8), a[..., None]], -1).numpy()
+
+
+def write_scenes(base):
+    """-> (nsvf_root, blender_root) under `base` (deterministic)"""
+    sys.path[:0] = [os.path.join(ROOT, "ar-nerf_amd")]
+    import synthetic as S
+    from datasets.png import write_png
+    sc = S.AnalyticScene(W=RES, H=RES, n_images=N_TRAIN + N_TEST, seed=11)
+    # (a) NSVF, off-centre bbox
+    nsvf = os.path.join(base, "Synthetic_NeRF", "Analytic")
+    os.makedirs(os.path.join(nsvf, "rgb"), exist_ok=True)
+    os.makedirs(os.path.join(nsvf, "pose"), exist_ok=True)
+    fx800 = 0.5 * 800 / np.tan(0.5 * CAMERA_ANGLE_X)
+    with open(os.path.join(nsvf, "intrinsics.txt"), "w") as f:
+        f.write(f"{fx800} 0. 0. 0.\n")
+    with open(os.path.join(nsvf, "bbox.txt"), "w") as f:
+        f.write("-0.61 -0.42 -0.50 0.39 0.58 0.55 0.01\n")
+    for i in range(N_TRAIN + N_TEST):
+        split = "0" if i < N_TRAIN else "2"
+        write_png(os.path.join(nsvf, "rgb", f"{split}_{i:04d}.png"), _rgba(sc, i))
+        c2w = np.eye(4)
+        c2w[:3] = sc.poses[i].double().numpy()
+        c2w[:3, 3] += np.array([0.11, -0.08, 0.025])
+        np.savetxt(os.path.join(nsvf, "pose", f"{split}_{i:04d}.txt"), c2w)
+    # (b) Blender: [right up back] matrices at a radius != 1.5 (the loader rescales to 1.5)
+    blender = os.path.join(base, "nerf_synthetic", "analytic")
+    os.makedirs(os.path.join(blender, "train"), exist_ok=True)
+    os.makedirs(os.path.join(blender, "test"), exist_ok=True)
+    for split, idx in (("train", range(N_TRAIN)), ("test", range(N_TRAIN, N_TRAIN + N_TEST))):
+        frames = []
+        for i in idx:
+            c2w = np.eye(4)
+            c2w[:3] = sc.poses[i].double().numpy()
+            c2w[:3, 1:3] *= -1  # [right down front] -> [right up back]
+            c2w[:3, 3] *= 4.0 / 1.5
+            name = f"{split}/r_{i}"
+            write_png(os.path.join(blender, name + ".png"), _rgba(sc, i))
+            frames.append({"file_path": "./" + name, "transform_matrix": c2w.tolist()})
+        with open(os.path.join(blender, f"transforms_{split}.json"), "w") as f:
+            json.dump({"camera_angle_x": CAMERA_ANGLE_X, "frames": frames}, f)
+    return nsvf, blender
+
+
+def install_stubs():
+    from PIL import Image
+    imageio = types.ModuleType("imageio")
+    imageio.imread = lambda p: np.asarray(Image.open(p))
+    sys.modules["imageio"] = imageio
+    cv2 = types.ModuleType("cv2")
+
+    def resize(img, wh):
+        if (img.shape[1], img.shape[0]) != tuple(wh):
+            raise RuntimeError("cv2 stub: resizing is not available here")
+        return img
+    cv2.resize = resize
+    sys.modules["cv2"] = cv2
+    kornia = types.ModuleType("kornia")
+
+    def create_meshgrid(H, W, normalized_coordinates=True, device=None, dtype=torch.float32):
+        assert not normalized_coordinates
+        ys, xs = torch.meshgrid(torch.arange(H, dtype=dtype), torch.arange(W, dtype=dtype), indexing="ij")
+        return torch.stack([xs, ys], -1)[None]
+    kornia.create_meshgrid = create_meshgrid
+    sys.modules["kornia"] = kornia
+    sys.modules.setdefault("matplotlib", types.ModuleType("matplotlib"))
+    sys.modules.setdefault("matplotlib.pyplot", types.ModuleType("matplotlib.pyplot"))
+    for k in list(sys.modules):  # (this repo's datasets package, imported by the scene writer)
+        if k == "datasets" or k.startswith("datasets."):
+            del sys.modules[k]
+    pkg = types.ModuleType("datasets")  # the reference's datasets/ without its __init__ (EXR / RTMV imports)
+    pkg.__path__ = [os.path.join(REF, "datasets")]
+    sys.modules["datasets"] = pkg
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def summarize(prefix, ds, out):
+    rays = ds.rays.numpy() if torch.is_tensor(ds.rays) else np.asarray(ds.rays)
+    out[prefix + "K"] = ds.K.numpy()
+    out[prefix + "img_wh"] = np.array(ds.img_wh)
+    out[prefix + "poses"] = ds.poses.numpy()
+    out[prefix + "directions"] = ds.directions.numpy()
+    out[prefix + "rays_sha"] = np.array(sha(rays.astype(np.float32)))
+    out[prefix + "rays_sub"] = rays[:, ::53]
+    out[prefix + "rays_shape"] = np.array(rays.shape)
+
+
+def main():
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        nsvf, blender = write_scenes(tmp)
+        install_stubs()
+        from datasets.nerf import NeRFDataset
+        from datasets.nsvf import NSVFDataset
+        ds_kw = dict(downsample=RES / 800)
+        for split in ("train", "test"):
+            d = NSVFDataset(nsvf, split=split, **ds_kw)
+            summarize(f"nsvf_{split}_", d, out)
+            out["nsvf_shift"], out["nsvf_scale"] = np.asarray(d.shift), np.array(d.scale)
+            d = NeRFDataset(blender, split=split, **ds_kw)
+            summarize(f"nerf_{split}_", d, out)
+    path = os.path.join(HERE, "loaders.npz")
+    np.savez_compressed(path, **out)
+    print(path, os.path.getsize(path))
+
+
+if __name__ == "__main__":
+    main()
