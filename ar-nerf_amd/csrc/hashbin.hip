@@ -480,15 +480,17 @@ __device__ __forceinline__ void adam4(const AdamArgs& a, size_t base, uint32_t e
 
 template <bool FUSED = false>
 __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
-                                                          float* __restrict__ grad, BinWs ws, AdamArgs adam) {
+                                                          float* __restrict__ grad, BinWs ws, AdamArgs adam,
+                                                          uint32_t b_lo, uint32_t b_hi) {
+    // buckets [b_lo, b_hi) (a level range; all buckets: 0, nbt)
     extern __shared__ __attribute__((aligned(16))) double img[];  // [2][BENT]: feature-major, 8-byte stride
-    const uint32_t total = ws.items[nbt];
+    const uint32_t total = ws.items[b_hi];
     const int t = threadIdx.x, lane = t & 63;
     const bool overflow = ws.fb[MAXB] != 0;
     float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
     if (FUSED) adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
-    for (uint32_t it = blockIdx.x; it < total; it += gridDim.x) {
-        uint32_t lo = 0, hi = nbt;  // bucket b: items[b] <= it < items[b + 1]
+    for (uint32_t it = ws.items[b_lo] + blockIdx.x; it < total; it += gridDim.x) {
+        uint32_t lo = b_lo, hi = b_hi;  // bucket b: items[b] <= it < items[b + 1]
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (ws.items[mid] <= it) lo = mid; else hi = mid;
@@ -631,7 +633,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         __syncthreads();
     }
     if (FUSED) {  // buckets without records: Adam with a zero gradient (moments still decay)
-        for (uint32_t b = blockIdx.x; b < nbt; b += gridDim.x) {
+        for (uint32_t b = b_lo + blockIdx.x; b < b_hi; b += gridDim.x) {
             if (ws.tot[b] != 0u || !fused_bucket(ws, b, overflow)) continue;
             const uint32_t l = bucket_level(ba, b), lb = b - ba.bbase[l];
             const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
@@ -655,8 +657,9 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
 // Adam (+ gradient zeroing) of the binned buckets the fused accumulation did
 // not step: one workgroup per bucket, from the gradient in memory.
 __global__ void __launch_bounds__(256) hash_adam_residual_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
-                                                                  float* __restrict__ grad, BinWs ws, AdamArgs adam) {
-    const uint32_t b = blockIdx.x;
+                                                                  float* __restrict__ grad, BinWs ws, AdamArgs adam,
+                                                                  uint32_t b_lo) {
+    const uint32_t b = b_lo + blockIdx.x;
     if (b >= nbt || fused_bucket(ws, b, ws.fb[MAXB] != 0)) return;
     float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
     adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
@@ -707,7 +710,7 @@ size_t ngp_hash_backward_binned_workspace(int64_t max_samples) {
 static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                        const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* workspace,
                        int64_t max_samples, int level_lo, int merge_hi, int phase, void* stream,
-                       const AdamArgs* adam = nullptr) {
+                       const AdamArgs* adam = nullptr, int acc_lo = 0, int acc_hi = L) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
@@ -724,6 +727,9 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
     uint32_t nbt;
     st = bin_args(grid, tiles_cap, level_lo, merge_hi, ba, nbt);
     if (st) return st;
+    // phase 4 over the buckets of levels [acc_lo, acc_hi) only (levels below level_lo have none)
+    NGP_CHECK_ARG(0 <= acc_lo && acc_lo <= acc_hi && acc_hi <= L);
+    const uint32_t b_lo = ba.bbase[acc_lo], b_hi = ba.bbase[acc_hi];
     BinWs ws;
     bin_ws_bytes(tiles_cap, &ws, workspace);
     hipStream_t s = as_stream(stream);
@@ -751,10 +757,11 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
         }
         static const unsigned capB = resident_blocks(hash_accum_kernel<false>, ACC_T, lds);
         if (adam) {
-            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<true><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam));
-            NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<nbt, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam));
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<true><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam, b_lo, b_hi));
+            if (b_hi > b_lo)
+                NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<b_hi - b_lo, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam, b_lo));
         } else {
-            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<false><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}));
+            NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<false><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}, b_lo, b_hi));
         }
     }
     return ngp_launch_status();
@@ -822,6 +829,13 @@ int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* w
     static const float dummy[1] = {0.f};
     return hash_binned(dummy, 1, nullptr, nullptr, grid, nullptr, grad_table, workspace, max_samples, level_lo,
                        merge_hi, 4, stream);
+}
+
+int ngp_hash_binned_accum_levels(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
+                                 int level_lo, int merge_hi, int acc_level_lo, int acc_level_hi, void* stream) {
+    static const float dummy[1] = {0.f};
+    return hash_binned(dummy, 1, nullptr, nullptr, grid, nullptr, grad_table, workspace, max_samples, level_lo,
+                       merge_hi, 4, stream, nullptr, acc_level_lo, acc_level_hi);
 }
 
 }  // extern "C"

@@ -5,10 +5,13 @@ The reference's only parallelism is Lightning DDP over per-rank 8192-ray
 batches (train.py:288): gradients all-reduced every step, buffers broadcast
 from rank 0 every forward (SURVEY.md §2 "Collective call sites").  Here:
   * ZeRO-1 over the flat parameter vector: the fp32 gradient is
-    reduce-scattered (SUM) in two buckets -- [MLP | coarse hash levels] and
-    [fine hash levels] -- each rank runs FusedAdam on its 1/world shard of
-    every bucket only (fp32 master, moments; the 1/world mean is folded into
-    Adam), and the updated fp16 shadow the kernels read is all-gathered.
+    reduce-scattered (SUM) in three buckets -- [MLP | coarse hash levels],
+    [binned levels, first half], [binned levels, second half] -- each rank
+    runs FusedAdam on its 1/world shard of every bucket only (fp32 master,
+    moments; the 1/world mean is folded into Adam), and the updated fp16
+    shadow the kernels read is all-gathered; a bucket's reduce-scatter, Adam
+    and all-gather run on the comm stream as soon as its gradient is complete
+    (trainer._replay), beside the rest of the backward.
     Exact per element (the same Adam on the same summed gradient), a third
     less traffic than an all-reduce of the fp32 gradient (RS fp32 + AG fp16)
     and 1/world of the Adam work per rank;
@@ -43,15 +46,16 @@ def shard_cells(indices, coords, rank, world):
     return indices[lo:hi], coords[lo:hi]
 
 
-def zero_buckets(n_params, split, world, align=4):
-    """ZeRO-1 bucket bounds over a flat vector padded to n_pad: bucket 0 =
-    [0, s1), bucket 1 = [s1, n_pad), both multiples of world*align (equal
-    16-byte aligned shards); s1 = split rounded DOWN, so bucket 0 holds only
-    entries complete at `split` (a few of them fall into bucket 1)."""
+def zero_buckets(n_params, splits, world, align=4):
+    """ZeRO-1 bucket bounds over a flat vector padded to n_pad: buckets
+    [0, s_1), [s_1, s_2), ..., [s_k, n_pad), all multiples of world*align
+    (equal 16-byte aligned shards); each split rounded DOWN, so a bucket holds
+    only entries complete at its split (a few of them fall into the next
+    bucket).  Empty buckets are dropped.  splits: an int or an ascending list."""
     q = world * align
-    s1 = (split // q) * q
     n_pad = ((n_params + q - 1) // q) * q
-    return n_pad, [(0, s1), (s1, n_pad)] if s1 > 0 else [(0, n_pad)]
+    cuts = [0] + [(s // q) * q for s in ([splits] if isinstance(splits, int) else splits)] + [n_pad]
+    return n_pad, [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
 
 
 def _gloo(group):

@@ -60,6 +60,7 @@ def _lib():
         L.ngp_hash_binned_apply.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, c_int, vp]
         L.ngp_hash_binned_write.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, c_int, vp]
         L.ngp_hash_binned_accum.argtypes = [P, vp, vp, c_int64, c_int, c_int, vp]
+        L.ngp_hash_binned_accum_levels.argtypes = [P, vp, vp, c_int64, c_int, c_int, c_int, c_int, vp]
         L.ngp_hash_binned_apply_adam.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, c_int, vp, vp, vp,
                                                  vp, vp, c_float, c_float, c_float, vp, c_float, vp]
         L.ngp_hash_binned_accum_adam.argtypes = [P, vp, vp, c_int64, c_int, c_int, vp, vp, vp, vp, vp, c_float, c_float,
@@ -71,7 +72,8 @@ def _lib():
                   L.ngp_hash_backward, L.ngp_hash_backward_binned, L.ngp_hash_backward_levels,
                   L.ngp_hash_backward_levels_rep,
                   L.ngp_hash_binned_plan, L.ngp_hash_binned_apply, L.ngp_hash_binned_write,
-                  L.ngp_hash_binned_accum, L.ngp_hash_binned_apply_adam, L.ngp_hash_binned_accum_adam):
+                  L.ngp_hash_binned_accum, L.ngp_hash_binned_accum_levels, L.ngp_hash_binned_apply_adam,
+                  L.ngp_hash_binned_accum_adam):
             f.restype = c_int
         _declared = True
     return L

@@ -47,7 +47,7 @@ class NGPTrainer:
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
                  device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=None, bin_level_lo=None,
                  chunk_first=64, erode=False, lambda_distortion=0.0, bin_merge_hi=0, fused_adam=True, use_graphs=True,
-                 pair_steps=False):
+                 pair_steps=False, emulate_dp=False):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
@@ -70,6 +70,12 @@ class NGPTrainer:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        # the data-parallel (ZeRO-1, graph-segmented) step; emulate_dp = N runs it in one process
+        # with the shards of a world of N (this process = rank 0) and the collectives replaced by
+        # local copies of its shard -- one rank's compute at world N without the xGMI transfers
+        # (bench --emulate-dp N; only shard 0 of each bucket is stepped, so N > 1 is for timing)
+        self.dp = self.world > 1 or bool(emulate_dp)
+        self.dp_world = self.world if self.world > 1 else max(1, int(emulate_dp))
         dev = self.dev
         # ---- field parameters: fp32 master, fp16 shadow, Adam state, grad
         self.grid = HG.HashGrid(scale)
@@ -91,12 +97,14 @@ class NGPTrainer:
             bin_samples_per_ray = 512 if big else 128
         self.hash_backward = hash_backward
         self.bin_level_lo = 0 if hash_backward == "binned" else min(max(int(bin_level_lo), 0), self.grid.n_levels)
-        # ZeRO-1 layout (ddp.zero_buckets): buffers padded to n_pad, two
-        # buckets [MLP | coarse levels] [fine levels] split where the coarse
-        # (atomic) gradient is complete; rank r owns shard r of each bucket.
-        # All levels binned (bin_level_lo 0): bucket 0 is the MLP alone.
-        split = HG.MLP_PARAMS + 2 * int(self.grid.offsets[self.bin_level_lo])
-        self.n_pad, self.buckets = ddp.zero_buckets(n, split, self.world)
+        # ZeRO-1 layout (ddp.zero_buckets): buffers padded to n_pad, three
+        # buckets [MLP | coarse levels] [binned levels lo..mid) [mid..16),
+        # split where the coarse (atomic) gradient, then the first binned level
+        # range, are complete; rank r owns shard r of each bucket.  All levels
+        # binned (bin_level_lo 0): bucket 0 is the MLP alone.
+        self.bin_level_mid = (self.bin_level_lo + self.grid.n_levels + 1) // 2
+        splits = [HG.MLP_PARAMS + 2 * int(self.grid.offsets[lv]) for lv in (self.bin_level_lo, self.bin_level_mid)]
+        self.n_pad, self.buckets = ddp.zero_buckets(n, splits, self.dp_world)
         pb = torch.zeros(self.n_pad, device=dev)
         pb[:n] = init
         self._pbuf = pb
@@ -107,9 +115,9 @@ class NGPTrainer:
         self.grad = self._gbuf[:n]
         self.exp_avg = torch.zeros(self.n_pad, device=dev)
         self.exp_avg_sq = torch.zeros(self.n_pad, device=dev)
-        self.shards = [(a + (b - a) * self.rank // self.world, a + (b - a) * (self.rank + 1) // self.world)
+        self.shards = [(a + (b - a) * self.rank // self.dp_world, a + (b - a) * (self.rank + 1) // self.dp_world)
                        for a, b in self.buckets]
-        self._gshard = [torch.zeros(hi - lo, device=dev) for lo, hi in self.shards] if self.world > 1 else None
+        self._gshard = [torch.zeros(hi - lo, device=dev) for lo, hi in self.shards] if self.dp else None
         self.global_step = 0
         # ---- occupancy (models/networks.py:20-30, train.py:78-82)
         self.center = torch.zeros(1, 3, device=dev)
@@ -164,6 +172,8 @@ class NGPTrainer:
         # accumulation, whose own FusedAdam is fused into it (+5 %,
         # profiles/r02/ab/fused_adam.txt; bit-identical to one FusedAdam launch after the
         # backward, which fused_adam=False restores).
+        # (its own stream: sharing the march's side stream -- their work never overlaps in time --
+        # measured 6 % slower, the graph's branches then map onto fewer hardware queues)
         self.bwd_stream = torch.cuda.Stream(device=dev)
         self.fused_adam = bool(fused_adam)
         self._adam_hi = None
@@ -500,7 +510,7 @@ class NGPTrainer:
             return self.out_loss
         if (self.use_graphs and self._pending is not None and (gs % ui != 0 or self._updated_for == gs)
                 and gs >= self.warmup_steps and self.kernel_events is None and not self.no_prefetch):
-            if (self.pair_steps and self.world == 1 and self.timer is None and (gs + 1) % ui != 0
+            if (self.pair_steps and not self.dp and self.timer is None and (gs + 1) % ui != 0
                     and (gs + 2) % ui != 0 and gs // self.steps_per_epoch == (gs + 1) // self.steps_per_epoch):
                 return self._replay_pair(gt, directions, poses)
             return self._replay(gt, directions, poses, (gs + 1) % ui == 0)
@@ -547,21 +557,32 @@ class NGPTrainer:
             torch.cuda.current_stream().wait_event(ev)
         self._set_lr()
         key = (k, bool(update_after), gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype)
-        if self.world == 1:
+        if not self.dp:
             self._run_graph(key, lambda: self._graph_body(k, gt, directions, poses, update_after))
         else:  # collectives between graph segments (no RCCL inside captures)
+            cs, comm = torch.cuda.current_stream(), self.comm_stream
             self._run_graph(key + ("compute",), lambda: self._segment_compute(k, gt, directions, poses, update_after))
             if self.hash_backward != "atomic":
-                cs = torch.cuda.current_stream()
+                # coarse levels (side stream) -> bucket 0's reduce-scatter, Adam, all-gather on the
+                # comm stream while the binned levels run here in two level ranges, each range's
+                # bucket following it on the comm stream while the next range accumulates
                 self.bwd_stream.wait_stream(cs)
                 with torch.cuda.stream(self.bwd_stream):
                     self._run_graph(key + ("coarse",), self._segment_coarse)
-                self._run_graph(key + ("apply",), self._segment_apply)
-                self._reduce_grads_overlapped(self.bwd_stream)
+                comm.wait_stream(self.bwd_stream)
+                self._bucket_update(0)
+                nb = len(self.buckets)  # 3 unless a level range is empty
+                for i, seg in enumerate((self._segment_apply_a, self._segment_apply_b)):
+                    self._run_graph(key + ("apply", i), seg)
+                    comm.wait_stream(cs)
+                    for j in ((1,) if nb == 3 else ()) if i == 0 else range(2 if nb == 3 else 1, nb):
+                        self._bucket_update(j)
             else:
-                self._reduce_grads()
-            self._run_graph(key + ("adam",), self._segment_adam)
-            self._gather_params16()
+                comm.wait_stream(cs)
+                for i in range(len(self.buckets)):
+                    self._bucket_update(i)
+            cs.wait_stream(comm)
+            vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
             if update_after:  # (every 16 steps) eager: the update has its own collectives
                 self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=False)
                 self._march(1 - k, ("sample", 0, gt), directions, poses, torch.cuda.current_stream())
@@ -654,32 +675,48 @@ class NGPTrainer:
         """world > 1 graph segment (side stream): the atomic coarse hash levels."""
         self._coarse_levels()
 
-    def _segment_apply(self):
-        """world > 1 graph segment (main stream): the binned hash levels."""
+    def _segment_apply_a(self):
+        """world > 1 graph segment (main stream): the binned levels' record
+        write, then the accumulation of levels [bin_level_lo, bin_level_mid)."""
         HGL = HG._lib()
-        vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+        vren._ok(HGL.ngp_hash_binned_write(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
                                            HG.ctypes.byref(self.grid.desc), _p(self.denc),
                                            _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
-                                           self.bin_level_lo, self.bin_merge_hi, vren._stream()), "hash_binned_apply")
+                                           self.bin_level_lo, self.bin_merge_hi, vren._stream()), "hash_binned_write")
+        self._accum_levels(self.bin_level_lo, self.bin_level_mid)
 
-    def _reduce_grads_overlapped(self, coarse_stream):
-        """Reduce-scatter of bucket 0 ([MLP | coarse levels], complete once the
-        coarse segment on `coarse_stream` is) on the comm stream while the
-        binned levels run on the main stream, then bucket 1 after them; the
-        main stream waits for both and zeroes the local gradient."""
-        cs, comm = torch.cuda.current_stream(), self.comm_stream
-        comm.wait_stream(coarse_stream)
-        for i, ((a, b), gs) in enumerate(zip(self.buckets, self._gshard)):
-            if i == 1 or len(self.buckets) == 1:
-                comm.wait_stream(cs)
-            with torch.cuda.stream(comm):
-                ddp.reduce_scatter_(self._gbuf[a:b], gs, self.pg)
-        cs.wait_stream(comm)
-        self._gbuf.zero_()
+    def _segment_apply_b(self):
+        """world > 1 graph segment (main stream): accumulation of the binned
+        levels [bin_level_mid, 16) (beside bucket 1's reduce-scatter)."""
+        self._accum_levels(self.bin_level_mid, self.grid.n_levels)
 
-    def _segment_adam(self):
-        self._adam_shards()
-        vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
+    def _accum_levels(self, lo, hi):
+        vren._ok(HG._lib().ngp_hash_binned_accum_levels(
+            HG.ctypes.byref(self.grid.desc), _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
+            self.bin_level_lo, self.bin_merge_hi, lo, hi, vren._stream()), "hash_binned_accum_levels")
+
+    def _bucket_update(self, i):
+        """On the comm stream: reduce-scatter of gradient bucket i into this
+        rank's shard, the bucket's local gradient zeroed, FusedAdam on the
+        shard, all-gather of the shard's fp16 shadow."""
+        a, b = self.buckets[i]
+        with torch.cuda.stream(self.comm_stream):
+            self._rs(i)
+            self._gbuf[a:b].zero_()
+            self._adam_shard(i, vren._stream())
+            self._ag(i)
+
+    def _rs(self, i):
+        (a, b), (lo, hi), gs = self.buckets[i], self.shards[i], self._gshard[i]
+        if self.world == 1:  # (emulation: this rank's shard of the local gradient)
+            gs.copy_(self._gbuf[lo:hi])
+        else:
+            ddp.reduce_scatter_(self._gbuf[a:b], gs, self.pg)
+
+    def _ag(self, i):
+        (a, b), (lo, hi) = self.buckets[i], self.shards[i]
+        if self.world > 1:  # (emulation: the shard's shadow is in place already)
+            ddp.all_gather_(self._p16buf[a:b], self._p16buf[lo:hi], self.pg)
 
     def _graph_body(self, k, gt, directions, poses, update_after=False):
         self.cur = k
@@ -803,7 +840,7 @@ class NGPTrainer:
             # (world > 1 graph segments: the hash backward runs as two more
             # graphs -- coarse levels on the side stream, binned levels here --
             # so the reduce-scatter of the [MLP | coarse] bucket overlaps the
-            # binned levels; _replay / _segment_coarse / _segment_apply)
+            # binned levels; _replay / _segment_coarse / _segment_apply_a, _b)
             cs.wait_stream(bs)
             return self.out_loss
         self._ev("hash_bwd", 0)
@@ -814,7 +851,7 @@ class NGPTrainer:
             # single process: the MLP + coarse levels' Adam right after them on the side stream
             # (no all-reduce orders it after the whole gradient), folding the coarse gradient
             # replicas itself; the binned levels' Adam inside their accumulation (fused_adam)
-            adam_split = apply_adam and self.world == 1
+            adam_split = apply_adam and not self.dp
             fused = self.fused_adam and adam_split
             self._adam_hi = split if fused else self.n_params
             fold_in_adam = adam_split and self.rep_buf is not None
@@ -854,11 +891,11 @@ class NGPTrainer:
                                            HG.ctypes.byref(self.grid.desc),
                                            _p(self.denc), _p(self.grad[HG.MLP_PARAMS:]), s), "hash_backward")
         self._ev("hash_bwd", 1)
-        if self.world == 1 and apply_adam:
+        if not self.dp and apply_adam:
             self._ev("adam", 0)
             self._adam(0, self.n_params, s)
             self._ev("adam", 1)
-        elif self.world > 1 and not self._segmented:
+        elif self.dp and not self._segmented:
             self._reduce_grads()
             if apply_adam:
                 self._adam_shards()
@@ -871,26 +908,29 @@ class NGPTrainer:
         buffers, then the local gradient is zeroed for the next step (RCCL over
         xGMI; outside graph captures).  apply_adam=False callers (tests) find
         the summed shards in _gshard."""
-        for (a, b), gs in zip(self.buckets, self._gshard):
-            ddp.reduce_scatter_(self._gbuf[a:b], gs, self.pg)
+        for i in range(len(self.buckets)):
+            self._rs(i)
         self._gbuf.zero_()
 
     def _adam_shards(self):
-        """FusedAdam on this rank's shard of every bucket: fp32 master,
-        moments and fp16 shadow of the shard, from the reduced gradient shard
-        (the 1/world mean folded in; the shard buffer zeroed)."""
-        s = vren._stream()
-        for (lo, hi), gs in zip(self.shards, self._gshard):
-            q = lambda t: _p(t[lo:hi])  # noqa: E731
-            vren._ok(self.L.ngp_adam_step_dev(q(self._pbuf), _p(gs), q(self.exp_avg), q(self.exp_avg_sq),
-                                              q(self._p16buf), hi - lo, _p(self.lr_dev), ctypes_float(0.9),
-                                              ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
-                                              ctypes_float(1.0 / self.world), 1, s), "adam")
+        for i in range(len(self.buckets)):
+            self._adam_shard(i, vren._stream())
+
+    def _adam_shard(self, i, s):
+        """FusedAdam on this rank's shard of bucket i: fp32 master, moments
+        and fp16 shadow of the shard, from the reduced gradient shard (the
+        1/world mean folded in; the shard buffer zeroed)."""
+        lo, hi = self.shards[i]
+        q = lambda t: _p(t[lo:hi])  # noqa: E731
+        vren._ok(self.L.ngp_adam_step_dev(q(self._pbuf), _p(self._gshard[i]), q(self.exp_avg), q(self.exp_avg_sq),
+                                          q(self._p16buf), hi - lo, _p(self.lr_dev), ctypes_float(0.9),
+                                          ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                                          ctypes_float(1.0 / self.world), 1, s), "adam")
 
     def _gather_params16(self):
         """All-gather of the updated fp16 shadow the kernels read."""
-        for (a, b), (lo, hi) in zip(self.buckets, self.shards):
-            ddp.all_gather_(self._p16buf[a:b], self._p16buf[lo:hi], self.pg)
+        for i in range(len(self.buckets)):
+            self._ag(i)
 
     def full_params(self):
         """The fp32 master vector, complete on every rank (world > 1: each rank
@@ -903,7 +943,7 @@ class NGPTrainer:
     def fused_params(self):
         """Parameters whose Adam runs inside the binned accumulation (the binned
         hash levels; single process, hybrid/binned backward), 0 otherwise."""
-        if not (self.fused_adam and self.world == 1 and self.hash_backward != "atomic"):
+        if not (self.fused_adam and not self.dp and self.hash_backward != "atomic"):
             return 0
         return self.n_params - (HG.MLP_PARAMS + 2 * self.grid.offsets[self.bin_level_lo])
 

@@ -110,6 +110,11 @@ def parse():
     ap.add_argument("--hash-backward", default="hybrid", choices=["hybrid", "binned", "atomic"])
     ap.add_argument("--bin-level-lo", type=int, default=None,
                     help="hybrid hash backward: first binned level (default: trainer's, 8 / 0 for cascaded scenes)")
+    ap.add_argument("--emulate-dp", type=int, default=0, metavar="N",
+                    help="(world 1) run the data-parallel step of a world of N ranks as rank 0 -- graph segments, "
+                         "ZeRO-1 shards of 1/N, per-bucket reduce-scatter / sharded Adam / all-gather on the comm "
+                         "stream -- with the collectives as local copies: one rank's compute at world N without "
+                         "the xGMI transfers (only shard 0 is stepped: a timing mode)")
     ap.add_argument("--pair-steps", action="store_true",
                     help="two consecutive steady-state steps per graph replay (trainer pair_steps)")
     ap.add_argument("--bin-merge-hi", type=int, default=0,
@@ -203,6 +208,9 @@ def inference_bench(trainer, res, frames, world, rank):
     return {"fps": round(world * frames / t, 2), "ms_per_frame": round(t / frames * 1e3, 3), "frames_per_rank": frames,
             "resolution": [res, res], "n_gpus": world, "iterations_per_frame": round(iters / frames, 1),
             "samples_per_ray": round(samples / (frames * n), 2), "graphs": True,
+            # the trained state (hence samples/ray) varies run to run: these two are the comparable figures
+            "ms_per_frame_per_sample_per_ray": round(t / frames * 1e3 / max(samples / (frames * n), 1e-9), 4),
+            "samples_per_s": round(world * samples / t),
             "host_loop_ms_per_frame": round(t_host * 1e3, 3), "host_loop_bit_exact": same,
             "workload": "full-frame test render of the trained model (black bg), march+field+composite per "
                         "iteration in HIP graphs (16 iterations, then 8 per replay while rays remain), one host sync per graph"}
@@ -287,7 +295,7 @@ def main():
     erode = args.erode == "on" or (args.erode == "auto" and args.scale > 0.5)
     trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward,
                          bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray, erode=erode,
-                         bin_merge_hi=args.bin_merge_hi, pair_steps=args.pair_steps)
+                         bin_merge_hi=args.bin_merge_hi, pair_steps=args.pair_steps, emulate_dp=args.emulate_dp)
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
     WORK = active_work(trainer)
     R = args.batch
@@ -425,8 +433,11 @@ def main():
     step_bound = {"hbm_bytes_per_step": round(hbm_bytes), "mlp_flops_per_step": round(flops),
                   "ms_per_step_at_peak": round(bound_ms, 4), "rays_per_s_at_peak": round(R / (bound_ms * 1e-3)),
                   "adam_ms_at_peak": round(adam_ms, 4),
+                  "step_fraction_of_bound": round(bound_ms / (t_el / args.steps * 1e3), 4),
                   "note": "sum of the ops' algorithmic work at HBM / MFMA peak, serial; dense FusedAdam alone "
-                          "(34 B/param) costs adam_ms_at_peak per step"}
+                          "(34 B/param) costs adam_ms_at_peak per step. rays_per_s_at_peak is this design's "
+                          "floor under exact FusedAdam semantics: the north_star's 1e8 rays/s lies above it "
+                          "(DESIGN.md section 7)"}
     loss = float(trainer.out_loss.sum().item())
     psnr = psnr_eval(trainer, scene, args.psnr_views, args.psnr_res) if (rank == 0 and args.psnr_views > 0) else None
     infer = inference_bench(trainer, args.infer_res, args.infer_frames, world, rank) if args.infer_frames > 0 else None
@@ -443,7 +454,7 @@ def main():
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_el / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp16 field (MLP weight gradients on bf16 MFMA operands) / fp32 march, composite, Adam",
+            "dtype": "fp16 field (MLP forward, backward and weight gradients on fp16 MFMA operands, fp32 accumulate) / fp32 march, composite, Adam",
             "data": "synthetic (analytic sphere+box scene, 100 views 800x800, Lego intrinsics; random-init weights "
                     f"trained {args.pretrain} setup steps)",
             "config": {"workload": (f"{'lego' if args.scale <= 0.5 else 'garden'}-shaped training step: {R} rays/rank, "
@@ -454,7 +465,7 @@ def main():
                        "field_evaluated_per_ray": round(ev_s, 2),
                        "graphs": trainer.use_graphs,
                        "chunk_first": trainer.chunk_first,
-                       "parallelism": f"dp{world}", "last_loss": round(loss, 5),
+                       "parallelism": f"dp{world}" + (f" (data-parallel step of world {args.emulate_dp} emulated: collectives as local copies)" if args.emulate_dp else ""), "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
                        "erode": trainer.erode,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},

@@ -395,6 +395,12 @@ int ngp_hash_binned_write(const float* xyzs, int64_t n, const int64_t* n_dev, co
                           int64_t max_samples, int level_lo, int merge_hi, void* stream);
 int ngp_hash_binned_accum(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
                           int level_lo, int merge_hi, void* stream);
+/* ngp_hash_binned_accum over the buckets of levels [acc_level_lo,
+ * acc_level_hi) only (levels below level_lo have none): the data-parallel
+ * step sums the binned levels in two level ranges so that the first range's
+ * gradient reduce-scatter overlaps the second range's accumulation. */
+int ngp_hash_binned_accum_levels(const ngp_hashgrid_t* grid, float* grad_table, void* workspace, int64_t max_samples,
+                                 int level_lo, int merge_hi, int acc_level_lo, int acc_level_hi, void* stream);
 /* ngp_hash_binned_apply with FusedAdam of the binned levels' parameters
  * (apex FusedAdam, train.py:146-152, as ngp_adam_step_dev): a bucket whose
  * whole gradient one workgroup sums (one chunk, no direct adds, no overflow)

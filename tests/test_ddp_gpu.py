@@ -163,10 +163,10 @@ def test_two_ranks_match_one_process_on_the_concatenated_batch():
 
 def _seg_worker(rank, world, port, q):
     """world-2 rank: step 0 eager, step 1 a segmented graph replay (the ZeRO-1
-    reduce-scatter between compute segments); lr 0 keeps the parameters at
-    their initial values, so both runs see the same field.  The reduced
-    gradient shards of step 1 are copied out inside the captured Adam
-    segment."""
+    reduce-scatter of each bucket on the comm stream as soon as its level range
+    is complete); lr 0 keeps the parameters at their initial values, so both
+    runs see the same field.  The reduced gradient shard of each bucket is
+    copied out right before its Adam (trainer._adam_shard)."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -176,20 +176,21 @@ def _seg_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         tr, sc = _seg_trainer(R)
-        got = []
-        orig = tr._adam_shards
+        got = {}
+        orig = tr._adam_shard
 
-        def spy():  # (recorded into the captured Adam segment: replays refresh the copies)
-            got[:] = [g.clone() for g in tr._gshard]
-            orig()
-        tr._adam_shards = spy
+        def spy(i, s):  # (on the stream the Adam runs on: the last step's copies win)
+            got[i] = tr._gshard[i].clone()
+            orig(i, s)
+        tr._adam_shard = spy
         gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
         for _ in range(2):
             tr.train_step(gt, dirs, poses)
         tr.drain()
         torch.cuda.synchronize()
         assert len(tr._graphs) >= 1 and tr.n_prefetched >= 1  # step 1 was a graph replay
-        q.put((rank, {"shards": [g.cpu().numpy() for g in got], "buckets": tr.buckets, "bin_lo": tr.bin_level_lo}))
+        q.put((rank, {"shards": [got[i].cpu().numpy() for i in range(len(tr.buckets))], "buckets": tr.buckets,
+                      "bin_lo": tr.bin_level_lo}))
     finally:
         dist.destroy_process_group()
 
