@@ -286,6 +286,73 @@ __device__ __forceinline__ int64_t composite_loss_ray(
 // [2] += gradient-carrying samples, summed per block in LDS, then one atomic
 // per counter per block into stripe blockIdx % NGP_STAT_STRIPES (one address
 // for all 2048 blocks serialised ~40 us of the kernel on the memory side).
+// ---- decoupled look-back (ordered compaction across blocks in one launch)
+// Workspace {ticket, done, generation, pad, status[blocks]}, zeroed once by
+// the caller.  A block takes a ticket (its position in dispatch order: it
+// only ever waits on blocks that started before it), publishes its
+// aggregate, and one wave walks back over the status words 64 at a time,
+// summing aggregates until the closest inclusive prefix; the last block to
+// finish resets the ticket and advances the generation, so the words of the
+// previous launch never match.  A status word carries its own value, so the
+// hand-off is one 8-byte agent-scope atomic each way (sc1 store / sc1 poll,
+// MI355X_MICROARCH.md "Valid forms"): no release / acquire fences -- an
+// acquire poll or a release per block (L2 write-back of the whole XCD) made
+// the step 60 % slower.  The lists themselves are read by later launches.
+struct LookbackWs {
+    uint32_t tick, done, gen, pad;
+    unsigned long long status[1];  // [blocks]
+};
+constexpr unsigned long long LB_AGG = 1ull << 40, LB_INCL = 2ull << 40, LB_VAL = (1ull << 40) - 1;
+__device__ __forceinline__ unsigned long long lb_word(uint32_t gen, unsigned long long flag, int64_t v) {
+    return ((unsigned long long)(gen & 0x3fffffu) << 42) | flag | ((unsigned long long)v & LB_VAL);
+}
+// whole wave: publishes aggregate A of block b, returns the exclusive prefix
+// of the blocks before it, publishes b's inclusive prefix
+__device__ __forceinline__ int64_t lookback_prefix(LookbackWs* __restrict__ lb, uint32_t b, uint32_t gen, int64_t A,
+                                                   int lane) {
+    if (lane == 0)
+        __hip_atomic_store(&lb->status[b], lb_word(gen, b == 0 ? LB_INCL : LB_AGG, A), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    int64_t P = 0;
+    for (int64_t j = (int64_t)b - 1; j >= 0; j -= 64) {
+        const int64_t q = j - lane;
+        unsigned long long wv = LB_INCL;  // (q < 0: before block 0, an inclusive 0)
+        // bounded: a predecessor publishes its aggregate without waiting on anyone, so this
+        // ends in microseconds; the bound only keeps a corrupted workspace from hanging the
+        // GPU (counted in g_guard_hits, the result is then wrong)
+        for (uint32_t spin = 0;; ++spin) {
+            if (q >= 0) wv = __hip_atomic_load(&lb->status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool ok = q < 0 || ((uint32_t)(wv >> 42) == (gen & 0x3fffffu) && (wv & (3ull << 40)) != 0);
+            if (__all(ok)) break;
+            if (spin == (1u << 22)) {
+                if (lane == 0) atomicAdd(&g_guard_hits, 1ull);
+                wv = LB_INCL;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const bool incl = (wv & (3ull << 40)) == LB_INCL;
+        const uint64_t m = __ballot(incl);
+        const int k = m ? __ffsll((unsigned long long)m) - 1 : 63;
+        int64_t v = lane <= k ? (int64_t)(wv & LB_VAL) : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        P += v;
+        if (m) break;
+    }
+    if (lane == 0 && b > 0)
+        __hip_atomic_store(&lb->status[b], lb_word(gen, LB_INCL, P + A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return P;
+}
+// one thread per block, after the block's last use of its ticket
+__device__ __forceinline__ void lookback_finish(LookbackWs* __restrict__ lb, uint32_t gen, uint32_t nb) {
+    if (__hip_atomic_fetch_add(&lb->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1) {
+        __hip_atomic_store(&lb->tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&lb->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&lb->gen, gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
@@ -924,6 +991,117 @@ __global__ void __launch_bounds__(256) chunk_rest_kernel(const float* __restrict
     if (lane == 0) counts[n] = (!done && N > first) ? (int32_t)(end - first) : 0;
 }
 
+// Round-2 list in one launch: chunk_rest_kernel's counts + the exclusive scan
+// across rows + the map of ray_segments.  Block b owns rows [64b, 64b + 64):
+// its waves compute the counts of 8 rows each (first-chunk loads of all 8
+// rows issued before any transmittance), wave 0 scans them, and the prefix
+// over earlier blocks comes from a decoupled look-back: each block publishes
+// its aggregate, then its inclusive prefix, as one 64-bit status word
+// {generation, flag, value}; wave 0 reads the 64 predecessors before it at a
+// time and stops at the closest inclusive one.  Block ids come from an atomic
+// ticket (dispatch order), so a block only ever waits on blocks that started
+// before it and publish their aggregate without waiting -- no deadlock at any
+// grid size.  The last block to finish resets the ticket and advances the
+// generation (stale status words of the previous launch never match).
+#ifndef NGP_CS_ROWS
+#define NGP_CS_ROWS 64
+#endif
+constexpr int CS_ROWS = NGP_CS_ROWS, CS_THREADS = 512, CS_RPW = CS_ROWS / (CS_THREADS / 64);
+constexpr int CS_LOG = CS_ROWS == 64 ? 6 : CS_ROWS == 32 ? 5 : 4;
+static_assert(CS_ROWS == 64 || CS_ROWS == 32 || CS_ROWS == 16, "row block");
+
+__global__ void __launch_bounds__(CS_THREADS) chunk_segments_kernel(
+    const float* __restrict__ sigmas, const float* __restrict__ deltas, const int64_t* __restrict__ rays_a,
+    int64_t n_rows, int first, int last, float T_thr, LookbackWs* __restrict__ lb, int64_t* __restrict__ start_ws,
+    int64_t* __restrict__ total, int64_t* __restrict__ total_acc, int32_t* __restrict__ sample_idx) {
+    __shared__ int32_t cnt_s[CS_ROWS];
+    __shared__ int32_t lofs[65];  // (wave 0 writes all 64 lanes' entries; [CS_ROWS] = the block's total)
+    __shared__ int64_t src[64];
+    __shared__ uint32_t sh_b;
+    __shared__ int64_t sh_prefix;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t nb = gridDim.x;
+    const uint32_t gen = __hip_atomic_load(&lb->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) sh_b = __hip_atomic_fetch_add(&lb->tick, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t b = sh_b;
+    const int64_t r0 = (int64_t)b * CS_ROWS, r1 = min(r0 + CS_ROWS, n_rows);
+    // ---- counts (chunk_rest_kernel's arithmetic)
+    int64_t st[CS_RPW], Nr[CS_RPW];
+    float sg0[CS_RPW], dl0[CS_RPW];
+#pragma unroll
+    for (int i = 0; i < CS_RPW; ++i) {
+        const int64_t r = r0 + w * CS_RPW + i;
+        st[i] = r < r1 ? rays_a[3 * r + 1] : 0;
+        Nr[i] = r < r1 ? rays_a[3 * r + 2] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < CS_RPW; ++i) {
+        const int64_t M = min(Nr[i], (int64_t)first);
+        sg0[i] = dl0[i] = 0.f;
+        if (lane < M) { sg0[i] = sigmas[st[i] + lane]; dl0[i] = deltas[st[i] + lane]; }
+    }
+#pragma unroll
+    for (int i = 0; i < CS_RPW; ++i) {
+        const int64_t M = min(Nr[i], (int64_t)first);
+        float T = 1.0f;
+        bool done = false;
+        for (int64_t k0 = 0; k0 < M && !done; k0 += 64) {
+            const int cnt = (int)(M - k0 < 64 ? M - k0 : 64);
+            float sg = sg0[i], dl = dl0[i];
+            if (k0 > 0) {
+                sg = dl = 0.f;
+                if (lane < cnt) { sg = sigmas[st[i] + k0 + lane]; dl = deltas[st[i] + k0 + lane]; }
+            }
+            const float om = 1.0f - (1.0f - __expf(-sg * dl));
+            const ChunkT ct = chunk_transmittance(om, cnt, T, T_thr, lane);
+            done = ct.hit;
+            T = __shfl(ct.Tn, ct.stop - 1, 64);
+        }
+        const int64_t end = last > 0 ? min(Nr[i], (int64_t)last) : Nr[i];
+        if (lane == 0) cnt_s[w * CS_RPW + i] = (!done && Nr[i] > first) ? (int32_t)(end - first) : 0;
+    }
+    __syncthreads();
+    if (w == 0) {
+        // ---- own rows: exclusive scan
+        const int64_t r = r0 + lane;
+        const int32_t c = r < r1 ? cnt_s[lane % CS_ROWS] : 0;
+        int32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        lofs[lane] = x - c;
+        const int32_t A = __shfl(x, 63, 64);
+        if (lane == 63) lofs[CS_ROWS] = x;
+        src[lane] = r < r1 ? rays_a[3 * r + 1] + first : 0;
+        // ---- look-back
+        const int64_t P = lookback_prefix(lb, b, gen, A, lane);
+        if (lane == 0) {
+            sh_prefix = P;
+            if (b == nb - 1) {
+                *total = P + A;
+                if (total_acc) *total_acc += P + A;
+            }
+        }
+    }
+    __syncthreads();
+    const int64_t prefix = sh_prefix;
+    if (t < r1 - r0) start_ws[r0 + t] = prefix + lofs[t];
+    const int32_t nbe = lofs[CS_ROWS];
+    for (int32_t q = t; q < nbe; q += CS_THREADS) {
+        int lo = 0, hi = CS_ROWS;  // lofs[lo] <= q < lofs[hi]
+#pragma unroll
+        for (int k = 0; k < CS_LOG; ++k) {
+            const int mid = (lo + hi) >> 1;
+            if (lofs[mid] <= q) lo = mid; else hi = mid;
+        }
+        sample_idx[prefix + q] = (int32_t)(src[lo] + (q - lofs[lo]));
+    }
+    if (t == 0) lookback_finish(lb, gen, nb);
+}
+
 }  // namespace ngp
 
 using namespace ngp;
@@ -968,6 +1146,30 @@ int ngp_chunk_counts_range(const int64_t* rays_a, int64_t n_rows, int first, int
         NGP_TIMED(NGP_K_CHUNK, as_stream(stream), chunk_rest_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, as_stream(stream)>>>(sigmas, deltas, rays_a, n_rows,
                                                                                       first, last, T_threshold, counts));
     }
+    return ngp_launch_status();
+}
+
+size_t ngp_chunk_segments_workspace(int64_t n_rows) {
+    const int64_t blocks = n_rows > 0 ? (n_rows + CS_ROWS - 1) / CS_ROWS : 1;
+    return 16 + 8 * (size_t)blocks;
+}
+
+int ngp_chunk_segments(const float* sigmas, const float* deltas, const int64_t* rays_a, int64_t n_rows, int first,
+                       int last, float T_threshold, void* lookback_ws, int64_t* start_ws, int64_t* total,
+                       int64_t* total_acc, int32_t* sample_idx, void* stream) {
+    NGP_CHECK_ARG(n_rows >= 0 && first >= 1 && (last <= 0 || last > first) && total);
+    hipStream_t s = as_stream(stream);
+    if (n_rows == 0) {
+        active_scan_kernel<<<1, 1024, 0, s>>>(nullptr, 0, start_ws, total, total_acc);  // total = 0
+        return ngp_launch_status();
+    }
+    NGP_CHECK_ARG(sigmas && deltas && rays_a && lookback_ws && start_ws && sample_idx &&
+                  ((uintptr_t)lookback_ws & 7) == 0);
+    const int64_t blocks = (n_rows + CS_ROWS - 1) / CS_ROWS;
+    NGP_CHECK_ARG(blocks <= (int64_t)0x7fffffff);
+    NGP_TIMED(NGP_K_SEGMENTS, s, chunk_segments_kernel<<<(unsigned)blocks, CS_THREADS, 0, s>>>(
+        sigmas, deltas, rays_a, n_rows, first, last, T_threshold, (LookbackWs*)lookback_ws, start_ws, total,
+        total_acc, sample_idx));
     return ngp_launch_status();
 }
 

@@ -195,6 +195,9 @@ class NGPTrainer:
         # more than it saves: profiles/r02/ab/chunk_rounds.txt)
         self.chunk_first = int(chunk_first)
         self.eval_counts = torch.empty(R, dtype=torch.int32, device=dev)
+        # round-2 list in one launch (counts + look-back scan + map): its look-back workspace, zeroed once
+        self._cs_ws = torch.zeros((vren.lib().ngp_chunk_segments_workspace(R) + 7) // 8, dtype=torch.int64,
+                                  device=dev)
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
@@ -266,7 +269,12 @@ class NGPTrainer:
                     rays_a=torch.empty(R, 3, dtype=torch.int64, device=dev),
                     n_samples=torch.zeros(1, dtype=torch.int64, device=dev),
                     xyzs=torch.empty(cap, 3, **f), dirs=torch.empty(cap, 3, **f), deltas=torch.empty(cap, **f),
-                    ts=torch.empty(cap, **f), slot_t=torch.empty(cap, **f), slot_dt=torch.empty(cap, **f))
+                    ts=torch.empty(cap, **f), slot_t=torch.empty(cap, **f), slot_dt=torch.empty(cap, **f),
+                    # the chunked forward's round-1 list (first chunk_first samples of every row),
+                    # built by the march itself (_march): off the step's critical path
+                    eval_idx1=torch.empty(cap, dtype=torch.int32, device=dev),
+                    eval_total1=torch.zeros(1, dtype=torch.int64, device=dev),
+                    act_start1=torch.empty(R, dtype=torch.int64, device=dev), eval1_K=0)
 
     def _bind(self, m):
         for k, v in m.items():
@@ -424,6 +432,15 @@ class NGPTrainer:
             vren._ok(L.ngp_march_train_compact(_p(m["rays_o"]), _p(m["rays_d"]), _p(m["rays_a"]), R,
                                                _p(m["slot_t"]), _p(m["slot_dt"]), self.max_samples, _p(m["xyzs"]),
                                                _p(m["dirs"]), _p(m["deltas"]), _p(m["ts"]), s), "march_compact")
+            # round 1 of the chunked forward: the list of each row's first chunk_first samples
+            # (counts min(N_r, K) + scan + list in one launch), here beside the previous step
+            # instead of at the head of this batch's step; evaluated-sample count into stats[4]
+            # (stats[3] is round 2's: the two streams never add to one counter)
+            K = self.chunk_first
+            m["eval1_K"] = K if (K > 0 and R <= 65536) else 0
+            if m["eval1_K"]:
+                vren._ok(L.ngp_ray_segments_capped(_p(m["rays_a"]), R, K, _p(m["act_start1"]), _p(m["eval_total1"]),
+                                                   _p(self.stats[4:]), _p(m["eval_idx1"]), s), "segments_capped")
             if side:
                 self._ev("march_side", 1, stream)
 
@@ -480,7 +497,8 @@ class NGPTrainer:
     def stat_totals(self):
         """(marched, composited, active, evaluated) samples accumulated since
         stats was last zeroed (sum over the stripes)."""
-        return [int(v) for v in self.stats.view(STAT_STRIPES, STAT_STRIDE)[:, :4].sum(0).tolist()]
+        t = [int(v) for v in self.stats.view(STAT_STRIPES, STAT_STRIDE)[:, :5].sum(0).tolist()]
+        return t[:3] + [t[3] + t[4]]  # (evaluated: round 2's count + round 1's, counted by the march)
 
     def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True, next_batch=None):
         """One training step on a batch (train.py:174-200).  img/pix (R) i64,
@@ -777,20 +795,21 @@ class NGPTrainer:
         self._ev("field_fwd", 0)
         if self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
-            if R <= 65536:  # counts min(N_r, K) + scan + list in one launch
-                vren._ok(L.ngp_ray_segments_capped(_p(self.rays_a), R, K, _p(self.act_start), _p(self.eval_total),
-                                                   _p(self.stats[3:]), _p(self.eval_idx), s), "segments_capped")
+            if self.eval1_K == K:  # built by this batch's march
+                self._field_indexed(s, self.eval_idx1, self.eval_total1)
             else:
                 vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, None, None, ctypes_float(1e-4),
                                             _p(self.eval_counts), s), "chunk_counts")
                 vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, 0, _p(self.act_start),
                                             _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
-            self._field_indexed(s)
-            # second round [K, N_r) of the rows still transparent after K samples
-            vren._ok(L.ngp_chunk_counts_range(_p(self.rays_a), R, K, 0, _p(self.sigmas), _p(self.deltas),
-                                              ctypes_float(1e-4), _p(self.eval_counts), s), "chunk_counts")
-            vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, K, _p(self.act_start),
-                                        _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
+                self._field_indexed(s)
+            # second round [K, N_r) of the rows still transparent after K samples: counts, scan
+            # and list in one launch (ngp_chunk_segments; the two launches it replaces cost a
+            # launch gap and a second pass over rays_a)
+            vren._ok(L.ngp_chunk_segments(_p(self.sigmas), _p(self.deltas), _p(self.rays_a), R, K, 0,
+                                          ctypes_float(1e-4), _p(self._cs_ws), _p(self.act_start),
+                                          _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s),
+                     "chunk_segments")
             self._field_indexed(s)
         else:  # encode + MLPs in one launch over every marched sample
             self._ev("hash_encode", 0)
@@ -814,8 +833,9 @@ class NGPTrainer:
                                       _p(self.out_depth), _p(self.out_loss), _p(self.n_active), None, None, None,
                                       _p(self.stats), s), "composite_loss")
         self._ev("composite", 1)
-        # compacted gradient-carrying samples: scan + map (a per-block atomic
-        # reservation inside composite_loss serialises on one address and was slower)
+        # compacted gradient-carrying samples: scan + map (a per-block atomic reservation inside
+        # composite_loss serialises on one address, and an ordered decoupled look-back across its
+        # 2048 four-row blocks made the launch 5x longer: both measured slower)
         vren._ok(L.ngp_active_samples(_p(self.n_active), _p(self.rays_a), R, _p(self.act_start),
                                       _p(self.n_active_total), _p(self.sample_idx), s), "active_samples")
         self._ev("composite_loss", 1)
@@ -966,12 +986,15 @@ class NGPTrainer:
                                           ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
                                           ctypes_float(1.0 / self.world), 1, s), "adam")
 
-    def _field_indexed(self, s):
+    def _field_indexed(self, s, idx=None, total=None):
         """Field forward (encode + MLPs in one launch) over the listed samples
-        eval_idx[:eval_total]; the pair-major encoding kept for the backward."""
+        idx[:total] (default eval_idx[:eval_total]); the pair-major encoding
+        kept for the backward."""
+        idx = self.eval_idx if idx is None else idx
+        total = self.eval_total if total is None else total
         self._ev("hash_encode", 0)
-        vren._ok(HG._lib().ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.eval_total),
-                                                _p(self.eval_idx), HG.ctypes.byref(self.grid.desc),
+        vren._ok(HG._lib().ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, _p(total),
+                                                _p(idx), HG.ctypes.byref(self.grid.desc),
                                                 _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc),
                                                 _p(self.sigmas), _p(self.rgbs), None, s), "field_encode_mlp")
         self._ev("hash_encode", 1)

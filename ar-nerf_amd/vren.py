@@ -75,6 +75,7 @@ def _declare(L):
         "ngp_chunk_counts": [vp, c_int64, c_int, vp, vp, c_float, vp, vp],
         "ngp_chunk_counts_range": [vp, c_int64, c_int, c_int, vp, vp, c_float, vp, vp],
         "ngp_ray_segments": [vp, vp, c_int64, c_int, vp, vp, vp, vp, vp],
+        "ngp_chunk_segments": [vp, vp, vp, c_int64, c_int, c_int, c_float, vp, vp, vp, vp, vp, vp],
         "ngp_ray_segments_capped": [vp, c_int64, c_int, vp, vp, vp, vp, vp],
         "ngp_adam_step": [vp, vp, vp, vp, vp, c_int64, c_float, c_float, c_float, c_float, c_int64, c_float, c_int,
                           vp],
@@ -99,6 +100,8 @@ def _declare(L):
     L.ngp_occupancy_sorted_workspace.restype = ctypes.c_size_t
     L.ngp_occupied_cells_workspace.argtypes = [c_int64]
     L.ngp_occupied_cells_workspace.restype = ctypes.c_size_t
+    L.ngp_chunk_segments_workspace.argtypes = [c_int64]
+    L.ngp_chunk_segments_workspace.restype = ctypes.c_size_t
     L.ngp_render_test_capacity.argtypes = [c_int64, c_int]
     L.ngp_render_test_capacity.restype = c_int64
     L.ngp_guard_hits.argtypes = []

@@ -127,6 +127,9 @@ def parse():
     ap.add_argument("--quality-steps", type=int, default=30000,
                     help="test-PSNR check after the reference schedule (scripts/quality_30k.py: product defaults vs "
                          "exact mode, each in a child process; 0: skip)")
+    ap.add_argument("--no-oracle-quality", action="store_true",
+                    help="skip the test-PSNR check against the fp32-oracle fixtures (tests/golden/make_quality.py: "
+                         "2000 steps of the reference's schedule on a small problem, product defaults and exact mode)")
     ap.add_argument("--infer-frames", type=int, default=20, help="timed full-frame test renders (0: skip)")
     ap.add_argument("--infer-res", type=int, default=800)
     return ap.parse_args()
@@ -214,6 +217,36 @@ def inference_bench(trainer, res, frames, world, rank):
             "host_loop_ms_per_frame": round(t_host * 1e3, 3), "host_loop_bit_exact": same,
             "workload": "full-frame test render of the trained model (black bg), march+field+composite per "
                         "iteration in HIP graphs (16 iterations, then 8 per replay while rays remain), one host sync per graph"}
+
+
+def oracle_quality():
+    """J1 (north_star "PSNR within 0.2 dB of reference"): the product trained
+    on the fp32-oracle fixture problem (tests/golden/make_quality.py: the
+    reference's training-loop glue on the CPU oracle, 2000 steps of 2048 rays,
+    same scene / init / batches), defaults and exact mode, against the
+    committed fixtures: the oracle with the reference's fp16 tcnn-module
+    boundary (gradients rounded to fp16 unscaled there, as tinycudann's torch
+    modules do) and with that boundary in fp32 (the product's precision).
+    Fixtures are data (JSON); the oracle itself does not run here."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_quality as MQ
+
+    def fx(name):
+        p = os.path.join(ROOT, "tests", "golden", name)
+        return json.load(open(p))["test_psnr"] if os.path.exists(p) else None
+    ref = [v for v in (fx("quality_oracle.json"), fx("quality_oracle_occ1.json"), fx("quality_oracle_occ2.json"))
+           if v is not None]
+    f32 = fx("quality_oracle_f32out.json")
+    out = {"oracle_fp32_boundary": f32, "oracle_reference_precision": ref, "steps": MQ.CFG["epochs"] *
+           MQ.CFG["steps_per_epoch"], "problem": "analytic scene 100x100, 20 train / 4 test views, 2048-ray batches"}
+    for mode, kw in (("default", {}), ("exact", dict(chunk_first=0, hash_backward="atomic"))):
+        r = MQ.product_run("cuda", **kw)
+        out[f"product_{mode}"] = r["test_psnr"]
+        if f32 is not None:
+            out[f"delta_{mode}_vs_fp32_boundary_db"] = round(r["test_psnr"] - f32, 3)
+        if ref:
+            out[f"delta_{mode}_vs_reference_precision_db"] = round(r["test_psnr"] - max(ref), 3)
+    return out
 
 
 def cpu_model():
@@ -449,6 +482,9 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "scripts"))
         import quality_30k
         quality = quality_30k.run(steps=args.quality_steps)
+    oracle_q = None
+    if rank == 0 and world == 1 and not args.no_oracle_quality:
+        oracle_q = oracle_quality()
     if rank == 0:
         out = {
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
@@ -481,6 +517,7 @@ def main():
                                f"streams; roofline: see roofline.measured"),
             "cpu_baseline": cpu,
             "quality": quality,
+            "quality_vs_fp32_oracle": oracle_q,
             "inference": infer,
         }
         print(json.dumps(out), flush=True)

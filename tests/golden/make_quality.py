@@ -138,12 +138,43 @@ def load_fixture():
         return json.load(f)
 
 
+def _patch_f32_outputs(O):
+    """tinycudann's torch modules return fp16 (tcnn's output precision), so in
+    the reference the gradients the glue hands back to them -- dL/dh from
+    TruncExp (custom_functions.py:162-173, computed in fp32 under autocast and
+    cast back across the fp16 output) and dL/drgb from VolumeRenderer -- are
+    rounded to fp16 without a loss scale (tcnn applies its scale inside its
+    own backward), flushing magnitudes below 2^-24 to zero.  This variant
+    returns the same VALUES (fp16-rounded) as fp32 tensors, so those
+    gradients stay fp32: the precision the product's MLP backward keeps
+    (per-sample scaled fp16).  On the CPU (no autocast) TruncExp then also
+    runs in fp32, as it does on the GPU."""
+    T = O.tcnn_stub
+
+    def nwe_forward(self, x01):
+        Ws, _ = O.mlp_layers(self.params[:self.n_mlp], self.dims)
+        enc = O._HashEncodeFn.apply(self.params[self.n_mlp:], x01.float().contiguous(), self.spec, self._mn, self._mx)
+        return O.mlp_forward(enc, Ws)
+
+    def net_forward(self, x):
+        Ws, _ = O.mlp_layers(self.params, self.dims)
+        out = O.mlp_forward(x.float(), Ws)[:, :self.n_out]
+        if self.act == "Sigmoid":
+            out = O.rh(torch.sigmoid(out))
+        return out
+    T.NetworkWithInputEncoding.forward = nwe_forward
+    T.Network.forward = net_forward
+
+
 def main():
     import hashgrid as HG  # (the product's init: before the stubs replace `vren`)
     flat = HG.init_params(HG.HashGrid(CFG["scale"]), seed=CFG["init_seed"], device="cpu")
     import make_golden as MG
     MG.install_stubs()
     import oracle as O
+    f32_out = os.environ.get("TCNN_OUT", "f16") == "f32"
+    if f32_out:  # (variant) the tcnn modules hand fp32 outputs to the glue: no fp16 rounding of dL/dh, dL/drgb
+        _patch_f32_outputs(O)
     vren = sys.modules["vren"]
     from losses import NeRFLoss
     from models.networks import NGP
@@ -217,7 +248,9 @@ def main():
            "occupied_cells": int((model.density_grid > 0).sum()),
            "cpu_threads": nthreads, "wall_s": round(time.time() - t0, 1), "occ_seed": occ,
            "what": "reference train.py loop glue + oracle fp32-autograd kernels (make_quality.py)"}
-    path = os.path.join(HERE, "quality_oracle.json" if occ == 0 else f"quality_oracle_occ{occ}.json")
+    out["tcnn_out"] = "f32" if f32_out else "f16"
+    name = "quality_oracle" + ("" if occ == 0 else f"_occ{occ}") + ("_f32out" if f32_out else "")
+    path = os.path.join(HERE, name + ".json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps({k: out[k] for k in ("test_psnr", "test_psnr_views", "wall_s")}))

@@ -355,3 +355,51 @@ def test_ray_segments_lists(n_rows):
     st, total, idx = expect(torch.clamp(N, max=K), 0)
     assert torch.equal(st_ws.cpu(), st) and int(tot) == total
     assert torch.equal(sidx[:total].cpu().long(), idx)
+
+
+@pytest.mark.parametrize("n_rows,first,last", [(1, 64, 0), (63, 64, 0), (8192, 64, 0), (8193, 5, 0), (8192, 100, 150),
+                                               (70000, 64, 0)])
+def test_chunk_segments_equals_counts_then_segments(n_rows, first, last):
+    """ngp_chunk_segments (one launch: round-2 counts + look-back scan + map)
+    equals ngp_chunk_counts_range followed by ngp_ray_segments: start
+    offsets, total, accumulator and the index list, bit for bit -- three
+    launches in a row on one workspace (the ticket / generation reset), incl.
+    grids larger than the GPU holds at once (70000 rows: 1094 blocks) and
+    rows longer than one 64-sample chunk (first 100)."""
+    import ctypes
+    L = vren.lib()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    g = torch.Generator().manual_seed(n_rows + first)
+    N = torch.randint(0, 260, (n_rows,), generator=g)
+    N[torch.rand(n_rows, generator=g) < 0.2] = 0
+    start = torch.cumsum(N, 0) - N
+    n_s = int(N.sum()) + 1
+    rays_a = torch.stack([torch.arange(n_rows), start, N], 1).to(DEV)
+    dense = torch.rand(n_rows, generator=g) < 0.5  # rows terminating in the first chunk vs transparent ones
+    row = torch.repeat_interleave(torch.arange(n_rows), N)
+    sig = torch.rand(n_s, generator=g) * 2
+    sig[:-1] *= torch.where(dense[row], 50.0, 1.0)
+    sig = sig.to(DEV)
+    dl = (torch.rand(n_s, generator=g) * 0.02).to(DEV)
+    cnt = torch.empty(n_rows, dtype=torch.int32, device=DEV)
+    vren._ok(L.ngp_chunk_counts_range(p(rays_a), n_rows, first, last, p(sig), p(dl), ctypes.c_float(1e-4), p(cnt),
+                                      vren._stream()), "counts")
+    st_ref = torch.empty(n_rows, dtype=torch.int64, device=DEV)
+    tot_ref, acc_ref = torch.zeros(1, dtype=torch.int64, device=DEV), torch.full((1,), 7, dtype=torch.int64, device=DEV)
+    idx_ref = torch.full((n_s,), -1, dtype=torch.int32, device=DEV)
+    vren._ok(L.ngp_ray_segments(p(cnt), p(rays_a), n_rows, first, p(st_ref), p(tot_ref), p(acc_ref), p(idx_ref),
+                                vren._stream()), "segments")
+    ws = torch.zeros((L.ngp_chunk_segments_workspace(n_rows) + 7) // 8, dtype=torch.int64, device=DEV)
+    acc = torch.full((1,), 7, dtype=torch.int64, device=DEV)
+    for it in range(3):
+        st = torch.full((n_rows,), -5, dtype=torch.int64, device=DEV)
+        tot = torch.zeros(1, dtype=torch.int64, device=DEV)
+        idx = torch.full((n_s,), -1, dtype=torch.int32, device=DEV)
+        vren._ok(L.ngp_chunk_segments(p(sig), p(dl), p(rays_a), n_rows, first, last, ctypes.c_float(1e-4), p(ws),
+                                      p(st), p(tot), p(acc), p(idx), vren._stream()), "chunk_segments")
+        torch.cuda.synchronize()
+        T = int(tot_ref)
+        assert int(tot) == T and int(acc) == 7 + (it + 1) * T
+        assert torch.equal(st, st_ref) and torch.equal(idx[:T], idx_ref[:T])
+    if n_rows >= 1000:  # some rows terminate inside the first chunk, some go on
+        assert 0 < int(tot_ref) < int(N.sum())
