@@ -1,0 +1,18 @@
+# Garden-shaped (BASELINE config 4 shape) bench variants: gpurun -- bash scripts/ab_garden.sh TAG REPS "flagsA" "flagsB" ...
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=$1; REPS=$2; shift 2
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+for rep in $(seq 1 $REPS); do
+  i=0
+  for flags in "$@"; do
+    i=$((i+1))
+    timeout -k 10 300 python -u bench.py --scale 16 --batch 16384 --steps 300 --warmup 10 --no-cpu-baseline --quality-steps 0 \
+        --psnr-views 0 --infer-frames 0 --no-oracle-quality --breakdown-steps 20 $flags > "$OUT/v${i}_$rep.json" 2> "$OUT/v${i}_$rep.err"
+    python3 -c "
+import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d['kernels']
+print('v'+sys.argv[2], sys.argv[3], round(d['value']/1e6,3), 'M rays/s', round(d['ms_per_step']*1e3,1), 'us/step', ' '.join(f'{n}={k[n][\"ms_per_step\"]*1e3:.0f}' for n in ('hash_write','hash_accum','hash_bwd_coarse','mlp_bwd','hash_encode') if n in k))" "$OUT/v${i}_$rep.json" "$i" "[$flags]"
+  done
+done

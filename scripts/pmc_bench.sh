@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 RE=${1:-field_fwd}
 OUT=gpurun_out/pmc_${2:-run}
 mkdir -p "$OUT"
-BENCH="python3 bench.py --steps 10 --warmup 2 --psnr-views 0 --no-cpu-baseline --infer-frames 0 --quality-steps 0"
+BENCH="python3 bench.py --steps 10 --warmup 2 --psnr-views 0 --no-cpu-baseline --infer-frames 0 --quality-steps 0 --no-oracle-quality"
 pass() {
     name=$1; shift
     timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$RE" -d "$OUT/$name" -o run -f csv -- $BENCH > "$OUT/$name.log" 2>&1
@@ -23,5 +23,6 @@ want sqw && pass sqw SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACT
 want sq && pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA
 want tcp && pass tcp TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_LATENCY_sum
 want wrq && pass wrq TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum WRITE_SIZE
-want enc && pass enc TA_TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_avr TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE
+want enc && pass enc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE
 want lds && pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT
+true
