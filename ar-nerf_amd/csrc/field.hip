@@ -692,6 +692,12 @@ __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& 
 // same fp16 values re-scaled to one power of two per layer and block
 // (tcnn's fp16 operands with the role of its loss scale, no global scale to
 // tune).
+// (diagnostics only: scripts/diag/mlpbwd_phases.hip defines these to stamp the
+// phases of a block iteration and the kernel's edges; empty in the product build)
+#ifndef NGP_BWD_PHASE
+#define NGP_BWD_PHASE(k)
+#define NGP_BWD_EDGE(k)
+#endif
 constexpr int CW = 8, NT1 = 19, NT2 = 11, CSCRW = NT1 * TTILE;
 constexpr int COOP_LDS_HALFS = SCR + CW * CSCRW;
 static_assert(NGP_MLP_PARAMS <= CW * CSCRW && NT2 <= NT1, "raw weight staging / phase-2 tiles exceed the scratch");
@@ -777,11 +783,13 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
     __shared__ int emin[2][5][CW];
     _Float16* sw = smem;
     _Float16* scr = smem + SCR;
+    NGP_BWD_EDGE(0);
     stage_raw_weights(mlp, scr);  // (the scratch is free until the loop)
     __syncthreads();
     load_fwd_weights(scr, sw, true);
     load_bwd_weights(scr, sw);
     __syncthreads();
+    NGP_BWD_EDGE(1);
     const int64_t N = n_dev ? *n_dev : n;
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -825,6 +833,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         In nxt;
         load_in(i_next, nxt);
         i_next = row_index(base + s + 2 * stride);
+        NGP_BWD_PHASE(0);
         const int64_t j = base + s;
         const bool valid = j < N;
         const h8 e = cur.e;
@@ -836,6 +845,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         const h4 shh = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3]};
         h4 h3[4], h4v[4];
         const h4 o = color_net(pack(shh, hh), sw, s, g, h3, h4v);
+        NGP_BWD_PHASE(1);
         // ---- output layer: sigmoid backward on rows 0..2
         f4 dout = z;
         if (g == 0) {
@@ -915,6 +925,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
                 if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
             }
         }
+        NGP_BWD_PHASE(2);
         cur = nxt;
         // ---- weight gradients: fp16 operands (tcnn's precision), K = samples.  The G
         // (gradient) tiles of a layer are re-scaled from their per-sample exponent E_s
@@ -930,6 +941,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
             for (int l = 0; l < 5; ++l) emin[par][l][wid] = wmin[l];
         }
         __syncthreads();  // every wave's phase-2 reads of the previous iteration are done; emin[par] complete
+        NGP_BWD_PHASE(3);
         uint32_t fac[5];
         int Bl[5];
 #pragma unroll
@@ -951,8 +963,10 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         put_tile(mine + P_C * TTILE, shh, s, g);
         put_tile(mine + (P_C + 1) * TTILE, hh, s, g);
         __syncthreads();
+        NGP_BWD_PHASE(4);
         coop_dw<4>(scr, wid, s, g, coop_n1(wid), coop_k1, acc1, Bl);
         __syncthreads();  // phase-1 reads done: the regions take the phase-2 tiles
+        NGP_BWD_PHASE(5);
         // ---- phase 2 (layers 2, 1)
         put_tile(mine + Q_DH * TTILE, mul_h4(dhh, fac[3]), s, g);
 #pragma unroll
@@ -963,13 +977,16 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j
         put_tile_pair(mine + (Q_E + (g >> 1)) * TTILE, h4{e[0], e[1], e[2], e[3]}, h4{e[4], e[5], e[6], e[7]}, s, g & 1);
         __syncthreads();
+        NGP_BWD_PHASE(6);
         coop_dw<2>(scr, wid, s, g, coop_n2(wid), coop_k2, acc2, Bl);
+        NGP_BWD_PHASE(7);
     }
     // each output tile lives in exactly one wave of the block: one global add
     // per weight.  Wave w of every block owns the same tiles, so the adds of a
     // lane start at a block-dependent rotation (same-address adds serialise at
     // the memory-side atomic unit: 12 -> 7 us per launch; per-block partial
     // rows + a reduction launch measured slower).
+    NGP_BWD_EDGE(2);
     const int n1 = coop_n1(wid), nadd = 4 * (n1 + coop_n2(wid));
     const int rot = (int)(blockIdx.x % (unsigned)nadd);
 #pragma unroll 1
@@ -985,6 +1002,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         const int w = ow + (o0 + 4 * g + r) * in_dim + i0 + s;
         atomicAdd(&grad_mlp[w], v);
     }
+    NGP_BWD_EDGE(3);
 }
 
 
