@@ -231,25 +231,27 @@ __device__ __forceinline__ int P32inv(int i) { return i < 16 ? 8 * (i >> 2) + (i
 // 16-byte loads of the row-major buffer, each half scattered to its permuted
 // LDS position (8 consecutive halfs share one row) -- no 20 KB raw staging
 // buffer, so the MLP-only forward fits more blocks per CU.
+// the 8 halfs v of the row-major buffer at flat index i0 (a multiple of 8) into
+// the forward image: their row, each column at its permuted position
+__device__ __forceinline__ void place_fwd8(int i0, h8 v, _Float16* sw) {
+    int row, col0;  // destination row start, and the first column
+    bool p64 = false, p32 = false;
+    if (i0 < OW2) { row = SW1 + (i0 >> 5) * R32; col0 = i0 & 31; }
+    else if (i0 < OW3) { row = SW2 + ((i0 - OW2) >> 6) * R64; col0 = (i0 - OW2) & 63; p64 = true; }
+    else if (i0 < OW4) { row = SW3 + ((i0 - OW3) >> 5) * R32; col0 = (i0 - OW3) & 31; p32 = true; }
+    else if (i0 < OW5) { row = SW4 + ((i0 - OW4) >> 6) * R64; col0 = (i0 - OW4) & 63; p64 = true; }
+    else { row = SW5 + ((i0 - OW5) >> 6) * R64; col0 = (i0 - OW5) & 63; p64 = true; }
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        const int col = col0 + jj;
+        sw[row + (p64 ? P64inv(col) : p32 ? P32inv(col) : col)] = v[jj];
+    }
+}
+
 __device__ __forceinline__ void load_fwd_weights_direct(const _Float16* __restrict__ mlp, _Float16* sw, bool color) {
     const h8* src = reinterpret_cast<const h8*>(mlp);
     const int nv = (color ? NGP_MLP_PARAMS : OW3) / 8;
-    for (int c = threadIdx.x; c < nv; c += blockDim.x) {
-        const h8 v = src[c];
-        const int i0 = 8 * c;
-        int row, col0;  // destination row start, and the first column
-        bool p64 = false, p32 = false;
-        if (i0 < OW2) { row = SW1 + (i0 >> 5) * R32; col0 = i0 & 31; }
-        else if (i0 < OW3) { row = SW2 + ((i0 - OW2) >> 6) * R64; col0 = (i0 - OW2) & 63; p64 = true; }
-        else if (i0 < OW4) { row = SW3 + ((i0 - OW3) >> 5) * R32; col0 = (i0 - OW3) & 31; p32 = true; }
-        else if (i0 < OW5) { row = SW4 + ((i0 - OW4) >> 6) * R64; col0 = (i0 - OW4) & 63; p64 = true; }
-        else { row = SW5 + ((i0 - OW5) >> 6) * R64; col0 = (i0 - OW5) & 63; p64 = true; }
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            const int col = col0 + jj;
-            sw[row + (p64 ? P64inv(col) : p32 ? P32inv(col) : col)] = v[jj];
-        }
-    }
+    for (int c = threadIdx.x; c < nv; c += blockDim.x) place_fwd8(8 * c, src[c], sw);
 }
 
 // Density net on one column block: returns h (rows 4g+r of sample s) and
@@ -586,6 +588,36 @@ __device__ __forceinline__ void load_bwd_weights(const _Float16* __restrict__ ml
     for (int e = t; e < 32 * 64; e += nt) { const int i = e >> 6, o = e & 63; sw[BT1 + i * RT64 + o] = mlp[OW1 + o * 32 + i]; }
 }
 
+// The backward's weight images (load_fwd_weights + load_bwd_weights) straight
+// from global memory in one pass: a thread item is two rows (o, o+1) x 8
+// columns of one matrix, two 16-byte loads; the forward image takes each half
+// at its permuted position, the transposed matrices a 4-byte pair {W[o][i],
+// W[o+1][i]} per column (no raw staging buffer, no barrier between the
+// passes: 6.4 -> ~3 us per block, scripts/diag/mlpbwd_phases.py).
+__device__ __forceinline__ void load_bwd_weights_direct(const _Float16* __restrict__ mlp, _Float16* sw) {
+    // items: W1 32 row pairs x 4 column blocks, W2 8 x 8, W3 32 x 4, W4 32 x 8, W5 8 x 8
+    constexpr int N1 = 128, N2 = 64, N3 = 128, N4 = 256, N5 = 64, NI = N1 + N2 + N3 + N4 + N5;
+    for (int it = threadIdx.x; it < NI; it += blockDim.x) {
+        int ow, lg_cb, li, bt, rt, skip;  // matrix offset, log2(column blocks), local item, bwd image, row, skipped cols
+        if (it < N1) { ow = OW1; lg_cb = 2; li = it; bt = BT1; rt = RT64; skip = 0; }
+        else if (it < N1 + N2) { ow = OW2; lg_cb = 3; li = it - N1; bt = BT2; rt = RT16; skip = 0; }
+        else if (it < N1 + N2 + N3) { ow = OW3; lg_cb = 2; li = it - N1 - N2; bt = BT3; rt = RT64; skip = 16; }
+        else if (it < NI - N5) { ow = OW4; lg_cb = 3; li = it - N1 - N2 - N3; bt = BT4; rt = RT64; skip = 0; }
+        else { ow = OW5; lg_cb = 3; li = it - (NI - N5); bt = BT5; rt = RT16; skip = 0; }
+        const int in_dim = 8 << lg_cb, o = 2 * (li >> lg_cb), i0 = 8 * (li & ((1 << lg_cb) - 1));
+        const int f0 = ow + o * in_dim + i0;
+        const h8 a = *reinterpret_cast<const h8*>(mlp + f0);
+        const h8 b = *reinterpret_cast<const h8*>(mlp + f0 + in_dim);
+        place_fwd8(f0, a, sw);
+        place_fwd8(f0 + in_dim, b, sw);
+        if (i0 >= skip) {  // (W3: only the h columns 16..31 are transposed)
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj)
+                *reinterpret_cast<h2v*>(sw + bt + (i0 - skip + jj) * rt + o) = h2v{a[jj], b[jj]};
+        }
+    }
+}
+
 __device__ __forceinline__ float max4(f4 v) { return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))); }
 // Per-sample power-of-two scales of the data chain: a gradient tile travels in
 // fp16 as value x 2^E, E per sample (the same in its four lanes), chosen from
@@ -784,10 +816,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
     _Float16* sw = smem;
     _Float16* scr = smem + SCR;
     NGP_BWD_EDGE(0);
-    stage_raw_weights(mlp, scr);  // (the scratch is free until the loop)
-    __syncthreads();
-    load_fwd_weights(scr, sw, true);
-    load_bwd_weights(scr, sw);
+    load_bwd_weights_direct(mlp, sw);
     __syncthreads();
     NGP_BWD_EDGE(1);
     const int64_t N = n_dev ? *n_dev : n;
