@@ -478,6 +478,10 @@ __device__ __forceinline__ void adam4(const AdamArgs& a, size_t base, uint32_t e
                bc2);
 }
 
+// (diagnostics only: scripts/diag/accum_phases.hip stamps an item's phases; empty in the product build)
+#ifndef NGP_ACC_PHASE
+#define NGP_ACC_PHASE(k)
+#endif
 template <bool FUSED = false>
 __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
                                                           float* __restrict__ grad, BinWs ws, AdamArgs adam,
@@ -490,6 +494,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
     float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
     if (FUSED) adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
     for (uint32_t it = ws.items[b_lo] + blockIdx.x; it < total; it += gridDim.x) {
+        NGP_ACC_PHASE(0);
         uint32_t lo = b_lo, hi = b_hi;  // bucket b: items[b] <= it < items[b + 1]
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -504,6 +509,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         const bool own = nch == 1 && !overflow && ws.fb[b] == 0;
         const bool fz = FUSED && nch == 1 && !overflow;  // fused_bucket
         const bool flagged = ws.fb[b] != 0;               // direct adds in the range
+        NGP_ACC_PHASE(1);
         // A fused bucket's Adam state (p, m, v of the range) is loaded before
         // the records are summed, so its HBM latency hides behind the LDS
         // accumulation instead of following it (the flush then only computes
@@ -525,6 +531,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         for (uint32_t e = t; e < 2 * BENT / 2; e += blockDim.x)
             reinterpret_cast<double2*>(img)[e] = make_double2(0.0, 0.0);
         __syncthreads();
+        NGP_ACC_PHASE(2);
         const uint32_t r0 = ws.rstart[b] + c * CH, r1 = min(ws.rstart[b + 1], r0 + CH);
         constexpr int U = FUSED ? 2 : 4;  // records in flight per thread (FUSED: registers hold the Adam state)
         // software-pipelined: the next iteration's records are loaded before
@@ -586,6 +593,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
             for (int u = 0; u < U; ++u) v[u] = vn[u];
         }
         __syncthreads();
+        NGP_ACC_PHASE(3);
         float* g = grad + gbase;
         // entries 2e, 2e+1 x features 0, 1 -> grad[4e .. 4e+3]
         auto image4 = [&](uint32_t e) {
@@ -631,6 +639,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
             }
         }
         __syncthreads();
+        NGP_ACC_PHASE(4);
     }
     if (FUSED) {  // buckets without records: Adam with a zero gradient (moments still decay)
         for (uint32_t b = b_lo + blockIdx.x; b < b_hi; b += gridDim.x) {
