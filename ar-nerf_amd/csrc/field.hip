@@ -485,6 +485,10 @@ __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restric
 // rows and runs the MLPs on four 16-sample column blocks read back in the
 // MFMA B layout -- the separate MLP launch (its fixed cost, the encoding's
 // re-read) disappears and the MLP math overlaps other waves' gathers.
+// (diagnostics only: scripts/diag/fem_phases.hip stamps each wave's phases; empty in the product build)
+#ifndef NGP_FEM_PHASE
+#define NGP_FEM_PHASE(k)
+#endif
 constexpr int XROW = 40;  // halfs per parked encoding row (32 + pad: conflict-free 16-B reads)
 constexpr int FEM_WAVES = 8;  // 512-thread blocks: the 24 KB weight image shared by 8 waves (4 waves/SIMD)
 template <bool COLOR>
@@ -511,6 +515,7 @@ __global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const 
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x + wv * 64; base < N; base += stride) {
         const int64_t j = base + lane;
         const bool valid = j < N;
+        NGP_FEM_PHASE(0);
         const int64_t i = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
         float in[3];
         load_x01(xyzs, i, valid, ga, in);
@@ -526,6 +531,7 @@ __global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const 
             *reinterpret_cast<h4*>(row + 4 * pr) = e4;
         }
         xi[wv][lane] = valid ? (int32_t)i : -1;
+        NGP_FEM_PHASE(1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -556,6 +562,7 @@ __global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const 
                 }
             }
         }
+        NGP_FEM_PHASE(2);
         __builtin_amdgcn_wave_barrier();  // this iteration's LDS reads before the next one's writes (in order per wave)
     }
 }

@@ -1,6 +1,7 @@
 # Alternating A/B/n of bench configurations, each "lib::flags" with lib = "" (the tree's
-# ar-nerf_amd/lib/libngp_amd.so) or "base" (ar-nerf_amd/lib_base/libngp_amd.so, built by
-# scripts/build_base_lib.sh or by hand from a variant of the sources).
+# ar-nerf_amd/lib/libngp_amd.so), "base" (ar-nerf_amd/lib_base/libngp_amd.so, built by
+# scripts/build_base_lib.sh or by hand from a variant of the sources) or another directory
+# name under ar-nerf_amd/ holding a variant's libngp_amd.so.
 # gpurun -- bash scripts/ab_lib.sh TAG REPS "::" "base::" "::--no-defer-color" ...
 set -e
 cd "$GRAFT_REPO_ROOT"
@@ -13,7 +14,9 @@ for rep in $(seq 1 $REPS); do
   for cfg in "$@"; do
     i=$((i+1))
     lib=${cfg%%::*}; flags=${cfg#*::}
-    if [ "$lib" = base ]; then LIB=ar-nerf_amd/lib_base/libngp_amd.so; else LIB=ar-nerf_amd/lib/libngp_amd.so; fi
+    if [ "$lib" = base ]; then LIB=ar-nerf_amd/lib_base/libngp_amd.so
+    elif [ -n "$lib" ]; then LIB=ar-nerf_amd/$lib/libngp_amd.so
+    else LIB=ar-nerf_amd/lib/libngp_amd.so; fi
     NGP_AMD_LIB=$PWD/$LIB timeout -k 10 200 python -u bench.py --steps 1000 --warmup 10 --no-cpu-baseline \
         --quality-steps 0 --no-oracle-quality --psnr-views 0 --infer-frames 0 --breakdown-steps 20 $flags \
         > "$OUT/v${i}_$rep.json" 2> "$OUT/v${i}_$rep.err"
