@@ -117,8 +117,9 @@ def parse():
                          "the xGMI transfers (only shard 0 is stepped: a timing mode)")
     ap.add_argument("--pair-steps", action="store_true",
                     help="two consecutive steady-state steps per graph replay (trainer pair_steps)")
-    ap.add_argument("--bin-merge-hi", type=int, default=0,
-                    help="binned levels below this merge runs of equal corner pairs along a ray")
+    ap.add_argument("--bin-merge-hi", type=int, default=None,
+                    help="binned levels below this merge runs of equal corner pairs along a ray (default: "
+                         "trainer's, 11 / 0 for cascaded scenes)")
     ap.add_argument("--bin-samples-per-ray", type=int, default=None,
                     help="binned hash-backward workspace per ray (default: trainer's, 128 / 512 for cascaded scenes)")
     ap.add_argument("--erode", default="auto", choices=["auto", "on", "off"],
@@ -503,6 +504,7 @@ def main():
                        "chunk_first": trainer.chunk_first,
                        "parallelism": f"dp{world}" + (f" (data-parallel step of world {args.emulate_dp} emulated: collectives as local copies)" if args.emulate_dp else ""), "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
+                       "bin_merge_hi": trainer.bin_merge_hi,
                        "erode": trainer.erode,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
             "roofline": roof,
