@@ -439,10 +439,22 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         float4 M = reinterpret_cast<float4*>(m)[i], V = reinterpret_cast<float4*>(v)[i];
         const int64_t j = i - rep_lo4;
         if (rep && j >= 0 && j < rep4) {  // gradient replicas (ngp_hash_backward_levels_rep), folded in order
+            // (the first 8 replicas' loads all issued before any is summed or cleared: one round trip)
             float4* r4 = reinterpret_cast<float4*>(rep);
-            for (int r = 0; r < nrep; ++r) {
-                const float4 b = r4[r * rep4 + j];
-                Gd.x += b.x; Gd.y += b.y; Gd.z += b.z; Gd.w += b.w;
+            constexpr int RB = 8;
+            float4 b[RB];
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+                if (r < nrep) b[r] = r4[r * rep4 + j];
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+                if (r < nrep) { Gd.x += b[r].x; Gd.y += b[r].y; Gd.z += b[r].z; Gd.w += b[r].w; }
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+                if (r < nrep) r4[r * rep4 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = RB; r < nrep; ++r) {
+                const float4 c = r4[r * rep4 + j];
+                Gd.x += c.x; Gd.y += c.y; Gd.z += c.z; Gd.w += c.w;
                 r4[r * rep4 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
