@@ -68,6 +68,7 @@ constexpr int MAXB = 2048;                       // buckets over all levels
 constexpr int TILE = 256;                        // samples per count/write tile
 constexpr int RPT = TILE * 4 / 256;              // records per thread per level
 constexpr uint32_t CH = 32768;                   // records per pass-5 chunk
+constexpr uint32_t IB_CAP = 8192;                // items with a direct item -> bucket entry
 constexpr uint32_t F_C0 = 1u << 28;              // record carries corner x only (pair split)
 constexpr uint32_t F_SINGLE = 1u << 29;          // record {i0 | F_SINGLE, g0, g1, 0}: one entry, summed run
 
@@ -83,6 +84,7 @@ struct BinWs {
     uint32_t* tot;     // [MAXB] records per bucket
     uint32_t* rstart;  // [MAXB + 1] bucket region starts
     uint32_t* items;   // [MAXB + 1] chunk prefix
+    uint32_t* ib;      // [IB_CAP] item -> its bucket (the accumulation's lookup; binary search beyond)
     uint32_t* ofs;     // [NSLOT][tiles_cap] counts, then exclusive offsets over tiles
     uint4* rec;        // [tiles_cap * TILE * 4 * L]
 };
@@ -91,7 +93,8 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static size_t bin_ws_bytes(int64_t tiles, BinWs* w, void* base) {
     const size_t o_fb = 0, o_tot = align256((MAXB + 1) * 4), o_rs = o_tot + align256(MAXB * 4),
-                 o_it = o_rs + align256((MAXB + 1) * 4), o_ofs = o_it + align256((MAXB + 1) * 4);
+                 o_it = o_rs + align256((MAXB + 1) * 4), o_ib = o_it + align256((MAXB + 1) * 4),
+                 o_ofs = o_ib + align256(IB_CAP * 4);
     const size_t o_rec = align256(o_ofs + (size_t)tiles * NSLOT * 4);
     const size_t total = o_rec + (size_t)tiles * TILE * 4 * L * sizeof(uint4);
     if (w) {
@@ -100,6 +103,7 @@ static size_t bin_ws_bytes(int64_t tiles, BinWs* w, void* base) {
         w->tot = reinterpret_cast<uint32_t*>(b + o_tot);
         w->rstart = reinterpret_cast<uint32_t*>(b + o_rs);
         w->items = reinterpret_cast<uint32_t*>(b + o_it);
+        w->ib = reinterpret_cast<uint32_t*>(b + o_ib);
         w->ofs = reinterpret_cast<uint32_t*>(b + o_ofs);
         w->rec = reinterpret_cast<uint4*>(b + o_rec);
     }
@@ -269,6 +273,9 @@ __global__ void __launch_bounds__(MAXB / 2) hash_plan_kernel(uint32_t nbt, BinWs
     ws.items[b0 + 1] = c[t] - c1;
     ws.items[b1 + 1] = c[t];
     if (t == 0) { ws.rstart[0] = 0; ws.items[0] = 0; }
+    // item -> bucket table (one entry per chunk; usually one chunk per bucket)
+    for (uint32_t it = c[t] - c1 - c0; it < c[t] - c1 && it < IB_CAP; ++it) ws.ib[it] = b0;
+    for (uint32_t it = c[t] - c1; it < c[t] && it < IB_CAP; ++it) ws.ib[it] = b1;
 }
 
 // MODE bits: 2 = store each record from registers at its rank (the product
@@ -496,9 +503,13 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
     for (uint32_t it = ws.items[b_lo] + blockIdx.x; it < total; it += gridDim.x) {
         NGP_ACC_PHASE(0);
         uint32_t lo = b_lo, hi = b_hi;  // bucket b: items[b] <= it < items[b + 1]
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (ws.items[mid] <= it) lo = mid; else hi = mid;
+        if (it < IB_CAP) {  // (the plan's item -> bucket table: one load, not a dependent search)
+            lo = ws.ib[it];
+        } else {
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (ws.items[mid] <= it) lo = mid; else hi = mid;
+            }
         }
         const uint32_t b = lo, c = it - ws.items[b], nch = ws.items[b + 1] - ws.items[b];
         int l = 0;
