@@ -505,20 +505,36 @@ __global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const 
     __shared__ __attribute__((aligned(16))) _Float16 xs[FEM_WAVES][64 * XROW];
     __shared__ int32_t xi[FEM_WAVES][64];
     __shared__ LevelLds lv;
-    load_fwd_weights_direct(mlp, sw, COLOR);
-    load_levels(ga, lv);
-    __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, s = lane & 15, g = lane >> 4;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    // the first iteration's index and position (count -> index -> position:
+    // dependent round trips) are requested before the weight image is built,
+    // so the two overlap (most waves run one iteration)
+    int64_t i_first = 0;
+    float in_first[3];
+    {
+        const int64_t j = (int64_t)blockIdx.x * blockDim.x + wv * 64 + lane;
+        const bool valid = j < N;
+        i_first = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
+        load_x01(xyzs, i_first, valid, ga, in_first);
+    }
+    load_fwd_weights_direct(mlp, sw, COLOR);
+    load_levels(ga, lv);
+    __syncthreads();
+    bool first = true;
     // wave-uniform trip count (the MFMAs need every lane)
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x + wv * 64; base < N; base += stride) {
         const int64_t j = base + lane;
         const bool valid = j < N;
         NGP_FEM_PHASE(0);
-        const int64_t i = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
-        float in[3];
-        load_x01(xyzs, i, valid, ga, in);
+        int64_t i = i_first;
+        float in[3] = {in_first[0], in_first[1], in_first[2]};
+        if (!first) {
+            i = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
+            load_x01(xyzs, i, valid, ga, in);
+        }
+        first = false;
         _Float16* row = &xs[wv][lane * XROW];
 #pragma unroll 1
         for (int pr = 0; pr < 8; ++pr) {
@@ -823,9 +839,6 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
     _Float16* sw = smem;
     _Float16* scr = smem + SCR;
     NGP_BWD_EDGE(0);
-    load_bwd_weights_direct(mlp, sw);
-    __syncthreads();
-    NGP_BWD_EDGE(1);
     const int64_t N = n_dev ? *n_dev : n;
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -859,9 +872,15 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
     };
     const int64_t stride = (int64_t)gridDim.x * CW * 16;
     const int64_t j0 = (int64_t)blockIdx.x * CW * 16 + 16 * wid + s;
+    // the first iteration's inputs (count -> index -> rows: three dependent
+    // round trips) are requested before the weight images are staged, so the
+    // two overlap
     In cur;
     load_in(row_index(j0), cur);
     int32_t i_next = row_index(j0 + stride);
+    load_bwd_weights_direct(mlp, sw);
+    __syncthreads();
+    NGP_BWD_EDGE(1);
     int par = 0;
     // block-uniform trip count: every wave reaches every barrier
     for (int64_t bb = (int64_t)blockIdx.x * CW * 16; bb < N; bb += stride, par ^= 1) {
