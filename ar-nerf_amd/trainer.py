@@ -212,9 +212,10 @@ class NGPTrainer:
         # in the record write (one single-entry record per corner for a whole run: fewer records
         # written and accumulated).  Default for one-cascade scenes: levels 8-10 (consecutive
         # samples share a level-10 cell ~3 times on Lego; +1.2 % mean of 5 alternating pairs, 4 of 5,
-        # profiles/r03/ab/bin_merge_hi.txt); cascaded scenes keep 0 (unmeasured there).
+        # profiles/r03/ab/bin_merge_hi.txt); cascaded scenes, whose every level is binned: all 16
+        # (garden-shaped step 7.0 -> 8.3 M rays/s, profiles/r03/ab/garden_bin_merge_hi.txt).
         if bin_merge_hi is None:
-            bin_merge_hi = 0 if big else 11
+            bin_merge_hi = 16 if big else 11
         self.bin_merge_hi = int(bin_merge_hi)
         if hash_backward != "atomic":
             self.bin_max_samples = R * bin_samples_per_ray

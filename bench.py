@@ -119,7 +119,7 @@ def parse():
                     help="two consecutive steady-state steps per graph replay (trainer pair_steps)")
     ap.add_argument("--bin-merge-hi", type=int, default=None,
                     help="binned levels below this merge runs of equal corner pairs along a ray (default: "
-                         "trainer's, 11 / 0 for cascaded scenes)")
+                         "trainer's, 11 / 16 for cascaded scenes)")
     ap.add_argument("--bin-samples-per-ray", type=int, default=None,
                     help="binned hash-backward workspace per ray (default: trainer's, 128 / 512 for cascaded scenes)")
     ap.add_argument("--erode", default="auto", choices=["auto", "on", "off"],

@@ -56,6 +56,29 @@ def test_product_train_step_matches_reference_glue(case):
     # sits on T_thr within that bound may end one sample apart
     # (test_composite_train_fw_bw pins the per-ray form of this); 2 of the batch
     assert abs(int(res["vr_samples"]) - int(fx["vr_samples"])) <= 2
+    # ... and per ray: a ray composites its samples until the transmittance falls below
+    # T_thr = 1e-4 (volumerendering.cu:40-41), T after sample k = 1 - the sum of the weights up
+    # to k -- counted here from each side's weights (a zero weight of a tiny alpha does not end
+    # a ray).  A ray whose count differs from the glue's must be borderline: the glue's
+    # transmittance after the earlier of the two boundary samples within 5 % (log scale) of
+    # T_thr (the sigma bound of test_field_forward_parity moves ln T by far less than that).
+    rays_a, ws_fx, ws_pr = fx["rays_a"], fx["ws"].astype(np.float64), res["ws"].detach().cpu().double().numpy()
+
+    def count(ws):
+        t_after = 1.0 - np.cumsum(ws)
+        below = np.nonzero(t_after < 1e-4)[0]
+        return int(below[0]) + 1 if below.size else ws.size
+
+    flipped = 0
+    for r in range(rays_a.shape[0]):
+        s0, nr = int(rays_a[r, 1]), int(rays_a[r, 2])
+        c_fx, c_pr = count(ws_fx[s0:s0 + nr]), count(ws_pr[s0:s0 + nr])
+        if c_fx == c_pr:
+            continue
+        flipped += 1
+        t_after = 1.0 - float(np.sum(ws_fx[s0:s0 + min(c_fx, c_pr)]))
+        assert abs(np.log(max(t_after, 1e-30)) - np.log(1e-4)) < 0.05, (r, c_fx, c_pr, t_after)
+    print(f"{case}: {flipped} of {rays_a.shape[0]} rays end one side of T_thr apart, all borderline")
     loss_d = NeRFLoss(30, "raw", float(fx["scale"]), 0.0, lambda_distortion=0.0)(res, {"rgb": gt})
     loss = sum(v.mean() for v in loss_d.values())
     assert abs(float(loss) - float(fx["loss"])) <= 1e-2 * abs(float(fx["loss"]))
