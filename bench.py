@@ -118,8 +118,10 @@ def parse():
     ap.add_argument("--chunk-first", type=int, default=None,
                     help="chunked field evaluation: first round's samples per row (0: every marched sample in one "
                          "launch; default: trainer's, 64)")
-    ap.add_argument("--pair-steps", action="store_true",
-                    help="two consecutive steady-state steps per graph replay (trainer pair_steps)")
+    ap.add_argument("--no-pair-steps", action="store_true",
+                    help="one steady-state step per graph replay (default: two consecutive steps per replay, "
+                         "trainer pair_steps: one replay boundary per two steps, +1.1 %, 5 of 5 pairs, "
+                         "profiles/r03/ab/pair_steps_r3d.txt)")
     ap.add_argument("--bin-merge-hi", type=int, default=None,
                     help="binned levels below this merge runs of equal corner pairs along a ray (default: "
                          "trainer's, 11 / 16 for cascaded scenes)")
@@ -332,7 +334,7 @@ def main():
     erode = args.erode == "on" or (args.erode == "auto" and args.scale > 0.5)
     trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward,
                          bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray, erode=erode,
-                         bin_merge_hi=args.bin_merge_hi, pair_steps=args.pair_steps, emulate_dp=args.emulate_dp,
+                         bin_merge_hi=args.bin_merge_hi, pair_steps=not args.no_pair_steps, emulate_dp=args.emulate_dp,
                          **({} if args.chunk_first is None else {"chunk_first": args.chunk_first}))
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
     WORK = active_work(trainer)
@@ -509,6 +511,7 @@ def main():
                        "parallelism": f"dp{world}" + (f" (data-parallel step of world {args.emulate_dp} emulated: collectives as local copies)" if args.emulate_dp else ""), "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
                        "bin_merge_hi": trainer.bin_merge_hi,
+                       "steps_per_graph_replay": 2 if trainer.pair_steps and world == 1 and not args.emulate_dp else 1,
                        "erode": trainer.erode,
                        "test_psnr_synthetic": round(psnr, 2) if psnr is not None else None},
             "roofline": roof,

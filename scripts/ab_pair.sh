@@ -13,8 +13,8 @@ run() {
     python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value']/1e6,3), 'M rays/s', round(d['ms_per_step']*1e3,1), 'us/step')" "$OUT/$name.json" "$name"
 }
 for rep in 1 2 3; do
-run single_$rep
-run pair_$rep --pair-steps
+run single_$rep --no-pair-steps
+run pair_$rep
 done
 run emulate_dp_1 --emulate-dp
 run emulate_dp_2 --emulate-dp

@@ -278,3 +278,41 @@ def test_fused_adam_matches_separate_adam_cascaded():
         assert float((fa == fb).float().mean()) > 0.999
         assert float((fa - fb).abs().max()) <= 2e-6 * max(1.0, float(fb.abs().max()))
         assert float((a[:HG.MLP_PARAMS] - b[:HG.MLP_PARAMS]).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
+
+
+def test_pair_step_replays_match_single_steps():
+    """Two consecutive steady-state steps per graph replay (pair_steps, the
+    bench's default) train like one step per replay.  Float atomics make any
+    two runs differ (Adam turns the order noise of near-zero gradients into
+    O(lr) steps), so the bar is statistical: after the same schedule from the
+    same seed, the pair run is as close to a single-step run as a second
+    single-step run is, and the losses agree; the pair path did run, and a
+    second call with other inputs than the pair was captured with raises
+    instead of returning stale results."""
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    outs = []
+    for pair in (False, False, True):
+        tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, warmup_steps=16, pair_steps=pair)
+        tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
+        losses = []
+        for _ in range(120):
+            losses.append(float(tr.train_step(gt_img, dirs, poses).mean()))
+        tr.drain()
+        torch.cuda.synchronize()
+        n_pair = sum(1 for k in tr._graphs if k[0] == "pair")
+        outs.append((tr.params.clone(), sum(losses[-20:]) / 20, n_pair, tr.global_step))
+        if pair:
+            # the first call of a pair runs both steps; the second must get the same inputs
+            while not tr._ran_ahead:
+                tr.train_step(gt_img, dirs, poses)
+            with pytest.raises(RuntimeError):
+                tr.train_step(gt_img.clone(), dirs, poses)
+    (pa, la, na, sa), (pb, lb, nb, sb), (pp, lp, npair, sp) = outs
+    assert na == nb == 0 and npair >= 1 and sa == sb == sp == 120
+    noise = float((pb - pa).norm())
+    print(f"pair vs single {float((pp - pa).norm()):.3f}, single vs single {noise:.3f} (|p| {float(pa.norm()):.1f}); "
+          f"losses {la:.5f} {lb:.5f} {lp:.5f}")
+    assert float((pp - pa).norm()) <= 3 * noise + 1e-3 * float(pa.norm())
+    assert abs(lp - la) <= 0.1 * abs(la) + 3 * abs(lb - la)
