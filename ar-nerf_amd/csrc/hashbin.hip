@@ -291,11 +291,15 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
     static_assert((MODE & 2) || NBL == 64, "MODE 0 (diagnostics) scans one wave of buckets");
     __shared__ LevelLds lv;
     __shared__ uint32_t base[NSLOT];          // this tile's first slot in each bucket region
-    // hist is double-buffered by level parity: the MODE-2 path has no barrier
-    // between a level's rank atomics and the next level's reset
-    __shared__ uint32_t hist2[2][NBL], loff[NBL + 1];
-    __shared__ uint4 stage[TILE * 4];         // one level's records, sorted by bucket
+    __shared__ uint32_t hist2[2][NBL], loff[NBL + 1];  // MODE 0: one level's counts
+    __shared__ uint4 stage[TILE * 4];         // MODE 0: one level's records, sorted by bucket
     __shared__ uint8_t sbk[TILE * 4];
+    // MODE 2 ranks every level's records in its own counters (reusing stage[]'s
+    // LDS), cleared once per tile: the level loop then has no barrier, whose
+    // implied wait for all outstanding memory operations would hold each level
+    // on the previous level's record stores
+    uint32_t* const hall = reinterpret_cast<uint32_t*>(stage);
+    static_assert(sizeof(stage) >= NSLOT * sizeof(uint32_t), "stage[] holds the per-level counters");
     load_levels(ga, lv);
     const int64_t N = n_dev ? *n_dev : n;
     const int64_t ntiles = (N + TILE - 1) / TILE;
@@ -309,6 +313,7 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
                 base[i] = lb < (int)(ba.bbase[l + 1] - ba.bbase[l])
                               ? ws.rstart[ba.bbase[l] + lb] + ws.ofs[(size_t)i * ba.tiles_cap + tile]
                               : 0u;
+                if (MODE & 2) hall[i] = 0;
             }
         }
         float in[RPT][3];
@@ -320,11 +325,14 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
         for (int k = 0; k < RPT; ++k)
             gd[k] = valid[k] ? *reinterpret_cast<const float2*>(denc + (j0 + k * 64 + (t >> 2)) * 32 + 2 * ba.lo)
                              : float2{0.f, 0.f};
+        if (MODE & 2) __syncthreads();  // base[], hall[] ready
 #pragma unroll 1
         for (int l = ba.lo; l < L; ++l) {
-            uint32_t* hist = hist2[l & 1];
-            if (t < NBL) hist[t] = 0;
-            __syncthreads();  // also: base[] ready; previous level's stage[] reads done
+            uint32_t* hist = (MODE & 2) ? hall + l * NBL : hist2[l & 1];
+            if (!(MODE & 2)) {
+                if (t < NBL) hist[t] = 0;
+                __syncthreads();  // also: base[] ready; previous level's stage[] reads done
+            }
 #pragma unroll
             for (int k = 0; k < RPT; ++k)  // next level's dL/denc, loaded ahead
                 gn[k] = valid[k] && l + 1 < L
