@@ -295,9 +295,8 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
     __shared__ uint4 stage[TILE * 4];         // MODE 0: one level's records, sorted by bucket
     __shared__ uint8_t sbk[TILE * 4];
     // MODE 2 ranks every level's records in its own counters (reusing stage[]'s
-    // LDS), cleared once per tile: the level loop then has no barrier, whose
-    // implied wait for all outstanding memory operations would hold each level
-    // on the previous level's record stores
+    // LDS), cleared once per tile: the level loop then has no barrier, so a wave
+    // does not wait at every level for the block's slowest wave
     uint32_t* const hall = reinterpret_cast<uint32_t*>(stage);
     static_assert(sizeof(stage) >= NSLOT * sizeof(uint32_t), "stage[] holds the per-level counters");
     load_levels(ga, lv);
