@@ -288,7 +288,8 @@ def test_pair_step_replays_match_single_steps():
     same seed, the pair run is as close to a single-step run as a second
     single-step run is, and the losses agree; the pair path did run, and a
     second call with other inputs than the pair was captured with raises
-    instead of returning stale results."""
+    instead of returning stale results; the device step / batch counters end
+    where one step per replay leaves them."""
     sc = S.AnalyticScene(W=100, H=100, n_images=10)
     dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
     gt_img = sc.gt_images(device=DEV)
@@ -302,15 +303,17 @@ def test_pair_step_replays_match_single_steps():
         tr.drain()
         torch.cuda.synchronize()
         n_pair = sum(1 for k in tr._graphs if k[0] == "pair")
-        outs.append((tr.params.clone(), sum(losses[-20:]) / 20, n_pair, tr.global_step))
+        outs.append((tr.params.clone(), sum(losses[-20:]) / 20, n_pair, tr.global_step, tr.dctr[:2].clone()))
         if pair:
             # the first call of a pair runs both steps; the second must get the same inputs
             while not tr._ran_ahead:
                 tr.train_step(gt_img, dirs, poses)
             with pytest.raises(RuntimeError):
                 tr.train_step(gt_img.clone(), dirs, poses)
-    (pa, la, na, sa), (pb, lb, nb, sb), (pp, lp, npair, sp) = outs
+    (pa, la, na, sa, ca), (pb, lb, nb, sb, cb), (pp, lp, npair, sp, cp) = outs
     assert na == nb == 0 and npair >= 1 and sa == sb == sp == 120
+    # device counters (Adam steps taken, batches drawn) end where one step per replay leaves them
+    assert torch.equal(cp, ca) and torch.equal(ca, cb) and int(ca[0]) == 120, (ca, cb, cp)
     noise = float((pb - pa).norm())
     print(f"pair vs single {float((pp - pa).norm()):.3f}, single vs single {noise:.3f} (|p| {float(pa.norm()):.1f}); "
           f"losses {la:.5f} {lb:.5f} {lp:.5f}")
