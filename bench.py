@@ -138,6 +138,8 @@ def parse():
                          "2000 steps of the reference's schedule on a small problem, product defaults and exact mode)")
     ap.add_argument("--infer-frames", type=int, default=20, help="timed full-frame test renders (0: skip)")
     ap.add_argument("--infer-res", type=int, default=800)
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="world > 1 process group (nccl = RCCL; gloo only to rehearse the path with ranks sharing a GPU)")
     return ap.parse_args()
 
 
@@ -151,12 +153,18 @@ def setup_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
+        # (--dist-backend gloo with more ranks than GPUs: a rehearsal of the world > 1 bench
+        # path on a one-GPU box, ranks sharing the card; the measured path is RCCL, one GPU per rank)
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
-    return world, rank, local
+    return world, rank, torch.cuda.current_device()
 
 
 def psnr_eval(trainer, scene, n_views, res, seed=123):
@@ -324,7 +332,7 @@ def pmc_traffic(members, launches):
 
 def main():
     args = parse()
-    world, rank, local = setup_dist(args)
+    world, rank, local = setup_dist(args)  # local: this rank's device index
     dev = torch.device("cuda", local)
     torch.manual_seed(0)
     scene = S.AnalyticScene(W=args.res, H=args.res, n_images=args.images, scale=args.scale)
