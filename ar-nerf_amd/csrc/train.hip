@@ -857,7 +857,7 @@ __global__ void __launch_bounds__(1024) active_scan_kernel(const int32_t* __rest
     }
     if (tid == 0) {
         *total = carry_s;
-        if (total_acc) *total_acc += carry_s;
+        if (total_acc) atomicAdd((unsigned long long*)total_acc, (unsigned long long)carry_s);
     }
 }
 
@@ -935,7 +935,7 @@ __global__ void __launch_bounds__(SEG_THREADS) segments_kernel(const int32_t* __
     const int32_t nb = lofs[SEG_ROWS];
     if (blockIdx.x == gridDim.x - 1 && t == 0) {
         *total = prefix + nb;
-        if (total_acc) *total_acc += prefix + nb;
+        if (total_acc) atomicAdd((unsigned long long*)total_acc, (unsigned long long)(prefix + nb));
     }
     // 3) map: entry q of this block belongs to the row whose [lofs, lofs+c) holds it
     for (int32_t q = t; q < nb; q += SEG_THREADS) {
@@ -1025,7 +1025,8 @@ static_assert(CS_ROWS == 64 || CS_ROWS == 32 || CS_ROWS == 16, "row block");
 __global__ void __launch_bounds__(CS_THREADS) chunk_segments_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ deltas, const int64_t* __restrict__ rays_a,
     int64_t n_rows, int first, int last, float T_thr, LookbackWs* __restrict__ lb, int64_t* __restrict__ start_ws,
-    int64_t* __restrict__ total, int64_t* __restrict__ total_acc, int32_t* __restrict__ sample_idx) {
+    int64_t* __restrict__ total, int64_t* __restrict__ total_acc, const int64_t* __restrict__ total_acc_add,
+    int32_t* __restrict__ sample_idx) {
     __shared__ int32_t cnt_s[CS_ROWS];
     __shared__ int32_t lofs[65];  // (wave 0 writes all 64 lanes' entries; [CS_ROWS] = the block's total)
     __shared__ int64_t src[64];
@@ -1094,7 +1095,9 @@ __global__ void __launch_bounds__(CS_THREADS) chunk_segments_kernel(
             sh_prefix = P;
             if (b == nb - 1) {
                 *total = P + A;
-                if (total_acc) *total_acc += P + A;
+                if (total_acc)
+                    atomicAdd((unsigned long long*)total_acc,
+                              (unsigned long long)(P + A + (total_acc_add ? *total_acc_add : 0)));
             }
         }
     }
@@ -1168,8 +1171,9 @@ size_t ngp_chunk_segments_workspace(int64_t n_rows) {
 
 int ngp_chunk_segments(const float* sigmas, const float* deltas, const int64_t* rays_a, int64_t n_rows, int first,
                        int last, float T_threshold, void* lookback_ws, int64_t* start_ws, int64_t* total,
-                       int64_t* total_acc, int32_t* sample_idx, void* stream) {
+                       int64_t* total_acc, const int64_t* total_acc_add, int32_t* sample_idx, void* stream) {
     NGP_CHECK_ARG(n_rows >= 0 && first >= 1 && (last <= 0 || last > first) && total);
+    NGP_CHECK_ARG(!total_acc_add || total_acc);
     hipStream_t s = as_stream(stream);
     if (n_rows == 0) {
         active_scan_kernel<<<1, 1024, 0, s>>>(nullptr, 0, start_ws, total, total_acc);  // total = 0
@@ -1181,7 +1185,7 @@ int ngp_chunk_segments(const float* sigmas, const float* deltas, const int64_t* 
     NGP_CHECK_ARG(blocks <= (int64_t)0x7fffffff);
     NGP_TIMED(NGP_K_SEGMENTS, s, chunk_segments_kernel<<<(unsigned)blocks, CS_THREADS, 0, s>>>(
         sigmas, deltas, rays_a, n_rows, first, last, T_threshold, (LookbackWs*)lookback_ws, start_ws, total,
-        total_acc, sample_idx));
+        total_acc, total_acc_add, sample_idx));
     return ngp_launch_status();
 }
 

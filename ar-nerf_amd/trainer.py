@@ -186,9 +186,13 @@ class NGPTrainer:
         self.out_depth, self.out_loss = torch.empty(R, **f), torch.empty(R, **f)
         # running totals: [0] marched, [1] composited (vr_samples), [2] gradient-carrying,
         # [3] field-evaluated samples
-        # striped counters (ngp_composite_loss: NGP_STAT_STRIPES x NGP_STAT_STRIDE);
-        # [0, 3] = field-evaluated samples (ngp_ray_segments total_acc)
+        # striped counters (ngp_composite_loss: NGP_STAT_STRIPES x NGP_STAT_STRIDE), written by the
+        # compositing kernel only; field-evaluated samples in their own 128-B line (eval_stats[0],
+        # main stream only: the list launches of the step that evaluates them add both rounds'
+        # totals, device-scope atomics) -- no counter word shares a cache line with a writer on
+        # another stream
         self.stats = torch.zeros(STAT_STRIPES * STAT_STRIDE, dtype=torch.int64, device=dev)
+        self.eval_stats = torch.zeros(STAT_STRIDE, dtype=torch.int64, device=dev)
         # chunked field evaluation (ngp_chunk_counts): first `chunk_first` samples of
         # every row, then the rest of the rows not yet terminated (0 = every sample).
         # (More rounds evaluate 22 % fewer samples, but each extra encode launch costs
@@ -441,13 +445,13 @@ class NGPTrainer:
                                                _p(m["dirs"]), _p(m["deltas"]), _p(m["ts"]), s), "march_compact")
             # round 1 of the chunked forward: the list of each row's first chunk_first samples
             # (counts min(N_r, K) + scan + list in one launch), here beside the previous step
-            # instead of at the head of this batch's step; evaluated-sample count into stats[4]
-            # (stats[3] is round 2's: the two streams never add to one counter)
+            # instead of at the head of this batch's step; its length eval_total1 is counted
+            # into eval_stats by the round-2 list launch of the step that evaluates it
             K = self.chunk_first
             m["eval1_K"] = K if (K > 0 and R <= 65536) else 0
             if m["eval1_K"]:
                 vren._ok(L.ngp_ray_segments_capped(_p(m["rays_a"]), R, K, _p(m["act_start1"]), _p(m["eval_total1"]),
-                                                   _p(self.stats[4:]), _p(m["eval_idx1"]), s), "segments_capped")
+                                                   None, _p(m["eval_idx1"]), s), "segments_capped")
             if side:
                 self._ev("march_side", 1, stream)
 
@@ -501,11 +505,17 @@ class NGPTrainer:
             ev[name][-1][1].record(st)
 
     # ---------------------------------------------------------------- step
+    def reset_stats(self):
+        """Zero the sample counters (stat_totals) on the current stream."""
+        self.stats.zero_()
+        self.eval_stats.zero_()
+
     def stat_totals(self):
-        """(marched, composited, active, evaluated) samples accumulated since
-        stats was last zeroed (sum over the stripes)."""
-        t = [int(v) for v in self.stats.view(STAT_STRIPES, STAT_STRIDE)[:, :5].sum(0).tolist()]
-        return t[:3] + [t[3] + t[4]]  # (evaluated: round 2's count + round 1's, counted by the march)
+        """(marched, composited, active, evaluated) samples of the steps run
+        since reset_stats() (sum over the stripes; evaluated = both chunked
+        rounds, 0 when chunk_first == 0: every marched sample is evaluated)."""
+        t = [int(v) for v in self.stats.view(STAT_STRIPES, STAT_STRIDE)[:, :3].sum(0).tolist()]
+        return t + [int(self.eval_stats[0])]
 
     def step(self, img_idxs, pix_idxs, rgb_gt, directions, poses, noise=None, apply_adam=True, next_batch=None):
         """One training step on a batch (train.py:174-200).  img/pix (R) i64,
@@ -515,7 +525,7 @@ class NGPTrainer:
         nxt = None if next_batch is None else ("idx", next_batch[0], next_batch[1], None)
         return self._step(("idx", img_idxs, pix_idxs, noise), rgb_gt, directions, poses, apply_adam, nxt)
 
-    def train_step(self, gt, directions, poses):
+    def train_step(self, gt, directions, poses, allow_pair=True):
         """One training step on a batch drawn on device from the training set
         (gt (n_img, HW, 3) u8 images -- or f32 colours, e.g. alpha-blended
         data -- directions (HW,3), poses (n_img,3,4)):
@@ -523,7 +533,10 @@ class NGPTrainer:
         The next step's batch is drawn and marched ahead on the side stream.
         Steady-state steps (batch already marched ahead, no occupancy update
         now or next step) replay a captured HIP graph of the whole step
-        (NGP_GRAPHS=0: always eager)."""
+        (NGP_GRAPHS=0: always eager).  pair_steps: a call may run this step
+        AND the next in one replay (the next call then only advances the
+        count); allow_pair=False keeps this call to one step, e.g. the last
+        step of a measured window."""
         gs, ui = self.global_step, self.update_interval
         self._throttle()
         if self._ran_ahead:  # this step was the second half of the previous call's two-step graph
@@ -535,7 +548,7 @@ class NGPTrainer:
             return self.out_loss
         if (self.use_graphs and self._pending is not None and (gs % ui != 0 or self._updated_for == gs)
                 and gs >= self.warmup_steps and self.kernel_events is None and not self.no_prefetch):
-            if (self.pair_steps and not self.dp and self.timer is None and (gs + 1) % ui != 0
+            if (allow_pair and self.pair_steps and not self.dp and self.timer is None and (gs + 1) % ui != 0
                     and (gs + 2) % ui != 0 and gs // self.steps_per_epoch == (gs + 1) // self.steps_per_epoch):
                 return self._replay_pair(gt, directions, poses)
             return self._replay(gt, directions, poses, (gs + 1) % ui == 0)
@@ -808,14 +821,16 @@ class NGPTrainer:
                 vren._ok(L.ngp_chunk_counts(_p(self.rays_a), R, K, None, None, ctypes_float(1e-4),
                                             _p(self.eval_counts), s), "chunk_counts")
                 vren._ok(L.ngp_ray_segments(_p(self.eval_counts), _p(self.rays_a), R, 0, _p(self.act_start),
-                                            _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s), "segments")
+                                            _p(self.eval_total), _p(self.eval_stats), _p(self.eval_idx), s),
+                         "segments")
                 self._field_indexed(s)
             # second round [K, N_r) of the rows still transparent after K samples: counts, scan
             # and list in one launch (ngp_chunk_segments; the two launches it replaces cost a
             # launch gap and a second pass over rays_a)
             vren._ok(L.ngp_chunk_segments(_p(self.sigmas), _p(self.deltas), _p(self.rays_a), R, K, 0,
                                           ctypes_float(1e-4), _p(self._cs_ws), _p(self.act_start),
-                                          _p(self.eval_total), _p(self.stats[3:]), _p(self.eval_idx), s),
+                                          _p(self.eval_total), _p(self.eval_stats),
+                                          _p(self.eval_total1) if self.eval1_K == K else None, _p(self.eval_idx), s),
                      "chunk_segments")
             self._field_indexed(s)
         else:  # encode + MLPs in one launch over every marched sample

@@ -349,12 +349,19 @@ def main():
     R = args.batch
 
     def run(n):
-        """n training steps, each on a batch drawn on device (trainer.train_step:
-        pixels, ground truth and noise from a counter-based RNG); batch i+1 is
-        drawn and marched on the side stream during step i."""
+        """Exactly n training steps, each on a batch drawn on device
+        (trainer.train_step: pixels, ground truth and noise from a counter-based
+        RNG); batch i+1 is drawn and marched on the side stream during step i.
+        The last call never starts a two-step replay, so no step of this window
+        runs in the next one (nor one of the previous window in this one)."""
         for i in range(n):
-            trainer.train_step(gt_images, directions, poses)
+            trainer.train_step(gt_images, directions, poses, allow_pair=i < n - 1)
         trainer.drain()
+
+    def adam_steps():
+        """steps completed on the device so far (the device step counter; call
+        after a synchronize)"""
+        return int(trainer.dctr[0].item())
 
     t0 = time.time()
     run(args.pretrain)
@@ -370,11 +377,13 @@ def main():
     run(64)  # capture this timer's graph variants
     torch.cuda.synchronize()
     full.reset()
-    trainer.stats.zero_()
+    trainer.reset_stats()
+    s_bd = adam_steps()
     t_bd = time.perf_counter()
     run(n_bd)
     torch.cuda.synchronize()
     t_bd = (time.perf_counter() - t_bd) / n_bd
+    ran_bd = adam_steps() - s_bd
     trainer.timer = None
     bd_summary, bd_steps, bd_timeline = full.summary(), full.steps(), full.timeline()
     marched_bd, composited_bd, active_bd, evaluated_bd = trainer.stat_totals()
@@ -382,8 +391,9 @@ def main():
         evaluated_bd = marched_bd
     fused_p = trainer.fused_params()
     pw = {"params": trainer.params.numel(), "fused_params": fused_p, "adam_params": trainer.params.numel() - fused_p}
-    units_bd = {"marched": marched_bd / n_bd, "evaluated": evaluated_bd / n_bd, "composited": composited_bd / n_bd,
-                "active": active_bd / n_bd, **pw}
+    nb = max(1, ran_bd)  # (== n_bd: run() runs exactly n steps)
+    units_bd = {"marched": marched_bd / nb, "evaluated": evaluated_bd / nb, "composited": composited_bd / nb,
+                "active": active_bd / nb, **pw}
 
     def op_row(name, summary, units):
         bound, terms, members = WORK[name]
@@ -420,7 +430,9 @@ def main():
     # ---- timed region: plain graph replays (no instrumentation: even two
     # stamp kernels per step cost ~3 %)
     run(args.warmup)
-    trainer.stats.zero_()
+    torch.cuda.synchronize()
+    trainer.reset_stats()
+    s_timed = adam_steps()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -431,6 +443,9 @@ def main():
     if world > 1:
         dist.barrier()
     t_el = time.perf_counter() - t_start
+    ran_timed = adam_steps() - s_timed
+    if ran_timed != args.steps:
+        raise RuntimeError(f"timed window ran {ran_timed} steps, expected {args.steps}")
     marched, composited, active, evaluated = trainer.stat_totals()
     # ---- roofline region: the same number of graph-replayed steps again, with
     # one stamp before the dominant op's first kernel and one after its last
@@ -441,19 +456,21 @@ def main():
     run(64)  # capture this timer's graph variants
     torch.cuda.synchronize()
     dom.reset()
-    trainer.stats.zero_()
+    trainer.reset_stats()
+    s_rf = adam_steps()
     t_rf = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
     t_rf = (time.perf_counter() - t_rf) / args.steps
+    ran_rf = adam_steps() - s_rf
     trainer.timer = None
     span = dom.read_span()
     dom_summary = {members[0]: (sum(span) / len(span), 1.0)} if span else bd_summary
     m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         e_rf = m_rf
-    units_rf = {"marched": m_rf / args.steps, "evaluated": e_rf / args.steps, "composited": c_rf / args.steps,
-                "active": a_rf / args.steps, **pw}
+    nr = max(1, ran_rf)
+    units_rf = {"marched": m_rf / nr, "evaluated": e_rf / nr, "composited": c_rf / nr, "active": a_rf / nr, **pw}
     t_max = torch.tensor([t_el], device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -465,8 +482,24 @@ def main():
     units = {"marched": marched / args.steps, "evaluated": evaluated / args.steps,
              "composited": composited / args.steps, "active": active / args.steps, **pw}
     rm_s, vr_s, ev_s = units["marched"] / R, units["composited"] / R, units["evaluated"] / R
+    # the roofline window's units (the same replays as its stamps) against the other two
+    # windows': per-step sample counts of one training state agree to a few % (windows of
+    # 20+ steps); a larger gap means a window's counters did not cover its steps
+    units_check = {"steps_run": {"breakdown": ran_bd, "timed": ran_timed, "roofline": ran_rf}}
+    dev_max = 0.0
+    for basis in ("active", "evaluated", "composited"):
+        vals = {"breakdown": units_bd[basis], "timed": units[basis], "roofline": units_rf[basis]}
+        units_check[f"{basis}_per_step"] = {k: round(v, 1) for k, v in vals.items()}
+        ref_v = units[basis]
+        if ref_v > 0:
+            dev_max = max(dev_max, max(abs(v - ref_v) / ref_v for v in vals.values()))
+    units_check["max_rel_dev_vs_timed"] = round(dev_max, 4)
+    units_check["ok"] = bool(dev_max <= 0.03 and ran_rf == args.steps and ran_bd == n_bd)
+    if not units_check["ok"]:
+        print(f"[bench] WARNING: per-step unit counts disagree across windows: {units_check}", file=sys.stderr)
     roof = op_row(dominant, dom_summary, units_rf)
     roof = dict(op=dominant, traffic=pmc_traffic(members, bd_summary), traffic_unit="bytes per step", **roof,
+                units_check=units_check,
                 measured=f"device wall-clock stamps before / after the op inside the captured graphs of "
                          f"{args.steps} graph-replayed steps run right after the timed ones "
                          f"({t_rf * 1e3:.4f} ms/step with the 2 stamps; ktimer)")

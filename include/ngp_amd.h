@@ -499,7 +499,7 @@ int ngp_chunk_counts_range(const int64_t* rays_a, int64_t n_rows, int first, int
 /* Sample list of per-row segments: sample_idx[start_r + k] = rays_a[r].start +
  * first + k for k < counts[r] (start = exclusive prefix of counts, in
  * start_ws (n_rows) i64); *total = the list length, *total_acc += it
- * (nullable). */
+ * (nullable; a device-scope atomic add). */
 /* ngp_chunk_counts_range (sigmas given) + ngp_ray_segments of those counts
  * in ONE launch: the list of round-2 samples [first, min(N_r, last)) of the
  * rows still transparent after `first` samples, its per-row starts and total
@@ -507,11 +507,14 @@ int ngp_chunk_counts_range(const int64_t* rays_a, int64_t n_rows, int first, int
  * through `lookback_ws`: ngp_chunk_segments_workspace(n_rows) bytes, 8-byte
  * aligned, ZEROED once by the caller and then owned by the call site (the
  * kernel leaves it ready for the next launch; never shared by concurrent
- * launches).  Same outputs as the two calls. */
+ * launches).  Same outputs as the two calls.  total_acc_add (nullable, needs
+ * total_acc): a device count added into *total_acc with the total -- the
+ * round-1 list length of a list built earlier, so a step's evaluated samples
+ * are counted by the step that evaluates them. */
 size_t ngp_chunk_segments_workspace(int64_t n_rows);
 int ngp_chunk_segments(const float* sigmas, const float* deltas, const int64_t* rays_a, int64_t n_rows, int first,
                        int last, float T_threshold, void* lookback_ws, int64_t* start_ws, int64_t* total,
-                       int64_t* total_acc, int32_t* sample_idx, void* stream);
+                       int64_t* total_acc, const int64_t* total_acc_add, int32_t* sample_idx, void* stream);
 int ngp_ray_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_rows, int first,
                      int64_t* start_ws, int64_t* total, int64_t* total_acc, int32_t* sample_idx,
                      void* stream);

@@ -4,21 +4,33 @@ oracle in fp32 autograd -- the training-quality anchor (north_star "PSNR
 within 0.2 dB of reference") that tests/test_quality_gpu.py holds the
 product to.
 
-What runs (train.py:158-200 without Lightning / apex / AMP):
+What runs (train.py:158-200 without Lightning / apex; Lightning's
+precision=16 AMP loss scaling restated, see below):
   NeRFSystem.on_train_start -> NGP.mark_invisible_cells (networks.py:209-250)
   per step: NGP.update_density_grid every 16 steps, warm-up below 256
             (networks.py:252-281, train.py:175-178);
             render(model, rays_o, rays_d) (rendering.py:13-54, train path:
             RayMarcher / VolumeRenderer autograd, white background);
             NeRFLoss 'raw' (losses.py:63-82), loss = sum of means;
-            loss.backward(); FusedAdam(lr, eps=1e-15) on the model's
-            parameters (train.py:146), lr = CosineAnnealingLR(num_epochs,
-            lr/30) stepped per epoch (train.py:149-151)
+            backward through the GradScaler that Trainer(precision=16)
+            attaches (train.py:291 -> torch.cuda.amp.GradScaler, PyTorch's
+            defaults): (loss * S).backward() with S = 2^16 initially, the
+            gradients unscaled by 1/S in fp32; a step whose gradients hold
+            an inf / nan is skipped (no Adam step, S halved), S doubles after
+            2000 consecutive clean steps;
+            FusedAdam(lr, eps=1e-15) on the model's parameters (train.py:146),
+            lr = CosineAnnealingLR(num_epochs, lr/30) stepped per epoch
+            (train.py:149-151)
   at the end: render(test_time=True) of held-out views (rendering.py:162-253)
             composited on white (the scene's GT background) -> mean PSNR.
 with `vren` = oracle (C restatement of the .cu kernels) and `tinycudann` =
-oracle.tcnn_stub (fp16 storage points, fp32 autograd: no fp16 / bf16
-gradient operands, no loss scale) -- installed by make_golden.install_stubs.
+oracle.tcnn_stub (fp16 storage points, fp16 module outputs -- so the glue's
+gradients into the modules, dL/dh and dL/drgb, are rounded to fp16 AT THE
+LOSS SCALE S, as under AMP on the GPU -- and fp32 autograd inside the
+modules) -- installed by make_golden.install_stubs.
+(Rounds 1-3 ran this without the GradScaler: the fp16 boundary then flushed
+gradients below 2^-24 that the reference's scaled backward keeps; those
+fixtures did not model the reference and were replaced.)
 
 Shared with the product run (tests/test_quality_gpu.py), so both train the
 same problem: the scene (synthetic.AnalyticScene, TRAIN / TEST below), the
@@ -208,6 +220,11 @@ def main():
     thr = 0.01 * 1024 / 3 ** 0.5
     n_steps = CFG["epochs"] * CFG["steps_per_epoch"]
     losses, t0 = [], time.time()
+    # Lightning precision=16 (train.py:291): torch.cuda.amp.GradScaler with its defaults
+    # (init_scale 2^16, growth 2 every 2000 clean steps, backoff 0.5).  The fp32-boundary
+    # variant needs no scale (a power-of-two scale is exact there).
+    use_scaler = os.environ.get("GRAD_SCALER", "1") == "1" and not f32_out
+    scaler = dict(scale=65536.0 if use_scaler else 1.0, growth_tracker=0, skipped=[], adam_steps=0)
     occ = int(os.environ.get("OCC_SEED", "0"))  # (spread runs: other occupancy draws)
     torch.manual_seed(CFG["batch_seed"] - 1 - occ)  # the glue's occupancy draws
     for step in range(n_steps):
@@ -225,12 +242,27 @@ def main():
         loss = sum(v.mean() for v in loss_d.values())
         for p in params:
             p.grad = None
-        loss.backward()
+        S = scaler["scale"]
+        (loss * S if use_scaler else loss).backward()
         lr = lr_at(step)
-        for p in params:
-            m, v = state[p]
-            g = p.grad if p.grad is not None else torch.zeros_like(p)
-            O.adam_(p.data, g.contiguous(), m, v, lr, step + 1)
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
+        # GradScaler.unscale_: grads * (1/S) in fp32, found_inf over all of them
+        found_inf = use_scaler and not all(bool(torch.isfinite(g).all()) for g in grads)
+        if found_inf:  # GradScaler.step skips optimizer.step(); update() halves the scale
+            scaler["skipped"].append(step)
+            scaler["scale"] = S * 0.5
+            scaler["growth_tracker"] = 0
+        else:
+            inv = 1.0 / S
+            scaler["adam_steps"] += 1
+            for p, g in zip(params, grads):
+                m, v = state[p]
+                O.adam_(p.data, (g * inv if use_scaler else g).contiguous(), m, v, lr, scaler["adam_steps"])
+            if use_scaler:
+                scaler["growth_tracker"] += 1
+                if scaler["growth_tracker"] == 2000:
+                    scaler["scale"] = S * 2.0
+                    scaler["growth_tracker"] = 0
         losses.append(float(loss.detach()))
         if step % 50 == 0 or step == n_steps - 1:
             print(f"[make_quality] step {step} loss {losses[-1]:.5f} rm_s {int(res['rm_samples']) / CFG['batch']:.1f} "
@@ -249,6 +281,10 @@ def main():
            "cpu_threads": nthreads, "wall_s": round(time.time() - t0, 1), "occ_seed": occ,
            "what": "reference train.py loop glue + oracle fp32-autograd kernels (make_quality.py)"}
     out["tcnn_out"] = "f32" if f32_out else "f16"
+    out["grad_scaler"] = ({"init_scale": 65536.0, "final_scale": scaler["scale"], "skipped_steps": scaler["skipped"],
+                           "adam_steps": scaler["adam_steps"], "growth_interval": 2000, "backoff": 0.5,
+                           "what": "Lightning precision=16 (train.py:291): torch.cuda.amp.GradScaler defaults"}
+                          if use_scaler else None)
     name = "quality_oracle" + ("" if occ == 0 else f"_occ{occ}") + ("_f32out" if f32_out else "")
     path = os.path.join(HERE, name + ".json")
     with open(path, "w") as f:

@@ -163,13 +163,15 @@ def test_chunked_forward_matches_full(first, table_init):
         loss = tr.step(img.to(DEV), pix.to(DEV), gt, dirs, poses, noise=noise.to(DEV), apply_adam=False)
         torch.cuda.synchronize()
         terminated = bool((tr.n_active < tr.rays_a[:, 2]).any())
-        runs.append((loss.clone(), tr.out_rgb.clone(), tr.out_op.clone(), tr.grad.clone(), int(tr.stats[3]),
-                     int(tr.n_samples.item()), terminated))
-    (l0, r0, o0, g0, _, n0, _), (l1, r1, o1, g1, ev1, n1, term) = runs
+        # evaluated samples of the step: round 1 + round 2 (stat_totals()[3]; 0 for chunk == 0)
+        first_round = int(tr.rays_a[:, 2].clamp(max=chunk).sum()) if chunk else 0
+        runs.append((loss.clone(), tr.out_rgb.clone(), tr.out_op.clone(), tr.grad.clone(), tr.stat_totals()[3],
+                     int(tr.n_samples.item()), terminated, first_round))
+    (l0, r0, o0, g0, _, n0, _, _), (l1, r1, o1, g1, ev1, n1, term, fr1) = runs
     assert n0 == n1
     assert torch.equal(l0, l1) and torch.equal(r0, r1) and torch.equal(o0, o1)
     assert float((g1 - g0).norm() / g0.norm()) < 1e-5
-    assert ev1 <= n1
+    assert fr1 <= ev1 <= n1
     if term and first == 8:  # some row stops early: its tail is never evaluated
         assert ev1 < n1
 

@@ -391,15 +391,19 @@ def test_chunk_segments_equals_counts_then_segments(n_rows, first, last):
                                 vren._stream()), "segments")
     ws = torch.zeros((L.ngp_chunk_segments_workspace(n_rows) + 7) // 8, dtype=torch.int64, device=DEV)
     acc = torch.full((1,), 7, dtype=torch.int64, device=DEV)
+    add = torch.full((1,), 11, dtype=torch.int64, device=DEV)  # total_acc_add: a round-1 count added with it
+    acc_expect = 7
     for it in range(3):
         st = torch.full((n_rows,), -5, dtype=torch.int64, device=DEV)
         tot = torch.zeros(1, dtype=torch.int64, device=DEV)
         idx = torch.full((n_s,), -1, dtype=torch.int32, device=DEV)
         vren._ok(L.ngp_chunk_segments(p(sig), p(dl), p(rays_a), n_rows, first, last, ctypes.c_float(1e-4), p(ws),
-                                      p(st), p(tot), p(acc), p(idx), vren._stream()), "chunk_segments")
+                                      p(st), p(tot), p(acc), p(add) if it % 2 else None, p(idx), vren._stream()),
+                 "chunk_segments")
         torch.cuda.synchronize()
         T = int(tot_ref)
-        assert int(tot) == T and int(acc) == 7 + (it + 1) * T
+        acc_expect += T + (11 if it % 2 else 0)
+        assert int(tot) == T and int(acc) == acc_expect
         assert torch.equal(st, st_ref) and torch.equal(idx[:T], idx_ref[:T])
     if n_rows >= 1000:  # some rows terminate inside the first chunk, some go on
         assert 0 < int(tot_ref) < int(N.sum())
