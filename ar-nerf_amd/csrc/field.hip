@@ -583,6 +583,157 @@ __global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const 
     }
 }
 
+// ------------------------------ fused encode + MLP forward, register form
+// field_encode_mlp_kernel's arithmetic (bit-identical outputs) with two
+// changes in the structure:
+//  * the encoding never goes through LDS: a lane keeps its sample's 16 level
+//    dwords (fp16x2 features) in registers, and a 4 x 4 transpose of 4-dword
+//    groups across the wave's four 16-lane rows (two v_permlane32_swap and
+//    two v_permlane16_swap stages) lands, for column block c, the operand
+//    enc[16c + s][8g .. 8g+7] in lane (s, g) -- the B layout of
+//    v_mfma_f32_16x16x32_f16; a block then needs only the 24 KB weight image,
+//    so occupancy is set by registers, not by the 40 KB of parked rows;
+//  * LPR levels are gathered per round (their loads issued together), so a
+//    lane's chain of dependent gather rounds is 16 / LPR long instead of 8;
+//  * 64-sample chunks are dealt to waves interleaved over the whole grid
+//    (chunk k -> wave k / G of block k % G): every resident block gets the
+//    same number of chunks within one, so no CU holds two blocks' worth of
+//    work while others hold one (the one-pass ceil(N/512)-block form left
+//    ~20 % of the CUs doubly loaded).
+// 4 x 4 transpose of 4-dword groups across the wave's 16-lane rows: on entry
+// register group r (E[4r..4r+3]) of lane row q holds group r of the row's
+// sample; on exit group c of lane row g holds group g of row c's sample.
+__device__ __forceinline__ void transpose_rows4(uint32_t E[16]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        // stage 1: upper 32 lanes of groups 0 / 1 <-> lower 32 lanes of groups 2 / 3
+        const auto a = __builtin_amdgcn_permlane32_swap(E[k], E[8 + k], false, false);
+        E[k] = a[0];
+        E[8 + k] = a[1];
+        const auto b = __builtin_amdgcn_permlane32_swap(E[4 + k], E[12 + k], false, false);
+        E[4 + k] = b[0];
+        E[12 + k] = b[1];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        // stage 2: odd rows of groups 0 / 2 <-> even rows of groups 1 / 3
+        const auto a = __builtin_amdgcn_permlane16_swap(E[k], E[4 + k], false, false);
+        E[k] = a[0];
+        E[4 + k] = a[1];
+        const auto b = __builtin_amdgcn_permlane16_swap(E[8 + k], E[12 + k], false, false);
+        E[8 + k] = b[0];
+        E[12 + k] = b[1];
+    }
+}
+
+__device__ __forceinline__ uint32_t pack_h2(float a, float b) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
+}
+
+#ifndef NGP_FEM_LPR
+#define NGP_FEM_LPR 2  // 4: the loads of 4 levels in flight need > 128 VGPRs (spills)
+#endif
+#ifndef NGP_FEM2_WAVES
+#define NGP_FEM2_WAVES 8
+#endif
+constexpr int FEM2_WAVES = NGP_FEM2_WAVES, FEM_LPR = NGP_FEM_LPR;
+static_assert(L % FEM_LPR == 0, "levels per round");
+template <bool COLOR>
+__global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_mlp_reg_kernel(
+    const float* __restrict__ xyzs, const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev,
+    const int32_t* __restrict__ sidx, GridArgs ga, const uint32_t* __restrict__ table,
+    const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm, float* __restrict__ sigmas,
+    float* __restrict__ rgbs, _Float16* __restrict__ h_out) {
+    __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
+    __shared__ LevelLds lv;
+    const int64_t N = n_dev ? *n_dev : n;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, s = lane & 15, g = lane >> 4;
+    const int64_t G = gridDim.x;
+    const int64_t chunks = (N + 63) >> 6;
+    int64_t k = (int64_t)wv * G + blockIdx.x;  // first chunk of this wave (wave-uniform)
+    // the first chunk's index and position (count -> index -> position: dependent round
+    // trips) requested before the weight image is built, so the two overlap
+    int64_t i_first = 0;
+    float in_first[3];
+    {
+        const int64_t j = k * 64 + lane;
+        const bool valid = k < chunks && j < N;
+        i_first = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
+        load_x01(xyzs, i_first, valid, ga, in_first);
+    }
+    load_fwd_weights_direct(mlp, sw, COLOR);
+    load_levels(ga, lv);
+    __syncthreads();
+    bool first = true;
+    for (; k < chunks; k += (int64_t)FEM2_WAVES * G) {
+        const int64_t j = k * 64 + lane;
+        const bool valid = j < N;
+        int64_t i = i_first;
+        float in[3] = {in_first[0], in_first[1], in_first[2]};
+        if (!first) {
+            i = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
+            load_x01(xyzs, i, valid, ga, in);
+        }
+        first = false;
+        uint32_t E[16];  // level l's two features, fp16x2
+        // rounds of FEM_LPR levels, not unrolled (an unrolled chain hoists every round's
+        // loads: 256 VGPRs); each round shifts its levels into the top of E, so after the
+        // last round E[l] holds level l
+#pragma unroll 1
+        for (int r = 0; r < L / FEM_LPR; ++r) {
+            float w[FEM_LPR][8];
+            uint32_t v[FEM_LPR][8];
+#pragma unroll
+            for (int q = 0; q < FEM_LPR; ++q) gather_level_u(in, level_u(lv, FEM_LPR * r + q), table, w[q], v[q]);
+#pragma unroll
+            for (int q = 0; q < 16 - FEM_LPR; ++q) E[q] = E[q + FEM_LPR];
+#pragma unroll
+            for (int q = 0; q < FEM_LPR; ++q) {
+                float a0, a1;
+                sum_level(w[q], v[q], a0, a1);
+                E[16 - FEM_LPR + q] = pack_h2(a0, a1);
+            }
+        }
+        if (valid && enc_pm) {
+#pragma unroll
+            for (int pr = 0; pr < 8; ++pr)
+                *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(E[2 * pr], E[2 * pr + 1]);
+        }
+        transpose_rows4(E);
+        const int32_t imine = valid ? (int32_t)i : -1;
+        // column blocks in a loop (not unrolled: register pressure); block c's operand is
+        // E[0..3] after c rotations by one group
+#pragma unroll 1
+        for (int c = 0; c < 4; ++c) {
+            const int32_t ic = __shfl(imine, 16 * c + s, 64);
+            const bool ok = ic >= 0;
+            const h8 e = __builtin_bit_cast(h8, make_uint4(E[0], E[1], E[2], E[3]));
+#pragma unroll
+            for (int q = 0; q < 12; ++q) E[q] = E[q + 4];
+            h4 h1[4];
+            const h4 hh = density_net(e, sw, s, g, h1);
+            if (ok) {
+                if (h_out) *reinterpret_cast<h4*>(h_out + (int64_t)ic * 16 + 4 * g) = hh;
+                if (g == 0) sigmas[ic] = expf((float)hh[0]);  // TruncExp forward (custom_functions.py:165-167)
+            }
+            if constexpr (COLOR) {
+                const float dx = ok ? dirs[3 * (int64_t)ic] : 0.f, dy = ok ? dirs[3 * (int64_t)ic + 1] : 0.f,
+                            dz = ok ? dirs[3 * (int64_t)ic + 2] : 1.f;
+                float sh[4];
+                sh4_select(dx, dy, dz, g, sh);
+                const h8 cin = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3], hh[0], hh[1], hh[2], hh[3]};
+                h4 h3[4], h4v[4];
+                const h4 o = color_net(cin, sw, s, g, h3, h4v);
+                if (ok && g == 0) {
+                    rgbs[3 * (int64_t)ic] = sigmoid_h(o[0]);
+                    rgbs[3 * (int64_t)ic + 1] = sigmoid_h(o[1]);
+                    rgbs[3 * (int64_t)ic + 2] = sigmoid_h(o[2]);
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ backward
 // MLP backward helpers: v_mfma_f32_16x16x16_f16, whose B operand layout
 // B[k = 4g + j][n = s] IS the accumulator layout, so every gradient tile of
@@ -1286,6 +1437,23 @@ int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const 
     NGP_CHECK_ARG(xyzs && table_f16 && mlp_f16 && sigmas && (dirs != nullptr) == (rgbs != nullptr));
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0);
     hipStream_t s = as_stream(stream);
+    // register form (default) or the LDS-parked form (NGP_FEM_LDS=1, A/B)
+    static const bool reg_form = !(getenv("NGP_FEM_LDS") && getenv("NGP_FEM_LDS")[0] == '1');
+    if (reg_form) {
+        // grid = every resident block (the chunks are dealt over the whole grid)
+        if (!dirs) {
+            static const unsigned capd = resident_blocks(field_encode_mlp_reg_kernel<false>, 64 * FEM2_WAVES, 0);
+            NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_reg_kernel<false><<<std::max(1u, std::min(capd, (unsigned)((n + 64 * FEM2_WAVES - 1) / (64 * FEM2_WAVES)))), 64 * FEM2_WAVES, 0, s>>>(
+                xyzs, nullptr, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16,
+                (_Float16*)enc_pm, sigmas, nullptr, (_Float16*)h_f16));
+            return ngp_launch_status();
+        }
+        static const unsigned capr = resident_blocks(field_encode_mlp_reg_kernel<true>, 64 * FEM2_WAVES, 0);
+        NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_reg_kernel<true><<<std::max(1u, std::min(capr, (unsigned)((n + 64 * FEM2_WAVES - 1) / (64 * FEM2_WAVES)))), 64 * FEM2_WAVES, 0, s>>>(
+            xyzs, dirs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16,
+            (_Float16*)enc_pm, sigmas, rgbs, (_Float16*)h_f16));
+        return ngp_launch_status();
+    }
     if (!dirs) {
         static const unsigned capd = resident_blocks(field_encode_mlp_kernel<false>, 64 * FEM_WAVES, 0);
         NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_kernel<false><<<std::max(1u, std::min(capd, (unsigned)((n + 511) / 512))), 64 * FEM_WAVES, 0, s>>>(

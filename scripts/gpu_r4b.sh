@@ -1,0 +1,11 @@
+# Round 4: parity of the changed kernels + counters, the bench unit check, and an A/B of the forward forms.
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-r4b}; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests/test_field_gpu.py tests/test_vren_gpu.py tests/test_trainer_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+tail -n 2 $OUT/pytest.log
+Q="--no-cpu-baseline --quality-steps 0 --psnr-views 0 --infer-frames 0 --no-oracle-quality"
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 $Q > $OUT/bench20.json 2> $OUT/bench20.err
+python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[1], d['value'], d['ms_per_step'], r['frac'], r['ms_per_step'], json.dumps(r['units_check']))" $OUT/bench20.json
+bash scripts/ab_env.sh ${1:-r4b}/ab 2 "||" "|NGP_FEM_LDS=1|" "lib_w4||"

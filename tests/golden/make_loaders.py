@@ -1,9 +1,11 @@
 """Generate tests/golden/loaders.npz: the REFERENCE's own dataset loaders
-(datasets/nsvf.py NSVFDataset, datasets/nerf.py NeRFDataset, with their
-ray_utils.get_ray_directions and color_utils.read_image; read from
-/root/reference, never copied) run on small synthetic scenes written by
-write_scenes() below -- the fixture tests/test_loaders_golden_cpu.py holds
-this repo's loaders (ar-nerf_amd/datasets) to.
+(datasets/nsvf.py NSVFDataset, datasets/nerf.py NeRFDataset,
+datasets/colmap.py ColmapDataset with datasets/colmap_utils.py's binary
+readers, ray_utils.get_ray_directions / center_poses / create_spheric_poses
+and color_utils.read_image; read from /root/reference, never copied) run on
+small synthetic scenes written by write_scenes() below -- the fixture
+tests/test_loaders_golden_cpu.py holds this repo's loaders
+(ar-nerf_amd/datasets) to.
 
 The scenes: the analytic sphere+box (synthetic.AnalyticScene) at 100x100,
 (a) in NSVF layout under a 'Synthetic_NeRF' directory (rgb/{0,2}_*.png,
@@ -11,7 +13,15 @@ pose/*.txt, intrinsics.txt, bbox.txt) with RGBA frames whose alpha varies,
 so read_image's alpha blend onto white runs, and a bbox whose centre is off
 the origin (the pose shift / scale path); (b) in Blender layout
 (transforms_{train,test}.json with camera_angle_x and [right up back]
-transform matrices, RGBA PNGs).  Downsample 100/800 so the loaders' frame
+transform matrices, RGBA PNGs); (c) a COLMAP sparse model (sparse/0/
+{cameras,images,points3D}.bin written by this repo's writer in COLMAP's
+documented binary layout: one PINHOLE camera with fx != fy and an
+off-centre principal point, 10 images whose ids are not in name order --
+the loader's argsort by name -- posed in a rotated, shifted, scaled world so
+center_poses and the min-distance rescale do work, 64 points) with RGBA
+frames in images/ (ColmapDataset reads them with blend_a=False: rgb x alpha)
+-- splits train (i % 8 != 0), test (i % 8 == 0) and test_traj (120 spheric
+poses).  Downsample 100/800 for (a), (b) and 1 for (c), so the loaders' frame
 size equals the PNGs': no cv2.resize (cv2 is not in this container).
 
 Modules the reference imports but this container lacks are stubbed with
@@ -93,6 +103,61 @@ def write_scenes(base):
     return nsvf, blender
 
 
+N_COLMAP = 10
+
+
+def _rotmat2qvec(R):
+    """unit quaternion (w, x, y, z) of a rotation matrix (Shepperd's method)"""
+    tr = np.trace(R)
+    if tr > 0:
+        S = np.sqrt(tr + 1.0) * 2
+        q = [0.25 * S, (R[2, 1] - R[1, 2]) / S, (R[0, 2] - R[2, 0]) / S, (R[1, 0] - R[0, 1]) / S]
+    elif R[0, 0] > R[1, 1] and R[0, 0] > R[2, 2]:
+        S = np.sqrt(1.0 + R[0, 0] - R[1, 1] - R[2, 2]) * 2
+        q = [(R[2, 1] - R[1, 2]) / S, 0.25 * S, (R[0, 1] + R[1, 0]) / S, (R[0, 2] + R[2, 0]) / S]
+    elif R[1, 1] > R[2, 2]:
+        S = np.sqrt(1.0 + R[1, 1] - R[0, 0] - R[2, 2]) * 2
+        q = [(R[0, 2] - R[2, 0]) / S, (R[0, 1] + R[1, 0]) / S, 0.25 * S, (R[1, 2] + R[2, 1]) / S]
+    else:
+        S = np.sqrt(1.0 + R[2, 2] - R[0, 0] - R[1, 1]) * 2
+        q = [(R[1, 0] - R[0, 1]) / S, (R[0, 2] + R[2, 0]) / S, (R[1, 2] + R[2, 1]) / S, 0.25 * S]
+    q = np.array(q)
+    return q / np.linalg.norm(q)
+
+
+def write_colmap_scene(base):
+    """-> root of a COLMAP-layout scene under `base` (deterministic)"""
+    sys.path[:0] = [os.path.join(ROOT, "ar-nerf_amd")]
+    import synthetic as S
+    from datasets.png import write_png
+    from datasets import colmap_utils as CU
+    sc = S.AnalyticScene(W=RES, H=RES, n_images=N_COLMAP, seed=23)
+    root = os.path.join(base, "colmap_scene")
+    os.makedirs(os.path.join(root, "images"), exist_ok=True)
+    os.makedirs(os.path.join(root, "sparse", "0"), exist_ok=True)
+    # world = A (analytic frame): rotation about a tilted axis, shift, scale 3.7
+    ax = np.array([0.3, -0.5, 0.8]); ax /= np.linalg.norm(ax); th = 0.7
+    K_ = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    Rw = np.eye(3) + np.sin(th) * K_ + (1 - np.cos(th)) * K_ @ K_
+    tw, sw = np.array([1.3, -0.4, 2.2]), 3.7
+    cams = {1: CU.Camera(1, "PINHOLE", RES, RES, np.array([131.5, 127.25, 51.0, 48.5]))}
+    order = [3, 7, 0, 9, 1, 5, 8, 2, 6, 4]  # image ids not in name order
+    images = {}
+    for n, i in enumerate(order):
+        c2w = np.eye(4)
+        c2w[:3, :3] = Rw @ sc.poses[i, :, :3].double().numpy()
+        c2w[:3, 3] = sw * (Rw @ sc.poses[i, :, 3].double().numpy()) + tw
+        w2c = np.linalg.inv(c2w)
+        name = f"frame_{i:03d}.png"
+        images[n + 1] = CU.Image(n + 1, _rotmat2qvec(w2c[:3, :3]), w2c[:3, 3], 1, name, None, None)
+        write_png(os.path.join(root, "images", name), _rgba(sc, i))
+    g = np.random.default_rng(5)
+    pts = {k + 1: CU.Point3D(k + 1, sw * (Rw @ g.uniform(-0.5, 0.5, 3)) + tw, g.integers(0, 256, 3), 0.5, None, None)
+           for k in range(64)}
+    CU.write_model_binary(os.path.join(root, "sparse", "0"), cams, images, pts)
+    return root
+
+
 def install_stubs():
     from PIL import Image
     imageio = types.ModuleType("imageio")
@@ -139,11 +204,20 @@ def summarize(prefix, ds, out):
     out[prefix + "rays_shape"] = np.array(rays.shape)
 
 
+def summarize_colmap(prefix, ds, out):
+    summarize(prefix, ds, out)
+    out[prefix + "pts3d"] = np.asarray(ds.pts3d)
+    out[prefix + "blender_trans"] = np.asarray(ds.blender_trans)
+    out[prefix + "blender_scale"] = np.array(ds.blender_scale)
+
+
 def main():
     out = {}
     with tempfile.TemporaryDirectory() as tmp:
         nsvf, blender = write_scenes(tmp)
+        colmap = write_colmap_scene(tmp)
         install_stubs()
+        from datasets.colmap import ColmapDataset
         from datasets.nerf import NeRFDataset
         from datasets.nsvf import NSVFDataset
         ds_kw = dict(downsample=RES / 800)
@@ -153,6 +227,10 @@ def main():
             out["nsvf_shift"], out["nsvf_scale"] = np.asarray(d.shift), np.array(d.scale)
             d = NeRFDataset(blender, split=split, **ds_kw)
             summarize(f"nerf_{split}_", d, out)
+            d = ColmapDataset(colmap, split=split)
+            summarize_colmap(f"colmap_{split}_", d, out)
+        d = ColmapDataset(colmap, split="test_traj")
+        out["colmap_test_traj_poses"] = d.poses.numpy()
     path = os.path.join(HERE, "loaders.npz")
     np.savez_compressed(path, **out)
     print(path, os.path.getsize(path))
