@@ -835,6 +835,25 @@ __device__ __forceinline__ h4 mul_h4(h4 v, uint32_t f2) {
     return __builtin_bit_cast(h4, make_uint2(__builtin_bit_cast(uint32_t, __builtin_bit_cast(hx2, u.x) * f),
                                              __builtin_bit_cast(uint32_t, __builtin_bit_cast(hx2, u.y) * f)));
 }
+// v x 2^k (k <= 0) rounded once to fp16: one v_pk_mul_f16 by the fp16 factor
+// while 2^k is representable (k >= -24, subnormal factors included); below,
+// where the factor is not but the product may be (an fp16 subnormal or even
+// normal value), through fp32 -- the same single rounding
+__device__ __forceinline__ h4 scale_h4(h4 v, int k) {
+    if (k >= -24) return mul_h4(v, f16_pow2_x2(k));
+    const float f = ldexpf(1.0f, k);
+    return h4{(_Float16)((float)v[0] * f), (_Float16)((float)v[1] * f), (_Float16)((float)v[2] * f),
+              (_Float16)((float)v[3] * f)};
+}
+// max |c| over the units whose activation is nonzero (the ReLU' mask the
+// gradient tile gets; act = relu_h's fp16 output): the per-sample exponent
+// follows the values that are kept, not those of inactive units
+__device__ __forceinline__ float max4_act(f4 c, h4 act) {
+    const uint2 a = __builtin_bit_cast(uint2, act);
+    const float m0 = (a.x & 0xffffu) ? fabsf(c[0]) : 0.f, m1 = (a.x >> 16) ? fabsf(c[1]) : 0.f;
+    const float m2 = (a.y & 0xffffu) ? fabsf(c[2]) : 0.f, m3 = (a.y >> 16) ? fabsf(c[3]) : 0.f;
+    return fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+}
 // min over the wave's 16 samples of a per-sample int (lanes 0-15 hold samples 0-15)
 __device__ __forceinline__ int samples_min(int v) {
 #define NGP_DPP_ROR_I(x, n) __builtin_amdgcn_update_dpp(0, (x), 0x120 + (n), 0xf, 0xf, false)
@@ -1069,7 +1088,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             c4[t] = mfma16(lds4(sw + BT5 + (16 * t + s) * RT16 + 4 * g), do_h, z);
-            m = fmaxf(m, max4(c4[t]));
+            m = fmaxf(m, max4_act(c4[t], h4v[t]));
         }
         const int E4 = next_exp(sample_max(m), Eo);
         h4 da4h[4];
@@ -1087,7 +1106,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT4 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da4h[kt], c);
             c3[t] = c;
-            m = fmaxf(m, max4(c));
+            m = fmaxf(m, max4_act(c, h3[t]));
         }
         const int E3 = next_exp(sample_max(m), E4);
         h4 da3h[4];
@@ -1110,7 +1129,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             c1[t] = mfma16(lds4(sw + BT2 + (16 * t + s) * RT16 + 4 * g), dhh, z);
-            m = fmaxf(m, max4(c1[t]));
+            m = fmaxf(m, max4_act(c1[t], h1[t]));
         }
         const int E1 = next_exp(sample_max(m), Eh);
         h4 da1h[4];
@@ -1148,21 +1167,21 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         }
         __syncthreads();  // every wave's phase-2 reads of the previous iteration are done; emin[par] complete
         NGP_BWD_PHASE(3);
-        uint32_t fac[5];
+        int fk[5];  // per-sample re-scale exponents B - E_s (<= 0)
         int Bl[5];
 #pragma unroll
         for (int l = 0; l < 5; ++l) {
             const int4 a = *reinterpret_cast<const int4*>(&emin[par][l][0]);
             const int4 b = *reinterpret_cast<const int4*>(&emin[par][l][4]);
             Bl[l] = __builtin_amdgcn_readfirstlane(min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w))));
-            fac[l] = f16_pow2_x2(Bl[l] - Es[l]);
+            fk[l] = Bl[l] - Es[l];
         }
         // phase 1 (layers 5, 4, 3)
-        put_tile(mine + P_DO * TTILE, mul_h4(do_h, fac[0]), s, g);
+        put_tile(mine + P_DO * TTILE, scale_h4(do_h, fk[0]), s, g);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            put_tile(mine + (P_DA4 + t) * TTILE, mul_h4(da4h[t], fac[1]), s, g);
-            put_tile(mine + (P_DA3 + t) * TTILE, mul_h4(da3h[t], fac[2]), s, g);
+            put_tile(mine + (P_DA4 + t) * TTILE, scale_h4(da4h[t], fk[1]), s, g);
+            put_tile(mine + (P_DA3 + t) * TTILE, scale_h4(da3h[t], fk[2]), s, g);
             put_tile(mine + (P_H4 + t) * TTILE, h4v[t], s, g);
             put_tile(mine + (P_H3 + t) * TTILE, h3[t], s, g);
         }
@@ -1174,10 +1193,10 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         __syncthreads();  // phase-1 reads done: the regions take the phase-2 tiles
         NGP_BWD_PHASE(5);
         // ---- phase 2 (layers 2, 1)
-        put_tile(mine + Q_DH * TTILE, mul_h4(dhh, fac[3]), s, g);
+        put_tile(mine + Q_DH * TTILE, scale_h4(dhh, fk[3]), s, g);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            put_tile(mine + (Q_DA1 + t) * TTILE, mul_h4(da1h[t], fac[4]), s, g);
+            put_tile(mine + (Q_DA1 + t) * TTILE, scale_h4(da1h[t], fk[4]), s, g);
             put_tile(mine + (Q_H1 + t) * TTILE, h1[t], s, g);
         }
         // enc fragment: lane holds enc[8g + j] of sample s -> tile g>>1, units 8(g&1)+j

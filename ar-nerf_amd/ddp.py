@@ -5,8 +5,9 @@ The reference's only parallelism is Lightning DDP over per-rank 8192-ray
 batches (train.py:288): gradients all-reduced every step, buffers broadcast
 from rank 0 every forward (SURVEY.md §2 "Collective call sites").  Here:
   * ZeRO-1 over the flat parameter vector: the fp32 gradient is
-    reduce-scattered (SUM) in three buckets -- [MLP | coarse hash levels],
-    [binned levels, first half], [binned levels, second half] -- each rank
+    reduce-scattered (SUM) in 1 + K buckets -- [MLP | coarse hash levels],
+    then the binned levels in K level ranges (level_cuts, K = 4 by
+    default) -- each rank
     runs FusedAdam on its 1/world shard of every bucket only (fp32 master,
     moments; the 1/world mean is folded into Adam), and the updated fp16
     shadow the kernels read is all-gathered; a bucket's reduce-scatter, Adam
@@ -44,6 +45,17 @@ def shard_range(n, rank, world):
 def shard_cells(indices, coords, rank, world):
     lo, hi = shard_range(indices.shape[0], rank, world)
     return indices[lo:hi], coords[lo:hi]
+
+
+def level_cuts(lo, n_levels, k):
+    """[lo, c_1, ..., n_levels]: levels lo..n_levels-1 in k (at most one per
+    level) contiguous ranges whose sizes differ by at most one; [] when
+    there is no level to split."""
+    n = n_levels - lo
+    if n <= 0:
+        return []
+    k = max(1, min(int(k), n))
+    return [lo + (n * r) // k for r in range(k + 1)]
 
 
 def zero_buckets(n_params, splits, world, align=4):

@@ -47,7 +47,7 @@ class NGPTrainer:
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
                  device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=None, bin_level_lo=None,
                  chunk_first=64, erode=False, lambda_distortion=0.0, bin_merge_hi=None, fused_adam=True, use_graphs=True,
-                 pair_steps=False, emulate_dp=False):
+                 pair_steps=False, emulate_dp=False, dp_fine_buckets=4):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
@@ -97,13 +97,18 @@ class NGPTrainer:
             bin_samples_per_ray = 512 if big else 128
         self.hash_backward = hash_backward
         self.bin_level_lo = 0 if hash_backward == "binned" else min(max(int(bin_level_lo), 0), self.grid.n_levels)
-        # ZeRO-1 layout (ddp.zero_buckets): buffers padded to n_pad, three
-        # buckets [MLP | coarse levels] [binned levels lo..mid) [mid..16),
-        # split where the coarse (atomic) gradient, then the first binned level
-        # range, are complete; rank r owns shard r of each bucket.  All levels
-        # binned (bin_level_lo 0): bucket 0 is the MLP alone.
-        self.bin_level_mid = (self.bin_level_lo + self.grid.n_levels + 1) // 2
-        splits = [HG.MLP_PARAMS + 2 * int(self.grid.offsets[lv]) for lv in (self.bin_level_lo, self.bin_level_mid)]
+        # ZeRO-1 layout (ddp.zero_buckets): buffers padded to n_pad; bucket 0 =
+        # [MLP | coarse levels], then the binned levels in dp_fine_buckets level
+        # ranges (bin_cuts: [lo, c_1), [c_1, c_2), ...), each split where its
+        # gradient is complete -- the world > 1 step accumulates the ranges in
+        # turn and reduce-scatters / steps / all-gathers each range's bucket
+        # on the comm stream while the next range accumulates, so only the
+        # last range's chain is exposed after the backward; rank r owns shard
+        # r of each bucket.  All levels binned (bin_level_lo 0): bucket 0 is
+        # the MLP alone.
+        self.bin_cuts = ddp.level_cuts(self.bin_level_lo, self.grid.n_levels, dp_fine_buckets)
+        splits = [HG.MLP_PARAMS + 2 * int(self.grid.offsets[lv]) for lv in self.bin_cuts[:-1]] or \
+            [HG.MLP_PARAMS + 2 * int(self.grid.offsets[self.grid.n_levels])]
         self.n_pad, self.buckets = ddp.zero_buckets(n, splits, self.dp_world)
         pb = torch.zeros(self.n_pad, device=dev)
         pb[:n] = init
@@ -602,19 +607,22 @@ class NGPTrainer:
             self._run_graph(key + ("compute",), lambda: self._segment_compute(k, gt, directions, poses, update_after))
             if self.hash_backward != "atomic":
                 # coarse levels (side stream) -> bucket 0's reduce-scatter, Adam, all-gather on the
-                # comm stream while the binned levels run here in two level ranges, each range's
-                # bucket following it on the comm stream while the next range accumulates
+                # comm stream while the binned levels run here range by range (bin_cuts), each
+                # range's bucket following it on the comm stream while the next range accumulates
                 self.bwd_stream.wait_stream(cs)
                 with torch.cuda.stream(self.bwd_stream):
                     self._run_graph(key + ("coarse",), self._segment_coarse)
                 comm.wait_stream(self.bwd_stream)
                 self._bucket_update(0)
-                nb = len(self.buckets)  # 3 unless a level range is empty
-                for i, seg in enumerate((self._segment_apply_a, self._segment_apply_b)):
-                    self._run_graph(key + ("apply", i), seg)
+                nr = len(self.bin_cuts) - 1
+                for r in range(nr):
+                    self._run_graph(key + ("apply", r), lambda r=r: self._segment_apply(r))
                     comm.wait_stream(cs)
-                    for j in ((1,) if nb == 3 else ()) if i == 0 else range(2 if nb == 3 else 1, nb):
-                        self._bucket_update(j)
+                    # (a range's bucket; a bucket emptied by the alignment was dropped: the rest
+                    # follow the last range)
+                    for j in ([1 + r] if r < nr - 1 else range(1 + r, len(self.buckets))):
+                        if j < len(self.buckets):
+                            self._bucket_update(j)
             else:
                 comm.wait_stream(cs)
                 for i in range(len(self.buckets)):
@@ -713,20 +721,19 @@ class NGPTrainer:
         """world > 1 graph segment (side stream): the atomic coarse hash levels."""
         self._coarse_levels()
 
-    def _segment_apply_a(self):
-        """world > 1 graph segment (main stream): the binned levels' record
-        write, then the accumulation of levels [bin_level_lo, bin_level_mid)."""
-        HGL = HG._lib()
-        vren._ok(HGL.ngp_hash_binned_write(_p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                                           HG.ctypes.byref(self.grid.desc), _p(self.denc),
-                                           _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
-                                           self.bin_level_lo, self.bin_merge_hi, vren._stream()), "hash_binned_write")
-        self._accum_levels(self.bin_level_lo, self.bin_level_mid)
-
-    def _segment_apply_b(self):
-        """world > 1 graph segment (main stream): accumulation of the binned
-        levels [bin_level_mid, 16) (beside bucket 1's reduce-scatter)."""
-        self._accum_levels(self.bin_level_mid, self.grid.n_levels)
+    def _segment_apply(self, r):
+        """world > 1 graph segment r (main stream): accumulation of the binned
+        level range [bin_cuts[r], bin_cuts[r + 1]) (beside the previous
+        range's bucket chain on the comm stream); segment 0 first writes the
+        binned levels' records."""
+        if r == 0:
+            HGL = HG._lib()
+            vren._ok(HGL.ngp_hash_binned_write(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                               _p(self.sample_idx), HG.ctypes.byref(self.grid.desc), _p(self.denc),
+                                               _p(self.grad[HG.MLP_PARAMS:]), _p(self.bin_ws), self.bin_max_samples,
+                                               self.bin_level_lo, self.bin_merge_hi, vren._stream()),
+                     "hash_binned_write")
+        self._accum_levels(self.bin_cuts[r], self.bin_cuts[r + 1])
 
     def _accum_levels(self, lo, hi):
         vren._ok(HG._lib().ngp_hash_binned_accum_levels(
@@ -882,7 +889,7 @@ class NGPTrainer:
             # (world > 1 graph segments: the hash backward runs as two more
             # graphs -- coarse levels on the side stream, binned levels here --
             # so the reduce-scatter of the [MLP | coarse] bucket overlaps the
-            # binned levels; _replay / _segment_coarse / _segment_apply_a, _b)
+            # binned levels; _replay / _segment_coarse / _segment_apply)
             cs.wait_stream(bs)
             return self.out_loss
         self._ev("hash_bwd", 0)

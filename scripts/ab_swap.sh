@@ -7,6 +7,7 @@ TAG=$1; REPS=$2; DEST=$3; ALT=$4
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cp "$DEST" "$OUT/A.src"
+trap 'cp "$OUT/A.src" "$DEST"' EXIT  # the tree's source is restored however the loop ends
 for rep in $(seq 1 $REPS); do
   for v in A B; do
     if [ $v = A ]; then cp "$OUT/A.src" "$DEST"; else cp "$ALT" "$DEST"; fi
@@ -15,4 +16,3 @@ for rep in $(seq 1 $REPS); do
     python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value']/1e6,3), 'M rays/s', round(d['ms_per_step']*1e3,1), 'us/step')" "$OUT/${v}_$rep.json" "$v"
   done
 done
-cp "$OUT/A.src" "$DEST"

@@ -98,19 +98,29 @@ def test_shard_range_covers_exactly_once(n, world):
 
 
 @pytest.mark.parametrize("world", [1, 2, 8])
-def test_zero_buckets_split_where_the_gradient_is_complete(world):
-    """The trainer's three ZeRO-1 buckets ([MLP | coarse levels], binned
-    levels lo..mid, mid..16; trainer.NGPTrainer.__init__): contiguous, cover
-    the padded vector once, equal 16-byte shards per rank, and each split is
-    rounded DOWN -- a bucket never holds an entry of a later level range, so
-    its reduce-scatter may start once its own range is complete."""
+@pytest.mark.parametrize("lo,k", [(8, 4), (8, 2), (0, 4), (16, 4)])
+def test_zero_buckets_split_where_the_gradient_is_complete(world, lo, k):
+    """The trainer's ZeRO-1 buckets ([MLP | coarse levels], then the binned
+    levels lo..16 in k ranges, ddp.level_cuts; trainer.NGPTrainer.__init__):
+    contiguous, cover the padded vector once, equal 16-byte shards per rank,
+    and each split is rounded DOWN -- a bucket never holds an entry of a later
+    level range, so its reduce-scatter may start once its own range is
+    complete."""
     import hashgrid as HG
     grid = HG.HashGrid(0.5)
     n = HG.MLP_PARAMS + 2 * int(grid.offsets[grid.n_levels])
-    splits = [HG.MLP_PARAMS + 2 * int(grid.offsets[lv]) for lv in (8, 12)]
+    cuts = ddp.level_cuts(lo, grid.n_levels, k)
+    if lo == grid.n_levels:
+        assert cuts == []
+        return
+    assert cuts[0] == lo and cuts[-1] == grid.n_levels and len(cuts) == min(k, grid.n_levels - lo) + 1
+    sizes = [b - a for a, b in zip(cuts[:-1], cuts[1:])]
+    assert min(sizes) >= 1 and max(sizes) - min(sizes) <= 1
+    splits = [HG.MLP_PARAMS + 2 * int(grid.offsets[lv]) for lv in cuts[:-1]]
     n_pad, b = ddp.zero_buckets(n, splits, world)
     assert n_pad >= n and n_pad % (4 * world) == 0
     assert b[0][0] == 0 and b[-1][1] == n_pad and all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
-    assert len(b) == 3 and all((hi - lo) % (4 * world) == 0 for lo, hi in b)
-    assert b[0][1] <= splits[0] and b[1][1] <= splits[1] and splits[1] - b[1][1] < 4 * world
+    assert len(b) == len(cuts) and all((hi - lo_) % (4 * world) == 0 for lo_, hi in b)
+    for i, sp in enumerate(splits):
+        assert b[i][1] <= sp and sp - b[i][1] < 4 * world
     assert ddp.zero_buckets(n, splits[0], world)[1][0][1] == b[0][1]  # (an int split: two buckets)
