@@ -74,6 +74,36 @@ struct AdamArgs {
     float b1, b2, eps, grad_scale;
 };
 
+// Step completion ticket (ngp_step_ticket_set): the last kernels of a
+// training step (the Adam launches, `parties` of them) advance the per-step
+// device counters themselves once every block of every one of them has
+// finished -- in place of a separate increment launch that would join their
+// streams.  ws (caller-owned, zeroed once): [0..7] blocks arrived per party,
+// [8] parties complete; the last arriver resets them.
+struct StepTicket {
+    uint32_t* ws;
+    int64_t* counters;
+    int n, parties, party;
+};
+// every thread of the block, after its last read of the counters
+__device__ __forceinline__ void step_ticket_arrive(const StepTicket& t) {
+    if (!t.ws) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's counter loads have returned)
+    __syncthreads();                                  // every wave of the block is past its reads
+    if (threadIdx.x == 0) {
+        const uint32_t nb = gridDim.x * gridDim.y * gridDim.z;
+        if (atomicAdd(&t.ws[t.party], 1u) == nb - 1) {  // this launch's last block
+            atomicExch(&t.ws[t.party], 0u);
+            if (atomicAdd(&t.ws[8], 1u) == (uint32_t)t.parties - 1) {  // the step's last launch
+                atomicExch(&t.ws[8], 0u);
+                for (int i = 0; i < t.n; ++i) atomicAdd((unsigned long long*)&t.counters[i], 1ull);
+            }
+        }
+    }
+}
+// the ticket of the next participating launch (host side; none when unset)
+StepTicket ngp_step_ticket_next();
+
 // helper_math.h:280-283 clamp(f,a,b) = fmaxf(a, fminf(f,b)) -- keeps the
 // NaN behaviour of fminf/fmaxf that the marcher relies on.
 __device__ __forceinline__ float clampf(float f, float a, float b) { return fmaxf(a, fminf(f, b)); }

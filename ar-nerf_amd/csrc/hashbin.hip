@@ -685,21 +685,23 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
 // not step: one workgroup per bucket, from the gradient in memory.
 __global__ void __launch_bounds__(256) hash_adam_residual_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
                                                                   float* __restrict__ grad, BinWs ws, AdamArgs adam,
-                                                                  uint32_t b_lo) {
+                                                                  uint32_t b_lo, StepTicket ticket) {
     const uint32_t b = b_lo + blockIdx.x;
-    if (b >= nbt || fused_bucket(ws, b, ws.fb[MAXB] != 0)) return;
-    float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
-    adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
-    const uint32_t l = bucket_level(ba, b), lb = b - ba.bbase[l];
-    const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
-    const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
-    float4* g4 = reinterpret_cast<float4*>(grad + gbase);
-    const float sc = adam.grad_scale;
-    for (uint32_t e = threadIdx.x; e < 2 * ne / 4; e += blockDim.x) {
-        const float4 gv = g4[e];
-        adam4(adam, gbase, e, make_float4(gv.x * sc, gv.y * sc, gv.z * sc, gv.w * sc), lr, bc1, bc2);
-        g4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (b < nbt && !fused_bucket(ws, b, ws.fb[MAXB] != 0)) {  // (block-uniform)
+        float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
+        adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
+        const uint32_t l = bucket_level(ba, b), lb = b - ba.bbase[l];
+        const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
+        const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
+        float4* g4 = reinterpret_cast<float4*>(grad + gbase);
+        const float sc = adam.grad_scale;
+        for (uint32_t e = threadIdx.x; e < 2 * ne / 4; e += blockDim.x) {
+            const float4 gv = g4[e];
+            adam4(adam, gbase, e, make_float4(gv.x * sc, gv.y * sc, gv.z * sc, gv.w * sc), lr, bc1, bc2);
+            g4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
+    step_ticket_arrive(ticket);  // (after the accumulation launch before it: its reads are done too)
 }
 
 static int bin_args(const ngp_hashgrid_t* grid, int64_t tiles_cap, int lo, int merge_hi, BinArgs& ba,
@@ -786,7 +788,8 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
         if (adam) {
             NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<true><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam, b_lo, b_hi));
             if (b_hi > b_lo)
-                NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<b_hi - b_lo, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam, b_lo));
+                NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<b_hi - b_lo, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam, b_lo,
+                                                                                             ngp_step_ticket_next()));
         } else {
             NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<false><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}, b_lo, b_hi));
         }

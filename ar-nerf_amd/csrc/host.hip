@@ -29,7 +29,33 @@ void ngp_timing_mark(int id, int end, hipStream_t s) {
                                   ((int64_t)id * g_per + i) * 2 + (end ? 1 : 0));
 }
 
+static ngp::StepTicket g_ticket{nullptr, nullptr, 0, 0, 0};
+static int g_ticket_next = 0;
+
+ngp::StepTicket ngp::ngp_step_ticket_next() {
+    if (!g_ticket.ws) return StepTicket{nullptr, nullptr, 0, 0, 0};
+    StepTicket t = g_ticket;
+    t.party = g_ticket_next++;
+    if (t.party >= t.parties) t.ws = nullptr;  // (more launches than declared: checked by the setter's caller)
+    return t;
+}
+
 extern "C" {
+
+int ngp_step_ticket_set(void* ws, int64_t* counters, int n_counters, int parties) {
+    if (ws && (!counters || n_counters < 1 || n_counters > 8 || parties < 1 || parties > 8 ||
+               ((uintptr_t)ws & 3) != 0))
+        return NGP_EINVAL;
+    const int used = g_ticket_next;
+    const bool was = g_ticket.ws != nullptr;
+    const int declared = g_ticket.parties;
+    g_ticket = ngp::StepTicket{(uint32_t*)ws, ws ? counters : nullptr, ws ? n_counters : 0, ws ? parties : 0, 0};
+    g_ticket_next = 0;
+    // clearing after a capture: exactly `parties` launches must have taken a ticket
+    return (was && !ws && used != declared) ? NGP_ERANGE : NGP_OK;
+}
+
+size_t ngp_step_ticket_workspace(void) { return 64; }
 
 const char* ngp_version(void) { return "ngp_amd 0.2 gfx950"; }
 

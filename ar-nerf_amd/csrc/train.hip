@@ -431,7 +431,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2,
                                                    float grad_scale, int zero_grad, const float* __restrict__ lr_dev,
                                                    const int64_t* __restrict__ step_dev, float* __restrict__ rep = nullptr,
-                                                   int64_t rep_lo4 = 0, int64_t rep4 = 0, int nrep = 0) {
+                                                   int64_t rep_lo4 = 0, int64_t rep4 = 0, int nrep = 0,
+                                                   StepTicket ticket = StepTicket{nullptr, nullptr, 0, 0, 0}) {
     adam_bias(lr_dev, step_dev, b1, b2, lr, bc1, bc2);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -472,6 +473,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         reinterpret_cast<h4*>(p16)[i] = out;
         if (zero_grad) reinterpret_cast<float4*>(grad)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    step_ticket_arrive(ticket);
 }
 
 // --------------------------------------------------- occupancy grid update
@@ -1250,7 +1252,8 @@ int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_av
     if (blocks > 8192) blocks = 8192;
     NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
-                                                                 1.f, grad_scale, zero_grad, lr_dev, step_dev));
+                                                                 1.f, grad_scale, zero_grad, lr_dev, step_dev, nullptr, 0,
+                                                                 0, 0, ngp_step_ticket_next()));
     return ngp_launch_status();
 }
 
@@ -1271,7 +1274,7 @@ int ngp_adam_step_dev_rep(float* params, float* grads, float* exp_avg, float* ex
     NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
                                                                  1.f, grad_scale, zero_grad, lr_dev, step_dev, rep,
-                                                                 rep_offset / 4, rep_n / 4, n_rep));
+                                                                 rep_offset / 4, rep_n / 4, n_rep, ngp_step_ticket_next()));
     return ngp_launch_status();
 }
 

@@ -257,6 +257,16 @@ class NGPTrainer:
         # device step counters: [0] Adam steps taken, [1] batches drawn (RNG
         # counter), [2] device-sampled occupancy updates (their RNG counter)
         self.dctr = torch.zeros(3, dtype=torch.int64, device=dev)
+        # steady-state graphs of the fused single-process step: the step's two Adam launches
+        # (MLP + coarse levels on the side stream, the binned levels' residual Adam on the
+        # main stream) advance dctr[0:2] themselves through a completion ticket
+        # (ngp_step_ticket_set) -- no increment launch joining the step's streams at its end
+        # (NGP_STEP_TICKET=0: the increment launch)
+        self._ticket_ws = torch.zeros((vren.lib().ngp_step_ticket_workspace() + 3) // 4, dtype=torch.int32,
+                                      device=dev)
+        import os
+        self.step_ticket = os.environ.get("NGP_STEP_TICKET", "1") != "0"
+        self._ticket_active = False
         self._updated_for = -1  # global step whose occupancy update already ran (end of the previous graph)
         self.lr_dev = torch.full((1,), float(lr), device=dev)
         self._lr_set = float(lr)
@@ -763,6 +773,13 @@ class NGPTrainer:
         if self.world > 1:  # (emulation: the shard's shadow is in place already)
             ddp.all_gather_(self._p16buf[a:b], self._p16buf[lo:hi], self.pg)
 
+    def _ticket_ok(self):
+        """The step's counters advanced by its two Adam launches (fused
+        single-process hybrid step, no measurement stamps, which index their
+        rows by the counter)."""
+        return (self.step_ticket and self.fused_adam and not self.dp and self.hash_backward != "atomic"
+                and self.timer is None)
+
     def _graph_body(self, k, gt, directions, poses, update_after=False):
         self.cur = k
         self._bind(self.msets[k])
@@ -772,6 +789,16 @@ class NGPTrainer:
                 self.march_stream.wait_stream(cs)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
 
+            if self._ticket_ok():
+                vren._ok(self.L.ngp_step_ticket_set(_p(self._ticket_ws), _p(self.dctr), 2, 2), "step_ticket")
+                self._ticket_active = True
+                try:
+                    self._compute(self.rgb_gt, True, fork)
+                finally:
+                    self._ticket_active = False
+                    vren._ok(self.L.ngp_step_ticket_set(None, None, 0, 0), "step_ticket (launches != parties)")
+                cs.wait_stream(self.march_stream)
+                return
             self._compute(self.rgb_gt, True, fork)
             cs.wait_stream(self.march_stream)
             vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
@@ -910,6 +937,10 @@ class NGPTrainer:
                 self._coarse_levels(fold=not fold_in_adam)
                 self._ev("hash_bwd_coarse", 1)
                 if adam_split:
+                    if self._ticket_active:
+                        # the ticketed Adam launches advance the batch counter: the next batch's
+                        # draw (march stream, forked at the step start) reads it first
+                        bs.wait_stream(self.march_stream)
                     self._adam(0, split, vren._stream(), rep=fold_in_adam)
             cs.wait_event(planned)
             self._ev("hash_binned_apply", 0)

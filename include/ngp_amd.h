@@ -524,6 +524,21 @@ int ngp_ray_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_row
 int ngp_ray_segments_capped(const int64_t* rays_a, int64_t n_rows, int cap, int64_t* start_ws, int64_t* total,
                             int64_t* total_acc, int32_t* sample_idx, void* stream);
 
+/* Step completion ticket.  Between ngp_step_ticket_set(ws, counters, n,
+ * parties) and ngp_step_ticket_set(NULL, ...), the next `parties` launches of
+ * the Adam kernels (ngp_adam_step_dev / _dev_rep; the residual Adam of
+ * ngp_hash_binned_apply_adam / _accum_adam) take a ticket: when every block
+ * of every one of them has finished, the last one adds 1 to counters[0..n)
+ * (device-scope atomics) -- a step's Adam launches advance the step counters
+ * themselves, without a separate increment launch joined after them (the
+ * caller must order every other reader of the counters before those
+ * launches).  ws: ngp_step_ticket_workspace() bytes, 4-byte aligned, zeroed
+ * once, owned by the call site.  Clearing returns NGP_ERANGE if the number
+ * of launches that took a ticket differs from `parties`.  Host-side state of
+ * the library (like ngp_timing_set): set it around one capture at a time. */
+int ngp_step_ticket_set(void* ws, int64_t* counters, int n_counters, int parties);
+size_t ngp_step_ticket_workspace(void);
+
 /* apex FusedAdam step (train.py:146; weight decay 0) over n (multiple of 4)
  * fp32 params with grad *= grad_scale, bias corrections for `step` (1-based);
  * writes the fp16 shadow params_f16 and, if zero_grad, zeroes grads. */

@@ -10,21 +10,18 @@ and march noise of every step, drawn on the host and given to step()) -- on
 the device.  Occupancy cells are drawn by each side's own RNG (same
 distribution), so trajectories are compared through the PSNR.
 
-Two oracle fixtures, which differ in ONE place, the precision of the
-gradients the glue hands back into the tcnn modules:
+The fixtures, which differ in the precision at the tcnn-module boundary:
   * quality_oracle.json (+ _occ1 / _occ2: other occupancy draws) -- the
-    modules return fp16, as tinycudann's do, so dL/dh (TruncExp's backward)
-    and dL/drgb are rounded to fp16 WITHOUT a loss scale at that boundary,
-    exactly as in the reference (tcnn scales only inside its own backward):
-    magnitudes below 2^-24 flush to zero.  24.55-24.69 dB.
-  * quality_oracle_f32out.json -- the same glue with those gradients kept in
-    fp32: the precision of the product's MLP backward, which carries every
-    gradient in fp16 at a per-sample power-of-two scale (field.hip).
-At a trained state the two gradients differ by 30-58 % relative L2 in the
-density MLP and every hash level (scripts/quality_grad_check.py: the
-underflow), and the product trains to ~1.3 dB above the reference-precision
-runs.  The bar: the product within 0.2 dB of the like-precision oracle, and
-never more than 0.2 dB below the reference-precision runs."""
+    reference's precision: the tcnn modules return fp16, as tinycudann's do,
+    so the gradients the glue hands back into them (dL/dh from TruncExp's
+    backward, dL/drgb) are rounded to fp16 -- at the loss scale of the
+    GradScaler that Lightning's precision=16 attaches (train.py:291: init
+    2^16, x0.5 and a skipped step on inf / nan, x2 after 2000 clean steps),
+    as on the GPU; the gradients are unscaled in fp32 before Adam;
+  * quality_oracle_f32out.json -- the same glue with that boundary in fp32
+    (no rounding there at all).
+The bar: the product within 0.2 dB of the reference-precision runs (the
+range of the three occupancy draws, widened by 0.2 dB on each side)."""
 import json
 import os
 import sys
@@ -41,25 +38,27 @@ BAR_DB = 0.2  # north_star: PSNR within 0.2 dB of the reference
 
 def _fx(name):
     with open(os.path.join(GOLD, name)) as f:
-        return json.load(f)["test_psnr"]
+        return json.load(f)
 
 
 @pytest.mark.parametrize("mode", ["default", "exact"])
-def test_test_psnr_against_the_fp32_oracle_runs(mode):
+def test_test_psnr_against_the_reference_precision_oracle_runs(mode):
     """default: the product path (chunked field evaluation, hybrid hash
     backward); exact: every marched sample through the field, per-sample
     atomic hash backward.  Both take fp16 MFMA operands in the MLP forward
     and backward, weight gradients included (tcnn's precision)."""
     import make_quality as MQ
-    ref_prec = [_fx(n) for n in ("quality_oracle.json", "quality_oracle_occ1.json", "quality_oracle_occ2.json")]
-    f32_prec = _fx("quality_oracle_f32out.json")
+    refs = [_fx(n) for n in ("quality_oracle.json", "quality_oracle_occ1.json", "quality_oracle_occ2.json")]
+    assert all(r.get("grad_scaler") for r in refs), "the reference-precision fixtures model the AMP GradScaler"
+    ref_prec = [r["test_psnr"] for r in refs]
+    f32_prec = _fx("quality_oracle_f32out.json")["test_psnr"]
     kw = {} if mode == "default" else dict(chunk_first=0, hash_backward="atomic")
     res = MQ.product_run("cuda", **kw)
     p = res["test_psnr"]
-    print(f"[{mode}] product test PSNR {p:.3f} dB (views {res['test_psnr_views']}); fp32 oracle, fp32 tcnn "
-          f"boundary {f32_prec:.3f} dB ({p - f32_prec:+.3f}); fp32 oracle, fp16 tcnn boundary (the reference's "
-          f"precision) {min(ref_prec):.3f}-{max(ref_prec):.3f} dB ({p - max(ref_prec):+.3f}); final loss "
-          f"{res['final_loss_mean_last_100']:.3e}; {res['steps']} steps in {res['train_wall_s']} s")
+    print(f"[{mode}] product test PSNR {p:.3f} dB (views {res['test_psnr_views']}); fp32 oracle at the reference's "
+          f"precision (fp16 tcnn boundary under the GradScaler) {min(ref_prec):.3f}-{max(ref_prec):.3f} dB "
+          f"({p - sum(ref_prec) / len(ref_prec):+.3f} vs their mean); fp32 boundary {f32_prec:.3f} dB "
+          f"({p - f32_prec:+.3f}); final loss {res['final_loss_mean_last_100']:.3e}; {res['steps']} steps in "
+          f"{res['train_wall_s']} s")
     assert torch.isfinite(torch.tensor(res["loss_curve_every_50"])).all()
-    assert abs(p - f32_prec) <= BAR_DB, (p, f32_prec)
-    assert p >= min(ref_prec) - BAR_DB, (p, ref_prec)
+    assert min(ref_prec) - BAR_DB <= p <= max(ref_prec) + BAR_DB, (p, ref_prec)

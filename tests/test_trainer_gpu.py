@@ -321,3 +321,37 @@ def test_pair_step_replays_match_single_steps():
           f"losses {la:.5f} {lb:.5f} {lp:.5f}")
     assert float((pp - pa).norm()) <= 3 * noise + 1e-3 * float(pa.norm())
     assert abs(lp - la) <= 0.1 * abs(la) + 3 * abs(lb - la)
+
+
+def test_step_ticket_replays_match_the_increment_launch():
+    """Steady-state graphs advance the device step / batch counters from the
+    step's two Adam launches (ngp_step_ticket_set: the last block of the last
+    of them adds 1) instead of a separate increment launch joined after both:
+    after the same schedule from the same seed the counters end at the same
+    values, the ticket workspace is back to zero, the losses agree, and the
+    parameters differ from an
+    increment-launch run no more than two increment-launch runs differ from
+    each other (float-atomic order noise)."""
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    outs = []
+    for ticket in (False, False, True):
+        tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, warmup_steps=16)
+        tr.step_ticket = ticket
+        tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
+        losses = []
+        for _ in range(120):
+            losses.append(float(tr.train_step(gt_img, dirs, poses).mean()))
+        tr.drain()
+        torch.cuda.synchronize()
+        outs.append((tr.params.clone(), losses, tr.dctr.clone(), int(tr._ticket_ws.abs().sum()), len(tr._graphs)))
+    (pa, la, ca, _, ga), (pb, lb, cb, _, _), (pt, lt, ct, wt, gt_) = outs
+    assert ga >= 1 and gt_ >= 1  # graph replays ran
+    assert torch.equal(ct, ca) and torch.equal(ca, cb) and int(ca[0]) == 120, (ca, ct)
+    assert wt == 0
+    assert lt[0] == la[0]  # (same first batch; later losses carry float-atomic order noise)
+    assert abs(sum(lt[-20:]) - sum(la[-20:])) <= 0.1 * abs(sum(la[-20:])) + 3 * abs(sum(lb[-20:]) - sum(la[-20:]))
+    noise = float((pb - pa).norm())
+    print(f"ticket vs increment launch {float((pt - pa).norm()):.3f}, increment vs increment {noise:.3f}")
+    assert float((pt - pa).norm()) <= 3 * noise + 1e-3 * float(pa.norm())
