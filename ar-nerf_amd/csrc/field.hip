@@ -923,10 +923,20 @@ __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& 
 #define NGP_BWD_PHASE(k)
 #define NGP_BWD_EDGE(k)
 #endif
-constexpr int CW = 8, NT1 = 19, NT2 = 11, CSCRW = NT1 * TTILE;
+#ifndef NGP_BWD_REMAT
+#define NGP_BWD_REMAT 0
+#endif
+#ifndef NGP_BWD_CW
+#define NGP_BWD_CW 8  // waves per block (CW / 4 per SIMD); 12 fits the LDS (161 KB) at <= 168 VGPRs
+#endif
+constexpr int CW = NGP_BWD_CW, NT1 = 19, NT2 = 11, CSCRW = NT1 * TTILE;
 constexpr int COOP_LDS_HALFS = SCR + CW * CSCRW;
+static_assert(CW % 4 == 0, "waves per block: a multiple of 4");
 static_assert(NGP_MLP_PARAMS <= CW * CSCRW && NT2 <= NT1, "raw weight staging / phase-2 tiles exceed the scratch");
 static_assert(COOP_LDS_HALFS * 2 <= 160 * 1024, "cooperative MLP backward exceeds the LDS");
+// output tiles per phase (phase 1: layers 5, 4, 3 = 4 + 16 + 8; phase 2: layers 2, 1 = 4 + 8), dealt
+// to the CW waves in contiguous runs (tiles sharing a G operand stay together), at most KT1 / KT2 each
+constexpr int NK1 = 28, NK2 = 12, KT1 = (NK1 + CW - 1) / CW, KT2 = (NK2 + CW - 1) / CW;
 // phase-1 / phase-2 tile ids inside a wave's region
 constexpr int P_DO = 0, P_DA4 = 1, P_DA3 = 5, P_H4 = 9, P_H3 = 13, P_C = 17;
 constexpr int Q_DH = 0, Q_DA1 = 1, Q_H1 = 5, Q_E = 9;
@@ -949,12 +959,15 @@ __device__ __forceinline__ void coop_tile_ops(int k, int& gid, int& hid) {
     hid = Q_E + ((k - 32) & 1);
 }
 
-// phase 1: waves 0-3 own tiles 4w..4w+3, waves 4-7 own 16+3(w-4)..+2;
-// phase 2: waves 0-3 own 28+w, waves 4-7 own 32+2(w-4), +1
-__device__ __forceinline__ int coop_k1(int w, int t) { return w < 4 ? 4 * w + t : 16 + 3 * (w - 4) + t; }
-__device__ __forceinline__ int coop_n1(int w) { return w < 4 ? 4 : 3; }
-__device__ __forceinline__ int coop_k2(int w, int t) { return w < 4 ? 28 + w : 32 + 2 * (w - 4) + t; }
-__device__ __forceinline__ int coop_n2(int w) { return w < 4 ? 1 : 2; }
+// wave w owns tiles [start, start + n) of a phase of NK tiles: the first NK % CW waves one more
+template <int NK>
+__device__ __forceinline__ int coop_start(int w) { return w * (NK / CW) + min(w, NK % CW); }
+template <int NK>
+__device__ __forceinline__ int coop_count(int w) { return NK / CW + (w < NK % CW ? 1 : 0); }
+__device__ __forceinline__ int coop_k1(int w, int t) { return coop_start<NK1>(w) + t; }
+__device__ __forceinline__ int coop_n1(int w) { return coop_count<NK1>(w); }
+__device__ __forceinline__ int coop_k2(int w, int t) { return NK1 + coop_start<NK2>(w) + t; }
+__device__ __forceinline__ int coop_n2(int w) { return coop_count<NK2>(w); }
 
 // layer of output tile k: 0 = W5 (G = dL/dout), 1 = W4 (dL/da4), 2 = W3 (dL/da3),
 // 3 = W2 (dL/dh), 4 = W1 (dL/da1)
@@ -999,13 +1012,13 @@ __device__ __forceinline__ void coop_dw(const _Float16* scr, int w, int s, int g
         if (t < n) acc[t] = part[t] * sc[t] + acc[t];
 }
 
-__global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
+__global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
     const _Float16* __restrict__ enc, const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig,
     const float* __restrict__ dL_drgb, float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride) {
     extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
     // per-wave minima of the layers' per-sample exponents (double-buffered by iteration parity)
-    __shared__ int emin[2][5][CW];
+    __shared__ __attribute__((aligned(16))) int emin[2][5][CW];
     _Float16* sw = smem;
     _Float16* scr = smem + SCR;
     NGP_BWD_EDGE(0);
@@ -1014,7 +1027,11 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     _Float16* mine = scr + wid * CSCRW;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    f4 acc1[4] = {z, z, z, z}, acc2[2] = {z, z};
+    f4 acc1[KT1], acc2[KT2];
+#pragma unroll
+    for (int t = 0; t < KT1; ++t) acc1[t] = z;
+#pragma unroll
+    for (int t = 0; t < KT2; ++t) acc2[t] = z;
     struct In {
         h8 e;
         float dx, dy, dz, dsig, gr[3];
@@ -1059,6 +1076,14 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         load_in(i_next, nxt);
         i_next = row_index(base + s + 2 * stride);
         NGP_BWD_PHASE(0);
+#if NGP_BWD_REMAT
+        // the lane's (sample, group) re-derived opaquely per iteration: the LDS / global
+        // addresses built from them are recomputed here instead of held (or spilled) across the
+        // loop as loop-invariant registers
+        int lane_l = lane;
+        asm volatile("" : "+v"(lane_l));
+        const int s = lane_l & 15, g = lane_l >> 4;
+#endif
         const int64_t j = base + s;
         const bool valid = j < N;
         const h8 e = cur.e;
@@ -1171,9 +1196,13 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         int Bl[5];
 #pragma unroll
         for (int l = 0; l < 5; ++l) {
-            const int4 a = *reinterpret_cast<const int4*>(&emin[par][l][0]);
-            const int4 b = *reinterpret_cast<const int4*>(&emin[par][l][4]);
-            Bl[l] = __builtin_amdgcn_readfirstlane(min(min(min(a.x, a.y), min(a.z, a.w)), min(min(b.x, b.y), min(b.z, b.w))));
+            int mn = 1 << 30;
+#pragma unroll
+            for (int q = 0; q < CW; q += 4) {
+                const int4 a = *reinterpret_cast<const int4*>(&emin[par][l][q]);
+                mn = min(mn, min(min(a.x, a.y), min(a.z, a.w)));
+            }
+            Bl[l] = __builtin_amdgcn_readfirstlane(mn);
             fk[l] = Bl[l] - Es[l];
         }
         // phase 1 (layers 5, 4, 3)
@@ -1189,7 +1218,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         put_tile(mine + (P_C + 1) * TTILE, hh, s, g);
         __syncthreads();
         NGP_BWD_PHASE(4);
-        coop_dw<4>(scr, wid, s, g, coop_n1(wid), coop_k1, acc1, Bl);
+        coop_dw<KT1>(scr, wid, s, g, coop_n1(wid), coop_k1, acc1, Bl);
         __syncthreads();  // phase-1 reads done: the regions take the phase-2 tiles
         NGP_BWD_PHASE(5);
         // ---- phase 2 (layers 2, 1)
@@ -1203,7 +1232,7 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
         put_tile_pair(mine + (Q_E + (g >> 1)) * TTILE, h4{e[0], e[1], e[2], e[3]}, h4{e[4], e[5], e[6], e[7]}, s, g & 1);
         __syncthreads();
         NGP_BWD_PHASE(6);
-        coop_dw<2>(scr, wid, s, g, coop_n2(wid), coop_k2, acc2, Bl);
+        coop_dw<KT2>(scr, wid, s, g, coop_n2(wid), coop_k2, acc2, Bl);
         NGP_BWD_PHASE(7);
     }
     // each output tile lives in exactly one wave of the block: one global add
@@ -1218,8 +1247,13 @@ __global__ void __launch_bounds__(512) field_bwd_mlp_coop_kernel(
     for (int q0 = 0; q0 < nadd; ++q0) {
         const int q = (q0 + rot) % nadd, t = q >> 2, r = q & 3;
         const int t2 = t - n1;  // tiles t < n1: phase 1, else phase 2
-        const f4 a = t2 >= 0 ? (t2 == 0 ? acc2[0] : acc2[1])
-                             : (t == 0 ? acc1[0] : t == 1 ? acc1[1] : t == 2 ? acc1[2] : acc1[3]);
+        f4 a = acc1[0];
+#pragma unroll
+        for (int u = 1; u < KT1; ++u)
+            if (t == u) a = acc1[u];
+#pragma unroll
+        for (int u = 0; u < KT2; ++u)
+            if (t2 == u) a = acc2[u];
         const float v = r == 0 ? a[0] : r == 1 ? a[1] : r == 2 ? a[2] : a[3];
         const int k = t2 < 0 ? coop_k1(wid, t) : coop_k2(wid, t2);
         int ow, in_dim, o0, i0;
@@ -1527,9 +1561,9 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
         attr_set = true;
     }
     hipStream_t s = as_stream(stream);
-    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel, 512, clds);
+    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel, 64 * CW, clds);
     const unsigned cb = persistent_blocks(n, CW * 16, ccap);
-    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<<<cb, 512, clds, s>>>(
+    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<<<cb, 64 * CW, clds, s>>>(
         dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
         grad_mlp, enc_pm_stride));
     return ngp_launch_status();
