@@ -2,7 +2,9 @@
 """One step's kernel timeline (start offset, duration, queue, name) from a
 rocprofv3 kernel trace, plus per-queue busy time and the idle gaps between
 consecutive kernels of the main queue, over the last STEPS steps.
-usage: timeline.py run_kernel_trace.csv STEPS [step_index_from_end]"""
+usage: timeline.py run_kernel_trace.csv STEPS [step_index_from_end] [anchor]
+(anchor: a substring of the kernel that ends a step; default adam_kernel -- use e.g.
+sample_batch_kernel for the data-parallel step, which runs one Adam launch per bucket)"""
 import csv
 import sys
 from collections import defaultdict
@@ -11,9 +13,10 @@ from collections import defaultdict
 def main():
     path, steps = sys.argv[1], int(sys.argv[2])
     back = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    anchor = sys.argv[4] if len(sys.argv) > 4 else "adam_kernel"
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    anch = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    anch = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
     win = rows[anch[-steps - 1] + 1:anch[-1] + 1]
     q = defaultdict(list)
     for r in win:
