@@ -636,6 +636,9 @@ __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
 #ifndef NGP_FEM2_WAVES
 #define NGP_FEM2_WAVES 8
 #endif
+#ifndef NGP_FEM_REMAT
+#define NGP_FEM_REMAT 0
+#endif
 constexpr int FEM2_WAVES = NGP_FEM2_WAVES, FEM_LPR = NGP_FEM_LPR;
 static_assert(L % FEM_LPR == 0, "levels per round");
 template <bool COLOR>
@@ -666,7 +669,14 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
     __syncthreads();
     bool first = true;
     for (; k < chunks; k += (int64_t)FEM2_WAVES * G) {
+#if NGP_FEM_REMAT
+        int lane_l = lane;  // (opaque per iteration: lane-derived addresses are not held across the loop)
+        asm volatile("" : "+v"(lane_l));
+        const int s = lane_l & 15, g = lane_l >> 4;
+        const int64_t j = k * 64 + lane_l;
+#else
         const int64_t j = k * 64 + lane;
+#endif
         const bool valid = j < N;
         int64_t i = i_first;
         float in[3] = {in_first[0], in_first[1], in_first[2]};
@@ -731,6 +741,68 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
                 }
             }
         }
+    }
+}
+
+// One level of the coarse (atomic) hash backward for the wave's 16 consecutive
+// samples, lane = 4 s + 2 cx + f: corner c = cx | cy << 1 | cz << 2 of sample s
+// receives w_c * gd (gd = dL/denc[s][2 l + f]); runs of equal corners along the
+// 16 samples (lanes 4 apart) are merged by segmented suffix sums, and each
+// run's head adds its sum with one memory-side fp32 atomic into dst.
+__device__ __forceinline__ void coarse_scatter_level(const float in[3], bool valid, float gd, int l, const LevelLds& lv,
+                                                     float* __restrict__ dst, int lane, int cx, int f) {
+    const float sc = lv.scale[l];
+    const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
+    const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
+    float pos[3];
+    uint32_t pg[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float p = fmaf(sc, in[d], 0.5f);
+        const float fl = floorf(p);
+        pg[d] = (uint32_t)(int)fl;
+        pos[d] = p - fl;
+    }
+    // corner c = cx | (cy<<1) | (cz<<2); weight product in tcnn's d order.
+    // The four y/z corners are independent: their shuffles are issued
+    // together (one LDS round trip per scan step, not four).
+    uint32_t idx[4];
+    float v[4];
+    uint64_t heads[4];
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const int cy = yz & 1, cz = yz >> 1;
+        float wt = 1.0f;
+        wt *= cx ? pos[0] : 1 - pos[0];
+        wt *= cy ? pos[1] : 1 - pos[1];
+        wt *= cz ? pos[2] : 1 - pos[2];
+        idx[yz] = valid ? off + corner_index(pg[0] + cx, pg[1] + cy, pg[2] + cz, res, size, dense, pow2)
+                        : 0xffffffffu;
+        v[yz] = wt * gd;
+    }
+    uint32_t prev[4];
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) prev[yz] = __shfl_up(idx[yz], 4, 64);
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) heads[yz] = __ballot(lane < 4 || prev[yz] != idx[yz]);
+    if ((heads[0] & heads[1] & heads[2] & heads[3]) != ~0ull) {
+        // some runs: segmented suffix sums at lane stride 4
+#pragma unroll
+        for (int o4 = 4; o4 < 64; o4 <<= 1) {
+            float ov[4];
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz) ov[yz] = __shfl_down(v[yz], o4, 64);
+            // lanes lane+4, lane+8, ..., lane+o4 must all continue the run
+            const uint64_t span = ((0x1111111111111111ull & ((2ull << o4) - 1ull)) & ~1ull) << lane;
+#pragma unroll
+            for (int yz = 0; yz < 4; ++yz)
+                if (lane + o4 < 64 && (heads[yz] & span) == 0) v[yz] += ov[yz];
+        }
+    }
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const bool head = (heads[yz] >> lane) & 1ull;
+        if (head && valid) atomicAdd(&dst[2 * (size_t)idx[yz] + f], v[yz]);
     }
 }
 
@@ -924,7 +996,7 @@ __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& 
 #define NGP_BWD_EDGE(k)
 #endif
 #ifndef NGP_BWD_REMAT
-#define NGP_BWD_REMAT 0
+#define NGP_BWD_REMAT 1
 #endif
 #ifndef NGP_BWD_CW
 #define NGP_BWD_CW 8  // waves per block (CW / 4 per SIMD); 12 fits the LDS (161 KB) at <= 168 VGPRs
@@ -1012,13 +1084,34 @@ __device__ __forceinline__ void coop_dw(const _Float16* scr, int w, int s, int g
         if (t < n) acc[t] = part[t] * sc[t] + acc[t];
 }
 
+// The coarse (atomic) hash levels [0, hi) scattered by the MLP backward itself
+// (field_bwd_mlp_coop_kernel<true>): each wave adds its 16 samples' level
+// gradients straight from the registers that hold dL/denc, with
+// hash_bwd_kernel's arithmetic, run merging and replicas (coarse_scatter_level)
+// -- the atomics leave while the block's MFMA work goes on, instead of a launch
+// of their own beside the binned levels' record write.
+struct CoarseArgs {
+    const float* xyzs;
+    GridArgs ga;
+    float* grad;  // table gradient (entries x 2)
+    int hi;       // levels [0, hi)
+    float* rep;   // replicas of levels [0, rep_hi) (nullable)
+    int rep_hi;
+    uint32_t rep_stride;
+    int nrep;
+};
+
+template <bool COARSE>
 __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
     const _Float16* __restrict__ enc, const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig,
-    const float* __restrict__ dL_drgb, float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride) {
+    const float* __restrict__ dL_drgb, float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride,
+    CoarseArgs ca) {
     extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
     // per-wave minima of the layers' per-sample exponents (double-buffered by iteration parity)
     __shared__ __attribute__((aligned(16))) int emin[2][5][CW];
+    __shared__ LevelLds lv;  // (COARSE)
+    float* const grep = COARSE && ca.rep ? ca.rep + (size_t)(blockIdx.x % ca.nrep) * ca.rep_stride : ca.grad;
     _Float16* sw = smem;
     _Float16* scr = smem + SCR;
     NGP_BWD_EDGE(0);
@@ -1035,6 +1128,7 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     struct In {
         h8 e;
         float dx, dy, dz, dsig, gr[3];
+        int32_t ii;  // (COARSE) the sample, -1 past the end
     };
     // the sample of row jj (-1 past the end): listed rows' indices are loaded
     // two iterations ahead, so the dependent loads of the next iteration's
@@ -1056,6 +1150,7 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
             x.gr[0] = dL_drgb[3 * (int64_t)ii]; x.gr[1] = dL_drgb[3 * (int64_t)ii + 1];
             x.gr[2] = dL_drgb[3 * (int64_t)ii + 2];
         }
+        if constexpr (COARSE) x.ii = ii;
     };
     const int64_t stride = (int64_t)gridDim.x * CW * 16;
     const int64_t j0 = (int64_t)blockIdx.x * CW * 16 + 16 * wid + s;
@@ -1066,6 +1161,7 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     load_in(row_index(j0), cur);
     int32_t i_next = row_index(j0 + stride);
     load_bwd_weights_direct(mlp, sw);
+    if constexpr (COARSE) load_levels(ca.ga, lv);
     __syncthreads();
     NGP_BWD_EDGE(1);
     int par = 0;
@@ -1087,6 +1183,14 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         const int64_t j = base + s;
         const bool valid = j < N;
         const h8 e = cur.e;
+        // (COARSE) this iteration's sample positions, requested now: in by the scatter
+        float pxyz[3] = {0.f, 0.f, 0.f};
+        if constexpr (COARSE) {
+            if (cur.ii >= 0) {
+#pragma unroll
+                for (int d = 0; d < 3; ++d) pxyz[d] = ca.xyzs[3 * (int64_t)cur.ii + d];
+            }
+        }
         // ---- forward recompute
         h4 h1[4];
         const h4 hh = density_net(e, sw, s, g, h1);
@@ -1166,13 +1270,36 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         // ---- dL/denc = W1^T da1 (rows 16t + 4g + r of sample s), true units
         {
             const float r = ldexpf(1.0f, -E1);
+            f4 dco = z;  // (COARSE) rows 0-15: levels 0-7
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 f4 c = z;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT1 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da1h[kt], c);
                 c = c * r;
-                if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
+                if (t == 0) dco = c;
+                // (the coarse levels' rows are not stored when this kernel scatters them all)
+                if (valid && !(COARSE && t == 0 && ca.hi == 8)) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
+            }
+            if constexpr (COARSE) {
+                // lane = 4 s' + 2 cx + f takes sample s' = lane >> 2 (the wave's samples in row
+                // order, as hash_bwd_kernel groups them); dL/denc[s'][2 l + f] comes from lane
+                // (s', g = l >> 1), element 2 (l & 1) + f
+                const int sp = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1;
+                const int32_t isp = __shfl(cur.ii, sp, 64);
+                const bool vsp = isp >= 0;
+                const float xs[3] = {__shfl(pxyz[0], sp, 64), __shfl(pxyz[1], sp, 64), __shfl(pxyz[2], sp, 64)};
+                float in[3];
+#pragma unroll
+                for (int d = 0; d < 3; ++d)  // load_x01's arithmetic (models/networks.py:104)
+                    in[d] = (xs[d] - ca.ga.g.xyz_min[d]) / (ca.ga.g.xyz_max[d] - ca.ga.g.xyz_min[d]);
+#pragma unroll 1
+                for (int l = 0; l < ca.hi; ++l) {
+                    const int src = 16 * (l >> 1) + sp;
+                    const float a = __shfl((l & 1) ? dco[2] : dco[0], src, 64);
+                    const float b = __shfl((l & 1) ? dco[3] : dco[1], src, 64);
+                    coarse_scatter_level(in, vsp, f ? b : a, l, lv, l < ca.rep_hi ? grep : ca.grad, lane, cx, f);
+                }
             }
         }
         NGP_BWD_PHASE(2);
@@ -1319,63 +1446,8 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll 1
-        for (int l = lo; l < hi; ++l) {
-            const float gd = drow[wv][s][2 * l + f];
-            float* const dst = l < rep_hi ? grep : grad;
-            const float sc = lv.scale[l];
-            const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
-            const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
-            float pos[3];
-            uint32_t pg[3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                const float p = fmaf(sc, in[d], 0.5f);
-                const float fl = floorf(p);
-                pg[d] = (uint32_t)(int)fl;
-                pos[d] = p - fl;
-            }
-            // corner c = cx | (cy<<1) | (cz<<2); weight product in tcnn's d order.
-            // The four y/z corners are independent: their shuffles are issued
-            // together (one LDS round trip per scan step, not four).
-            uint32_t idx[4];
-            float v[4];
-            uint64_t heads[4];
-#pragma unroll
-            for (int yz = 0; yz < 4; ++yz) {
-                const int cy = yz & 1, cz = yz >> 1;
-                float wt = 1.0f;
-                wt *= cx ? pos[0] : 1 - pos[0];
-                wt *= cy ? pos[1] : 1 - pos[1];
-                wt *= cz ? pos[2] : 1 - pos[2];
-                idx[yz] = valid ? off + corner_index(pg[0] + cx, pg[1] + cy, pg[2] + cz, res, size, dense, pow2)
-                                : 0xffffffffu;
-                v[yz] = wt * gd;
-            }
-            uint32_t prev[4];
-#pragma unroll
-            for (int yz = 0; yz < 4; ++yz) prev[yz] = __shfl_up(idx[yz], 4, 64);
-#pragma unroll
-            for (int yz = 0; yz < 4; ++yz) heads[yz] = __ballot(lane < 4 || prev[yz] != idx[yz]);
-            if ((heads[0] & heads[1] & heads[2] & heads[3]) != ~0ull) {
-                // some runs: segmented suffix sums at lane stride 4
-#pragma unroll
-                for (int o4 = 4; o4 < 64; o4 <<= 1) {
-                    float ov[4];
-#pragma unroll
-                    for (int yz = 0; yz < 4; ++yz) ov[yz] = __shfl_down(v[yz], o4, 64);
-                    // lanes lane+4, lane+8, ..., lane+o4 must all continue the run
-                    const uint64_t span = ((0x1111111111111111ull & ((2ull << o4) - 1ull)) & ~1ull) << lane;
-#pragma unroll
-                    for (int yz = 0; yz < 4; ++yz)
-                        if (lane + o4 < 64 && (heads[yz] & span) == 0) v[yz] += ov[yz];
-                }
-            }
-#pragma unroll
-            for (int yz = 0; yz < 4; ++yz) {
-                const bool head = (heads[yz] >> lane) & 1ull;
-                if (head && valid) atomicAdd(&dst[2 * (size_t)idx[yz] + f], v[yz]);
-            }
-        }
+        for (int l = lo; l < hi; ++l)
+            coarse_scatter_level(in, valid, drow[wv][s][2 * l + f], l, lv, l < rep_hi ? grep : grad, lane, cx, f);
     }
 }
 
@@ -1402,6 +1474,27 @@ __global__ void __launch_bounds__(256) rep_reduce_kernel(float* __restrict__ gra
             }
         g4[i] = a;
     }
+}
+
+template <bool COARSE>
+static int launch_bwd_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                          const void* enc_f16, int64_t enc_pm_stride, const void* mlp_f16, const float* dL_dsigmas,
+                          const float* dL_drgbs, float* denc_ws, float* grad_mlp, const CoarseArgs& ca, void* stream) {
+    static bool attr_set = false;
+    const size_t clds = (size_t)COOP_LDS_HALFS * sizeof(_Float16);
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)field_bwd_mlp_coop_kernel<COARSE>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds) != hipSuccess)
+            return NGP_ERANGE;
+        attr_set = true;
+    }
+    hipStream_t s = as_stream(stream);
+    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel<COARSE>, 64 * CW, clds);
+    const unsigned cb = persistent_blocks(n, CW * 16, ccap);
+    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<COARSE><<<cb, 64 * CW, clds, s>>>(
+        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
+        grad_mlp, enc_pm_stride, ca));
+    return ngp_launch_status();
 }
 
 }  // namespace ngp
@@ -1552,21 +1645,32 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(dirs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp);
     NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
-    static bool attr_set = false;
-    const size_t clds = (size_t)COOP_LDS_HALFS * sizeof(_Float16);
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)field_bwd_mlp_coop_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)clds) != hipSuccess)
-            return NGP_ERANGE;
-        attr_set = true;
-    }
-    hipStream_t s = as_stream(stream);
-    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel, 64 * CW, clds);
-    const unsigned cb = persistent_blocks(n, CW * 16, ccap);
-    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<<<cb, 64 * CW, clds, s>>>(
-        dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
-        grad_mlp, enc_pm_stride));
-    return ngp_launch_status();
+    return launch_bwd_mlp<false>(dirs, n, n_dev, sample_idx, enc_f16, enc_pm_stride, mlp_f16, dL_dsigmas, dL_drgbs,
+                                 denc_ws, grad_mlp, CoarseArgs{}, stream);
+}
+
+int ngp_field_backward_mlp_coarse(const float* dirs, const float* xyzs, int64_t n, const int64_t* n_dev,
+                                  const int32_t* sample_idx, const void* enc_f16, int64_t enc_pm_stride,
+                                  const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws,
+                                  float* grad_mlp, const ngp_hashgrid_t* grid, float* grad_table, int level_hi,
+                                  float* rep, int rep_levels, int n_rep, void* stream) {
+    CoarseArgs ca{};
+    int st = grid_args(grid, ca.ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n >= 0 && 0 <= level_hi && level_hi <= L && 0 <= rep_levels && rep_levels <= level_hi);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(dirs && xyzs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp && grad_table);
+    NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
+    if (rep && rep_levels > 0) NGP_CHECK_ARG(n_rep >= 1 && n_rep <= 64 && ((uintptr_t)rep & 15) == 0);
+    ca.xyzs = xyzs;
+    ca.grad = grad_table;
+    ca.hi = level_hi;
+    ca.rep = rep_levels > 0 ? rep : nullptr;
+    ca.rep_hi = ca.rep ? rep_levels : 0;
+    ca.rep_stride = 2u * grid->offsets[rep_levels];
+    ca.nrep = ca.rep ? n_rep : 1;
+    return launch_bwd_mlp<true>(dirs, n, n_dev, sample_idx, enc_f16, enc_pm_stride, mlp_f16, dL_dsigmas, dL_drgbs,
+                                denc_ws, grad_mlp, ca, stream);
 }
 
 

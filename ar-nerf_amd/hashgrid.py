@@ -45,6 +45,8 @@ def _lib():
         L.ngp_density_input_grad.argtypes = [vp, c_int64, P, vp, vp, vp, vp, vp]
         L.ngp_field_backward.argtypes = [vp, vp, c_int64, vp, P, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_backward_mlp.argtypes = [vp, c_int64, vp, vp, vp, c_int64, vp, vp, vp, vp, vp, vp]
+        L.ngp_field_backward_mlp_coarse.argtypes = [vp, vp, c_int64, vp, vp, vp, c_int64, vp, vp, vp, vp, vp, P, vp,
+                                                    c_int, vp, c_int, c_int, vp]
         L.ngp_hash_encode.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
         L.ngp_field_forward_indexed.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp]
         L.ngp_field_mlp_forward.argtypes = [vp, vp, c_int64, vp, vp, vp, vp, vp, vp, vp]
@@ -68,6 +70,7 @@ def _lib():
         L.ngp_hash_backward_binned_workspace.argtypes = [c_int64]
         L.ngp_hash_backward_binned_workspace.restype = ctypes.c_size_t
         for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_density_input_grad, L.ngp_field_backward, L.ngp_field_backward_mlp,
+                  L.ngp_field_backward_mlp_coarse,
                   L.ngp_hash_encode, L.ngp_field_mlp_forward, L.ngp_field_forward_indexed, L.ngp_field_encode_mlp,
                   L.ngp_hash_backward, L.ngp_hash_backward_binned, L.ngp_hash_backward_levels,
                   L.ngp_hash_backward_levels_rep,

@@ -267,6 +267,10 @@ class NGPTrainer:
         import os
         self.step_ticket = os.environ.get("NGP_STEP_TICKET", "1") != "0"
         self._ticket_active = False
+        # single-process hybrid steps: the coarse (atomic) hash levels scattered by the MLP
+        # backward launch itself (ngp_field_backward_mlp_coarse) instead of a launch of their own
+        # beside the binned levels' record write (NGP_FUSED_COARSE=0: the separate launch)
+        self.fused_coarse = os.environ.get("NGP_FUSED_COARSE", "1") != "0"
         self._updated_for = -1  # global step whose occupancy update already ran (end of the previous graph)
         self.lr_dev = torch.full((1,), float(lr), device=dev)
         self._lr_set = float(lr)
@@ -908,9 +912,20 @@ class NGPTrainer:
                 planned = torch.cuda.Event()
                 planned.record(bs)
         self._ev("mlp_bwd", 0)
-        vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                                            _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
-                                            _p(self.denc), _p(self.grad), s), "field_backward_mlp")
+        # the coarse levels inside the MLP backward: single-process hybrid steps with Adam, whose
+        # coarse Adam folds the gradient replicas (otherwise the separate launch below)
+        fuse_coarse = (hybrid and self.fused_coarse and apply_adam and not self.dp and self.bin_level_lo > 0
+                       and self.rep_buf is not None)
+        if fuse_coarse:
+            vren._ok(HGL.ngp_field_backward_mlp_coarse(
+                _p(self.dirs), _p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx), _p(self.enc),
+                self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb), _p(self.denc), _p(self.grad),
+                HG.ctypes.byref(self.grid.desc), _p(self.grad[HG.MLP_PARAMS:]), self.bin_level_lo, _p(self.rep_buf),
+                self.coarse_rep_levels, max(1, self.coarse_rep), s), "field_backward_mlp_coarse")
+        else:
+            vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                                                _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
+                                                _p(self.denc), _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
         if self._segmented and hybrid:
             # (world > 1 graph segments: the hash backward runs as two more
@@ -933,9 +948,10 @@ class NGPTrainer:
             fold_in_adam = adam_split and self.rep_buf is not None
             bs.wait_stream(cs)
             with torch.cuda.stream(bs):
-                self._ev("hash_bwd_coarse", 0)
-                self._coarse_levels(fold=not fold_in_adam)
-                self._ev("hash_bwd_coarse", 1)
+                if not fuse_coarse:
+                    self._ev("hash_bwd_coarse", 0)
+                    self._coarse_levels(fold=not fold_in_adam)
+                    self._ev("hash_bwd_coarse", 1)
                 if adam_split:
                     if self._ticket_active:
                         # the ticketed Adam launches advance the batch counter: the next batch's

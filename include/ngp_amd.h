@@ -357,6 +357,19 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
                            const void* enc_f16, int64_t enc_pm_stride, const void* mlp_f16,
                            const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
                            void* stream);
+/* ngp_field_backward_mlp that also scatters the coarse hash levels [0,
+ * level_hi) into grad_table (entries x 2 fp32) -- ngp_hash_backward_levels_rep
+ * with fold = 0 (levels below rep_levels into the n_rep replicas at rep,
+ * folded later by ngp_adam_step_dev_rep) -- from the registers that hold
+ * dL/denc, with that function's arithmetic: one launch where the hybrid
+ * backward had two.  xyzs (n, 3) are the samples' positions.  With level_hi
+ * == 8 the denc rows of levels 0-7 are not written (nothing else reads them:
+ * the binned levels start at 8). */
+int ngp_field_backward_mlp_coarse(const float* dirs, const float* xyzs, int64_t n, const int64_t* n_dev,
+                                  const int32_t* sample_idx, const void* enc_f16, int64_t enc_pm_stride,
+                                  const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws,
+                                  float* grad_mlp, const ngp_hashgrid_t* grid, float* grad_table, int level_hi,
+                                  float* rep, int rep_levels, int n_rep, void* stream);
 int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                       const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* stream);
 

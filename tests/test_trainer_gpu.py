@@ -355,3 +355,45 @@ def test_step_ticket_replays_match_the_increment_launch():
     noise = float((pb - pa).norm())
     print(f"ticket vs increment launch {float((pt - pa).norm()):.3f}, increment vs increment {noise:.3f}")
     assert float((pt - pa).norm()) <= 3 * noise + 1e-3 * float(pa.norm())
+
+
+def test_fused_coarse_scatter_matches_the_separate_launch():
+    """The coarse (atomic) hash levels scattered by the MLP backward launch
+    (ngp_field_backward_mlp_coarse: the single-process step's default) add
+    the same gradient as the separate hash_bwd launch it replaces: the same
+    step from the same state, the MLP + coarse-level gradient the coarse Adam
+    launch consumes (gradient + its folded replicas) agrees per parameter
+    group to fp32 atomic-order noise."""
+    import hashgrid as HG
+    grads = []
+    for fused in (False, True):
+        sc, tr, img, pix, noise = _setup(table_init=0.2)
+        tr.fused_coarse = fused
+        seen = {}
+        orig = tr._adam
+
+        def spy(lo, hi, s, rep=False, tr=tr, seen=seen, orig=orig):
+            if lo == 0:  # the MLP + coarse levels' Adam: its gradient incl. the unfolded replicas
+                g = tr.grad[lo:hi].clone()
+                if rep:
+                    n = 2 * int(tr.grid.offsets[tr.coarse_rep_levels])
+                    g[HG.MLP_PARAMS:HG.MLP_PARAMS + n] += tr.rep_buf.view(tr.coarse_rep, n).sum(0)
+                seen["g"] = g
+            orig(lo, hi, s, rep)
+        tr._adam = spy
+        dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+        o, d = sc.rays(img, pix)
+        gt = sc.gt_rgb_rays(o, d).to(DEV)
+        tr.step(img.to(DEV), pix.to(DEV), gt, dirs, poses, noise=noise.to(DEV))
+        torch.cuda.synchronize()
+        grads.append((seen["g"].cpu(), tr))
+    (ga, tra), (gb, _) = grads
+    offs = [0, 3072, HG.MLP_PARAMS] + [HG.MLP_PARAMS + 2 * int(tra.grid.offsets[l]) for l in range(1, tra.bin_level_lo + 1)]
+    worst = 0.0
+    for a, b in zip(offs[:-1], offs[1:]):
+        ref = ga[a:b].double()
+        if float(ref.norm()) == 0:
+            continue
+        worst = max(worst, float((gb[a:b].double() - ref).norm() / ref.norm()))
+    print(f"fused coarse scatter vs separate launch: worst group relative L2 {worst:.2e}")
+    assert worst < 1e-5
