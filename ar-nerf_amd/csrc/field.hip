@@ -433,6 +433,61 @@ __device__ __forceinline__ void sum_level(const float w[8], const uint32_t v[8],
     }
 }
 
+// gather_level_u in two halves that keep fewer registers live across the
+// loads' latency: the loads alone (indices from the cell corner), then -- once
+// they have returned -- the corner weights recomputed from the position and
+// the fp32 corner sum (the same values, the same fmaf order)
+__device__ __forceinline__ void level_cell(const float in[3], const LevelU& u, uint32_t pg[3], float pos[3]) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        const float p = fmaf(u.sc, in[d], 0.5f);
+        const float fl = floorf(p);
+        pg[d] = (uint32_t)(int)fl;
+        pos[d] = p - fl;
+    }
+}
+__device__ __forceinline__ void gather_level_loads(const float in[3], const LevelU& u,
+                                                   const uint32_t* __restrict__ table, uint32_t v[8]) {
+    float pos[3];
+    uint32_t pg[3];
+    level_cell(in, u, pg, pos);
+    uint32_t i0[4], i1[4];
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) {
+        const uint32_t qy = pg[1] + (yz & 1), qz = pg[2] + (yz >> 1);
+        uint32_t r0, r1;
+        if (u.dense) {
+            r0 = pg[0] + qy * u.res + qz * u.res2;
+            r1 = r0 + 1u;
+        } else {
+            const uint32_t h = (qy * 2654435761u) ^ (qz * 805459861u);
+            r0 = (pg[0] * 1u) ^ h;
+            r1 = ((pg[0] + 1u) * 1u) ^ h;
+        }
+        i0[yz] = reduce_idx(r0, u);
+        i1[yz] = reduce_idx(r1, u);
+    }
+    const uint32_t* tl = table + u.off;
+#pragma unroll
+    for (int yz = 0; yz < 4; ++yz) fetch_pair(tl, i0[yz], i1[yz], u.dense || !u.pow2, v[2 * yz], v[2 * yz + 1]);
+}
+__device__ __forceinline__ uint32_t level_sum_h2(const float in[3], const LevelU& u, const uint32_t v[8]) {
+    float pos[3];
+    uint32_t pg[3];
+    level_cell(in, u, pg, pos);
+    float w[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        float wt = 1.0f;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) wt *= (c & (1 << d)) ? pos[d] : 1 - pos[d];
+        w[c] = wt;
+    }
+    float a0, a1;
+    sum_level(w, v, a0, a1);
+    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a0) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a1) << 16);
+}
+
 __device__ __forceinline__ void encode_level_u(const float in[3], const LevelU& u, const uint32_t* __restrict__ table,
                                                float& a0, float& a1) {
     float w[8];
@@ -637,7 +692,7 @@ __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
 #define NGP_FEM2_WAVES 8
 #endif
 #ifndef NGP_FEM_REMAT
-#define NGP_FEM_REMAT 0
+#define NGP_FEM_REMAT 1
 #endif
 constexpr int FEM2_WAVES = NGP_FEM2_WAVES, FEM_LPR = NGP_FEM_LPR;
 static_assert(L % FEM_LPR == 0, "levels per round");
@@ -691,18 +746,13 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
         // last round E[l] holds level l
 #pragma unroll 1
         for (int r = 0; r < L / FEM_LPR; ++r) {
-            float w[FEM_LPR][8];
             uint32_t v[FEM_LPR][8];
 #pragma unroll
-            for (int q = 0; q < FEM_LPR; ++q) gather_level_u(in, level_u(lv, FEM_LPR * r + q), table, w[q], v[q]);
+            for (int q = 0; q < FEM_LPR; ++q) gather_level_loads(in, level_u(lv, FEM_LPR * r + q), table, v[q]);
 #pragma unroll
             for (int q = 0; q < 16 - FEM_LPR; ++q) E[q] = E[q + FEM_LPR];
 #pragma unroll
-            for (int q = 0; q < FEM_LPR; ++q) {
-                float a0, a1;
-                sum_level(w[q], v[q], a0, a1);
-                E[16 - FEM_LPR + q] = pack_h2(a0, a1);
-            }
+            for (int q = 0; q < FEM_LPR; ++q) E[16 - FEM_LPR + q] = level_sum_h2(in, level_u(lv, FEM_LPR * r + q), v[q]);
         }
         if (valid && enc_pm) {
 #pragma unroll

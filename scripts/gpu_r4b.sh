@@ -13,4 +13,4 @@ timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 $Q > $OUT/bench20.jso
 python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[1], d['value'], d['ms_per_step'], r['frac'], r['ms_per_step'], json.dumps(r['units_check']))" $OUT/bench20.json
 timeout -k 10 120 python -u scripts/diag/graph_join_cost.py 20000 > $OUT/graph_join.json 2> $OUT/graph_join.err && cat $OUT/graph_join.json
 timeout -k 10 120 python -u scripts/diag/graph_join_cost.py 2000 > $OUT/graph_join_short.json 2> $OUT/graph_join_short.err && cat $OUT/graph_join_short.json
-bash scripts/ab_env.sh ${1:-r4b}/ab 2 "||" "|NGP_FUSED_COARSE=0|" "lib_b12||" "lib_b12|NGP_FUSED_COARSE=0|" "|NGP_STEP_TICKET=0|" "|NGP_FEM_LDS=1|" "lib_w4||"
+bash scripts/ab_env.sh ${1:-r4b}/ab 2 "||" "|NGP_FUSED_COARSE=0|" "lib_b12||" "|NGP_STEP_TICKET=0|" "|NGP_FEM_LDS=1|" "lib_fl4||" "lib_fl8||"
