@@ -705,7 +705,10 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ LevelLds lv;
     const int64_t N = n_dev ? *n_dev : n;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, s = lane & 15, g = lane >> 4;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#if !NGP_FEM_REMAT
+    const int s = lane & 15, g = lane >> 4;
+#endif
     const int64_t G = gridDim.x;
     const int64_t chunks = (N + 63) >> 6;
     int64_t k = (int64_t)wv * G + blockIdx.x;  // first chunk of this wave (wave-uniform)
