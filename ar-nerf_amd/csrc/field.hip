@@ -973,7 +973,13 @@ __device__ __forceinline__ h4 scale_h4(h4 v, int k) {
 // max |c| over the units whose activation is nonzero (the ReLU' mask the
 // gradient tile gets; act = relu_h's fp16 output): the per-sample exponent
 // follows the values that are kept, not those of inactive units
+#ifndef NGP_BWD_MASKED
+#define NGP_BWD_MASKED 1  // 0: the exponent from all units (rounds 1-3)
+#endif
 __device__ __forceinline__ float max4_act(f4 c, h4 act) {
+#if !NGP_BWD_MASKED
+    return max4(c);
+#endif
     const uint2 a = __builtin_bit_cast(uint2, act);
     const float m0 = (a.x & 0xffffu) ? fabsf(c[0]) : 0.f, m1 = (a.x >> 16) ? fabsf(c[1]) : 0.f;
     const float m2 = (a.y & 0xffffu) ? fabsf(c[2]) : 0.f, m3 = (a.y >> 16) ? fabsf(c[3]) : 0.f;

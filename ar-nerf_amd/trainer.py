@@ -267,10 +267,12 @@ class NGPTrainer:
         import os
         self.step_ticket = os.environ.get("NGP_STEP_TICKET", "1") != "0"
         self._ticket_active = False
-        # single-process hybrid steps: the coarse (atomic) hash levels scattered by the MLP
-        # backward launch itself (ngp_field_backward_mlp_coarse) instead of a launch of their own
-        # beside the binned levels' record write (NGP_FUSED_COARSE=0: the separate launch)
-        self.fused_coarse = os.environ.get("NGP_FUSED_COARSE", "1") != "0"
+        # (opt-in, NGP_FUSED_COARSE=1) single-process hybrid steps: the coarse (atomic) hash levels
+        # scattered by the MLP backward launch itself (ngp_field_backward_mlp_coarse) instead of a
+        # launch of their own beside the binned levels' record write -- measured 4 % slower end to
+        # end (the MLP backward 60 -> 135-147 us: its waves stall behind their outstanding atomics;
+        # profiles/r04/ab/ab_r4b.txt)
+        self.fused_coarse = os.environ.get("NGP_FUSED_COARSE", "0") == "1"
         self._updated_for = -1  # global step whose occupancy update already ran (end of the previous graph)
         self.lr_dev = torch.full((1,), float(lr), device=dev)
         self._lr_set = float(lr)
