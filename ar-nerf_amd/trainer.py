@@ -257,15 +257,17 @@ class NGPTrainer:
         # device step counters: [0] Adam steps taken, [1] batches drawn (RNG
         # counter), [2] device-sampled occupancy updates (their RNG counter)
         self.dctr = torch.zeros(3, dtype=torch.int64, device=dev)
-        # steady-state graphs of the fused single-process step: the step's two Adam launches
-        # (MLP + coarse levels on the side stream, the binned levels' residual Adam on the
-        # main stream) advance dctr[0:2] themselves through a completion ticket
-        # (ngp_step_ticket_set) -- no increment launch joining the step's streams at its end
-        # (NGP_STEP_TICKET=0: the increment launch)
+        # (opt-in, NGP_STEP_TICKET=1) steady-state graphs of the fused single-process step: the
+        # step's two Adam launches (MLP + coarse levels on the side stream, the binned levels'
+        # residual Adam on the main stream) advance dctr[0:2] themselves through a completion
+        # ticket (ngp_step_ticket_set) instead of an increment launch joining the step's streams
+        # -- measured 2-4 % slower: the next forward then waits on three queues directly and the
+        # side Adam on the march queue (cross-queue edges cost ~13 us each inside a replayed
+        # graph, scripts/diag/graph_split_cost.py; profiles/r04/ab/ab_r4d.txt)
         self._ticket_ws = torch.zeros((vren.lib().ngp_step_ticket_workspace() + 3) // 4, dtype=torch.int32,
                                       device=dev)
         import os
-        self.step_ticket = os.environ.get("NGP_STEP_TICKET", "1") != "0"
+        self.step_ticket = os.environ.get("NGP_STEP_TICKET", "0") == "1"
         self._ticket_active = False
         # (opt-in, NGP_FUSED_COARSE=1) single-process hybrid steps: the coarse (atomic) hash levels
         # scattered by the MLP backward launch itself (ngp_field_backward_mlp_coarse) instead of a

@@ -336,7 +336,7 @@ def test_step_ticket_replays_match_the_increment_launch():
     dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
     gt_img = sc.gt_images(device=DEV)
     outs = []
-    for ticket in (False, False, True):
+    for ticket in (False, False, True):  # (opt-in path, NGP_STEP_TICKET=1)
         tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, warmup_steps=16)
         tr.step_ticket = ticket
         tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
