@@ -483,21 +483,27 @@ def main():
     units = {"marched": marched / args.steps, "evaluated": evaluated / args.steps,
              "composited": composited / args.steps, "active": active / args.steps, **pw}
     rm_s, vr_s, ev_s = units["marched"] / R, units["composited"] / R, units["evaluated"] / R
-    # the roofline window's units (the same replays as its stamps) against the other two
-    # windows': per-step sample counts of one training state agree to a few % (windows of
-    # 20+ steps); a larger gap means a window's counters did not cover its steps
+    # units per step of each window: every window's own counters over exactly its own steps
+    # (the roofline's units and its stamps cover the same replays).  Within a window the counts
+    # must nest -- gradient-carrying <= field-evaluated <= marched, composited <= marched,
+    # gradient-carrying <= composited + one per ray (the terminating sample); ACROSS windows they
+    # differ with the training state: on this workload the per-step composited samples swing
+    # ~1.7x with a ~35-step period (profiles/r04/units_drift.json), so windows of 20 steps see
+    # different work per step and only their own units are valid for them
     units_check = {"steps_run": {"breakdown": ran_bd, "timed": ran_timed, "roofline": ran_rf}}
-    dev_max = 0.0
-    for basis in ("active", "evaluated", "composited"):
-        vals = {"breakdown": units_bd[basis], "timed": units[basis], "roofline": units_rf[basis]}
-        units_check[f"{basis}_per_step"] = {k: round(v, 1) for k, v in vals.items()}
-        ref_v = units[basis]
-        if ref_v > 0:
-            dev_max = max(dev_max, max(abs(v - ref_v) / ref_v for v in vals.values()))
-    units_check["max_rel_dev_vs_timed"] = round(dev_max, 4)
-    units_check["ok"] = bool(dev_max <= 0.03 and ran_rf == args.steps and ran_bd == n_bd)
+    wins = {"breakdown": units_bd, "timed": units, "roofline": units_rf}
+    for basis in ("marched", "evaluated", "composited", "active"):
+        units_check[f"{basis}_per_step"] = {k: round(w[basis], 1) for k, w in wins.items()}
+    nested = all(w["active"] <= w["evaluated"] + 0.5 and w["evaluated"] <= w["marched"] + 0.5
+                 and w["composited"] <= w["marched"] + 0.5 and w["active"] <= w["composited"] + R + 0.5
+                 for w in wins.values())
+    steps_ok = ran_rf == args.steps and ran_bd == n_bd and ran_timed == args.steps
+    vals = [w["composited"] for w in wins.values() if w["composited"] > 0]
+    units_check["drift_composited_max_over_min"] = round(max(vals) / min(vals), 3) if vals else None
+    units_check["ok"] = bool(nested and steps_ok)
     if not units_check["ok"]:
-        print(f"[bench] WARNING: per-step unit counts disagree across windows: {units_check}", file=sys.stderr)
+        print(f"[bench] WARNING: a window's unit counts do not nest or its step count is off: {units_check}",
+              file=sys.stderr)
     roof = op_row(dominant, dom_summary, units_rf)
     roof = dict(op=dominant, traffic=pmc_traffic(members, bd_summary), traffic_unit="bytes per step", **roof,
                 units_check=units_check,
