@@ -432,7 +432,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    float grad_scale, int zero_grad, const float* __restrict__ lr_dev,
                                                    const int64_t* __restrict__ step_dev, float* __restrict__ rep = nullptr,
                                                    int64_t rep_lo4 = 0, int64_t rep4 = 0, int nrep = 0,
-                                                   StepTicket ticket = StepTicket{nullptr, nullptr, 0, 0, 0}) {
+                                                   StepTicket ticket = StepTicket{nullptr, nullptr, 0, 0, 0},
+                                                   float* __restrict__ zero = nullptr, int64_t zero4 = 0) {
     adam_bias(lr_dev, step_dev, b1, b2, lr, bc1, bc2);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -473,6 +474,9 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         reinterpret_cast<h4*>(p16)[i] = out;
         if (zero_grad) reinterpret_cast<float4*>(grad)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // (ngp_adam_step_dev_zero) a second range cleared by the same launch
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < zero4; i += stride)
+        reinterpret_cast<float4*>(zero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     step_ticket_arrive(ticket);
 }
 
@@ -1254,6 +1258,24 @@ int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_av
                                                                  (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
                                                                  1.f, grad_scale, zero_grad, lr_dev, step_dev, nullptr, 0,
                                                                  0, 0, ngp_step_ticket_next()));
+    return ngp_launch_status();
+}
+
+int ngp_adam_step_dev_zero(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16, int64_t n,
+                           const float* lr_dev, float beta1, float beta2, float eps, const int64_t* step_dev,
+                           float grad_scale, int zero_grad, float* zero, int64_t zero_n, void* stream) {
+    NGP_CHECK_ARG(n >= 0 && zero_n >= 0 && zero_n % 4 == 0 && (zero_n == 0 || (zero && ((uintptr_t)zero & 15) == 0)));
+    if (n == 0 && zero_n == 0) return NGP_OK;
+    NGP_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && params_f16 && lr_dev && step_dev);
+    if (n % 4 != 0) return NGP_ERANGE;
+    const int64_t n4 = n / 4, z4 = zero_n / 4;
+    int64_t blocks = (std::max(n4, z4) + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
+                                                                 (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
+                                                                 1.f, grad_scale, zero_grad, lr_dev, step_dev, nullptr, 0,
+                                                                 0, 0, StepTicket{nullptr, nullptr, 0, 0, 0}, zero, z4));
     return ngp_launch_status();
 }
 

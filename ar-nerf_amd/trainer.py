@@ -765,8 +765,7 @@ class NGPTrainer:
         a, b = self.buckets[i]
         with torch.cuda.stream(self.comm_stream):
             self._rs(i)
-            self._gbuf[a:b].zero_()
-            self._adam_shard(i, vren._stream())
+            self._adam_shard(i, vren._stream(), zero=(a, b))  # (the bucket's local gradient cleared by it)
             self._ag(i)
 
     def _rs(self, i):
@@ -1016,16 +1015,19 @@ class NGPTrainer:
         for i in range(len(self.buckets)):
             self._adam_shard(i, vren._stream())
 
-    def _adam_shard(self, i, s):
+    def _adam_shard(self, i, s, zero=None):
         """FusedAdam on this rank's shard of bucket i: fp32 master, moments
         and fp16 shadow of the shard, from the reduced gradient shard (the
-        1/world mean folded in; the shard buffer zeroed)."""
+        1/world mean folded in; the shard buffer zeroed).  zero = (a, b):
+        the launch also clears the local gradient _gbuf[a:b]."""
         lo, hi = self.shards[i]
         q = lambda t: _p(t[lo:hi])  # noqa: E731
-        vren._ok(self.L.ngp_adam_step_dev(q(self._pbuf), _p(self._gshard[i]), q(self.exp_avg), q(self.exp_avg_sq),
-                                          q(self._p16buf), hi - lo, _p(self.lr_dev), ctypes_float(0.9),
-                                          ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
-                                          ctypes_float(1.0 / self.world), 1, s), "adam")
+        za, zb = zero if zero is not None else (0, 0)
+        vren._ok(self.L.ngp_adam_step_dev_zero(q(self._pbuf), _p(self._gshard[i]), q(self.exp_avg), q(self.exp_avg_sq),
+                                               q(self._p16buf), hi - lo, _p(self.lr_dev), ctypes_float(0.9),
+                                               ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                                               ctypes_float(1.0 / self.world), 1,
+                                               _p(self._gbuf[za:zb]) if zb > za else None, zb - za, s), "adam")
 
     def _gather_params16(self):
         """All-gather of the updated fp16 shadow the kernels read."""

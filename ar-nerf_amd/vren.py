@@ -44,6 +44,8 @@ def _declare(L):
         "ngp_sample_batch_dev": [ctypes.c_uint64, vp, c_int64, c_int64, vp, c_int, c_int64, c_int64, vp, vp, c_int64,
                                  vp, vp, c_float, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_adam_step_dev": [vp, vp, vp, vp, vp, c_int64, vp, c_float, c_float, c_float, vp, c_float, c_int, vp],
+        "ngp_adam_step_dev_zero": [vp, vp, vp, vp, vp, c_int64, vp, c_float, c_float, c_float, vp, c_float, c_int, vp,
+                                   c_int64, vp],
         "ngp_adam_step_dev_rep": [vp, vp, vp, vp, vp, c_int64, vp, c_float, c_float, c_float, vp, c_float, c_int, vp,
                                   c_int64, c_int64, c_int, vp],
         "ngp_counters_inc": [vp, c_int, vp],

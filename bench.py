@@ -115,6 +115,8 @@ def parse():
                          "ZeRO-1 shards of 1/N, per-bucket reduce-scatter / sharded Adam / all-gather on the comm "
                          "stream -- with the collectives as local copies: one rank's compute at world N without "
                          "the xGMI transfers (only shard 0 is stepped: a timing mode)")
+    ap.add_argument("--dp-fine-buckets", type=int, default=None,
+                    help="world > 1 (or --emulate-dp): ZeRO-1 buckets of the binned hash levels (default: trainer's)")
     ap.add_argument("--chunk-first", type=int, default=None,
                     help="chunked field evaluation: first round's samples per row (0: every marched sample in one "
                          "launch; default: trainer's, 64)")
@@ -344,6 +346,7 @@ def main():
     trainer = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward,
                          bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray, erode=erode,
                          bin_merge_hi=args.bin_merge_hi, pair_steps=not args.no_pair_steps, emulate_dp=args.emulate_dp,
+                         **({} if args.dp_fine_buckets is None else {"dp_fine_buckets": args.dp_fine_buckets}),
                          **({} if args.chunk_first is None else {"chunk_first": args.chunk_first}))
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
     WORK = active_work(trainer)

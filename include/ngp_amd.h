@@ -565,6 +565,14 @@ int ngp_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq
 int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16,
                       int64_t n, const float* lr_dev, float beta1, float beta2, float eps,
                       const int64_t* step_dev, float grad_scale, int zero_grad, void* stream);
+/* ngp_adam_step_dev that also clears zero[0, zero_n) (zero_n a multiple of 4,
+ * 16-byte aligned) in the same launch -- the data-parallel step's bucket: its
+ * local gradient, read by the reduce-scatter before this Adam on the shard,
+ * cleared for the next step without a launch of its own. */
+int ngp_adam_step_dev_zero(float* params, float* grads, float* exp_avg, float* exp_avg_sq, void* params_f16,
+                           int64_t n, const float* lr_dev, float beta1, float beta2, float eps,
+                           const int64_t* step_dev, float grad_scale, int zero_grad, float* zero, int64_t zero_n,
+                           void* stream);
 /* ngp_adam_step_dev whose gradient over [rep_offset, rep_offset + rep_n) of
  * this range is grads + the n_rep replicas of ngp_hash_backward_levels_rep
  * (fold = 0; replica r at rep + r * rep_n), folded in replica order and

@@ -19,7 +19,7 @@ for rep in $(seq 1 $REPS); do
         > "$OUT/v${i}_$rep.json" 2> "$OUT/v${i}_$rep.err"
     python3 -c "
 import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d.get('kernels',{})
-print('v'+sys.argv[2], sys.argv[3], round(d['value']/1e6,3), 'M rays/s', round(d['ms_per_step']*1e3,1), 'us/step |',
+print('v'+sys.argv[2], sys.argv[3], round(d['value']/1e6,3), 'M rays/s', round(d['ms_per_step']*1e3,1), 'us/step', 'host', round(d.get('host_enqueue_ms_per_step', 0)*1e3,1), '|',
       ' '.join(f'{n}={v[\"avg_launch_ms\"]*1e3:.1f}' for n, v in list(k.items())[:8]))" "$OUT/v${i}_$rep.json" "$i" "[$cfg]"
   done
 done
