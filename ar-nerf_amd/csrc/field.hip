@@ -1188,6 +1188,9 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         h8 e;
         float dx, dy, dz, dsig, gr[3];
         int32_t ii;  // (COARSE) the sample, -1 past the end
+        float px, py, pz;  // (COARSE) its position, loaded with the other inputs: a later load would
+                           // be younger than the previous iteration's atomics, and waiting for it would
+                           // wait for all of them (vmcnt counts in issue order)
     };
     // the sample of row jj (-1 past the end): listed rows' indices are loaded
     // two iterations ahead, so the dependent loads of the next iteration's
@@ -1209,7 +1212,14 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
             x.gr[0] = dL_drgb[3 * (int64_t)ii]; x.gr[1] = dL_drgb[3 * (int64_t)ii + 1];
             x.gr[2] = dL_drgb[3 * (int64_t)ii + 2];
         }
-        if constexpr (COARSE) x.ii = ii;
+        if constexpr (COARSE) {
+            x.ii = ii;
+            x.px = x.py = x.pz = 0.f;
+            if (ii >= 0) {
+                x.px = ca.xyzs[3 * (int64_t)ii]; x.py = ca.xyzs[3 * (int64_t)ii + 1];
+                x.pz = ca.xyzs[3 * (int64_t)ii + 2];
+            }
+        }
     };
     const int64_t stride = (int64_t)gridDim.x * CW * 16;
     const int64_t j0 = (int64_t)blockIdx.x * CW * 16 + 16 * wid + s;
@@ -1242,14 +1252,7 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         const int64_t j = base + s;
         const bool valid = j < N;
         const h8 e = cur.e;
-        // (COARSE) this iteration's sample positions, requested now: in by the scatter
-        float pxyz[3] = {0.f, 0.f, 0.f};
-        if constexpr (COARSE) {
-            if (cur.ii >= 0) {
-#pragma unroll
-                for (int d = 0; d < 3; ++d) pxyz[d] = ca.xyzs[3 * (int64_t)cur.ii + d];
-            }
-        }
+
         // ---- forward recompute
         h4 h1[4];
         const h4 hh = density_net(e, sw, s, g, h1);
@@ -1347,7 +1350,7 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
                 const int sp = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1;
                 const int32_t isp = __shfl(cur.ii, sp, 64);
                 const bool vsp = isp >= 0;
-                const float xs[3] = {__shfl(pxyz[0], sp, 64), __shfl(pxyz[1], sp, 64), __shfl(pxyz[2], sp, 64)};
+                const float xs[3] = {__shfl(cur.px, sp, 64), __shfl(cur.py, sp, 64), __shfl(cur.pz, sp, 64)};
                 float in[3];
 #pragma unroll
                 for (int d = 0; d < 3; ++d)  // load_x01's arithmetic (models/networks.py:104)
