@@ -80,6 +80,23 @@ def _grad_step(batch, rank=0):
     return tr
 
 
+def _collect(procs, q, limit=240):
+    """the workers' results; fails as soon as a worker dies without one (its peer would
+    otherwise wait in a collective until the timeout)"""
+    import queue
+    import time
+    res, t0 = {}, time.time()
+    while len(res) < len(procs):
+        try:
+            r, d = q.get(timeout=2)
+            res[r] = d
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"a worker died: exit codes {[p.exitcode for p in procs]}"
+            assert time.time() - t0 < limit, "workers timed out"
+    return res
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -111,7 +128,7 @@ def test_two_ranks_match_one_process_on_the_concatenated_batch():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = _collect(procs, q)
     res = {r: {k: (v if k in ("prefetched", "buckets") else [torch.from_numpy(x) for x in v]
                    if k in ("bitfields", "shards") else torch.from_numpy(v)) for k, v in d.items()}
            for r, d in res.items()}
@@ -179,9 +196,9 @@ def _seg_worker(rank, world, port, q):
         got = {}
         orig = tr._adam_shard
 
-        def spy(i, s):  # (on the stream the Adam runs on: the last step's copies win)
+        def spy(i, s, zero=None):  # (on the stream the Adam runs on: the last step's copies win)
             got[i] = tr._gshard[i].clone()
-            orig(i, s)
+            orig(i, s, zero)
         tr._adam_shard = spy
         gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
         for _ in range(2):
@@ -223,7 +240,7 @@ def test_segmented_replay_reduces_the_whole_gradient_when_every_level_is_binned(
     procs = [ctx.Process(target=_seg_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = _collect(procs, q)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
