@@ -123,6 +123,7 @@ class NGPTrainer:
         self.shards = [(a + (b - a) * self.rank // self.dp_world, a + (b - a) * (self.rank + 1) // self.dp_world)
                        for a, b in self.buckets]
         self._gshard = [torch.zeros(hi - lo, device=dev) for lo, hi in self.shards] if self.dp else None
+        self._bk = None  # (_bucket_host)
         self.global_step = 0
         # ---- occupancy (models/networks.py:20-30, train.py:78-82)
         self.center = torch.zeros(1, 3, device=dev)
@@ -760,13 +761,35 @@ class NGPTrainer:
 
     def _bucket_update(self, i):
         """On the comm stream: reduce-scatter of gradient bucket i into this
-        rank's shard, the bucket's local gradient zeroed, FusedAdam on the
-        shard, all-gather of the shard's fp16 shadow."""
-        a, b = self.buckets[i]
-        with torch.cuda.stream(self.comm_stream):
-            self._rs(i)
-            self._adam_shard(i, vren._stream(), zero=(a, b))  # (the bucket's local gradient cleared by it)
-            self._ag(i)
+        rank's shard, FusedAdam on the shard (the same launch clears the
+        bucket's local gradient), all-gather of the shard's fp16 shadow.  The
+        step runs this for every bucket, so its host path is lean: views and
+        launch arguments built once (_bucket_host)."""
+        h = self._bucket_host()[i]
+        cs = self.comm_stream
+        with torch.cuda.stream(cs):
+            if self.world == 1:  # (emulation: this rank's shard of the local gradient)
+                h["shard"].copy_(h["src"])
+            else:
+                ddp.reduce_scatter_(h["full"], h["shard"], self.pg)
+            self._adam_shard(i, HG.c_void_p(cs.cuda_stream), zero=True)
+            if self.world > 1:
+                ddp.all_gather_(h["p16full"], h["p16shard"], self.pg)
+
+    def _bucket_host(self):
+        """per bucket: the tensors its collectives take and the argument tuple
+        of its Adam launch (ngp_adam_step_dev_zero minus the stream)"""
+        if getattr(self, "_bk", None) is None:
+            self._bk = []
+            f = ctypes_float
+            for i, ((a, b), (lo, hi)) in enumerate(zip(self.buckets, self.shards)):
+                q = lambda t: _p(t[lo:hi])  # noqa: E731
+                adam = (q(self._pbuf), _p(self._gshard[i]), q(self.exp_avg), q(self.exp_avg_sq), q(self._p16buf),
+                        hi - lo, _p(self.lr_dev), f(0.9), f(0.999), f(1e-15), _p(self.dctr), f(1.0 / self.world), 1,
+                        _p(self._gbuf[a:b]), b - a)
+                self._bk.append({"full": self._gbuf[a:b], "src": self._gbuf[lo:hi], "shard": self._gshard[i],
+                                 "p16full": self._p16buf[a:b], "p16shard": self._p16buf[lo:hi], "adam": adam})
+        return self._bk
 
     def _rs(self, i):
         (a, b), (lo, hi), gs = self.buckets[i], self.shards[i], self._gshard[i]
@@ -1015,19 +1038,15 @@ class NGPTrainer:
         for i in range(len(self.buckets)):
             self._adam_shard(i, vren._stream())
 
-    def _adam_shard(self, i, s, zero=None):
+    def _adam_shard(self, i, s, zero=False):
         """FusedAdam on this rank's shard of bucket i: fp32 master, moments
         and fp16 shadow of the shard, from the reduced gradient shard (the
-        1/world mean folded in; the shard buffer zeroed).  zero = (a, b):
-        the launch also clears the local gradient _gbuf[a:b]."""
-        lo, hi = self.shards[i]
-        q = lambda t: _p(t[lo:hi])  # noqa: E731
-        za, zb = zero if zero is not None else (0, 0)
-        vren._ok(self.L.ngp_adam_step_dev_zero(q(self._pbuf), _p(self._gshard[i]), q(self.exp_avg), q(self.exp_avg_sq),
-                                               q(self._p16buf), hi - lo, _p(self.lr_dev), ctypes_float(0.9),
-                                               ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
-                                               ctypes_float(1.0 / self.world), 1,
-                                               _p(self._gbuf[za:zb]) if zb > za else None, zb - za, s), "adam")
+        1/world mean folded in; the shard buffer zeroed).  zero: the launch
+        also clears the bucket's local gradient."""
+        args = self._bucket_host()[i]["adam"]
+        if not zero:
+            args = args[:-2] + (None, 0)
+        vren._ok(self.L.ngp_adam_step_dev_zero(*args, s), "adam")
 
     def _gather_params16(self):
         """All-gather of the updated fp16 shadow the kernels read."""

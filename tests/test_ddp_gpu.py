@@ -196,7 +196,7 @@ def _seg_worker(rank, world, port, q):
         got = {}
         orig = tr._adam_shard
 
-        def spy(i, s, zero=None):  # (on the stream the Adam runs on: the last step's copies win)
+        def spy(i, s, zero=False):  # (on the stream the Adam runs on: the last step's copies win)
             got[i] = tr._gshard[i].clone()
             orig(i, s, zero)
         tr._adam_shard = spy
