@@ -47,7 +47,7 @@ class NGPTrainer:
                  update_interval=16, warmup_steps=256, max_samples=MAX_SAMPLES, sample_capacity=None, seed=4,
                  device="cuda", process_group=None, hash_backward="hybrid", bin_samples_per_ray=None, bin_level_lo=None,
                  chunk_first=64, erode=False, lambda_distortion=0.0, bin_merge_hi=None, fused_adam=True, use_graphs=True,
-                 pair_steps=False, emulate_dp=False, dp_fine_buckets=4):
+                 pair_steps=False, emulate_dp=False, dp_fine_buckets=2):
         self.dev = torch.device(device)
         self.scale = float(scale)
         self.batch_size = batch_size
