@@ -6,6 +6,7 @@
 #pragma clang fp contract(off)
 
 #include "common.h"
+#include "transmittance.h"
 
 namespace ngp {
 
@@ -75,36 +76,7 @@ __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
     return v;
 }
 
-// Transmittance over one 64-sample chunk of a row, lane j < cnt holding
-// om_j = 1 - a_j: T after sample j is T_in x (inclusive product of om, a
-// fixed Hillis-Steele order -- the reference's serial product reassociated,
-// like the wave sums), Tk the transmittance in front of sample j.  stop = 1 +
-// the first j with T after it <= thr (where composite_train_fw breaks), else
-// cnt.  chunk_rest_kernel calls the same function, so the chunked field
-// evaluation sees exactly the composite's termination.  A serial readlane
-// walk here set the kernel time by the longest rows (hundreds of samples).
-struct ChunkT {
-    float Tk, Tn;
-    int stop;
-    bool hit;
-};
-__device__ __forceinline__ ChunkT chunk_transmittance(float om, int cnt, float T_in, float thr, int lane) {
-    float p = lane < cnt ? om : 1.0f;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const float y = __shfl_up(p, o, 64);
-        if (lane >= o) p *= y;
-    }
-    float pe = __shfl_up(p, 1, 64);
-    if (lane == 0) pe = 1.0f;
-    ChunkT r;
-    r.Tk = T_in * pe;
-    r.Tn = T_in * p;
-    const uint64_t h = __ballot(lane < cnt && r.Tn <= thr);
-    r.hit = h != 0ull;
-    r.stop = r.hit ? __ffsll((unsigned long long)h) : cnt;
-    return r;
-}
+// (ChunkT / chunk_transmittance: transmittance.h, shared with the field forward)
 
 // One row of rays_a on one wave; returns the composited sample count
 // (vr_samples' share of this ray) and, in na_out, the samples that carry

@@ -168,7 +168,7 @@ class NGPTrainer:
         self._ran_ahead = False
         self._pair_key = None
         self._bind(self.msets[0])
-        self.sigmas, self.rgbs = torch.empty(cap, **f), torch.empty(cap, 3, **f)
+        self.sigmas, self.rgbs = torch.zeros(cap, **f), torch.zeros(cap, 3, **f)  # (finite where never evaluated)
         # saved encoding: pair-major (8, cap, 4) for the split forward, else row-major (cap, 32)
         # hybrid hash backward: the atomic coarse levels run on their own
         # stream beside the binned fine levels (disjoint gradient ranges;
@@ -208,6 +208,11 @@ class NGPTrainer:
         # round-2 list in one launch (counts + look-back scan + map): its look-back workspace, zeroed once
         self._cs_ws = torch.zeros((vren.lib().ngp_chunk_segments_workspace(R) + 7) // 8, dtype=torch.int64,
                                   device=dev)
+        # (NGP_ROW_FWD=1: both rounds as ONE launch, a wave per row looping over its 64-sample
+        # chunks until the row terminates -- ngp_field_forward_rows; its row ticket, zeroed once)
+        self.row_forward = os.environ.get("NGP_ROW_FWD", "0") == "1"
+        self._rows_ws = torch.zeros((HG._lib().ngp_field_forward_rows_workspace() + 7) // 8, dtype=torch.int64,
+                                    device=dev)
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
@@ -472,7 +477,7 @@ class NGPTrainer:
             # instead of at the head of this batch's step; its length eval_total1 is counted
             # into eval_stats by the round-2 list launch of the step that evaluates it
             K = self.chunk_first
-            m["eval1_K"] = K if (K > 0 and R <= 65536) else 0
+            m["eval1_K"] = K if (K > 0 and R <= 65536 and not self.row_forward) else 0
             if m["eval1_K"]:
                 vren._ok(L.ngp_ray_segments_capped(_p(m["rays_a"]), R, K, _p(m["act_start1"]), _p(m["eval_total1"]),
                                                    None, _p(m["eval_idx1"]), s), "segments_capped")
@@ -877,7 +882,15 @@ class NGPTrainer:
         if fork is not None:
             fork()
         self._ev("field_fwd", 0)
-        if self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
+        if self.chunk_first > 0 and self.row_forward:  # every row's chunks until it terminates, one launch
+            self._ev("hash_encode", 0)
+            vren._ok(HGL.ngp_field_forward_rows(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a), R,
+                                                self.cap, ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
+                                                _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc),
+                                                _p(self.sigmas), _p(self.rgbs), _p(self._rows_ws),
+                                                _p(self.eval_stats), s), "field_forward_rows")
+            self._ev("hash_encode", 1)
+        elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
             if self.eval1_K == K:  # built by this batch's march
                 self._field_indexed(s, self.eval_idx1, self.eval_total1)

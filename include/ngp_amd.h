@@ -335,6 +335,26 @@ int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const in
 int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
                          const int32_t* sample_idx, const ngp_hashgrid_t* grid, const void* table_f16,
                          const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs, void* h_f16, void* stream);
+/* The chunked training forward of a whole batch in one launch: for every row
+ * r < n_rows of rays_a (ray, start, N), its samples start.. evaluated 64 at a
+ * time (encode + MLPs as ngp_field_encode_mlp: enc_pm (plane stride n,
+ * nullable), sigmas, rgbs, bit for bit) until the chunk in which the row's
+ * transmittance prod(exp(-sigma delta)) falls to T_threshold (the
+ * compositing kernel's termination, same arithmetic) -- every sample
+ * ngp_composite_loss reads is evaluated; later samples are left untouched.
+ * Replaces the two chunked rounds (ngp_ray_segments_capped +
+ * ngp_field_encode_mlp over the first 64 samples of every row, then
+ * ngp_chunk_segments + ngp_field_encode_mlp over the rest of the rows still
+ * transparent) for the model(xyzs, dirs) call of __render_rays_train
+ * (models/rendering.py:278: NGP.forward on every marched sample).  ticket_ws: a
+ * ngp_field_forward_rows_workspace()-byte buffer, zeroed once before the
+ * first launch (every launch leaves it zeroed); *evaluated (nullable) +=
+ * the evaluated samples. */
+size_t ngp_field_forward_rows_workspace(void);
+int ngp_field_forward_rows(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
+                           int64_t n_rows, int64_t n, float T_threshold, const ngp_hashgrid_t* grid,
+                           const void* table_f16, const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs,
+                           void* ticket_ws, int64_t* evaluated, void* stream);
 int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev,
                           const int32_t* sample_idx, const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16,
                           void* stream);

@@ -176,6 +176,41 @@ def test_chunked_forward_matches_full(first, table_init):
         assert ev1 < n1
 
 
+@pytest.mark.parametrize("table_init", [0.2, 2.0])
+def test_row_forward_matches_two_rounds_and_full(table_init):
+    """The one-launch row forward (ngp_field_forward_rows: a wave per row,
+    64-sample chunks until the row's transmittance falls to 1e-4) gives the
+    full forward's step exactly as the two chunked rounds do: loss and per-ray
+    outputs bit-identical, gradients equal up to atomic summation order; it
+    evaluates no more samples than the two rounds; and a second launch (the
+    row ticket reset by the first) repeats the step bit for bit."""
+    runs = []
+    for chunk, rows in ((0, False), (64, False), (64, True)):
+        sc, tr, img, pix, noise = _setup(table_init=table_init)
+        tr.chunk_first, tr.row_forward = chunk, rows
+        dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+        o, d = sc.rays(img, pix)
+        gt = sc.gt_rgb_rays(o, d).to(DEV)
+        tr.reset_stats()
+        loss = tr.step(img.to(DEV), pix.to(DEV), gt, dirs, poses, noise=noise.to(DEV), apply_adam=False)
+        torch.cuda.synchronize()
+        ev = tr.stat_totals()[3]
+        out = (loss.clone(), tr.out_rgb.clone(), tr.out_op.clone(), tr.grad.clone(), ev)
+        if rows:
+            tr.grad.zero_()
+            loss2 = tr.step(img.to(DEV), pix.to(DEV), gt, dirs, poses, noise=noise.to(DEV), apply_adam=False)
+            torch.cuda.synchronize()
+            assert torch.equal(loss2, out[0]) and torch.equal(tr.out_rgb, out[1])
+            assert tr.stat_totals()[3] == 2 * ev
+        runs.append(out)
+    (l0, r0, o0, g0, _), (l1, r1, o1, g1, ev1), (l2, r2, o2, g2, ev2) = runs
+    assert torch.equal(l0, l2) and torch.equal(r0, r2) and torch.equal(o0, o2)
+    assert torch.equal(l1, l2) and torch.equal(r1, r2)
+    assert float((g2 - g0).norm() / g0.norm()) < 1e-5
+    print(f"evaluated samples: two rounds {ev1}, row forward {ev2}")
+    assert 0 < ev2 <= ev1
+
+
 def test_repeated_step_gradients_agree_per_level():
     """The same step from the same state, repeated: every parameter group and
     hash level agrees to fp32 atomic-order noise (a lost or duplicated
