@@ -18,6 +18,7 @@ kernels read the live sample count from device memory.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -272,7 +273,6 @@ class NGPTrainer:
         # graph, scripts/diag/graph_split_cost.py; profiles/r04/ab/ab_r4d.txt)
         self._ticket_ws = torch.zeros((vren.lib().ngp_step_ticket_workspace() + 3) // 4, dtype=torch.int32,
                                       device=dev)
-        import os
         self.step_ticket = os.environ.get("NGP_STEP_TICKET", "0") == "1"
         self._ticket_active = False
         # (opt-in, NGP_FUSED_COARSE=1) single-process hybrid steps: the coarse (atomic) hash levels
