@@ -798,131 +798,128 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
     }
 }
 
-// Chunked field forward of a whole batch in ONE launch, one row of rays_a per
-// wave at a time: the wave evaluates the row's samples 64 at a time (the
-// gather rounds and MLPs of field_encode_mlp_reg_kernel, lane = sample
-// start + k0 + lane), carries the row's transmittance through
-// chunk_transmittance (the composite's product scan, the same function), and
-// stops after the chunk in which it falls to T_thr -- every sample the
-// composite reads is evaluated, as with the two-round lists (first 64 samples
-// of every row, then the whole rest of the rows still transparent), but
-// without the round-2 list pass and the second launch, and a long row's
-// samples past its terminating chunk are not evaluated (Lego-shaped steady
-// state: 240 K lane slots per batch instead of 304 K samples,
-// scripts/diag/row_chunks.py).  Rows are claimed through a device ticket
-// (resident blocks only; a wave claims its next row while it works on this
-// one, so CUs shared with the march simply take fewer rows); every wave's
-// last claim fails exactly once, and the one that draws the last ticket
-// value (n_rows + waves - 1: every other claim is done) resets the ticket
-// for the next launch.  evaluated += the evaluated samples (one atomic per
-// block).
-struct RowsTicket {
-    uint32_t next;
-};
+// Encode + MLPs of the 64-sample chunk [i0, i0 + cnt) on one wave (lane =
+// sample i0 + lane): field_encode_mlp_reg_kernel's body for a contiguous
+// chunk; returns this lane's sigma (0 past cnt) for a transmittance epilogue.
 template <bool COLOR>
-__global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_kernel(
+__device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs, const float* __restrict__ dirs,
+                                                  int64_t i0, int cnt, int64_t n, const GridArgs& ga,
+                                                  const LevelLds& lv, const uint32_t* __restrict__ table,
+                                                  const _Float16* sw, _Float16* __restrict__ enc_pm,
+                                                  float* __restrict__ sigmas, float* __restrict__ rgbs) {
+    int lane_l = threadIdx.x & 63;  // (opaque: lane-derived addresses are rematerialised, not held)
+    asm volatile("" : "+v"(lane_l));
+    const int s = lane_l & 15, g = lane_l >> 4;
+    const bool valid = lane_l < cnt;
+    const int64_t i = i0 + lane_l;
+    float in[3];
+    load_x01(xyzs, i, valid, ga, in);
+    uint32_t E[16];
+#pragma unroll 1
+    for (int rr = 0; rr < L / FEM_LPR; ++rr) {
+        uint32_t v[FEM_LPR][8];
+#pragma unroll
+        for (int q = 0; q < FEM_LPR; ++q) gather_level_loads(in, level_u(lv, FEM_LPR * rr + q), table, v[q]);
+#pragma unroll
+        for (int q = 0; q < 16 - FEM_LPR; ++q) E[q] = E[q + FEM_LPR];
+#pragma unroll
+        for (int q = 0; q < FEM_LPR; ++q) E[16 - FEM_LPR + q] = level_sum_h2(in, level_u(lv, FEM_LPR * rr + q), v[q]);
+    }
+    if (valid && enc_pm) {
+#pragma unroll
+        for (int pr = 0; pr < 8; ++pr)
+            *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(E[2 * pr], E[2 * pr + 1]);
+    }
+    transpose_rows4(E);
+    float sg = 0.f;
+#pragma unroll 1
+    for (int c = 0; c < 4; ++c) {
+        if (16 * c >= cnt) break;  // (wave-uniform: no sample in this or a later column block)
+        const bool ok = 16 * c + s < cnt;
+        const int64_t ic = i0 + 16 * c + s;
+        const h8 e = __builtin_bit_cast(h8, make_uint4(E[0], E[1], E[2], E[3]));
+#pragma unroll
+        for (int q = 0; q < 12; ++q) E[q] = E[q + 4];
+        h4 h1[4];
+        const h4 hh = density_net(e, sw, s, g, h1);
+        const float sig = expf((float)hh[0]);  // TruncExp forward (custom_functions.py:165-167)
+        if (ok && g == 0) sigmas[ic] = sig;
+        const float sgc = __shfl(sig, lane_l & 15, 64);  // sample 16 c + s's sigma to lane 16 c + s
+        if ((lane_l >> 4) == c) sg = sgc;
+        if constexpr (COLOR) {
+            const float dx = ok ? dirs[3 * ic] : 0.f, dy = ok ? dirs[3 * ic + 1] : 0.f, dz = ok ? dirs[3 * ic + 2] : 1.f;
+            float sh[4];
+            sh4_select(dx, dy, dz, g, sh);
+            const h8 cin = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3], hh[0], hh[1], hh[2], hh[3]};
+            h4 h3[4], h4v[4];
+            const h4 o = color_net(cin, sw, s, g, h3, h4v);
+            if (ok && g == 0) {
+                rgbs[3 * ic] = sigmoid_h(o[0]);
+                rgbs[3 * ic + 1] = sigmoid_h(o[1]);
+                rgbs[3 * ic + 2] = sigmoid_h(o[2]);
+            }
+        }
+    }
+    return sg;
+}
+
+// Round 1 of the chunked training forward with the round-2 counts fused in:
+// one wave per non-empty row (rows[], built beside the previous step by
+// ngp_rays_nonempty, so no wave holds more than its one chunk while rows are
+// fewer than resident waves), its first min(N, 64) samples encoded and run
+// through the MLPs, then the row's transmittance over them
+// (chunk_transmittance, the composite's product scan: the same function and
+// expressions as chunk_segments_kernel) -> rest[r] = N - 64 if the row is
+// still transparent after its first chunk, else 0.  The round-2 list is then
+// a plain scan of rest (ngp_ray_segments: no transmittance pass, no
+// look-back chain).  A wave per row rather than 64 packed list entries
+// (~8 % idle lanes on this step's rows); the sigmas never leave registers.
+template <bool COLOR>
+__global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_chunk_kernel(
     const float* __restrict__ xyzs, const float* __restrict__ dirs, const float* __restrict__ deltas,
-    const int64_t* __restrict__ rays_a, uint32_t n_rows, int64_t n, float T_thr, GridArgs ga,
-    const uint32_t* __restrict__ table, const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm,
-    float* __restrict__ sigmas, float* __restrict__ rgbs, RowsTicket* __restrict__ tk,
-    int64_t* __restrict__ evaluated) {
+    const int64_t* __restrict__ rays_a, const int32_t* __restrict__ rows, const int64_t* __restrict__ n_rows_dev,
+    int64_t n_rows, int64_t n, float T_thr, GridArgs ga, const uint32_t* __restrict__ table,
+    const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm, float* __restrict__ sigmas,
+    float* __restrict__ rgbs, int32_t* __restrict__ rest, int64_t* __restrict__ evaluated) {
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ LevelLds lv;
     __shared__ unsigned long long blk_eval;
-    const int lane = threadIdx.x & 63;
-    const uint32_t last_claim = n_rows + gridDim.x * FEM2_WAVES - 1;
-    auto claim = [&]() {
-        uint32_t r = 0;
-        if (lane == 0) r = __hip_atomic_fetch_add(&tk->next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return rfl(__shfl(r, 0, 64));
-    };
-    // the first row (claim -> rays_a: dependent round trips) requested before the
-    // weight image is built, so the two overlap
-    uint32_t r = claim();
-    int64_t start = 0, N = 0;
-    if (r < n_rows) { start = rays_a[3 * (int64_t)r + 1]; N = rays_a[3 * (int64_t)r + 2]; }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t NR = n_rows_dev ? *n_rows_dev : n_rows;
+    const int64_t G = gridDim.x, stride = (int64_t)FEM2_WAVES * G;
+    int64_t j = (int64_t)wv * G + blockIdx.x;  // the wave's first row (wave-uniform)
+    // its row (list -> rays_a: dependent round trips) requested before the weight image is built
+    int64_t r = 0, start = 0, N = 0;
+    if (j < NR) {
+        r = rows ? (int64_t)rows[j] : j;
+        start = rays_a[3 * r + 1];
+        N = rays_a[3 * r + 2];
+    }
     if (threadIdx.x == 0) blk_eval = 0ull;
     load_fwd_weights_direct(mlp, sw, COLOR);
     load_levels(ga, lv);
     __syncthreads();
     int64_t ev = 0;
-    while (r < n_rows) {
-        const uint32_t r_next = claim();  // (returns while this row is evaluated)
-        float T = 1.0f;
-        for (int64_t k0 = 0; k0 < N; k0 += 64) {
-            int lane_l = lane;  // (opaque per chunk: lane-derived addresses are not held across it)
-            asm volatile("" : "+v"(lane_l));
-            const int s = lane_l & 15, g = lane_l >> 4;
-            const int cnt = (int)(N - k0 < 64 ? N - k0 : 64);
-            const bool valid = lane_l < cnt;
-            const int64_t i = start + k0 + lane_l;
-            float in[3];
-            load_x01(xyzs, i, valid, ga, in);
-            const float dl = valid ? deltas[i] : 0.f;
-            uint32_t E[16];
-#pragma unroll 1
-            for (int rr = 0; rr < L / FEM_LPR; ++rr) {
-                uint32_t v[FEM_LPR][8];
-#pragma unroll
-                for (int q = 0; q < FEM_LPR; ++q) gather_level_loads(in, level_u(lv, FEM_LPR * rr + q), table, v[q]);
-#pragma unroll
-                for (int q = 0; q < 16 - FEM_LPR; ++q) E[q] = E[q + FEM_LPR];
-#pragma unroll
-                for (int q = 0; q < FEM_LPR; ++q)
-                    E[16 - FEM_LPR + q] = level_sum_h2(in, level_u(lv, FEM_LPR * rr + q), v[q]);
-            }
-            if (valid && enc_pm) {
-#pragma unroll
-                for (int pr = 0; pr < 8; ++pr)
-                    *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(E[2 * pr], E[2 * pr + 1]);
-            }
-            transpose_rows4(E);
-            float sg = 0.f;  // sigma of this lane's sample, for the transmittance
-#pragma unroll 1
-            for (int c = 0; c < 4; ++c) {
-                if (16 * c >= cnt) break;  // (wave-uniform: no sample in this or a later column block)
-                const int jc = 16 * c + s;
-                const bool ok = jc < cnt;
-                const int64_t ic = start + k0 + jc;
-                const h8 e = __builtin_bit_cast(h8, make_uint4(E[0], E[1], E[2], E[3]));
-#pragma unroll
-                for (int q = 0; q < 12; ++q) E[q] = E[q + 4];
-                h4 h1[4];
-                const h4 hh = density_net(e, sw, s, g, h1);
-                const float sig = expf((float)hh[0]);  // TruncExp forward (custom_functions.py:165-167)
-                if (ok && g == 0) sigmas[ic] = sig;
-                const float sgc = __shfl(sig, lane_l & 15, 64);
-                if ((lane_l >> 4) == c) sg = sgc;
-                if constexpr (COLOR) {
-                    const float dx = ok ? dirs[3 * ic] : 0.f, dy = ok ? dirs[3 * ic + 1] : 0.f,
-                                dz = ok ? dirs[3 * ic + 2] : 1.f;
-                    float sh[4];
-                    sh4_select(dx, dy, dz, g, sh);
-                    const h8 cin = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3],
-                                    hh[0], hh[1], hh[2], hh[3]};
-                    h4 h3[4], h4v[4];
-                    const h4 o = color_net(cin, sw, s, g, h3, h4v);
-                    if (ok && g == 0) {
-                        rgbs[3 * ic] = sigmoid_h(o[0]);
-                        rgbs[3 * ic + 1] = sigmoid_h(o[1]);
-                        rgbs[3 * ic + 2] = sigmoid_h(o[2]);
-                    }
-                }
-            }
+    for (; j < NR; j += stride) {
+        const int cnt = (int)(N < 64 ? N : 64);
+        int32_t rc = 0;
+        if (cnt > 0) {
+            const float dl = lane < cnt ? deltas[start + lane] : 0.f;
+            const float sg = encode_mlp_chunk<COLOR>(xyzs, dirs, start, cnt, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
+            const float om = 1.0f - (1.0f - __expf(-sg * dl));  // chunk_segments_kernel's expression
+            const ChunkT ct = chunk_transmittance(om, cnt, 1.0f, T_thr, lane);
+            rc = (!ct.hit && N > 64) ? (int32_t)(N - 64) : 0;
             ev += cnt;
-            // chunk_segments_kernel's expression for the opacity complement
-            const float om = 1.0f - (1.0f - __expf(-sg * dl));
-            const ChunkT ct = chunk_transmittance(om, cnt, T, T_thr, lane_l);
-            if (ct.hit) break;
-            T = __shfl(ct.Tn, ct.stop - 1, 64);
         }
-        r = r_next;
-        if (r < n_rows) { start = rays_a[3 * (int64_t)r + 1]; N = rays_a[3 * (int64_t)r + 2]; }
+        if (lane == 0) rest[r] = rc;
+        const int64_t jn = j + stride;
+        if (jn < NR) {
+            r = rows ? (int64_t)rows[jn] : jn;
+            start = rays_a[3 * r + 1];
+            N = rays_a[3 * r + 2];
+        }
     }
-    if (lane == 0) {
-        if (r == last_claim) __hip_atomic_store(&tk->next, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (ev) atomicAdd(&blk_eval, (unsigned long long)ev);
-    }
+    if (lane == 0 && ev) atomicAdd(&blk_eval, (unsigned long long)ev);
     __syncthreads();
     if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
 }
@@ -1806,25 +1803,26 @@ int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const 
     return ngp_launch_status();
 }
 
-size_t ngp_field_forward_rows_workspace(void) { return 64; }
-
-int ngp_field_forward_rows(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
-                           int64_t n_rows, int64_t n, float T_threshold, const ngp_hashgrid_t* grid,
-                           const void* table_f16, const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs,
-                           void* ticket_ws, int64_t* evaluated, void* stream) {
+int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
+                            const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
+                            float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
+                            void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int64_t* evaluated,
+                            void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
-    NGP_CHECK_ARG(n_rows >= 0 && n_rows <= 0x7f000000 && n >= 0);
+    NGP_CHECK_ARG(n_rows >= 0 && n >= 0);
     if (n_rows == 0) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && dirs && deltas && rays_a && table_f16 && mlp_f16 && sigmas && rgbs && ticket_ws);
+    NGP_CHECK_ARG(xyzs && dirs && deltas && rays_a && table_f16 && mlp_f16 && sigmas && rgbs && rest);
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0 &&
-                  ((uintptr_t)ticket_ws & 7) == 0 && ((uintptr_t)evaluated & 7) == 0);
+                  ((uintptr_t)evaluated & 7) == 0);
     hipStream_t s = as_stream(stream);
-    static const unsigned cap = resident_blocks(field_rows_kernel<true>, 64 * FEM2_WAVES, 0);
-    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_rows_kernel<true><<<cap, 64 * FEM2_WAVES, 0, s>>>(
-        xyzs, dirs, deltas, rays_a, (uint32_t)n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
-        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, (RowsTicket*)ticket_ws, evaluated));
+    // grid = every resident block: the rows are dealt over all resident waves
+    static const unsigned cap = resident_blocks(field_first_chunk_kernel<true>, 64 * FEM2_WAVES, 0);
+    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + FEM2_WAVES - 1) / FEM2_WAVES)));
+    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_first_chunk_kernel<true><<<blocks, 64 * FEM2_WAVES, 0, s>>>(
+        xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
+        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, evaluated));
     return ngp_launch_status();
 }
 

@@ -981,6 +981,62 @@ __global__ void __launch_bounds__(256) chunk_rest_kernel(const float* __restrict
     if (lane == 0) counts[n] = (!done && N > first) ? (int32_t)(end - first) : 0;
 }
 
+// The non-empty rows of rays_a in row order (rows[0..*n_rows)) for
+// field_first_chunk_kernel's one-wave-per-row round 1, and rest[r] = 0 for the
+// empty ones (that kernel writes the others).  One 1024-thread block, 8 rows
+// per thread per tile; runs on the march's side stream right after the
+// compaction, off the step's critical path.
+__global__ void __launch_bounds__(1024) rays_nonempty_kernel(const int64_t* __restrict__ rays_a, int64_t n_rays,
+                                                             int32_t* __restrict__ rows, int64_t* __restrict__ n_out,
+                                                             int32_t* __restrict__ rest) {
+    __shared__ int32_t wave_sums[16];
+    __shared__ int64_t carry_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    constexpr int PER = 8;
+    for (int64_t base = 0; base < n_rays; base += 1024 * PER) {
+        uint32_t f = 0;  // bit k: row base + 8 tid + k is non-empty
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int64_t i = base + (int64_t)tid * PER + k;
+            if (i < n_rays && rays_a[3 * i + 2] > 0) f |= 1u << k;
+        }
+        const int32_t local = __popc(f);
+        int32_t incl = local;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wave_sums[wid] = incl;
+        __syncthreads();
+        if (wid == 0) {
+            int32_t ws = lane < 16 ? wave_sums[lane] : 0;
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                const int32_t y = __shfl_up(ws, off, 64);
+                if (lane >= off) ws += y;
+            }
+            if (lane < 16) wave_sums[lane] = ws;  // inclusive over waves
+        }
+        __syncthreads();
+        const int64_t carry = carry_s;
+        int64_t o = carry + (wid > 0 ? wave_sums[wid - 1] : 0) + incl - local;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int64_t i = base + (int64_t)tid * PER + k;
+            if (i >= n_rays) break;
+            if (f >> k & 1u) rows[o++] = (int32_t)i;
+            else if (rest) rest[i] = 0;
+        }
+        __syncthreads();
+        if (tid == 0) carry_s = carry + wave_sums[15];
+        __syncthreads();
+    }
+    if (tid == 0) *n_out = carry_s;
+}
+
 // Round-2 list in one launch: chunk_rest_kernel's counts + the exclusive scan
 // across rows + the map of ray_segments.  Block b owns rows [64b, 64b + 64):
 // its waves compute the counts of 8 rows each (first-chunk loads of all 8
@@ -1139,6 +1195,14 @@ int ngp_chunk_counts_range(const int64_t* rays_a, int64_t n_rows, int first, int
         NGP_TIMED(NGP_K_CHUNK, as_stream(stream), chunk_rest_kernel<<<(unsigned)((n_rows + 3) / 4), 256, 0, as_stream(stream)>>>(sigmas, deltas, rays_a, n_rows,
                                                                                       first, last, T_threshold, counts));
     }
+    return ngp_launch_status();
+}
+
+int ngp_rays_nonempty(const int64_t* rays_a, int64_t n_rays, int32_t* rows, int64_t* n_rows, int32_t* rest,
+                      void* stream) {
+    NGP_CHECK_ARG(n_rays >= 0 && n_rays <= 0x7fffffff && n_rows);
+    NGP_CHECK_ARG(n_rays == 0 || (rays_a && rows));
+    NGP_TIMED(NGP_K_SEGMENTS, as_stream(stream), rays_nonempty_kernel<<<1, 1024, 0, as_stream(stream)>>>(rays_a, n_rays, rows, n_rows, rest));
     return ngp_launch_status();
 }
 

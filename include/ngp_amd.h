@@ -335,26 +335,30 @@ int ngp_hash_encode(const float* xyzs, int64_t n, const int64_t* n_dev, const in
 int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const int64_t* n_dev,
                          const int32_t* sample_idx, const ngp_hashgrid_t* grid, const void* table_f16,
                          const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs, void* h_f16, void* stream);
-/* The chunked training forward of a whole batch in one launch: for every row
- * r < n_rows of rays_a (ray, start, N), its samples start.. evaluated 64 at a
- * time (encode + MLPs as ngp_field_encode_mlp: enc_pm (plane stride n,
- * nullable), sigmas, rgbs, bit for bit) until the chunk in which the row's
- * transmittance prod(exp(-sigma delta)) falls to T_threshold (the
- * compositing kernel's termination, same arithmetic) -- every sample
- * ngp_composite_loss reads is evaluated; later samples are left untouched.
- * Replaces the two chunked rounds (ngp_ray_segments_capped +
- * ngp_field_encode_mlp over the first 64 samples of every row, then
- * ngp_chunk_segments + ngp_field_encode_mlp over the rest of the rows still
- * transparent) for the model(xyzs, dirs) call of __render_rays_train
- * (models/rendering.py:278: NGP.forward on every marched sample).  ticket_ws: a
- * ngp_field_forward_rows_workspace()-byte buffer, zeroed once before the
- * first launch (every launch leaves it zeroed); *evaluated (nullable) +=
- * the evaluated samples. */
-size_t ngp_field_forward_rows_workspace(void);
-int ngp_field_forward_rows(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
-                           int64_t n_rows, int64_t n, float T_threshold, const ngp_hashgrid_t* grid,
-                           const void* table_f16, const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs,
-                           void* ticket_ws, int64_t* evaluated, void* stream);
+/* The non-empty rows (N > 0) of rays_a, ascending, into rows[0..*n_rows);
+ * rest (nullable): rest[r] = 0 for every empty row (ngp_field_forward_first
+ * writes the others).  One launch (one workgroup; the list of a batch of
+ * rays, built beside the previous step). */
+int ngp_rays_nonempty(const int64_t* rays_a, int64_t n_rays, int32_t* rows, int64_t* n_rows, int32_t* rest,
+                      void* stream);
+/* Round 1 of the chunked training forward with the round-2 counts: for the
+ * rows rows[j], j < *n_rows_dev (rows NULL: rows 0..n_rows-1; n_rows_dev
+ * NULL: n_rows) of rays_a (ray, start, N), the first min(N, 64) samples
+ * encoded and run through the MLPs (enc_pm (plane stride n, nullable),
+ * sigmas, rgbs: ngp_field_encode_mlp's values bit for bit), then the row's
+ * transmittance over them (the compositing kernel's product scan) -> rest[r]
+ * = N - 64 if it is still above T_threshold after them, else 0 -- the counts
+ * ngp_chunk_counts_range(first = 64) gives, so ngp_ray_segments(rest, first =
+ * 64) lists the round-2 samples.  *evaluated (nullable) += the samples
+ * evaluated.  With ngp_rays_nonempty's list: one wave per non-empty row.
+ * Replaces, for the model(xyzs, dirs) call of __render_rays_train
+ * (models/rendering.py:278), round 1's ngp_field_encode_mlp + the round-2
+ * count / scan / list launch ngp_chunk_segments. */
+int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
+                            const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
+                            float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
+                            void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int64_t* evaluated,
+                            void* stream);
 int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev,
                           const int32_t* sample_idx, const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16,
                           void* stream);

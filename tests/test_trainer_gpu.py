@@ -178,12 +178,12 @@ def test_chunked_forward_matches_full(first, table_init):
 
 @pytest.mark.parametrize("table_init", [0.2, 2.0])
 def test_row_forward_matches_two_rounds_and_full(table_init):
-    """The one-launch row forward (ngp_field_forward_rows: a wave per row,
-    64-sample chunks until the row's transmittance falls to 1e-4) gives the
-    full forward's step exactly as the two chunked rounds do: loss and per-ray
-    outputs bit-identical, gradients equal up to atomic summation order; it
-    evaluates no more samples than the two rounds; and a second launch (the
-    row ticket reset by the first) repeats the step bit for bit."""
+    """The row forward's round 1 (ngp_field_forward_first: a wave per
+    non-empty row from ngp_rays_nonempty, the row's transmittance in its
+    epilogue -> the round-2 counts, then ngp_ray_segments) gives the full
+    forward's step exactly as the two chunked rounds do: loss and per-ray
+    outputs bit-identical, gradients equal up to atomic summation order, the
+    same samples evaluated; and a second step repeats it bit for bit."""
     runs = []
     for chunk, rows in ((0, False), (64, False), (64, True)):
         sc, tr, img, pix, noise = _setup(table_init=table_init)
@@ -208,7 +208,7 @@ def test_row_forward_matches_two_rounds_and_full(table_init):
     assert torch.equal(l1, l2) and torch.equal(r1, r2)
     assert float((g2 - g0).norm() / g0.norm()) < 1e-5
     print(f"evaluated samples: two rounds {ev1}, row forward {ev2}")
-    assert 0 < ev2 <= ev1
+    assert 0 < ev2 == ev1
 
 
 def test_repeated_step_gradients_agree_per_level():
