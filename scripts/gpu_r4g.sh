@@ -4,7 +4,7 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4g}; mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_trainer_gpu.py tests/test_field_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_trainer_gpu.py tests/test_field_gpu.py tests/test_vren_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
 tail -n 3 $OUT/pytest.log
 grep "evaluated samples" $OUT/pytest.log || true
 bash scripts/ab_env.sh ${1:-r4g}/ab 3 "||" "|NGP_ROW_FWD=1|"
@@ -14,4 +14,4 @@ NGP_ROW_FWD=1 timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/tr" -o run -f 
 python3 scripts/kstats.py "$OUT/tr/run_kernel_trace.csv" 200 > $OUT/kstats_rows.txt 2>&1 || true
 for b in 10 11 12; do python3 scripts/timeline.py "$OUT/tr/run_kernel_trace.csv" 20 $b; done > "$OUT/timeline_rows.txt"
 rm -rf "$OUT/tr"
-head -14 $OUT/kstats_rows.txt; head -30 $OUT/timeline_rows.txt
+head -16 $OUT/kstats_rows.txt; head -32 $OUT/timeline_rows.txt
