@@ -407,3 +407,26 @@ def test_chunk_segments_equals_counts_then_segments(n_rows, first, last):
         assert torch.equal(st, st_ref) and torch.equal(idx[:T], idx_ref[:T])
     if n_rows >= 1000:  # some rows terminate inside the first chunk, some go on
         assert 0 < int(tot_ref) < int(N.sum())
+
+
+@pytest.mark.parametrize("n_rows", [1, 100, 8192, 70000])
+def test_rays_nonempty_lists_rows_and_zeroes_empty_counts(n_rows):
+    """ngp_rays_nonempty: the rows with N > 0 in ascending order and their
+    count; rest[r] = 0 for every empty row, the others untouched (the row
+    forward's round 1 writes them)."""
+    import ctypes
+    L = vren.lib()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    g = torch.Generator().manual_seed(n_rows)
+    N = torch.randint(0, 300, (n_rows,), generator=g)
+    N[torch.rand(n_rows, generator=g) < 0.67] = 0
+    rays_a = torch.stack([torch.arange(n_rows), torch.cumsum(N, 0) - N, N], 1).to(DEV)
+    rows = torch.full((n_rows,), -1, dtype=torch.int32, device=DEV)
+    n_ne = torch.full((1,), -3, dtype=torch.int64, device=DEV)
+    rest = torch.full((n_rows,), 7, dtype=torch.int32, device=DEV)
+    vren._ok(L.ngp_rays_nonempty(p(rays_a), n_rows, p(rows), p(n_ne), p(rest), vren._stream()), "rays_nonempty")
+    torch.cuda.synchronize()
+    ref = torch.nonzero(N > 0).flatten()
+    assert int(n_ne) == ref.numel()
+    assert torch.equal(rows[:ref.numel()].cpu().long(), ref)
+    assert torch.equal(rest.cpu(), torch.where(N > 0, 7, 0).int())
