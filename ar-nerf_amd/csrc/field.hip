@@ -869,18 +869,24 @@ __device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs
 // fewer than resident waves), its first min(N, 64) samples encoded and run
 // through the MLPs, then the row's transmittance over them
 // (chunk_transmittance, the composite's product scan: the same function and
-// expressions as chunk_segments_kernel) -> rest[r] = N - 64 if the row is
-// still transparent after its first chunk, else 0.  The round-2 list is then
-// a plain scan of rest (ngp_ray_segments: no transmittance pass, no
-// look-back chain).  A wave per row rather than 64 packed list entries
-// (~8 % idle lanes on this step's rows); the sigmas never leave registers.
+// expressions as chunk_segments_kernel) -> rc = N - 64 if the row is still
+// transparent after its first chunk, else 0.  rest (nullable): rest[r] = rc
+// (the counts ngp_chunk_counts_range gives).  list2 (nullable): the row's
+// round-2 samples start + 64 .. start + N appended to list2 at a range
+// reserved by one atomic on *total2 (zero at launch): the round-2 list
+// without any scan -- rows land in reservation order, each row's samples
+// contiguous (the forward's outputs are per sample, so the order changes no
+// value); their count is added to *evaluated with the first chunks'.  A wave
+// per row rather than 64 packed list entries (~8 % idle lanes on this step's
+// rows); the sigmas never leave registers.
 template <bool COLOR>
 __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_chunk_kernel(
     const float* __restrict__ xyzs, const float* __restrict__ dirs, const float* __restrict__ deltas,
     const int64_t* __restrict__ rays_a, const int32_t* __restrict__ rows, const int64_t* __restrict__ n_rows_dev,
     int64_t n_rows, int64_t n, float T_thr, GridArgs ga, const uint32_t* __restrict__ table,
     const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm, float* __restrict__ sigmas,
-    float* __restrict__ rgbs, int32_t* __restrict__ rest, int64_t* __restrict__ evaluated) {
+    float* __restrict__ rgbs, int32_t* __restrict__ rest, int32_t* __restrict__ list2, int64_t* __restrict__ total2,
+    int64_t* __restrict__ evaluated) {
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ LevelLds lv;
     __shared__ unsigned long long blk_eval;
@@ -911,7 +917,14 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
             rc = (!ct.hit && N > 64) ? (int32_t)(N - 64) : 0;
             ev += cnt;
         }
-        if (lane == 0) rest[r] = rc;
+        if (rest && lane == 0) rest[r] = rc;
+        if (list2 && rc > 0) {
+            unsigned long long o = 0;
+            if (lane == 0) o = atomicAdd((unsigned long long*)total2, (unsigned long long)rc);
+            const int64_t o2 = (int64_t)__shfl(o, 0, 64);
+            for (int t = lane; t < rc; t += 64) list2[o2 + t] = (int32_t)(start + 64 + t);
+            ev += rc;
+        }
         const int64_t jn = j + stride;
         if (jn < NR) {
             r = rows ? (int64_t)rows[jn] : jn;
@@ -1806,14 +1819,15 @@ int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const 
 int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
                             const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
                             float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
-                            void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int64_t* evaluated,
-                            void* stream) {
+                            void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int32_t* list2,
+                            int64_t* total2, int64_t* evaluated, void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
     NGP_CHECK_ARG(n_rows >= 0 && n >= 0);
     if (n_rows == 0) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && dirs && deltas && rays_a && table_f16 && mlp_f16 && sigmas && rgbs && rest);
+    NGP_CHECK_ARG(xyzs && dirs && deltas && rays_a && table_f16 && mlp_f16 && sigmas && rgbs && (rest || list2));
+    NGP_CHECK_ARG(!list2 || (total2 && ((uintptr_t)total2 & 7) == 0));
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0 &&
                   ((uintptr_t)evaluated & 7) == 0);
     hipStream_t s = as_stream(stream);
@@ -1822,7 +1836,7 @@ int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* d
     const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + FEM2_WAVES - 1) / FEM2_WAVES)));
     NGP_TIMED(NGP_K_HASH_ENCODE, s, field_first_chunk_kernel<true><<<blocks, 64 * FEM2_WAVES, 0, s>>>(
         xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
-        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, evaluated));
+        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, list2, total2, evaluated));
     return ngp_launch_status();
 }
 

@@ -988,7 +988,7 @@ __global__ void __launch_bounds__(256) chunk_rest_kernel(const float* __restrict
 // compaction, off the step's critical path.
 __global__ void __launch_bounds__(1024) rays_nonempty_kernel(const int64_t* __restrict__ rays_a, int64_t n_rays,
                                                              int32_t* __restrict__ rows, int64_t* __restrict__ n_out,
-                                                             int32_t* __restrict__ rest) {
+                                                             int32_t* __restrict__ rest, int64_t* __restrict__ zero) {
     __shared__ int32_t wave_sums[16];
     __shared__ int64_t carry_s;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1034,7 +1034,10 @@ __global__ void __launch_bounds__(1024) rays_nonempty_kernel(const int64_t* __re
         if (tid == 0) carry_s = carry + wave_sums[15];
         __syncthreads();
     }
-    if (tid == 0) *n_out = carry_s;
+    if (tid == 0) {
+        *n_out = carry_s;
+        if (zero) *zero = 0;
+    }
 }
 
 // Round-2 list in one launch: chunk_rest_kernel's counts + the exclusive scan
@@ -1199,10 +1202,10 @@ int ngp_chunk_counts_range(const int64_t* rays_a, int64_t n_rows, int first, int
 }
 
 int ngp_rays_nonempty(const int64_t* rays_a, int64_t n_rays, int32_t* rows, int64_t* n_rows, int32_t* rest,
-                      void* stream) {
+                      int64_t* zero, void* stream) {
     NGP_CHECK_ARG(n_rays >= 0 && n_rays <= 0x7fffffff && n_rows);
     NGP_CHECK_ARG(n_rays == 0 || (rays_a && rows));
-    NGP_TIMED(NGP_K_SEGMENTS, as_stream(stream), rays_nonempty_kernel<<<1, 1024, 0, as_stream(stream)>>>(rays_a, n_rays, rows, n_rows, rest));
+    NGP_TIMED(NGP_K_SEGMENTS, as_stream(stream), rays_nonempty_kernel<<<1, 1024, 0, as_stream(stream)>>>(rays_a, n_rays, rows, n_rows, rest, zero));
     return ngp_launch_status();
 }
 

@@ -210,8 +210,8 @@ class NGPTrainer:
         self._cs_ws = torch.zeros((vren.lib().ngp_chunk_segments_workspace(R) + 7) // 8, dtype=torch.int64,
                                   device=dev)
         # (NGP_ROW_FWD=1: round 1 one wave per non-empty row with the row's transmittance in its
-        # epilogue -- ngp_field_forward_first -- so the round-2 list is a plain scan of its counts;
-        # chunk_first must then be 64, the wave width)
+        # epilogue, which appends the row's round-2 samples to the round-2 list itself --
+        # ngp_field_forward_first: no list launch; chunk_first must then be 64, the wave width)
         self.row_forward = os.environ.get("NGP_ROW_FWD", "0") == "1"
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -317,7 +317,7 @@ class NGPTrainer:
                     # row-forward round 1: the non-empty rows (built by the march), the round-2 counts
                     rows_ne=torch.empty(R, dtype=torch.int32, device=dev),
                     n_rows_ne=torch.zeros(1, dtype=torch.int64, device=dev),
-                    rest_counts=torch.zeros(R, dtype=torch.int32, device=dev))
+                    eval_total2=torch.zeros(1, dtype=torch.int64, device=dev))
 
     def _bind(self, m):
         for k, v in m.items():
@@ -485,8 +485,8 @@ class NGPTrainer:
                 vren._ok(L.ngp_ray_segments_capped(_p(m["rays_a"]), R, K, _p(m["act_start1"]), _p(m["eval_total1"]),
                                                    None, _p(m["eval_idx1"]), s), "segments_capped")
             elif K > 0 and self.row_forward:
-                vren._ok(L.ngp_rays_nonempty(_p(m["rays_a"]), R, _p(m["rows_ne"]), _p(m["n_rows_ne"]),
-                                             _p(m["rest_counts"]), s), "rays_nonempty")
+                vren._ok(L.ngp_rays_nonempty(_p(m["rays_a"]), R, _p(m["rows_ne"]), _p(m["n_rows_ne"]), None,
+                                             _p(m["eval_total2"]), s), "rays_nonempty")
             if side:
                 self._ev("march_side", 1, stream)
 
@@ -889,19 +889,19 @@ class NGPTrainer:
             fork()
         self._ev("field_fwd", 0)
         if self.chunk_first > 0 and self.row_forward:
-            # round 1: a wave per non-empty row (list and empty rows' zero counts from the march),
-            # its transmittance -> the round-2 counts; round 2: their plain scan + list, then the field
+            # round 1: a wave per non-empty row (the list built by the march), its transmittance
+            # deciding the row's round 2, whose samples it appends to the round-2 list itself (no
+            # list pass); round 2: the field over that list
             assert self.chunk_first == 64, "row forward: the first chunk is one wave (64 samples)"
             self._ev("hash_encode", 0)
             vren._ok(HGL.ngp_field_forward_first(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a),
                                                  _p(self.rows_ne), _p(self.n_rows_ne), R, self.cap, ctypes_float(1e-4),
                                                  HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
                                                  _p(self.params16), _p(self.enc), _p(self.sigmas), _p(self.rgbs),
-                                                 _p(self.rest_counts), _p(self.eval_stats), s), "field_forward_first")
+                                                 None, _p(self.eval_idx), _p(self.eval_total2), _p(self.eval_stats),
+                                                 s), "field_forward_first")
             self._ev("hash_encode", 1)
-            vren._ok(L.ngp_ray_segments(_p(self.rest_counts), _p(self.rays_a), R, 64, _p(self.act_start),
-                                        _p(self.eval_total), _p(self.eval_stats), _p(self.eval_idx), s), "segments")
-            self._field_indexed(s)
+            self._field_indexed(s, self.eval_idx, self.eval_total2)
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
             if self.eval1_K == K:  # built by this batch's march

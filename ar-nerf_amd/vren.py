@@ -78,7 +78,7 @@ def _declare(L):
         "ngp_chunk_counts": [vp, c_int64, c_int, vp, vp, c_float, vp, vp],
         "ngp_chunk_counts_range": [vp, c_int64, c_int, c_int, vp, vp, c_float, vp, vp],
         "ngp_ray_segments": [vp, vp, c_int64, c_int, vp, vp, vp, vp, vp],
-        "ngp_rays_nonempty": [vp, c_int64, vp, vp, vp, vp],
+        "ngp_rays_nonempty": [vp, c_int64, vp, vp, vp, vp, vp],
         "ngp_chunk_segments": [vp, vp, vp, c_int64, c_int, c_int, c_float, vp, vp, vp, vp, vp, vp, vp],
         "ngp_ray_segments_capped": [vp, c_int64, c_int, vp, vp, vp, vp, vp],
         "ngp_adam_step": [vp, vp, vp, vp, vp, c_int64, c_float, c_float, c_float, c_float, c_int64, c_float, c_int,

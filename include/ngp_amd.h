@@ -337,28 +337,35 @@ int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const 
                          const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs, void* h_f16, void* stream);
 /* The non-empty rows (N > 0) of rays_a, ascending, into rows[0..*n_rows);
  * rest (nullable): rest[r] = 0 for every empty row (ngp_field_forward_first
- * writes the others).  One launch (one workgroup; the list of a batch of
- * rays, built beside the previous step). */
+ * writes the others); zero (nullable): *zero = 0 (the round-2 list length
+ * ngp_field_forward_first appends to).  One launch (one workgroup; the list
+ * of a batch of rays, built beside the previous step). */
 int ngp_rays_nonempty(const int64_t* rays_a, int64_t n_rays, int32_t* rows, int64_t* n_rows, int32_t* rest,
-                      void* stream);
+                      int64_t* zero, void* stream);
 /* Round 1 of the chunked training forward with the round-2 counts: for the
  * rows rows[j], j < *n_rows_dev (rows NULL: rows 0..n_rows-1; n_rows_dev
  * NULL: n_rows) of rays_a (ray, start, N), the first min(N, 64) samples
  * encoded and run through the MLPs (enc_pm (plane stride n, nullable),
  * sigmas, rgbs: ngp_field_encode_mlp's values bit for bit), then the row's
- * transmittance over them (the compositing kernel's product scan) -> rest[r]
- * = N - 64 if it is still above T_threshold after them, else 0 -- the counts
- * ngp_chunk_counts_range(first = 64) gives, so ngp_ray_segments(rest, first =
- * 64) lists the round-2 samples.  *evaluated (nullable) += the samples
- * evaluated.  With ngp_rays_nonempty's list: one wave per non-empty row.
+ * transmittance over them (the compositing kernel's product scan) -> rc =
+ * N - 64 if it is still above T_threshold after them, else 0.  rest
+ * (nullable): rest[r] = rc -- the counts ngp_chunk_counts_range(first = 64)
+ * gives, so ngp_ray_segments(rest, first = 64) lists the round-2 samples.
+ * list2 (nullable; rest or list2 required): the round-2 samples themselves,
+ * start + 64 .. start + N of every row with rc > 0, appended at ranges
+ * reserved on *total2 (zero at the launch; its final value = the list's
+ * length): rows in no fixed order, each row's samples contiguous and
+ * ascending.  *evaluated (nullable) += the samples evaluated here plus, with
+ * list2, the listed ones.  With ngp_rays_nonempty's list: one wave per
+ * non-empty row.
  * Replaces, for the model(xyzs, dirs) call of __render_rays_train
  * (models/rendering.py:278), round 1's ngp_field_encode_mlp + the round-2
  * count / scan / list launch ngp_chunk_segments. */
 int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
                             const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
                             float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
-                            void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int64_t* evaluated,
-                            void* stream);
+                            void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int32_t* list2,
+                            int64_t* total2, int64_t* evaluated, void* stream);
 int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev,
                           const int32_t* sample_idx, const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16,
                           void* stream);

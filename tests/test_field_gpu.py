@@ -345,3 +345,81 @@ def test_hash_backward_levels_replicated(rep_levels, n_rep):
                                           vren._stream()) < 0
     assert L.ngp_hash_backward_levels_rep(p(x), n, p(n_dev), p(sidx), desc, p(denc), p(out), 0, 8, p(rep), 4, 0, 1,
                                           vren._stream()) < 0
+
+
+@pytest.mark.parametrize("scale", [0.5, 16.0])
+def test_forward_first_chunk_matches_encode_mlp_and_chunk_counts(scale):
+    """ngp_field_forward_first (the row forward's round 1: a wave per row, its
+    first min(N, 64) samples, the row's transmittance in the epilogue): the
+    evaluated samples' encoding / sigma / rgb bit-identical to
+    ngp_field_encode_mlp, no other sample touched; rest = the counts
+    ngp_chunk_counts_range(first 64) gives from the full forward's sigmas; and
+    with ngp_rays_nonempty's row list, the appended round-2 list holds exactly
+    ngp_ray_segments' samples (each row's run contiguous and ascending)."""
+    import ctypes
+    _, flat = _oracle_and_params(scale=scale)
+    x, d = _points(20000, scale)
+    n = x.shape[0]
+    grid = HG.HashGrid(scale)
+    p16 = flat.to(DEV).half()
+    x, d = x.to(DEV), d.to(DEV)
+    sig, rgb, enc, _ = HG.field_forward(x, d, grid, p16)
+    g = torch.Generator().manual_seed(5)
+    R = 400
+    N = torch.randint(1, 200, (R,), generator=g)
+    N[torch.rand(R, generator=g) < 0.5] = 0
+    N[3], N[4] = 64, 65  # chunk-boundary rows
+    while int(N.sum()) > n:
+        N = N // 2
+    start = torch.cumsum(N, 0) - N
+    rays_a = torch.stack([torch.arange(R), start, N], 1).to(DEV)
+    row = torch.repeat_interleave(torch.arange(R), N)
+    scale_row = torch.where(torch.rand(R, generator=g) < 0.5, 1.0, 1e-6)  # terminating vs transparent rows
+    deltas = torch.zeros(n)
+    deltas[:row.numel()] = (torch.rand(row.numel(), generator=g) + 0.5) * scale_row[row]
+    deltas = deltas.to(DEV)
+    L, Lv = HG._lib(), vren.lib()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    cnt_ref = torch.empty(R, dtype=torch.int32, device=DEV)
+    vren._ok(Lv.ngp_chunk_counts_range(vp(rays_a), R, 64, 0, vp(sig), vp(deltas), ctypes.c_float(1e-4), vp(cnt_ref),
+                                       vren._stream()), "counts")
+    first = torch.cat([torch.arange(int(s), int(s) + min(int(k), 64)) for s, k in zip(start, N)]).to(DEV)
+    # 1) every row (rows NULL), counts out
+    enc_pm = torch.full((8, n, 4), 7.0, dtype=torch.float16, device=DEV)
+    sig2, rgb2 = torch.full((n,), -1.0, device=DEV), torch.full((n, 3), -1.0, device=DEV)
+    rest = torch.full((R,), -9, dtype=torch.int32, device=DEV)
+    ev = torch.zeros(1, dtype=torch.int64, device=DEV)
+    vren._ok(L.ngp_field_forward_first(vp(x), vp(d), vp(deltas), vp(rays_a), None, None, R, n, ctypes.c_float(1e-4),
+                                       ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:]), vp(p16), vp(enc_pm), vp(sig2),
+                                       vp(rgb2), vp(rest), None, None, vp(ev), vren._stream()), "forward_first")
+    torch.cuda.synchronize()
+    rows_enc = enc_pm.permute(1, 0, 2).reshape(n, 32)
+    assert torch.equal(rows_enc[first].view(torch.int16), enc[first].view(torch.int16))
+    assert torch.equal(sig2[first], sig[first]) and torch.equal(rgb2[first], rgb[first])
+    untouched = torch.ones(n, dtype=torch.bool, device=DEV)
+    untouched[first] = False
+    assert bool((sig2[untouched] == -1.0).all()) and bool((rows_enc[untouched] == 7.0).all())
+    assert torch.equal(rest, cnt_ref) and int(ev) == first.numel()
+    assert 0 < int((cnt_ref > 0).sum()) < int((N > 64).sum())  # some long rows stop, some go on
+    # 2) the non-empty row list, round-2 list appended
+    rows = torch.empty(R, dtype=torch.int32, device=DEV)
+    n_ne, total2 = torch.zeros(1, dtype=torch.int64, device=DEV), torch.full((1,), 3, dtype=torch.int64, device=DEV)
+    vren._ok(Lv.ngp_rays_nonempty(vp(rays_a), R, vp(rows), vp(n_ne), None, vp(total2), vren._stream()), "nonempty")
+    list2 = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    ev.zero_()
+    vren._ok(L.ngp_field_forward_first(vp(x), vp(d), vp(deltas), vp(rays_a), vp(rows), vp(n_ne), R, n,
+                                       ctypes.c_float(1e-4), ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:]), vp(p16),
+                                       vp(enc_pm), vp(sig2), vp(rgb2), None, vp(list2), vp(total2), vp(ev),
+                                       vren._stream()), "forward_first_list")
+    st = torch.empty(R, dtype=torch.int64, device=DEV)
+    tot_ref, idx_ref = torch.zeros(1, dtype=torch.int64, device=DEV), torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    vren._ok(Lv.ngp_ray_segments(vp(cnt_ref), vp(rays_a), R, 64, vp(st), vp(tot_ref), None, vp(idx_ref),
+                                 vren._stream()), "segments")
+    torch.cuda.synchronize()
+    T = int(tot_ref)
+    assert int(total2) == T and int(ev) == first.numel() + T
+    got = list2[:T].long()
+    assert torch.equal(torch.sort(got)[0], torch.sort(idx_ref[:T].long())[0])
+    # runs of a row are contiguous and ascending: every step inside the list is +1 or a jump to another row's start
+    steps = got[1:] - got[:-1]
+    assert int((steps == 1).sum()) == T - int((cnt_ref > 0).sum())

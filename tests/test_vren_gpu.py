@@ -413,7 +413,7 @@ def test_chunk_segments_equals_counts_then_segments(n_rows, first, last):
 def test_rays_nonempty_lists_rows_and_zeroes_empty_counts(n_rows):
     """ngp_rays_nonempty: the rows with N > 0 in ascending order and their
     count; rest[r] = 0 for every empty row, the others untouched (the row
-    forward's round 1 writes them)."""
+    forward's round 1 writes them); the round-2 list length zeroed."""
     import ctypes
     L = vren.lib()
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
@@ -424,9 +424,10 @@ def test_rays_nonempty_lists_rows_and_zeroes_empty_counts(n_rows):
     rows = torch.full((n_rows,), -1, dtype=torch.int32, device=DEV)
     n_ne = torch.full((1,), -3, dtype=torch.int64, device=DEV)
     rest = torch.full((n_rows,), 7, dtype=torch.int32, device=DEV)
-    vren._ok(L.ngp_rays_nonempty(p(rays_a), n_rows, p(rows), p(n_ne), p(rest), vren._stream()), "rays_nonempty")
+    z = torch.full((1,), 5, dtype=torch.int64, device=DEV)
+    vren._ok(L.ngp_rays_nonempty(p(rays_a), n_rows, p(rows), p(n_ne), p(rest), p(z), vren._stream()), "rays_nonempty")
     torch.cuda.synchronize()
     ref = torch.nonzero(N > 0).flatten()
     assert int(n_ne) == ref.numel()
     assert torch.equal(rows[:ref.numel()].cpu().long(), ref)
-    assert torch.equal(rest.cpu(), torch.where(N > 0, 7, 0).int())
+    assert torch.equal(rest.cpu(), torch.where(N > 0, 7, 0).int()) and int(z) == 0
