@@ -20,6 +20,7 @@
 #pragma clang fp contract(off)
 
 #include <algorithm>
+#include <cstddef>
 
 #include "common.h"
 #include "grid.h"
@@ -937,6 +938,134 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
     if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
 }
 
+// Both chunked rounds in ONE launch through a device work queue.  A wave
+// claims a non-empty row (row ticket), evaluates its first chunk and the
+// row's transmittance over it (as field_first_chunk_kernel), and if the row is
+// still transparent reserves ceil((N - 64) / 64) queue items -- the row's
+// remaining samples in 64-sample chunks -- with the same 64-bit atomic that
+// counts the row as done: state = rows_done << 32 | items reserved, so a
+// consumer that sees every row done also sees the final item count (no fence:
+// one word).  Items are stored after the reservation as 8-byte agent-scope
+// words {first sample << 7 | count}.  A wave without rows left claims item
+// indices in order and polls its item's word (s_sleep between polls) until
+// it appears, or until every row is done and the index lies beyond the final
+// count -- then it exits.  So round 2 starts while round 1 is still running
+// (no list pass, no second launch, no tail between the rounds), and a row
+// past its first chunk is spread over many waves (no serial chunk chain).
+// Every consumer clears the item it took; the last wave out resets the
+// counters, so the workspace is zero for the next launch.  Polls are bounded
+// (a corrupted workspace cannot hang the GPU: counted in `guard`).
+struct RowQueueWs {
+    uint32_t row_ticket, pad0[31];
+    uint32_t item_ticket, pad1[31];
+    unsigned long long state, pad2[15];  // rows done << 32 | items reserved
+    uint32_t exits, pad3[31];
+    uint32_t guard, pad4[31];
+    unsigned long long items[1];  // [capacity]
+};
+template <bool COLOR>
+__global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_queue_kernel(
+    const float* __restrict__ xyzs, const float* __restrict__ dirs, const float* __restrict__ deltas,
+    const int64_t* __restrict__ rays_a, const int32_t* __restrict__ rows, const int64_t* __restrict__ n_rows_dev,
+    int64_t n_rows, int64_t n, float T_thr, GridArgs ga, const uint32_t* __restrict__ table,
+    const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm, float* __restrict__ sigmas,
+    float* __restrict__ rgbs, RowQueueWs* __restrict__ q, uint32_t capacity, int64_t* __restrict__ evaluated) {
+    __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
+    __shared__ LevelLds lv;
+    __shared__ unsigned long long blk_eval;
+    const int lane = threadIdx.x & 63;
+    const uint32_t NR = (uint32_t)(n_rows_dev ? *n_rows_dev : n_rows);
+    auto claim = [&](uint32_t* c) {
+        uint32_t v = 0;
+        if (lane == 0) v = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return rfl(__shfl(v, 0, 64));
+    };
+    auto load_row = [&](uint32_t j, int64_t& start, int64_t& N) {
+        const int64_t r = rows ? (int64_t)rows[j] : (int64_t)j;
+        start = rays_a[3 * r + 1];
+        N = rays_a[3 * r + 2];
+    };
+    // the first row (ticket -> list -> rays_a) requested before the weight image is built
+    uint32_t j = claim(&q->row_ticket);
+    int64_t start = 0, N = 0;
+    if (j < NR) load_row(j, start, N);
+    if (threadIdx.x == 0) blk_eval = 0ull;
+    load_fwd_weights_direct(mlp, sw, COLOR);
+    load_levels(ga, lv);
+    __syncthreads();
+    int64_t ev = 0;
+    // ---- round 1: rows
+    while (j < NR) {
+        const uint32_t jn = claim(&q->row_ticket);  // (returns while this row is evaluated)
+        const int cnt = (int)(N < 64 ? N : 64);
+        uint32_t k = 0;
+        if (cnt > 0) {
+            const float dl = lane < cnt ? deltas[start + lane] : 0.f;
+            const float sg = encode_mlp_chunk<COLOR>(xyzs, dirs, start, cnt, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
+            const float om = 1.0f - (1.0f - __expf(-sg * dl));  // chunk_segments_kernel's expression
+            const ChunkT ct = chunk_transmittance(om, cnt, 1.0f, T_thr, lane);
+            if (!ct.hit && N > 64) k = (uint32_t)((N - 64 + 63) / 64);
+            ev += cnt;
+        }
+        unsigned long long st = 0;
+        if (lane == 0)
+            st = __hip_atomic_fetch_add(&q->state, (1ull << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k) {
+            const uint32_t base = (uint32_t)__shfl((unsigned long long)(st & 0xffffffffull), 0, 64);
+            for (uint32_t t = lane; t < k; t += 64) {
+                const int64_t i0 = start + 64 + 64 * (int64_t)t;
+                const int64_t c = min((int64_t)64, start + N - i0);
+                if (base + t < capacity)
+                    __hip_atomic_store(&q->items[base + t], ((unsigned long long)i0 << 7) | (unsigned long long)c,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        j = jn;
+        if (j < NR) load_row(j, start, N);
+    }
+    // ---- round 2: items, in claim order
+    for (;;) {
+        const uint32_t b = claim(&q->item_ticket);
+        unsigned long long it = 0;
+        for (uint32_t spin = 0;; ++spin) {
+            bool stop = false;
+            if (lane == 0) {
+                if (b < capacity) it = __hip_atomic_load(&q->items[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!it) {
+                    const unsigned long long s2 = __hip_atomic_load(&q->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = (uint32_t)(s2 >> 32) >= NR && (uint32_t)s2 <= b;
+                    if (!stop && spin == (1u << 22)) {
+                        atomicAdd(&q->guard, 1u);
+                        stop = true;
+                    }
+                }
+            }
+            it = __shfl(it, 0, 64);
+            if (it || __shfl((int)stop, 0, 64)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!it) break;
+        if (lane == 0) __hip_atomic_store(&q->items[b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t i0 = (int64_t)(it >> 7);
+        const int c = (int)(it & 127ull);
+        encode_mlp_chunk<COLOR>(xyzs, dirs, i0, c, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
+        ev += c;
+    }
+    // ---- the last wave out resets the counters for the next launch
+    if (lane == 0) {
+        const uint32_t waves = gridDim.x * FEM2_WAVES;
+        if (__hip_atomic_fetch_add(&q->exits, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == waves - 1) {
+            __hip_atomic_store(&q->row_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q->item_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q->state, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&q->exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (ev) atomicAdd(&blk_eval, (unsigned long long)ev);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
+}
+
 // One level of the coarse (atomic) hash backward for the wave's 16 consecutive
 // samples, lane = 4 s + 2 cx + f: corner c = cx | cy << 1 | cz << 2 of sample s
 // receives w_c * gd (gd = dL/denc[s][2 l + f]); runs of equal corners along the
@@ -1837,6 +1966,42 @@ int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* d
     NGP_TIMED(NGP_K_HASH_ENCODE, s, field_first_chunk_kernel<true><<<blocks, 64 * FEM2_WAVES, 0, s>>>(
         xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
         (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, list2, total2, evaluated));
+    return ngp_launch_status();
+}
+
+size_t ngp_field_forward_rows_workspace(int64_t n_rows, int64_t n) {
+    return offsetof(RowQueueWs, items) + 8 * (size_t)(n_rows + n / 64 + 64);
+}
+
+unsigned ngp_field_forward_rows_guard(const void* ws) {
+    uint32_t g = 0;
+    if (!ws || hipMemcpy(&g, (const char*)ws + offsetof(RowQueueWs, guard), 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return ~0u;
+    return g;
+}
+
+int ngp_field_forward_rows(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
+                           const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
+                           float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
+                           void* enc_pm, float* sigmas, float* rgbs, void* queue_ws, int64_t* evaluated,
+                           void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n_rows >= 0 && n_rows < (1ll << 31) && n >= 0 && n < (1ll << 40));
+    if (n_rows == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && dirs && deltas && rays_a && table_f16 && mlp_f16 && sigmas && rgbs && queue_ws);
+    NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0 &&
+                  ((uintptr_t)queue_ws & 127) == 0 && ((uintptr_t)evaluated & 7) == 0);
+    const int64_t capacity = n_rows + n / 64 + 64;  // >= every row's ceil(rest / 64)
+    NGP_CHECK_ARG(capacity < (1ll << 32));
+    hipStream_t s = as_stream(stream);
+    // grid = every resident block (waves without rows take the queue's items)
+    static const unsigned cap = resident_blocks(field_rows_queue_kernel<true>, 64 * FEM2_WAVES, 0);
+    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_rows_queue_kernel<true><<<cap, 64 * FEM2_WAVES, 0, s>>>(
+        xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
+        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, (RowQueueWs*)queue_ws, (uint32_t)capacity,
+        evaluated));
     return ngp_launch_status();
 }
 

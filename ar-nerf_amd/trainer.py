@@ -211,8 +211,11 @@ class NGPTrainer:
                                   device=dev)
         # (NGP_ROW_FWD=1: round 1 one wave per non-empty row with the row's transmittance in its
         # epilogue, which appends the row's round-2 samples to the round-2 list itself --
-        # ngp_field_forward_first: no list launch; chunk_first must then be 64, the wave width)
-        self.row_forward = os.environ.get("NGP_ROW_FWD", "0") == "1"
+        # ngp_field_forward_first: no list launch; NGP_ROW_FWD=2: both rounds in one launch
+        # through a device work queue -- ngp_field_forward_rows; chunk_first must then be 64)
+        self.row_forward = int(os.environ.get("NGP_ROW_FWD", "0"))
+        self._rq_ws = torch.zeros((HG._lib().ngp_field_forward_rows_workspace(R, cap) + 7) // 8, dtype=torch.int64,
+                                  device=dev)
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
@@ -894,14 +897,22 @@ class NGPTrainer:
             # list pass); round 2: the field over that list
             assert self.chunk_first == 64, "row forward: the first chunk is one wave (64 samples)"
             self._ev("hash_encode", 0)
-            vren._ok(HGL.ngp_field_forward_first(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a),
-                                                 _p(self.rows_ne), _p(self.n_rows_ne), R, self.cap, ctypes_float(1e-4),
-                                                 HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
-                                                 _p(self.params16), _p(self.enc), _p(self.sigmas), _p(self.rgbs),
-                                                 None, _p(self.eval_idx), _p(self.eval_total2), _p(self.eval_stats),
-                                                 s), "field_forward_first")
-            self._ev("hash_encode", 1)
-            self._field_indexed(s, self.eval_idx, self.eval_total2)
+            if self.row_forward == 2:  # both rounds, one launch (device work queue)
+                vren._ok(HGL.ngp_field_forward_rows(
+                    _p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a), _p(self.rows_ne),
+                    _p(self.n_rows_ne), R, self.cap, ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
+                    _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc), _p(self.sigmas),
+                    _p(self.rgbs), _p(self._rq_ws), _p(self.eval_stats), s), "field_forward_rows")
+                self._ev("hash_encode", 1)
+            else:
+                vren._ok(HGL.ngp_field_forward_first(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a),
+                                                     _p(self.rows_ne), _p(self.n_rows_ne), R, self.cap,
+                                                     ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
+                                                     _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc),
+                                                     _p(self.sigmas), _p(self.rgbs), None, _p(self.eval_idx),
+                                                     _p(self.eval_total2), _p(self.eval_stats), s), "field_forward_first")
+                self._ev("hash_encode", 1)
+                self._field_indexed(s, self.eval_idx, self.eval_total2)
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
             if self.eval1_K == K:  # built by this batch's march

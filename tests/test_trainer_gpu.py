@@ -8,6 +8,8 @@ Tolerances: loss within 2e-3 relative (fp16 MLP storage points); per-ray
 rgb/opacity within 1e-3; gradients relative L2 <= 2e-2 (fp16 MFMA backward);
 Adam-updated params within 1e-5 absolute (|update| <= lr = 1e-2 per step,
 dominated by sign(g) for fresh moments)."""
+import ctypes
+
 import pytest
 import torch
 
@@ -176,16 +178,18 @@ def test_chunked_forward_matches_full(first, table_init):
         assert ev1 < n1
 
 
-@pytest.mark.parametrize("table_init", [0.2, 2.0])
-def test_row_forward_matches_two_rounds_and_full(table_init):
-    """The row forward's round 1 (ngp_field_forward_first: a wave per
-    non-empty row from ngp_rays_nonempty, the row's transmittance in its
-    epilogue -> the round-2 counts, then ngp_ray_segments) gives the full
-    forward's step exactly as the two chunked rounds do: loss and per-ray
-    outputs bit-identical, gradients equal up to atomic summation order, the
-    same samples evaluated; and a second step repeats it bit for bit."""
+@pytest.mark.parametrize("table_init,mode", [(0.2, 1), (2.0, 1), (0.2, 2), (2.0, 2)])
+def test_row_forward_matches_two_rounds_and_full(table_init, mode):
+    """The row forward -- mode 1: round 1 a wave per non-empty row from
+    ngp_rays_nonempty with the row's transmittance in its epilogue, which
+    appends the round-2 list (ngp_field_forward_first), then the field over
+    that list; mode 2: both rounds in one launch through a device work queue
+    (ngp_field_forward_rows) -- gives the full forward's step exactly as the
+    two chunked rounds do: loss and per-ray outputs bit-identical, gradients
+    equal up to atomic summation order, the same samples evaluated; and a
+    second step repeats it bit for bit (the queue workspace reset)."""
     runs = []
-    for chunk, rows in ((0, False), (64, False), (64, True)):
+    for chunk, rows in ((0, 0), (64, 0), (64, mode)):
         sc, tr, img, pix, noise = _setup(table_init=table_init)
         tr.chunk_first, tr.row_forward = chunk, rows
         dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
@@ -202,6 +206,10 @@ def test_row_forward_matches_two_rounds_and_full(table_init):
             torch.cuda.synchronize()
             assert torch.equal(loss2, out[0]) and torch.equal(tr.out_rgb, out[1])
             assert tr.stat_totals()[3] == 2 * ev
+            if rows == 2:
+                import hashgrid as HG
+                assert HG._lib().ngp_field_forward_rows_guard(ctypes.c_void_p(tr._rq_ws.data_ptr())) == 0
+                assert int(tr._rq_ws.abs().sum()) == 0  # (every counter and item cleared for the next launch)
         runs.append(out)
     (l0, r0, o0, g0, _), (l1, r1, o1, g1, ev1), (l2, r2, o2, g2, ev2) = runs
     assert torch.equal(l0, l2) and torch.equal(r0, r2) and torch.equal(o0, o2)
