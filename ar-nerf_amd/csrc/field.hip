@@ -942,23 +942,18 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
 // claims a non-empty row (row ticket), evaluates its first chunk and the
 // row's transmittance over it (as field_first_chunk_kernel), and if the row is
 // still transparent reserves ceil((N - 64) / 64) queue items -- the row's
-// remaining samples in 64-sample chunks -- with the same 64-bit atomic that
-// counts the row as done: state = rows_done << 32 | items reserved, so a
-// consumer that sees every row done also sees the final item count (no fence:
-// one word).  Items are stored after the reservation as 8-byte agent-scope
-// words {first sample << 7 | count}.  A wave without rows left claims item
-// indices in order and polls its item's word (s_sleep between polls) until
-// it appears, or until every row is done and the index lies beyond the final
-// count -- then it exits.  So round 2 starts while round 1 is still running
-// (no list pass, no second launch, no tail between the rounds), and a row
-// past its first chunk is spread over many waves (no serial chunk chain).
-// Every consumer clears the item it took; the last wave out resets the
-// counters, so the workspace is zero for the next launch.  Polls are bounded
-// (a corrupted workspace cannot hang the GPU: counted in `guard`).
+// remaining samples in 64-sample chunks -- and stores them as 8-byte
+// agent-scope words {first sample << 7 | count}.  Once out of rows a wave
+// takes stored items in index order and leaves at the first index not yet
+// stored (no waiting: see the loop), so round 2 starts while round 1 is still
+// running (no list pass, no second launch, no tail between the rounds) and a
+// row past its first chunk is spread over many waves (no serial chunk chain).
+// Every taker clears its item; the last wave out resets the counters, so the
+// workspace is zero for the next launch.
 struct RowQueueWs {
     uint32_t row_ticket, pad0[31];
     uint32_t item_ticket, pad1[31];
-    unsigned long long state, pad2[15];  // rows done << 32 | items reserved
+    unsigned long long state, pad2[15];  // items reserved
     uint32_t exits, pad3[31];
     uint32_t guard, pad4[31];
     unsigned long long items[1];  // [capacity]
@@ -1007,11 +1002,10 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_qu
             if (!ct.hit && N > 64) k = (uint32_t)((N - 64 + 63) / 64);
             ev += cnt;
         }
-        unsigned long long st = 0;
-        if (lane == 0)
-            st = __hip_atomic_fetch_add(&q->state, (1ull << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k) {
-            const uint32_t base = (uint32_t)__shfl((unsigned long long)(st & 0xffffffffull), 0, 64);
+            unsigned long long st = 0;
+            if (lane == 0) st = __hip_atomic_fetch_add(&q->state, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t base = (uint32_t)__shfl(st, 0, 64);
             for (uint32_t t = lane; t < k; t += 64) {
                 const int64_t i0 = start + 64 + 64 * (int64_t)t;
                 const int64_t c = min((int64_t)64, start + N - i0);
@@ -1023,29 +1017,33 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_qu
         j = jn;
         if (j < NR) load_row(j, start, N);
     }
-    // ---- round 2: items, in claim order
+    // ---- round 2: take stored items in index order, never waiting: an item is taken only once it is
+    // stored (CAS of the item ticket from t while items[t] != 0); a wave leaves at the first
+    // index not stored yet.  Every producer enters this loop after storing its items, so the last
+    // one to store finds every remaining item stored: each item is evaluated exactly once, and no
+    // wave holds a CU slot waiting (the march beside this launch needs those slots)
     for (;;) {
-        const uint32_t b = claim(&q->item_ticket);
         unsigned long long it = 0;
-        for (uint32_t spin = 0;; ++spin) {
-            bool stop = false;
-            if (lane == 0) {
-                if (b < capacity) it = __hip_atomic_load(&q->items[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (!it) {
-                    const unsigned long long s2 = __hip_atomic_load(&q->state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    stop = (uint32_t)(s2 >> 32) >= NR && (uint32_t)s2 <= b;
-                    if (!stop && spin == (1u << 22)) {
-                        atomicAdd(&q->guard, 1u);
-                        stop = true;
-                    }
+        uint32_t t = 0;
+        if (lane == 0) {
+            for (uint32_t fails = 0;; ++fails) {
+                t = __hip_atomic_load(&q->item_ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                it = t < capacity ? __hip_atomic_load(&q->items[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+                if (!it) break;
+                uint32_t expect = t;
+                if (__hip_atomic_compare_exchange_strong(&q->item_ticket, &expect, t + 1, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    break;
+                if (fails == (1u << 24)) {  // (each failure is another wave's success: bounded anyway)
+                    atomicAdd(&q->guard, 1u);
+                    it = 0;
+                    break;
                 }
             }
-            it = __shfl(it, 0, 64);
-            if (it || __shfl((int)stop, 0, 64)) break;
-            __builtin_amdgcn_s_sleep(2);
+            if (it) __hip_atomic_store(&q->items[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        it = __shfl(it, 0, 64);
         if (!it) break;
-        if (lane == 0) __hip_atomic_store(&q->items[b], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int64_t i0 = (int64_t)(it >> 7);
         const int c = (int)(it & 127ull);
         encode_mlp_chunk<COLOR>(xyzs, dirs, i0, c, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
