@@ -20,7 +20,6 @@
 #pragma clang fp contract(off)
 
 #include <algorithm>
-#include <cstddef>
 
 #include "common.h"
 #include "grid.h"
@@ -938,60 +937,55 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
     if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
 }
 
-// Both chunked rounds in ONE launch through a device work queue.  A wave
-// claims a non-empty row (row ticket), evaluates its first chunk and the
-// row's transmittance over it (as field_first_chunk_kernel), and if the row is
-// still transparent reserves ceil((N - 64) / 64) queue items -- the row's
-// remaining samples in 64-sample chunks -- and stores them as 8-byte
-// agent-scope words {first sample << 7 | count}.  Once out of rows a wave
-// takes stored items in index order and leaves at the first index not yet
-// stored (no waiting: see the loop), so round 2 starts while round 1 is still
-// running (no list pass, no second launch, no tail between the rounds) and a
-// row past its first chunk is spread over many waves (no serial chunk chain).
-// Every taker clears its item; the last wave out resets the counters, so the
-// workspace is zero for the next launch.
-struct RowQueueWs {
-    uint32_t row_ticket, pad0[31];
-    uint32_t item_ticket, pad1[31];
-    unsigned long long state, pad2[15];  // items reserved
-    uint32_t exits, pad3[31];
-    uint32_t guard, pad4[31];
-    unsigned long long items[1];  // [capacity]
-};
+// Both chunked rounds in ONE launch, each block its own work queue in LDS.
+// The non-empty rows are dealt over every wave of the grid as in
+// field_first_chunk_kernel (a wave's first row, then every G x waves-th):
+// the wave evaluates the row's first chunk and the row's transmittance over
+// it, and if the row is still transparent pushes the row's remaining samples
+// as 64-sample items {first sample << 7 | count} onto its block's queue (LDS
+// atomic; past RQ_CAP items the wave evaluates the overflow itself).  After
+// one barrier the block's waves take the items (LDS ticket) until none is
+// left.  So a row past its first chunk is spread over the 8 waves of its
+// block (no serial chunk chain), round 2 starts per block as soon as that
+// block's round 1 is done (no list pass, no second launch, no grid-wide
+// tail between the rounds), and nothing waits on another block: no global
+// atomics, no polling (a device-wide queue, polled or CAS-claimed by
+// thousands of waves, saturated the memory channel holding its counters:
+// 0.43 ms / 6.3 ms per launch).
+constexpr int RQ_CAP = 1024;
 template <bool COLOR>
-__global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_queue_kernel(
+__global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_block_kernel(
     const float* __restrict__ xyzs, const float* __restrict__ dirs, const float* __restrict__ deltas,
     const int64_t* __restrict__ rays_a, const int32_t* __restrict__ rows, const int64_t* __restrict__ n_rows_dev,
     int64_t n_rows, int64_t n, float T_thr, GridArgs ga, const uint32_t* __restrict__ table,
     const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm, float* __restrict__ sigmas,
-    float* __restrict__ rgbs, RowQueueWs* __restrict__ q, uint32_t capacity, int64_t* __restrict__ evaluated) {
+    float* __restrict__ rgbs, int64_t* __restrict__ evaluated) {
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ LevelLds lv;
     __shared__ unsigned long long blk_eval;
-    const int lane = threadIdx.x & 63;
-    const uint32_t NR = (uint32_t)(n_rows_dev ? *n_rows_dev : n_rows);
-    auto claim = [&](uint32_t* c) {
-        uint32_t v = 0;
-        if (lane == 0) v = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return rfl(__shfl(v, 0, 64));
-    };
-    auto load_row = [&](uint32_t j, int64_t& start, int64_t& N) {
-        const int64_t r = rows ? (int64_t)rows[j] : (int64_t)j;
+    __shared__ unsigned long long qi[RQ_CAP];
+    __shared__ uint32_t q_tail, q_head;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t NR = n_rows_dev ? *n_rows_dev : n_rows;
+    const int64_t G = gridDim.x, stride = (int64_t)FEM2_WAVES * G;
+    auto load_row = [&](int64_t j, int64_t& start, int64_t& N) {
+        const int64_t r = rows ? (int64_t)rows[j] : j;
         start = rays_a[3 * r + 1];
         N = rays_a[3 * r + 2];
     };
-    // the first row (ticket -> list -> rays_a) requested before the weight image is built
-    uint32_t j = claim(&q->row_ticket);
+    int64_t j = (int64_t)wv * G + blockIdx.x;  // the wave's first row (wave-uniform)
     int64_t start = 0, N = 0;
-    if (j < NR) load_row(j, start, N);
-    if (threadIdx.x == 0) blk_eval = 0ull;
+    if (j < NR) load_row(j, start, N);  // (requested before the weight image is built)
+    if (threadIdx.x == 0) {
+        blk_eval = 0ull;
+        q_tail = q_head = 0u;
+    }
     load_fwd_weights_direct(mlp, sw, COLOR);
     load_levels(ga, lv);
     __syncthreads();
     int64_t ev = 0;
-    // ---- round 1: rows
-    while (j < NR) {
-        const uint32_t jn = claim(&q->row_ticket);  // (returns while this row is evaluated)
+    // ---- round 1: the wave's rows
+    for (; j < NR; j += stride) {
         const int cnt = (int)(N < 64 ? N : 64);
         uint32_t k = 0;
         if (cnt > 0) {
@@ -1003,63 +997,38 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_qu
             ev += cnt;
         }
         if (k) {
-            unsigned long long st = 0;
-            if (lane == 0) st = __hip_atomic_fetch_add(&q->state, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t base = (uint32_t)__shfl(st, 0, 64);
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&q_tail, k);
+            base = rfl(__shfl(base, 0, 64));
             for (uint32_t t = lane; t < k; t += 64) {
                 const int64_t i0 = start + 64 + 64 * (int64_t)t;
-                const int64_t c = min((int64_t)64, start + N - i0);
-                if (base + t < capacity)
-                    __hip_atomic_store(&q->items[base + t], ((unsigned long long)i0 << 7) | (unsigned long long)c,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (base + t < RQ_CAP) qi[base + t] = ((unsigned long long)i0 << 7) | (unsigned long long)min((int64_t)64, start + N - i0);
+            }
+            // (queue full: this wave evaluates the rest of its row itself)
+            for (uint32_t t = base < RQ_CAP ? RQ_CAP - base : 0u; t < k; ++t) {
+                const int64_t i0 = start + 64 + 64 * (int64_t)t;
+                const int c = (int)min((int64_t)64, start + N - i0);
+                encode_mlp_chunk<COLOR>(xyzs, dirs, i0, c, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
+                ev += c;
             }
         }
-        j = jn;
-        if (j < NR) load_row(j, start, N);
+        const int64_t jn = j + stride;
+        if (jn < NR) load_row(jn, start, N);
     }
-    // ---- round 2: take stored items in index order, never waiting: an item is taken only once it is
-    // stored (CAS of the item ticket from t while items[t] != 0); a wave leaves at the first
-    // index not stored yet.  Every producer enters this loop after storing its items, so the last
-    // one to store finds every remaining item stored: each item is evaluated exactly once, and no
-    // wave holds a CU slot waiting (the march beside this launch needs those slots)
+    __syncthreads();  // every row of the block has pushed its items
+    // ---- round 2: the block's items
+    const uint32_t nq = min(q_tail, (uint32_t)RQ_CAP);
     for (;;) {
-        unsigned long long it = 0;
-        uint32_t t = 0;
-        if (lane == 0) {
-            for (uint32_t fails = 0;; ++fails) {
-                t = __hip_atomic_load(&q->item_ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                it = t < capacity ? __hip_atomic_load(&q->items[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-                if (!it) break;
-                uint32_t expect = t;
-                if (__hip_atomic_compare_exchange_strong(&q->item_ticket, &expect, t + 1, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    break;
-                if (fails == (1u << 24)) {  // (each failure is another wave's success: bounded anyway)
-                    atomicAdd(&q->guard, 1u);
-                    it = 0;
-                    break;
-                }
-            }
-            if (it) __hip_atomic_store(&q->items[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        it = __shfl(it, 0, 64);
-        if (!it) break;
-        const int64_t i0 = (int64_t)(it >> 7);
+        uint32_t h = 0;
+        if (lane == 0) h = atomicAdd(&q_head, 1u);
+        h = rfl(__shfl(h, 0, 64));
+        if (h >= nq) break;
+        const unsigned long long it = qi[h];
         const int c = (int)(it & 127ull);
-        encode_mlp_chunk<COLOR>(xyzs, dirs, i0, c, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
+        encode_mlp_chunk<COLOR>(xyzs, dirs, (int64_t)(it >> 7), c, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
         ev += c;
     }
-    // ---- the last wave out resets the counters for the next launch
-    if (lane == 0) {
-        const uint32_t waves = gridDim.x * FEM2_WAVES;
-        if (__hip_atomic_fetch_add(&q->exits, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == waves - 1) {
-            __hip_atomic_store(&q->row_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&q->item_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&q->state, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&q->exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (ev) atomicAdd(&blk_eval, (unsigned long long)ev);
-    }
+    if (lane == 0 && ev) atomicAdd(&blk_eval, (unsigned long long)ev);
     __syncthreads();
     if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
 }
@@ -1967,39 +1936,25 @@ int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* d
     return ngp_launch_status();
 }
 
-size_t ngp_field_forward_rows_workspace(int64_t n_rows, int64_t n) {
-    return offsetof(RowQueueWs, items) + 8 * (size_t)(n_rows + n / 64 + 64);
-}
-
-unsigned ngp_field_forward_rows_guard(const void* ws) {
-    uint32_t g = 0;
-    if (!ws || hipMemcpy(&g, (const char*)ws + offsetof(RowQueueWs, guard), 4, hipMemcpyDeviceToHost) != hipSuccess)
-        return ~0u;
-    return g;
-}
-
 int ngp_field_forward_rows(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
                            const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
                            float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
-                           void* enc_pm, float* sigmas, float* rgbs, void* queue_ws, int64_t* evaluated,
-                           void* stream) {
+                           void* enc_pm, float* sigmas, float* rgbs, int64_t* evaluated, void* stream) {
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
-    NGP_CHECK_ARG(n_rows >= 0 && n_rows < (1ll << 31) && n >= 0 && n < (1ll << 40));
+    NGP_CHECK_ARG(n_rows >= 0 && n >= 0 && n < (1ll << 50));
     if (n_rows == 0) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && dirs && deltas && rays_a && table_f16 && mlp_f16 && sigmas && rgbs && queue_ws);
+    NGP_CHECK_ARG(xyzs && dirs && deltas && rays_a && table_f16 && mlp_f16 && sigmas && rgbs);
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0 &&
-                  ((uintptr_t)queue_ws & 127) == 0 && ((uintptr_t)evaluated & 7) == 0);
-    const int64_t capacity = n_rows + n / 64 + 64;  // >= every row's ceil(rest / 64)
-    NGP_CHECK_ARG(capacity < (1ll << 32));
+                  ((uintptr_t)evaluated & 7) == 0);
     hipStream_t s = as_stream(stream);
-    // grid = every resident block (waves without rows take the queue's items)
-    static const unsigned cap = resident_blocks(field_rows_queue_kernel<true>, 64 * FEM2_WAVES, 0);
-    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_rows_queue_kernel<true><<<cap, 64 * FEM2_WAVES, 0, s>>>(
+    // grid = every resident block: the rows are dealt over all resident waves
+    static const unsigned cap = resident_blocks(field_rows_block_kernel<true>, 64 * FEM2_WAVES, 0);
+    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + FEM2_WAVES - 1) / FEM2_WAVES)));
+    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_rows_block_kernel<true><<<blocks, 64 * FEM2_WAVES, 0, s>>>(
         xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
-        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, (RowQueueWs*)queue_ws, (uint32_t)capacity,
-        evaluated));
+        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, evaluated));
     return ngp_launch_status();
 }
 

@@ -52,11 +52,7 @@ def _lib():
         L.ngp_field_mlp_forward.argtypes = [vp, vp, c_int64, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_encode_mlp.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_forward_rows.argtypes = [vp, vp, vp, vp, vp, vp, c_int64, c_int64, c_float, P, vp, vp, vp, vp, vp, vp,
-                                             vp, vp]
-        L.ngp_field_forward_rows_workspace.argtypes = [c_int64, c_int64]
-        L.ngp_field_forward_rows_workspace.restype = ctypes.c_size_t
-        L.ngp_field_forward_rows_guard.argtypes = [vp]
-        L.ngp_field_forward_rows_guard.restype = ctypes.c_uint
+                                             vp]
         L.ngp_field_forward_first.argtypes = [vp, vp, vp, vp, vp, vp, c_int64, c_int64, c_float, P, vp, vp, vp, vp, vp,
                                               vp, vp, vp, vp, vp]
         L.ngp_hash_backward.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]

@@ -211,11 +211,10 @@ class NGPTrainer:
                                   device=dev)
         # (NGP_ROW_FWD=1: round 1 one wave per non-empty row with the row's transmittance in its
         # epilogue, which appends the row's round-2 samples to the round-2 list itself --
-        # ngp_field_forward_first: no list launch; NGP_ROW_FWD=2: both rounds in one launch
-        # through a device work queue -- ngp_field_forward_rows; chunk_first must then be 64)
+        # ngp_field_forward_first: no list launch; NGP_ROW_FWD=2: both rounds in one launch,
+        # each workgroup queueing its rows' round-2 chunks in LDS for its own waves --
+        # ngp_field_forward_rows; chunk_first must then be 64)
         self.row_forward = int(os.environ.get("NGP_ROW_FWD", "0"))
-        self._rq_ws = torch.zeros((HG._lib().ngp_field_forward_rows_workspace(R, cap) + 7) // 8, dtype=torch.int64,
-                                  device=dev)
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
@@ -897,12 +896,12 @@ class NGPTrainer:
             # list pass); round 2: the field over that list
             assert self.chunk_first == 64, "row forward: the first chunk is one wave (64 samples)"
             self._ev("hash_encode", 0)
-            if self.row_forward == 2:  # both rounds, one launch (device work queue)
+            if self.row_forward == 2:  # both rounds, one launch (per-workgroup LDS queues)
                 vren._ok(HGL.ngp_field_forward_rows(
                     _p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a), _p(self.rows_ne),
                     _p(self.n_rows_ne), R, self.cap, ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
                     _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc), _p(self.sigmas),
-                    _p(self.rgbs), _p(self._rq_ws), _p(self.eval_stats), s), "field_forward_rows")
+                    _p(self.rgbs), _p(self.eval_stats), s), "field_forward_rows")
                 self._ev("hash_encode", 1)
             else:
                 vren._ok(HGL.ngp_field_forward_first(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a),

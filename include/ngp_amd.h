@@ -346,23 +346,16 @@ int ngp_rays_nonempty(const int64_t* rays_a, int64_t n_rays, int32_t* rows, int6
  * rows[j], j < *n_rows_dev (rows NULL: 0..n_rows-1; n_rows_dev NULL: n_rows)
  * of rays_a, the first min(N, 64) samples, then -- for the rows whose
  * transmittance is still above T_threshold after them -- every later
- * sample, in 64-sample work items taken from a device queue while round 1 is
- * still running.  Evaluates exactly ngp_field_forward_first + the round-2
- * list's samples (ngp_field_encode_mlp's values bit for bit; no other sample
- * touched).  queue_ws: ngp_field_forward_rows_workspace(n_rows, n) bytes,
- * 128-byte aligned, zeroed once before the first launch (every launch leaves
- * it zeroed); ngp_field_forward_rows_guard(queue_ws) = bounded polls that
- * gave up (0 unless the workspace was corrupted).  *evaluated (nullable) +=
- * the evaluated samples.  Replaces, for the model(xyzs, dirs) call of
- * __render_rays_train (models/rendering.py:278), both rounds' field launches
- * and the round-2 list launch. */
-size_t ngp_field_forward_rows_workspace(int64_t n_rows, int64_t n);
-unsigned ngp_field_forward_rows_guard(const void* queue_ws);
+ * sample, in 64-sample items each workgroup queues in LDS for its own waves.
+ * Evaluates exactly ngp_field_forward_first's samples + its round-2 list's
+ * (ngp_field_encode_mlp's values bit for bit; no other sample touched).
+ * *evaluated (nullable) += the evaluated samples.  Replaces, for the
+ * model(xyzs, dirs) call of __render_rays_train (models/rendering.py:278),
+ * both rounds' field launches and the round-2 list launch. */
 int ngp_field_forward_rows(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
                            const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
                            float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
-                           void* enc_pm, float* sigmas, float* rgbs, void* queue_ws, int64_t* evaluated,
-                           void* stream);
+                           void* enc_pm, float* sigmas, float* rgbs, int64_t* evaluated, void* stream);
 /* Round 1 of the chunked training forward with the round-2 counts: for the
  * rows rows[j], j < *n_rows_dev (rows NULL: rows 0..n_rows-1; n_rows_dev
  * NULL: n_rows) of rays_a (ray, start, N), the first min(N, 64) samples

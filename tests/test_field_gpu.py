@@ -425,17 +425,16 @@ def test_forward_first_chunk_matches_encode_mlp_and_chunk_counts(scale):
     # runs of a row are contiguous and ascending: every step inside the list is +1 or a jump to another row's start
     steps = got[1:] - got[:-1]
     assert int((steps == 1).sum()) == T - int((cnt_ref > 0).sum())
-    # 3) both rounds in one launch (ngp_field_forward_rows, device work queue): exactly the first chunks + the
-    # round-2 list evaluated, same values, nothing else touched; twice on one workspace (reset by the launch)
+    # 3) both rounds in one launch (ngp_field_forward_rows, per-workgroup LDS queues): exactly the first chunks +
+    # the round-2 list evaluated, same values, nothing else touched; with and without the row list
     both = torch.zeros(n, dtype=torch.bool, device=DEV)
     both[first] = True
     both[got] = True
-    ws = torch.zeros((L.ngp_field_forward_rows_workspace(R, n) + 7) // 8, dtype=torch.int64, device=DEV)
     for it in range(2):
         enc_pm.fill_(7.0); sig2.fill_(-1.0); rgb2.fill_(-1.0); ev.zero_()
         vren._ok(L.ngp_field_forward_rows(vp(x), vp(d), vp(deltas), vp(rays_a), vp(rows) if it else None,
                                           vp(n_ne) if it else None, R, n, ctypes.c_float(1e-4), ctypes.byref(grid.desc),
-                                          vp(p16[HG.MLP_PARAMS:]), vp(p16), vp(enc_pm), vp(sig2), vp(rgb2), vp(ws),
+                                          vp(p16[HG.MLP_PARAMS:]), vp(p16), vp(enc_pm), vp(sig2), vp(rgb2),
                                           vp(ev), vren._stream()), "forward_rows")
         torch.cuda.synchronize()
         rows_enc = enc_pm.permute(1, 0, 2).reshape(n, 32)
@@ -443,4 +442,3 @@ def test_forward_first_chunk_matches_encode_mlp_and_chunk_counts(scale):
         assert torch.equal(sig2[both], sig[both]) and torch.equal(rgb2[both], rgb[both])
         assert bool((sig2[~both] == -1.0).all()) and bool((rows_enc[~both] == 7.0).all())
         assert int(ev) == int(both.sum())
-        assert L.ngp_field_forward_rows_guard(vp(ws)) == 0 and int(ws.abs().sum()) == 0
