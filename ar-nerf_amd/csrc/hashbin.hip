@@ -687,9 +687,13 @@ __global__ void __launch_bounds__(256) hash_adam_residual_kernel(GridArgs ga, Bi
                                                                   float* __restrict__ grad, BinWs ws, AdamArgs adam,
                                                                   uint32_t b_lo, StepTicket ticket) {
     const uint32_t b = b_lo + blockIdx.x;
-    if (b < nbt && !fused_bucket(ws, b, ws.fb[MAXB] != 0)) {  // (block-uniform)
-        float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
-        adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
+    const bool mine = b < nbt && !fused_bucket(ws, b, ws.fb[MAXB] != 0);  // (block-uniform)
+    float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
+    if (mine) adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
+    // (after the block's counter reads -- and the accumulation launch before it is done reading
+    // too -- not after its stores, which the arrival's vmcnt(0) would wait for)
+    step_ticket_arrive(ticket);
+    if (mine) {
         const uint32_t l = bucket_level(ba, b), lb = b - ba.bbase[l];
         const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
         const size_t gbase = 2 * ((size_t)ga.g.offsets[l] + ((size_t)lb << BSHIFT));
@@ -701,7 +705,6 @@ __global__ void __launch_bounds__(256) hash_adam_residual_kernel(GridArgs ga, Bi
             g4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
-    step_ticket_arrive(ticket);  // (after the accumulation launch before it: its reads are done too)
 }
 
 static int bin_args(const ngp_hashgrid_t* grid, int64_t tiles_cap, int lo, int merge_hi, BinArgs& ba,

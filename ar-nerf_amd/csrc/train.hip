@@ -407,6 +407,9 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    StepTicket ticket = StepTicket{nullptr, nullptr, 0, 0, 0},
                                                    float* __restrict__ zero = nullptr, int64_t zero4 = 0) {
     adam_bias(lr_dev, step_dev, b1, b2, lr, bc1, bc2);
+    // (the block's counter reads are done: it arrives now, not after its stores, which the
+    // arrival's vmcnt(0) would otherwise wait for)
+    step_ticket_arrive(ticket);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         float4 P = reinterpret_cast<float4*>(p)[i], Gd = reinterpret_cast<float4*>(grad)[i];
@@ -449,7 +452,6 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
     // (ngp_adam_step_dev_zero) a second range cleared by the same launch
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < zero4; i += stride)
         reinterpret_cast<float4*>(zero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    step_ticket_arrive(ticket);
 }
 
 // --------------------------------------------------- occupancy grid update
