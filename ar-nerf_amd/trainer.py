@@ -209,12 +209,13 @@ class NGPTrainer:
         # round-2 list in one launch (counts + look-back scan + map): its look-back workspace, zeroed once
         self._cs_ws = torch.zeros((vren.lib().ngp_chunk_segments_workspace(R) + 7) // 8, dtype=torch.int64,
                                   device=dev)
-        # (NGP_ROW_FWD=1: round 1 one wave per non-empty row with the row's transmittance in its
-        # epilogue, which appends the row's round-2 samples to the round-2 list itself --
-        # ngp_field_forward_first: no list launch; NGP_ROW_FWD=2: both rounds in one launch,
-        # each workgroup queueing its rows' round-2 chunks in LDS for its own waves --
-        # ngp_field_forward_rows; chunk_first must then be 64)
-        self.row_forward = int(os.environ.get("NGP_ROW_FWD", "0"))
+        # row forward (NGP_ROW_FWD=1, the default since round 4: +2 %, 9 of 9 alternating pairs,
+        # profiles/r04/ab/row_forward_variants.txt): round 1 one wave per non-empty row with the
+        # row's transmittance in its epilogue, which appends the row's round-2 samples to the
+        # round-2 list itself (ngp_field_forward_first: no list launch); NGP_ROW_FWD=2: both
+        # rounds in one launch, each workgroup queueing its rows' round-2 chunks in LDS for its
+        # own waves (ngp_field_forward_rows); 0: the two-round lists below
+        self.row_forward = int(os.environ.get("NGP_ROW_FWD", "1"))
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
@@ -482,15 +483,21 @@ class NGPTrainer:
             # instead of at the head of this batch's step; its length eval_total1 is counted
             # into eval_stats by the round-2 list launch of the step that evaluates it
             K = self.chunk_first
-            m["eval1_K"] = K if (K > 0 and R <= 65536 and not self.row_forward) else 0
+            rows = self._rows_fwd(K)
+            m["eval1_K"] = K if (K > 0 and R <= 65536 and not rows) else 0
             if m["eval1_K"]:
                 vren._ok(L.ngp_ray_segments_capped(_p(m["rays_a"]), R, K, _p(m["act_start1"]), _p(m["eval_total1"]),
                                                    None, _p(m["eval_idx1"]), s), "segments_capped")
-            elif K > 0 and self.row_forward:
+            elif rows:
                 vren._ok(L.ngp_rays_nonempty(_p(m["rays_a"]), R, _p(m["rows_ne"]), _p(m["n_rows_ne"]), None,
                                              _p(m["eval_total2"]), s), "rays_nonempty")
             if side:
                 self._ev("march_side", 1, stream)
+
+    def _rows_fwd(self, K):
+        """The row forward runs the chunked evaluation (its first chunk is one
+        wave: chunk_first 64; other chunk sizes take the two-round lists)."""
+        return bool(self.row_forward) and K == 64
 
     def _can_prefetch(self):
         """The next batch may be marched ahead unless the next step begins with
@@ -890,11 +897,10 @@ class NGPTrainer:
         if fork is not None:
             fork()
         self._ev("field_fwd", 0)
-        if self.chunk_first > 0 and self.row_forward:
+        if self._rows_fwd(self.chunk_first):
             # round 1: a wave per non-empty row (the list built by the march), its transmittance
             # deciding the row's round 2, whose samples it appends to the round-2 list itself (no
             # list pass); round 2: the field over that list
-            assert self.chunk_first == 64, "row forward: the first chunk is one wave (64 samples)"
             self._ev("hash_encode", 0)
             if self.row_forward == 2:  # both rounds, one launch (per-workgroup LDS queues)
                 vren._ok(HGL.ngp_field_forward_rows(
