@@ -4,10 +4,10 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4g}; mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_trainer_gpu.py tests/test_field_gpu.py tests/test_vren_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 tail -n 3 $OUT/pytest.log
-grep "evaluated samples" $OUT/pytest.log || true
-bash scripts/ab_env.sh ${1:-r4g}/ab 3 "||" "|NGP_ROW_FWD=1|" "|NGP_ROW_FWD=2|" "|NGP_STEP_TICKET=1|" "|NGP_ROW_FWD=2 NGP_STEP_TICKET=1|"
+grep -E "evaluated samples|passed|failed" $OUT/pytest.log | tail -6 || true
+bash scripts/ab_env.sh ${1:-r4g}/ab 3 "|NGP_ROW_FWD=0|" "||" "|NGP_ROW_FWD=2|" "|NGP_STEP_TICKET=1|" "|NGP_ROW_FWD=2 NGP_STEP_TICKET=1|"
 Q="--psnr-views 0 --no-cpu-baseline --quality-steps 0 --no-oracle-quality --infer-frames 0 --breakdown-steps 1"
 NGP_ROW_FWD=${ROWMODE:-2} timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/tr" -o run -f csv -- python3 bench.py --steps 200 --warmup 5 $Q \
     > "$OUT/b.json" 2> "$OUT/b.err"
