@@ -282,13 +282,13 @@ def test_segmented_replay_reduces_the_whole_gradient_when_every_level_is_binned(
     assert worst < 1e-3
 
 
-def _emu_trainer(use_graphs):
+def _emu_trainer(use_graphs, k=2):
     import synthetic as S
     from trainer import NGPTrainer
     sc = S.AnalyticScene(W=100, H=100, n_images=10)
     dev = torch.device("cuda", 0)
     tr = NGPTrainer(scale=0.5, batch_size=R, device=dev, seed=3, warmup_steps=0, update_interval=10 ** 6,
-                    emulate_dp=1, use_graphs=use_graphs)
+                    emulate_dp=1, use_graphs=use_graphs, dp_fine_buckets=k)
     with torch.no_grad():
         g = torch.Generator().manual_seed(11)
         tr.params[10240:] = ((torch.rand(tr.n_params - 10240, generator=g) * 2 - 1) * 0.5).to(dev)
@@ -298,7 +298,8 @@ def _emu_trainer(use_graphs):
     return tr, sc
 
 
-def test_segmented_replay_matches_the_unsegmented_step_in_one_process():
+@pytest.mark.parametrize("k", [2, 4])
+def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k):
     """the world > 1 step's per-bucket pipeline (graph segments,
     reduce-scatter / sharded Adam / all-gather of each bucket on the comm
     stream while the next level range accumulates on the main stream) run in
@@ -311,7 +312,7 @@ def test_segmented_replay_matches_the_unsegmented_step_in_one_process():
     atomic-order noise of the MLP and coarse-level gradients."""
     runs = []
     for graphs in (True, False):
-        tr, sc = _emu_trainer(graphs)
+        tr, sc = _emu_trainer(graphs, k)
         p0 = tr.params.clone()
         gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
         for _ in range(3):
@@ -319,7 +320,7 @@ def test_segmented_replay_matches_the_unsegmented_step_in_one_process():
         tr.drain()
         torch.cuda.synchronize()
         if graphs:
-            assert any("compute" in k for k in tr._graphs) and len(tr.bin_cuts) == 5  # replayed, 1 + 4 buckets
+            assert any("compute" in g for g in tr._graphs) and len(tr.bin_cuts) == k + 1  # replayed; 1 + k buckets
         runs.append(((tr.params - p0).cpu(), tr.buckets, (tr.params16.float() - tr.params.half().float()).abs().max()))
     (dA, buckets, s16a), (dB, _, s16b) = runs
     assert float(s16a) == 0.0 and float(s16b) == 0.0  # every rank's shadow all-gathered in full
