@@ -216,6 +216,9 @@ class NGPTrainer:
         # rounds in one launch, each workgroup queueing its rows' round-2 chunks in LDS for its
         # own waves (ngp_field_forward_rows); 0: the two-round lists below
         self.row_forward = int(os.environ.get("NGP_ROW_FWD", "1"))
+        # where the next batch's march forks off the step (A/B: NGP_MARCH_AT = start | fwd | mlp)
+        self.march_at = os.environ.get("NGP_MARCH_AT", "start")
+        assert self.march_at in ("start", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
@@ -894,7 +897,7 @@ class NGPTrainer:
         it runs at the step's start, beside the gather-bound encode rather
         than the VALU-bound MLP backward (+1.5 %, profiles/r02/ab/prefetch_at.txt)."""
         L, s, HGL, R = self.L, vren._stream(), HG._lib(), self.batch_size
-        if fork is not None:
+        if fork is not None and self.march_at == "start":
             fork()
         self._ev("field_fwd", 0)
         if self._rows_fwd(self.chunk_first):
@@ -946,6 +949,8 @@ class NGPTrainer:
                                               s), "field_encode_mlp")
             self._ev("hash_encode", 1)
         self._ev("field_fwd", 1)
+        if fork is not None and self.march_at == "fwd":
+            fork()
         bg = self.bg
         if self.random_bg:  # rendering.py:287-288, one colour per batch, drawn on device (graph-safe)
             bg = self._bg_rand
@@ -994,6 +999,8 @@ class NGPTrainer:
                                                 _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
                                                 _p(self.denc), _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
+        if fork is not None and self.march_at == "mlp":
+            fork()
         if self._segmented and hybrid:
             # (world > 1 graph segments: the hash backward runs as two more
             # graphs -- coarse levels on the side stream, binned levels here --

@@ -1,0 +1,9 @@
+# Round 4: where the next batch's march forks off the step, with the row forward (A/B).
+# usage: gpurun -- bash scripts/gpu_r4h.sh TAG
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-r4h2}; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_trainer_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+tail -n 1 $OUT/pytest.log
+bash scripts/ab_env.sh ${1:-r4h2}/ab 3 "||" "|NGP_MARCH_AT=fwd|" "|NGP_MARCH_AT=mlp|"
