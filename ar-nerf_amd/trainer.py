@@ -216,9 +216,10 @@ class NGPTrainer:
         # rounds in one launch, each workgroup queueing its rows' round-2 chunks in LDS for its
         # own waves (ngp_field_forward_rows); 0: the two-round lists below
         self.row_forward = int(os.environ.get("NGP_ROW_FWD", "1"))
-        # where the next batch's march forks off the step (A/B: NGP_MARCH_AT = start | fwd | mlp)
+        # where the next batch's march forks off the step (A/B: NGP_MARCH_AT = start | r1 (after the
+        # row forward's round 1) | fwd | mlp)
         self.march_at = os.environ.get("NGP_MARCH_AT", "start")
-        assert self.march_at in ("start", "fwd", "mlp")
+        assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
         self.act_start = torch.empty(R, dtype=torch.int64, device=dev)
@@ -920,6 +921,8 @@ class NGPTrainer:
                                                      _p(self.sigmas), _p(self.rgbs), None, _p(self.eval_idx),
                                                      _p(self.eval_total2), _p(self.eval_stats), s), "field_forward_first")
                 self._ev("hash_encode", 1)
+                if fork is not None and self.march_at == "r1":
+                    fork()
                 self._field_indexed(s, self.eval_idx, self.eval_total2)
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first

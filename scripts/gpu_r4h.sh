@@ -6,4 +6,4 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4h2}; mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest tests/test_trainer_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
 tail -n 1 $OUT/pytest.log
-bash scripts/ab_env.sh ${1:-r4h2}/ab 3 "||" "|NGP_MARCH_AT=fwd|" "|NGP_MARCH_AT=mlp|"
+bash scripts/ab_env.sh ${1:-r4h2}/ab 3 "||" "|NGP_MARCH_AT=r1|" "|NGP_MARCH_AT=fwd|"
