@@ -216,9 +216,10 @@ class NGPTrainer:
         # rounds in one launch, each workgroup queueing its rows' round-2 chunks in LDS for its
         # own waves (ngp_field_forward_rows); 0: the two-round lists below
         self.row_forward = int(os.environ.get("NGP_ROW_FWD", "1"))
-        # where the next batch's march forks off the step (A/B: NGP_MARCH_AT = start | r1 (after the
-        # row forward's round 1) | fwd | mlp)
-        self.march_at = os.environ.get("NGP_MARCH_AT", "start")
+        # where the next batch's march forks off the step: after the row forward's round 1 (default:
+        # round 1 runs alone, the march beside round 2 / composite / MLP backward; +2.1 %, 3 of 3
+        # pairs, profiles/r04/ab/march_fork_position.txt), or NGP_MARCH_AT = start | fwd | mlp
+        self.march_at = os.environ.get("NGP_MARCH_AT", "r1")
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -894,11 +895,18 @@ class NGPTrainer:
     def _compute(self, rgb_gt, apply_adam, fork):
         """Field forward (chunked), compositing + loss + its backward, field
         backward, [all-reduce], Adam -- on the current stream, no host sync.
-        fork() (nullable) launches the next batch's march on the side stream;
-        it runs at the step's start, beside the gather-bound encode rather
-        than the VALU-bound MLP backward (+1.5 %, profiles/r02/ab/prefetch_at.txt)."""
+        fork() (nullable) launches the next batch's march on the side stream,
+        where self.march_at says: by default right after the row forward's
+        round 1 (which then has the chip to itself; the march overlaps round
+        2, the composite and the MLP backward: +2.1 %,
+        profiles/r04/ab/march_fork_position.txt); before the row forward, at
+        the step's start (round 2: +1.5 % against after the composite,
+        profiles/r02/ab/prefetch_at.txt)."""
         L, s, HGL, R = self.L, vren._stream(), HG._lib(), self.batch_size
-        if fork is not None and self.march_at == "start":
+        at = self.march_at
+        if at == "r1" and not (self._rows_fwd(self.chunk_first) and self.row_forward == 1):
+            at = "start"  # (no round-1 launch of its own to fork after)
+        if fork is not None and at == "start":
             fork()
         self._ev("field_fwd", 0)
         if self._rows_fwd(self.chunk_first):
@@ -921,7 +929,7 @@ class NGPTrainer:
                                                      _p(self.sigmas), _p(self.rgbs), None, _p(self.eval_idx),
                                                      _p(self.eval_total2), _p(self.eval_stats), s), "field_forward_first")
                 self._ev("hash_encode", 1)
-                if fork is not None and self.march_at == "r1":
+                if fork is not None and at == "r1":
                     fork()
                 self._field_indexed(s, self.eval_idx, self.eval_total2)
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
@@ -952,7 +960,7 @@ class NGPTrainer:
                                               s), "field_encode_mlp")
             self._ev("hash_encode", 1)
         self._ev("field_fwd", 1)
-        if fork is not None and self.march_at == "fwd":
+        if fork is not None and at == "fwd":
             fork()
         bg = self.bg
         if self.random_bg:  # rendering.py:287-288, one colour per batch, drawn on device (graph-safe)
@@ -1002,7 +1010,7 @@ class NGPTrainer:
                                                 _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
                                                 _p(self.denc), _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
-        if fork is not None and self.march_at == "mlp":
+        if fork is not None and at == "mlp":
             fork()
         if self._segmented and hybrid:
             # (world > 1 graph segments: the hash backward runs as two more

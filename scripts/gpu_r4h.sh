@@ -4,6 +4,6 @@ set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4h2}; mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_trainer_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 tail -n 1 $OUT/pytest.log
-bash scripts/ab_env.sh ${1:-r4h2}/ab 3 "||" "|NGP_MARCH_AT=r1|" "|NGP_MARCH_AT=fwd|"
+bash scripts/ab_env.sh ${1:-r4h2}/ab 3 "||" "|NGP_MARCH_AT=start|"
