@@ -6,4 +6,4 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4h2}; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 tail -n 1 $OUT/pytest.log
-bash scripts/ab_env.sh ${1:-r4h2}/ab 3 "||" "|NGP_MARCH_AT=start|"
+bash scripts/ab_env.sh ${1:-r4h2}/ab 3 "||" "|NGP_MARCH_AT=start|" "lib_l4r||" "lib_w4r||"
