@@ -181,7 +181,7 @@ class NGPTrainer:
         # backward, which fused_adam=False restores).
         # (its own stream: sharing the march's side stream -- their work never overlaps in time --
         # measured 6 % slower, the graph's branches then map onto fewer hardware queues)
-        self.bwd_stream = torch.cuda.Stream(device=dev, priority=-1 if os.environ.get("NGP_BWD_PRIO") == "high" else 0)
+        self.bwd_stream = torch.cuda.Stream(device=dev)
         self.fused_adam = bool(fused_adam)
         self._adam_hi = None
         # the training forward: encode + MLPs in one launch (ngp_field_encode_mlp), the

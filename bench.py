@@ -337,8 +337,6 @@ def main():
     args = parse()
     world, rank, local = setup_dist(args)  # local: this rank's device index
     dev = torch.device("cuda", local)
-    if os.environ.get("NGP_MAIN_PRIO") == "high":  # (A/B) the step's main chain on a high-priority queue
-        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     torch.manual_seed(0)
     scene = S.AnalyticScene(W=args.res, H=args.res, n_images=args.images, scale=args.scale)
     gt_images = scene.gt_images(device=dev)  # (n_img, HW, 3) u8, resident in HBM
