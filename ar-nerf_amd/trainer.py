@@ -216,10 +216,13 @@ class NGPTrainer:
         # rounds in one launch, each workgroup queueing its rows' round-2 chunks in LDS for its
         # own waves (ngp_field_forward_rows); 0: the two-round lists below
         self.row_forward = int(os.environ.get("NGP_ROW_FWD", "1"))
-        # where the next batch's march forks off the step: after the row forward's round 1 (default:
-        # round 1 runs alone, the march beside round 2 / composite / MLP backward; +2.1 %, 3 of 3
-        # pairs, profiles/r04/ab/march_fork_position.txt), or NGP_MARCH_AT = start | fwd | mlp
-        self.march_at = os.environ.get("NGP_MARCH_AT", "r1")
+        # where the next batch's march forks off the step: after the row forward's round 1 on the
+        # single-cascade (Lego-shaped) scenes (round 1 runs alone, the march beside round 2 /
+        # composite / MLP backward: +2.1 %, 6 of 6 pairs, profiles/r04/ab/march_fork_position.txt);
+        # at the step's start on cascaded scenes, whose march is 3/4 of a forward-sized step and
+        # beside the MLP backward slows it 1.7x (garden-shaped: -6 %, profiles/r04/ab/garden_r4.txt);
+        # NGP_MARCH_AT = start | r1 | fwd | mlp overrides
+        self.march_at = os.environ.get("NGP_MARCH_AT", "r1" if self.cascades == 1 else "start")
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)

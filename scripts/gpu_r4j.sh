@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4q}; mkdir -p $OUT
 for rep in 1 2; do
   i=0
-  for envs in "" "NGP_ROW_FWD=0 NGP_MARCH_AT=start"; do
+  for envs in "" "NGP_ROW_FWD=0"; do
     i=$((i+1))
     env $envs timeout -k 10 300 python -u bench.py --scale 16 --batch 16384 --steps 300 --warmup 10 --no-cpu-baseline \
         --quality-steps 0 --psnr-views 0 --infer-frames 0 --no-oracle-quality --breakdown-steps 20 > "$OUT/v${i}_$rep.json" 2> "$OUT/v${i}_$rep.err"
