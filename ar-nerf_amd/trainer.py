@@ -224,7 +224,6 @@ class NGPTrainer:
         # NGP_MARCH_AT = start | r1 | fwd | mlp overrides
         self.march_at = os.environ.get("NGP_MARCH_AT", "r1" if self.cascades == 1 else "start")
         self.plan_after = os.environ.get("NGP_PLAN_AFTER", "0") == "1"  # (A/B, _compute)
-        self.r1_event = os.environ.get("NGP_R1_EVENT", "0") == "1"  # (A/B, _compute)
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -515,7 +514,7 @@ class NGPTrainer:
         return (self._pending is None and (self.global_step + 1) % self.update_interval != 0
                 and not self.no_prefetch)
 
-    def prefetch(self, src, directions, poses, after=None):
+    def prefetch(self, src, directions, poses):
         """March the NEXT batch into the idle buffer set on the side stream so
         it overlaps the current step's field / loss / backward / Adam.  Called
         by step() once the current set is bound: everything the side stream
@@ -526,10 +525,8 @@ class NGPTrainer:
         if not self._can_prefetch():
             return False
         k = 1 - self.cur
-        ready = after
-        if ready is None:
-            ready = torch.cuda.Event()
-            ready.record(torch.cuda.current_stream())
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream())
         self.march_stream.wait_event(ready)
         self._march(k, src, directions, poses, self.march_stream)
         ev = torch.cuda.Event()
@@ -747,11 +744,8 @@ class NGPTrainer:
         cs = torch.cuda.current_stream()
         fork = None
         if not update_after:
-            def fork(after=None):  # after: an event to start from (default: everything enqueued on cs)
-                if after is None:
-                    self.march_stream.wait_stream(cs)
-                else:
-                    self.march_stream.wait_event(after)
+            def fork():
+                self.march_stream.wait_stream(cs)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
         self._segmented = True
         try:
@@ -850,11 +844,8 @@ class NGPTrainer:
         self._bind(self.msets[k])
         cs = torch.cuda.current_stream()
         if not update_after:
-            def fork(after=None):  # after: an event to start from (default: everything enqueued on cs)
-                if after is None:
-                    self.march_stream.wait_stream(cs)
-                else:
-                    self.march_stream.wait_event(after)
+            def fork():
+                self.march_stream.wait_stream(cs)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
 
             if self._ticket_ok():
@@ -896,7 +887,7 @@ class NGPTrainer:
         self._ev("raygen_march", 1)
         fork = None
         if next_src is not None and apply_adam:
-            fork = lambda after=None: self.prefetch(next_src, directions, poses, after)  # noqa: E731
+            fork = lambda: self.prefetch(next_src, directions, poses)  # noqa: E731
         if apply_adam:
             self._set_lr()
         out = self._compute(rgb_gt, apply_adam, fork)
@@ -942,16 +933,9 @@ class NGPTrainer:
                                                      _p(self.sigmas), _p(self.rgbs), None, _p(self.eval_idx),
                                                      _p(self.eval_total2), _p(self.eval_stats), s), "field_forward_first")
                 self._ev("hash_encode", 1)
-                r1 = None
                 if fork is not None and at == "r1":
-                    if self.r1_event:  # round 2 captured first (it keeps round 1's queue), the march from this point
-                        r1 = torch.cuda.Event()
-                        r1.record(torch.cuda.current_stream())
-                    else:
-                        fork()
+                    fork()
                 self._field_indexed(s, self.eval_idx, self.eval_total2)
-                if r1 is not None:
-                    fork(r1)
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
             if self.eval1_K == K:  # built by this batch's march
