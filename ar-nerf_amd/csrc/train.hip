@@ -332,9 +332,6 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
     float* __restrict__ out_rgb, float* __restrict__ out_op, float* __restrict__ out_depth,
     float* __restrict__ out_loss, int32_t* __restrict__ n_active, int32_t* __restrict__ sample_idx,
     unsigned long long* __restrict__ alloc, int64_t* __restrict__ n_active_total, int64_t* __restrict__ stats) {
-#ifdef NGP_COMPOSITE_PRIO  // (A/B) wave priority against the march's waves sharing the SIMDs
-    __builtin_amdgcn_s_setprio(NGP_COMPOSITE_PRIO);
-#endif
     __shared__ unsigned long long blk[3];
     __shared__ int64_t s_na[4];
     __shared__ unsigned long long s_base;

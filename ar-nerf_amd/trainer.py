@@ -223,7 +223,6 @@ class NGPTrainer:
         # beside the MLP backward slows it 1.7x (garden-shaped: -6 %, profiles/r04/ab/garden_r4.txt);
         # NGP_MARCH_AT = start | r1 | fwd | mlp overrides
         self.march_at = os.environ.get("NGP_MARCH_AT", "r1" if self.cascades == 1 else "start")
-        self.plan_after = os.environ.get("NGP_PLAN_AFTER", "0") == "1"  # (A/B, _compute)
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -989,10 +988,7 @@ class NGPTrainer:
         cs = torch.cuda.current_stream()
         hybrid = self.hash_backward != "atomic"
         bs = self.bwd_stream
-        if hybrid and self.plan_after:  # (A/B) the MLP backward captured first, the plan forked from before it
-            listed = torch.cuda.Event()
-            listed.record(cs)
-        if hybrid and not self.plan_after:  # bucket plan of the binned levels (xyzs / sample_idx) beside the MLP bwd
+        if hybrid:  # bucket plan of the binned fine levels (xyzs / sample_idx only) beside the MLP backward
             bs.wait_stream(cs)
             with torch.cuda.stream(bs):
                 vren._ok(HGL.ngp_hash_binned_plan(_p(self.xyzs), self.cap, _p(self.n_active_total),
@@ -1017,15 +1013,6 @@ class NGPTrainer:
                                                 _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
                                                 _p(self.denc), _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
-        if hybrid and self.plan_after:
-            bs.wait_event(listed)
-            with torch.cuda.stream(bs):
-                vren._ok(HGL.ngp_hash_binned_plan(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                  _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
-                                                  _p(self.bin_ws), self.bin_max_samples, self.bin_level_lo,
-                                                  self.bin_merge_hi, vren._stream()), "hash_binned_plan")
-                planned = torch.cuda.Event()
-                planned.record(bs)
         if fork is not None and at == "mlp":
             fork()
         if self._segmented and hybrid:
