@@ -407,123 +407,124 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
     wc.dil = wc.sum ? wc.sum + p.n_sum32 : nullptr;
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t r = (int64_t)blockIdx.x * 4 + w;
-    if (r >= n_rays) return;
-    float o[3], d[3], dinv[3];
-    load_ray(rays_o, rays_d, r, o, d, dinv);
-    const float t2 = hits_t[2 * r + 1];
-    const float t0 = start_t(hits_t, noise, r, p);
-    const float dt = NGP_SQRT3 / p.max_samples;
-    float* st = slot_t + r * (int64_t)p.max_samples;
-    float* sd = slot_dt + r * (int64_t)p.max_samples;
-    if (!(0 <= t0) || !(t0 < t2)) {
-        if (lane == 0) counts[r] = 0;
-        return;
-    }
-    // Conservative early out (exact): points every half 4^3-block along
-    // [t0, t2]; the walk's every probe lies within one block of one of them,
-    // so if no point's block has an occupied cell within one block
-    // (dilated summary), the walk emits nothing.  Most rays crossing the box
-    // miss the object and cost this instead of a full lattice walk.
-    if (wc.dil) {
-        const float mb = fminf(0.5f, p.scale);
-        const float dn = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-        const float step = 0.45f * (4.0f * 2.0f * mb / p.grid_size) / dn;
-        const int npts = (int)ceilf((t2 - t0) / step) + 1;
-        const float gm1 = p.grid_size - 1.0f, mbi = 1 / mb;
-        bool near = false;
-        for (int j0 = 0; j0 < npts && !near; j0 += 64) {
-            const int j = j0 + lane;
-            bool b = false;
-            if (j < npts) {
-                const float t = fminf(t0 + (float)j * step, t2);
-                const float x = o[0] + t * d[0], y = o[1] + t * d[1], z = o[2] + t * d[2];
-                const int nx = (int)clampf(0.5f * (x * mbi + 1) * p.grid_size, 0.0f, gm1);
-                const int ny = (int)clampf(0.5f * (y * mbi + 1) * p.grid_size, 0.0f, gm1);
-                const int nz = (int)clampf(0.5f * (z * mbi + 1) * p.grid_size, 0.0f, gm1);
-                const uint32_t wi = morton3((uint32_t)nx >> 2, (uint32_t)ny >> 2, (uint32_t)nz >> 2);
-                b = (wc.dil[wi >> 5] >> (wi & 31u)) & 1u;
-            }
-            near = __ballot(b) != 0ull;
-        }
-        if (!near) {
+    // one ray per wave; a grid capped below the rays (NGP_MARCH_BLOCKS, A/B) strides over them
+    for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < n_rays; r += (int64_t)gridDim.x * 4) {
+        float o[3], d[3], dinv[3];
+        load_ray(rays_o, rays_d, r, o, d, dinv);
+        const float t2 = hits_t[2 * r + 1];
+        const float t0 = start_t(hits_t, noise, r, p);
+        const float dt = NGP_SQRT3 / p.max_samples;
+        float* st = slot_t + r * (int64_t)p.max_samples;
+        float* sd = slot_dt + r * (int64_t)p.max_samples;
+        if (!(0 <= t0) || !(t0 < t2)) {
             if (lane == 0) counts[r] = 0;
-            return;
+            continue;
         }
-    }
-    LatSeg& sg = segs[w];
-    int nseg = 0;
-    const int k_end = lat_build(t0, t2, dt, sg, nseg, lane == 0);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (k_end < 0) {  // segment table overflow: the serial walk on lane 0
-        if (lane == 0) {
-            float t = t0, x, y, z, dts;
-            int N = 0;
-            while (0 <= t && t < t2 && N < p.max_samples)
-            {
-                const float tc = t;
-                if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) { st[N] = tc; sd[N] = dts; N++; }
+        // Conservative early out (exact): points every half 4^3-block along
+        // [t0, t2]; the walk's every probe lies within one block of one of them,
+        // so if no point's block has an occupied cell within one block
+        // (dilated summary), the walk emits nothing.  Most rays crossing the box
+        // miss the object and cost this instead of a full lattice walk.
+        if (wc.dil) {
+            const float mb = fminf(0.5f, p.scale);
+            const float dn = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+            const float step = 0.45f * (4.0f * 2.0f * mb / p.grid_size) / dn;
+            const int npts = (int)ceilf((t2 - t0) / step) + 1;
+            const float gm1 = p.grid_size - 1.0f, mbi = 1 / mb;
+            bool near = false;
+            for (int j0 = 0; j0 < npts && !near; j0 += 64) {
+                const int j = j0 + lane;
+                bool b = false;
+                if (j < npts) {
+                    const float t = fminf(t0 + (float)j * step, t2);
+                    const float x = o[0] + t * d[0], y = o[1] + t * d[1], z = o[2] + t * d[2];
+                    const int nx = (int)clampf(0.5f * (x * mbi + 1) * p.grid_size, 0.0f, gm1);
+                    const int ny = (int)clampf(0.5f * (y * mbi + 1) * p.grid_size, 0.0f, gm1);
+                    const int nz = (int)clampf(0.5f * (z * mbi + 1) * p.grid_size, 0.0f, gm1);
+                    const uint32_t wi = morton3((uint32_t)nx >> 2, (uint32_t)ny >> 2, (uint32_t)nz >> 2);
+                    b = (wc.dil[wi >> 5] >> (wi & 31u)) & 1u;
+                }
+                near = __ballot(b) != 0ull;
             }
-            counts[r] = N;
-        }
-        return;
-    }
-    int c = 0, N = 0, q0 = 0;  // window start (a visited point), samples, its segment
-    while (c < k_end && N < p.max_samples) {
-        while (q0 + 1 < nseg && c >= sg.K[q0 + 1]) ++q0;
-        const int k = c + lane;
-        int q = q0;
-        while (q + 1 < nseg && k >= sg.K[q + 1]) ++q;
-        const bool live = k < k_end;
-        const float tk = live ? lat_t(sg, q, k) : 0.f;
-        bool occ = false;
-        int nxt = k_end;
-        if (live) {
-            float x, y, z, dts, T;
-            occ = march_probe<true>(tk, o, d, dinv, p, x, y, z, dts, wc, T);
-            nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
-        }
-        const uint64_t occm = __ballot(occ && live);
-        // The walk's chain through the window, in parallel: J_b(i) = the
-        // 2^b-th successor of window point i (64 = out of the window),
-        // built by pointer doubling; every lane then climbs from point 0
-        // with binary lifting to the last chain point <= itself -- it is
-        // on the chain iff that is itself.  (Successors only move forward.)
-        int J[6];
-        J[0] = live ? min(nxt - c, 64) : 64;
-#pragma unroll
-        for (int b = 1; b < 6; ++b) {
-            const int prev = J[b - 1];
-            const int v = __builtin_amdgcn_ds_bpermute(min(prev, 63) << 2, prev);
-            J[b] = prev >= 64 ? 64 : v;
-        }
-        int cur = 0;
-#pragma unroll
-        for (int b = 5; b >= 0; --b) {
-            const int v = __builtin_amdgcn_ds_bpermute(min(cur, 63) << 2, J[b]);
-            const int to = cur >= 64 ? 64 : v;
-            if (to <= lane) cur = to;
-        }
-        uint64_t vis = __ballot(cur == lane);
-        const int last = 63 - __builtin_clzll(vis);  // the chain's last point in the window
-        const int pnt = __builtin_amdgcn_readlane(nxt, last);   // k_end if it ends the walk
-        vis &= occm;
-        // emit the chain's occupied points, at most up to max_samples
-        const int room = p.max_samples - N;
-        const int nv = __builtin_popcountll(vis);
-        if ((vis >> lane) & 1ull) {
-            const int rank = __builtin_popcountll(vis & ((1ull << lane) - 1ull));
-            if (rank < room) {
-                st[N + rank] = tk;
-                sd[N + rank] = dt;
+            if (!near) {
+                if (lane == 0) counts[r] = 0;
+                continue;
             }
         }
-        N += min(nv, room);
-        c = pnt;
+        LatSeg& sg = segs[w];
+        int nseg = 0;
+        const int k_end = lat_build(t0, t2, dt, sg, nseg, lane == 0);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (k_end < 0) {  // segment table overflow: the serial walk on lane 0
+            if (lane == 0) {
+                float t = t0, x, y, z, dts;
+                int N = 0;
+                while (0 <= t && t < t2 && N < p.max_samples)
+                {
+                    const float tc = t;
+                    if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) { st[N] = tc; sd[N] = dts; N++; }
+                }
+                counts[r] = N;
+            }
+            continue;
+        }
+        int c = 0, N = 0, q0 = 0;  // window start (a visited point), samples, its segment
+        while (c < k_end && N < p.max_samples) {
+            while (q0 + 1 < nseg && c >= sg.K[q0 + 1]) ++q0;
+            const int k = c + lane;
+            int q = q0;
+            while (q + 1 < nseg && k >= sg.K[q + 1]) ++q;
+            const bool live = k < k_end;
+            const float tk = live ? lat_t(sg, q, k) : 0.f;
+            bool occ = false;
+            int nxt = k_end;
+            if (live) {
+                float x, y, z, dts, T;
+                occ = march_probe<true>(tk, o, d, dinv, p, x, y, z, dts, wc, T);
+                nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
+            }
+            const uint64_t occm = __ballot(occ && live);
+            // The walk's chain through the window, in parallel: J_b(i) = the
+            // 2^b-th successor of window point i (64 = out of the window),
+            // built by pointer doubling; every lane then climbs from point 0
+            // with binary lifting to the last chain point <= itself -- it is
+            // on the chain iff that is itself.  (Successors only move forward.)
+            int J[6];
+            J[0] = live ? min(nxt - c, 64) : 64;
+    #pragma unroll
+            for (int b = 1; b < 6; ++b) {
+                const int prev = J[b - 1];
+                const int v = __builtin_amdgcn_ds_bpermute(min(prev, 63) << 2, prev);
+                J[b] = prev >= 64 ? 64 : v;
+            }
+            int cur = 0;
+    #pragma unroll
+            for (int b = 5; b >= 0; --b) {
+                const int v = __builtin_amdgcn_ds_bpermute(min(cur, 63) << 2, J[b]);
+                const int to = cur >= 64 ? 64 : v;
+                if (to <= lane) cur = to;
+            }
+            uint64_t vis = __ballot(cur == lane);
+            const int last = 63 - __builtin_clzll(vis);  // the chain's last point in the window
+            const int pnt = __builtin_amdgcn_readlane(nxt, last);   // k_end if it ends the walk
+            vis &= occm;
+            // emit the chain's occupied points, at most up to max_samples
+            const int room = p.max_samples - N;
+            const int nv = __builtin_popcountll(vis);
+            if ((vis >> lane) & 1ull) {
+                const int rank = __builtin_popcountll(vis & ((1ull << lane) - 1ull));
+                if (rank < room) {
+                    st[N + rank] = tk;
+                    sd[N + rank] = dt;
+                }
+            }
+            N += min(nv, room);
+            c = pnt;
+        }
+        if (lane == 0) counts[r] = N;
     }
-    if (lane == 0) counts[r] = N;
 }
 
 // Dense ray-ordered outputs from the slots: one wave per ray, lanes over the
@@ -605,6 +606,11 @@ __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict_
 using namespace ngp;
 
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+// (A/B) a cap on the training march's grid (env NGP_MARCH_BLOCKS; 0 / unset: one 4-ray block per 4 rays)
+static inline unsigned march_blocks(unsigned b) {
+    static const unsigned cap = getenv("NGP_MARCH_BLOCKS") ? (unsigned)atoi(getenv("NGP_MARCH_BLOCKS")) : 0u;
+    return cap && cap < b ? cap : b;
+}
 
 extern "C" {
 
@@ -771,7 +777,7 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
         NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && slot_t && slot_dt);
         const size_t lds = march_summary_lds(p);
         if (march_simple(p))  // one cascade, esf 0: the wave-per-ray lattice walk
-            NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<nblk(n_rays, 4), 256, lds, s>>>(
+            NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<march_blocks(nblk(n_rays, 4)), 256, lds, s>>>(
                                           rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt));
         else
             NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false><<<nblk(n_rays, 4 * MARCH_RPW), 256, lds, s>>>(
