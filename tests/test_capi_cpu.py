@@ -117,3 +117,35 @@ def test_gradient_replica_entry_points_check_arguments_without_launching():
     assert L.ngp_adam_step_dev_rep(p, p, p, p, p, 64, p, f(0.9), f(0.999), f(1e-15), p, f(1.0), 1, C.c_void_p(20),
                                    0, 8, 8, None) == -1
 
+
+
+def test_row_forward_entry_points_check_arguments_without_launching():
+    """ngp_field_forward_first / ngp_field_forward_rows / ngp_rays_nonempty
+    (round 4): argument checks on the host, before any launch (NGP_EINVAL =
+    -1); zero rows are a no-op."""
+    import ctypes as C
+    L, Lv = HG._lib(), vren.lib()
+    g = HG.HashGrid(0.5)
+    d = C.byref(g.desc)
+    p = C.c_void_p(256)  # never dereferenced: every call below fails its checks first (or has nothing to do)
+    f = C.c_float(1e-4)
+    # neither the counts nor the round-2 list asked for; the list without its length; a misaligned length
+    assert L.ngp_field_forward_first(p, p, p, p, None, None, 8, 64, f, d, p, p, p, p, p, None, None, None, None,
+                                     None) == -1
+    assert L.ngp_field_forward_first(p, p, p, p, None, None, 8, 64, f, d, p, p, p, p, p, None, p, None, None,
+                                     None) == -1
+    assert L.ngp_field_forward_first(p, p, p, p, None, None, 8, 64, f, d, p, p, p, p, p, None, p, C.c_void_p(260),
+                                     None, None) == -1
+    assert L.ngp_field_forward_first(None, None, None, None, None, None, -1, 64, f, d, None, None, None, None, None,
+                                     None, None, None, None, None) == -1
+    assert L.ngp_field_forward_first(None, None, None, None, None, None, 0, 64, f, d, None, None, None, None, None,
+                                     None, None, None, None, None) == 0
+    # missing inputs; a misaligned table
+    assert L.ngp_field_forward_rows(None, p, p, p, None, None, 8, 64, f, d, p, p, p, p, p, None, None) == -1
+    assert L.ngp_field_forward_rows(p, p, p, p, None, None, 8, 64, f, d, C.c_void_p(258), p, p, p, p, None,
+                                    None) == -1
+    assert L.ngp_field_forward_rows(None, None, None, None, None, None, 0, 64, f, d, None, None, None, None, None,
+                                    None, None) == 0
+    assert Lv.ngp_rays_nonempty(p, 8, None, p, None, None, None) == -1
+    assert Lv.ngp_rays_nonempty(p, -1, p, p, None, None, None) == -1
+    assert Lv.ngp_rays_nonempty(p, 8, p, None, None, None, None) == -1
