@@ -1177,10 +1177,7 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
                 lambda_distortion};
     // one row per wave: every row's dependent load chain in flight at once
     // (a few rows per wave serialised their memory latencies)
-    // (A/B: NGP_COMPOSITE_BLOCKS caps the grid; the blocks stride over the rows 4 at a time)
-    static const int64_t cap = getenv("NGP_COMPOSITE_BLOCKS") ? atoll(getenv("NGP_COMPOSITE_BLOCKS")) : 0;
-    const int64_t blocks = std::min<int64_t>((n_rays + 3) / 4, cap > 0 ? cap : (1 << 20));
-    NGP_TIMED(NGP_K_COMPOSITE, as_stream(stream), composite_loss_wave_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(
+    NGP_TIMED(NGP_K_COMPOSITE, as_stream(stream), composite_loss_wave_kernel<<<(unsigned)std::min<int64_t>((n_rays + 3) / 4, 1 << 20), 256, 0, as_stream(stream)>>>(
         sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
         out_depth, out_loss, n_active, sample_idx, (unsigned long long*)alloc_ws, n_active_total, stats));
     return ngp_launch_status();
