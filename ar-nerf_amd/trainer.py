@@ -507,6 +507,13 @@ class NGPTrainer:
         wave: chunk_first 64; other chunk sizes take the two-round lists)."""
         return bool(self.row_forward) and K == 64
 
+    def march_fork_point(self):
+        """Where the next batch's march forks off the step (march_at; "r1"
+        needs the row forward's own round-1 launch, else the step's start)."""
+        if self.march_at == "r1" and not (self._rows_fwd(self.chunk_first) and self.row_forward == 1):
+            return "start"
+        return self.march_at
+
     def _can_prefetch(self):
         """The next batch may be marched ahead unless the next step begins with
         an occupancy update (that batch must see the new bitfield)."""
@@ -906,9 +913,7 @@ class NGPTrainer:
         the step's start (round 2: +1.5 % against after the composite,
         profiles/r02/ab/prefetch_at.txt)."""
         L, s, HGL, R = self.L, vren._stream(), HG._lib(), self.batch_size
-        at = self.march_at
-        if at == "r1" and not (self._rows_fwd(self.chunk_first) and self.row_forward == 1):
-            at = "start"  # (no round-1 launch of its own to fork after)
+        at = self.march_fork_point()
         if fork is not None and at == "start":
             fork()
         self._ev("field_fwd", 0)

@@ -560,7 +560,7 @@ def main():
                        "graphs": trainer.use_graphs,
                        "chunk_first": trainer.chunk_first,
                        "row_forward": trainer.row_forward if trainer._rows_fwd(trainer.chunk_first) else 0,
-                       "march_fork": trainer.march_at,
+                       "march_fork": trainer.march_fork_point(),
                        "parallelism": f"dp{world}" + (f" (data-parallel step of world {args.emulate_dp} emulated: collectives as local copies)" if args.emulate_dp else ""), "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
                        "bin_merge_hi": trainer.bin_merge_hi,
