@@ -937,153 +937,6 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
     if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
 }
 
-// field_first_chunk_kernel with each row's first chunk split over a PAIR of
-// waves (NGP_ROW_SPLIT=1, A/B): wave h of the pair gathers levels [8h, 8h+8)
-// of the 64 samples (4 dependent gather rounds instead of 8), the halves are
-// swapped through LDS, each wave runs the MLPs of two of the four 16-sample
-// column blocks, the sigmas meet in LDS and wave 0 of the pair takes the
-// row's transmittance and appends its round-2 samples.  Same values as
-// field_first_chunk_kernel, bit for bit (the same gathers, level sums and
-// MLP code on the same inputs).  Round 1 holds fewer rows than the chip has
-// wave slots, so the second wave of a row is nearly free; the exchange costs
-// two workgroup barriers per row.
-constexpr int SPLIT_WAVES = 4;  // 2 rows per workgroup
-static_assert(FEM_LPR <= 8 && 8 % FEM_LPR == 0, "levels per round within a half");
-template <bool COLOR>
-__global__ void __launch_bounds__(64 * SPLIT_WAVES, SPLIT_WAVES) field_first_chunk_split_kernel(
-    const float* __restrict__ xyzs, const float* __restrict__ dirs, const float* __restrict__ deltas,
-    const int64_t* __restrict__ rays_a, const int32_t* __restrict__ rows, const int64_t* __restrict__ n_rows_dev,
-    int64_t n_rows, int64_t n, float T_thr, GridArgs ga, const uint32_t* __restrict__ table,
-    const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm, float* __restrict__ sigmas,
-    float* __restrict__ rgbs, int32_t* __restrict__ rest, int32_t* __restrict__ list2, int64_t* __restrict__ total2,
-    int64_t* __restrict__ evaluated) {
-    __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
-    __shared__ LevelLds lv;
-    __shared__ unsigned long long blk_eval;
-    __shared__ uint32_t xE[SPLIT_WAVES][8][64];  // each wave's 8 level words, lane-major per word
-    __shared__ float xS[SPLIT_WAVES / 2][64];      // the pair's row's sigmas
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, pr = wv >> 1, h = wv & 1;
-    const int64_t NR = n_rows_dev ? *n_rows_dev : n_rows;
-    const int64_t G = gridDim.x, stride = (int64_t)(SPLIT_WAVES / 2) * G;
-    int64_t j = (int64_t)pr * G + blockIdx.x;  // the pair's first row
-    // block-uniform round count (pair 0 has the most rows): every wave meets every barrier
-    const int64_t j0 = blockIdx.x;
-    const int64_t rounds = j0 < NR ? (NR - j0 + stride - 1) / stride : 0;
-    int64_t r = 0, start = 0, N = 0;
-    auto load_row = [&](int64_t jj) {
-        r = rows ? (int64_t)rows[jj] : jj;
-        start = rays_a[3 * r + 1];
-        N = rays_a[3 * r + 2];
-    };
-    if (j < NR) load_row(j);  // (requested before the weight image is built)
-    if (threadIdx.x == 0) blk_eval = 0ull;
-    load_fwd_weights_direct(mlp, sw, COLOR);
-    load_levels(ga, lv);
-    __syncthreads();
-    int64_t ev = 0;
-    for (int64_t it = 0; it < rounds; ++it, j += stride) {
-        const bool have = j < NR;
-        const int cnt = have ? (int)(N < 64 ? N : 64) : 0;
-        int lane_l = lane;
-        asm volatile("" : "+v"(lane_l));
-        const int s = lane_l & 15, g = lane_l >> 4;
-        const bool valid = lane_l < cnt;
-        const int64_t i = start + lane_l;
-        const float dl = (h == 0 && valid) ? deltas[i] : 0.f;
-        uint32_t H[8];  // levels 8h .. 8h+7
-        if (cnt > 0) {
-            float in[3];
-            load_x01(xyzs, i, valid, ga, in);
-#pragma unroll 1
-            for (int rr = 0; rr < 8 / FEM_LPR; ++rr) {
-                uint32_t v[FEM_LPR][8];
-#pragma unroll
-                for (int q = 0; q < FEM_LPR; ++q) gather_level_loads(in, level_u(lv, 8 * h + FEM_LPR * rr + q), table, v[q]);
-#pragma unroll
-                for (int q = 0; q < 8 - FEM_LPR; ++q) H[q] = H[q + FEM_LPR];
-#pragma unroll
-                for (int q = 0; q < FEM_LPR; ++q) H[8 - FEM_LPR + q] = level_sum_h2(in, level_u(lv, 8 * h + FEM_LPR * rr + q), v[q]);
-            }
-            if (valid && enc_pm) {
-#pragma unroll
-                for (int p2 = 0; p2 < 4; ++p2)
-                    *reinterpret_cast<uint2*>(enc_pm + ((int64_t)(4 * h + p2) * n + i) * 4) = make_uint2(H[2 * p2], H[2 * p2 + 1]);
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) xE[wv][q][lane_l] = H[q];
-        }
-        __syncthreads();  // both halves of every row in the workgroup are in LDS
-        float sgl = 0.f;
-        if (cnt > 0) {
-            uint32_t E[16];  // (selects, not an index by h: the array stays in registers)
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t x = xE[wv ^ 1][q][lane_l];
-                E[q] = h ? x : H[q];
-                E[8 + q] = h ? H[q] : x;
-            }
-            transpose_rows4(E);
-            if (h) {  // column blocks 2 and 3: block c's operand is E[0..3] after c rotations by one group
-#pragma unroll
-                for (int q = 0; q < 8; ++q) E[q] = E[q + 8];
-            }
-#pragma unroll 1
-            for (int c = 2 * h; c < 2 * h + 2; ++c) {
-                if (16 * c >= cnt) break;  // (wave-uniform)
-                const bool ok = 16 * c + s < cnt;
-                const int64_t ic = start + 16 * c + s;
-                const h8 e = __builtin_bit_cast(h8, make_uint4(E[0], E[1], E[2], E[3]));
-#pragma unroll
-                for (int q = 0; q < 12; ++q) E[q] = E[q + 4];
-                h4 h1[4];
-                const h4 hh = density_net(e, sw, s, g, h1);
-                const float sig = expf((float)hh[0]);  // TruncExp forward (custom_functions.py:165-167)
-                if (g == 0) {
-                    xS[pr][16 * c + s] = sig;
-                    if (ok) sigmas[ic] = sig;
-                }
-                if constexpr (COLOR) {
-                    const float dx = ok ? dirs[3 * ic] : 0.f, dy = ok ? dirs[3 * ic + 1] : 0.f,
-                                dz = ok ? dirs[3 * ic + 2] : 1.f;
-                    float sh[4];
-                    sh4_select(dx, dy, dz, g, sh);
-                    const h8 cin = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3],
-                                    hh[0], hh[1], hh[2], hh[3]};
-                    h4 h3[4], h4v[4];
-                    const h4 o = color_net(cin, sw, s, g, h3, h4v);
-                    if (ok && g == 0) {
-                        rgbs[3 * ic] = sigmoid_h(o[0]);
-                        rgbs[3 * ic + 1] = sigmoid_h(o[1]);
-                        rgbs[3 * ic + 2] = sigmoid_h(o[2]);
-                    }
-                }
-            }
-        }
-        __syncthreads();  // the row's sigmas are in LDS
-        if (h == 0 && cnt > 0) {
-            sgl = lane < cnt ? xS[pr][lane] : 0.f;
-            const float om = 1.0f - (1.0f - __expf(-sgl * dl));  // chunk_segments_kernel's expression
-            const ChunkT ct = chunk_transmittance(om, cnt, 1.0f, T_thr, lane);
-            const int32_t rc = (!ct.hit && N > 64) ? (int32_t)(N - 64) : 0;
-            ev += cnt;
-            if (rest && lane == 0) rest[r] = rc;
-            if (list2 && rc > 0) {
-                unsigned long long o = 0;
-                if (lane == 0) o = atomicAdd((unsigned long long*)total2, (unsigned long long)rc);
-                const int64_t o2 = (int64_t)__shfl(o, 0, 64);
-                for (int t = lane; t < rc; t += 64) list2[o2 + t] = (int32_t)(start + 64 + t);
-                ev += rc;
-            }
-        } else if (h == 0 && have && rest && lane == 0) {
-            rest[r] = 0;
-        }
-        if (j + stride < NR) load_row(j + stride);
-    }
-    if (lane == 0 && ev) atomicAdd(&blk_eval, (unsigned long long)ev);
-    __syncthreads();
-    if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
-}
-
 // Both chunked rounds in ONE launch, each block its own work queue in LDS.
 // The non-empty rows are dealt over every wave of the grid as in
 // field_first_chunk_kernel (a wave's first row, then every G x waves-th):
@@ -2074,15 +1927,6 @@ int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* d
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0 &&
                   ((uintptr_t)evaluated & 7) == 0);
     hipStream_t s = as_stream(stream);
-    static const bool split = getenv("NGP_ROW_SPLIT") && getenv("NGP_ROW_SPLIT")[0] == '1';
-    if (split) {  // (A/B) a pair of waves per row
-        static const unsigned caps = resident_blocks(field_first_chunk_split_kernel<true>, 64 * SPLIT_WAVES, 0);
-        const unsigned blocks = std::max(1u, std::min(caps, (unsigned)((n_rows + SPLIT_WAVES / 2 - 1) / (SPLIT_WAVES / 2))));
-        NGP_TIMED(NGP_K_HASH_ENCODE, s, field_first_chunk_split_kernel<true><<<blocks, 64 * SPLIT_WAVES, 0, s>>>(
-            xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
-            (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, list2, total2, evaluated));
-        return ngp_launch_status();
-    }
     // grid = every resident block: the rows are dealt over all resident waves
     static const unsigned cap = resident_blocks(field_first_chunk_kernel<true>, 64 * FEM2_WAVES, 0);
     const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + FEM2_WAVES - 1) / FEM2_WAVES)));
