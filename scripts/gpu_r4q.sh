@@ -1,10 +1,10 @@
-# Round 4: quick re-check after a host-side change: trainer + DDP GPU tests, smoke, the driver's bench command.
+# Round 4: re-check of the final tree: the GPU suite, smoke, the driver's bench command.
 # usage: gpurun -- bash scripts/gpu_r4q.sh TAG
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r4q2}; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_trainer_gpu.py tests/test_ddp_gpu.py tests/test_quality_gpu.py -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
 tail -n 1 $OUT/pytest.log
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 tail -1 $OUT/smoke.log
