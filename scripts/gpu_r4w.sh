@@ -1,0 +1,5 @@
+# Round 4: march fork point x march grid cap (A/B).  usage: gpurun -- bash scripts/gpu_r4w.sh TAG
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+bash scripts/ab_env.sh ${1:-r4mx}/ab 3 "||" "|NGP_MARCH_BLOCKS=1024|" "|NGP_MARCH_AT=start NGP_MARCH_BLOCKS=1024|" "|NGP_MARCH_AT=start NGP_MARCH_BLOCKS=512|"
