@@ -2,4 +2,4 @@
 set -e
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-bash scripts/ab_env.sh ${1:-r4mx}/ab 3 "||" "|NGP_MARCH_BLOCKS=1024|" "|NGP_MARCH_AT=start NGP_MARCH_BLOCKS=1024|" "|NGP_MARCH_AT=start NGP_MARCH_BLOCKS=512|"
+bash scripts/ab_env.sh ${1:-r4mx}/ab ${REPS:-3} "||" "|NGP_MARCH_BLOCKS=1024|"
