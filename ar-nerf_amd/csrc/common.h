@@ -28,6 +28,35 @@ void ngp_timing_mark(int id, int end, hipStream_t s);
         ngp_timing_mark((id), 1, (s)); \
     } while (0)
 
+// Device probes (ngp_probe_set, host.hip): lane 0 of every wave of a probed
+// kernel stores its start and end time (GPU wall clock) into its own slot
+// of the step row (*step % ring) -- plain stores, no atomics (atomics from
+// every wave onto a few lines serialised and slowed the probed kernels 2-6x);
+// the host takes the min start / max end: the kernel's execution span as a
+// dispatch trace sees it, with no extra graph node and no change to the
+// captured graphs (the control block is a device symbol read at run time:
+// null = off).  Measurement plumbing only.
+struct ProbeCtl {
+    unsigned long long* buf;  // [ring][NGP_P_COUNT][NGP_PROBE_WAVES][2] (start, end)
+    const int64_t* step;
+    int64_t ring;
+};
+static __device__ ProbeCtl ngp_probe_ctl;
+void ngp_probe_register(void (*set)(const ProbeCtl&));
+static void ngp_probe_set_tu(const ProbeCtl& c) { (void)hipMemcpyToSymbol(HIP_SYMBOL(ngp_probe_ctl), &c, sizeof c); }
+static const int ngp_probe_registered = (ngp_probe_register(ngp_probe_set_tu), 0);
+__device__ __forceinline__ unsigned long long* ngp_probe_slot(int id) {
+    const ProbeCtl c = ngp_probe_ctl;
+    if (!c.buf) return nullptr;
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    return c.buf + (((*c.step % c.ring) * NGP_P_COUNT + id) * NGP_PROBE_WAVES + (w & (NGP_PROBE_WAVES - 1))) * 2;
+}
+#define NGP_PROBE_BEGIN(id)                                          \
+    unsigned long long* const ngp_probe_ = ngp_probe_slot(id);       \
+    if (ngp_probe_ && (threadIdx.x & 63) == 0) ngp_probe_[0] = (unsigned long long)wall_clock64()
+#define NGP_PROBE_END() \
+    if (ngp_probe_ && (threadIdx.x & 63) == 0) ngp_probe_[1] = (unsigned long long)wall_clock64()
+
 // Workgroups of `kernel` that fit on the whole device at once (occupancy x
 // CUs): the grid of a persistent kernel, so per-block prologues (LDS weight
 // images) are paid once per resident block, not once per tile.
@@ -73,36 +102,6 @@ struct AdamArgs {
     const int64_t* step_dev;
     float b1, b2, eps, grad_scale;
 };
-
-// Step completion ticket (ngp_step_ticket_set): the last kernels of a
-// training step (the Adam launches, `parties` of them) advance the per-step
-// device counters themselves once every block of every one of them has
-// finished -- in place of a separate increment launch that would join their
-// streams.  ws (caller-owned, zeroed once): [0..7] blocks arrived per party,
-// [8] parties complete; the last arriver resets them.
-struct StepTicket {
-    uint32_t* ws;
-    int64_t* counters;
-    int n, parties, party;
-};
-// every thread of the block, after its last read of the counters
-__device__ __forceinline__ void step_ticket_arrive(const StepTicket& t) {
-    if (!t.ws) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's counter loads have returned)
-    __syncthreads();                                  // every wave of the block is past its reads
-    if (threadIdx.x == 0) {
-        const uint32_t nb = gridDim.x * gridDim.y * gridDim.z;
-        if (atomicAdd(&t.ws[t.party], 1u) == nb - 1) {  // this launch's last block
-            atomicExch(&t.ws[t.party], 0u);
-            if (atomicAdd(&t.ws[8], 1u) == (uint32_t)t.parties - 1) {  // the step's last launch
-                atomicExch(&t.ws[8], 0u);
-                for (int i = 0; i < t.n; ++i) atomicAdd((unsigned long long*)&t.counters[i], 1ull);
-            }
-        }
-    }
-}
-// the ticket of the next participating launch (host side; none when unset)
-StepTicket ngp_step_ticket_next();
 
 // helper_math.h:280-283 clamp(f,a,b) = fmaxf(a, fminf(f,b)) -- keeps the
 // NaN behaviour of fminf/fmaxf that the marcher relies on.

@@ -534,111 +534,6 @@ __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restric
     }
 }
 
-// ------------------------------------------- fused encode + MLP forward
-// hash_encode_kernel's lane-per-sample gathers (same arithmetic) and the
-// field MLPs in one launch: a wave encodes 64 consecutive samples (one per
-// lane), writes the pair-major encoding for the backward, parks it in its LDS
-// rows and runs the MLPs on four 16-sample column blocks read back in the
-// MFMA B layout -- the separate MLP launch (its fixed cost, the encoding's
-// re-read) disappears and the MLP math overlaps other waves' gathers.
-// (diagnostics only: scripts/diag/fem_phases.hip stamps each wave's phases; empty in the product build)
-#ifndef NGP_FEM_PHASE
-#define NGP_FEM_PHASE(k)
-#endif
-constexpr int XROW = 40;  // halfs per parked encoding row (32 + pad: conflict-free 16-B reads)
-constexpr int FEM_WAVES = 8;  // 512-thread blocks: the 24 KB weight image shared by 8 waves (4 waves/SIMD)
-template <bool COLOR>
-__global__ void __launch_bounds__(64 * FEM_WAVES) field_encode_mlp_kernel(const float* __restrict__ xyzs,
-                                                               const float* __restrict__ dirs, int64_t n,
-                                                               const int64_t* __restrict__ n_dev,
-                                                               const int32_t* __restrict__ sidx, GridArgs ga,
-                                                               const uint32_t* __restrict__ table,
-                                                               const _Float16* __restrict__ mlp,
-                                                               _Float16* __restrict__ enc_pm,
-                                                               float* __restrict__ sigmas, float* __restrict__ rgbs,
-                                                               _Float16* __restrict__ h_out) {
-    __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
-    __shared__ __attribute__((aligned(16))) _Float16 xs[FEM_WAVES][64 * XROW];
-    __shared__ int32_t xi[FEM_WAVES][64];
-    __shared__ LevelLds lv;
-    const int64_t N = n_dev ? *n_dev : n;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, s = lane & 15, g = lane >> 4;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    // the first iteration's index and position (count -> index -> position:
-    // dependent round trips) are requested before the weight image is built,
-    // so the two overlap (most waves run one iteration)
-    int64_t i_first = 0;
-    float in_first[3];
-    {
-        const int64_t j = (int64_t)blockIdx.x * blockDim.x + wv * 64 + lane;
-        const bool valid = j < N;
-        i_first = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
-        load_x01(xyzs, i_first, valid, ga, in_first);
-    }
-    load_fwd_weights_direct(mlp, sw, COLOR);
-    load_levels(ga, lv);
-    __syncthreads();
-    bool first = true;
-    // wave-uniform trip count (the MFMAs need every lane)
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + wv * 64; base < N; base += stride) {
-        const int64_t j = base + lane;
-        const bool valid = j < N;
-        NGP_FEM_PHASE(0);
-        int64_t i = i_first;
-        float in[3] = {in_first[0], in_first[1], in_first[2]};
-        if (!first) {
-            i = valid ? (sidx ? (int64_t)sidx[j] : j) : 0;
-            load_x01(xyzs, i, valid, ga, in);
-        }
-        first = false;
-        _Float16* row = &xs[wv][lane * XROW];
-#pragma unroll 1
-        for (int pr = 0; pr < 8; ++pr) {
-            const LevelU u0 = level_u(lv, 2 * pr), u1 = level_u(lv, 2 * pr + 1);
-            float a0, a1, b0, b1;
-            encode_level_u(in, u0, table, a0, a1);
-            encode_level_u(in, u1, table, b0, b1);
-            const h4 e4 = h4{(_Float16)a0, (_Float16)a1, (_Float16)b0, (_Float16)b1};
-            if (valid && enc_pm) *reinterpret_cast<h4*>(enc_pm + ((int64_t)pr * n + i) * 4) = e4;
-            *reinterpret_cast<h4*>(row + 4 * pr) = e4;
-        }
-        xi[wv][lane] = valid ? (int32_t)i : -1;
-        NGP_FEM_PHASE(1);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 1
-        for (int c = 0; c < 4; ++c) {
-            const int src = 16 * c + s;
-            const int32_t ic = xi[wv][src];
-            const bool ok = ic >= 0;
-            const h8 e = *reinterpret_cast<const h8*>(&xs[wv][src * XROW + 8 * g]);
-            h4 h1[4];
-            const h4 hh = density_net(e, sw, s, g, h1);
-            if (ok) {
-                if (h_out) *reinterpret_cast<h4*>(h_out + (int64_t)ic * 16 + 4 * g) = hh;
-                if (g == 0) sigmas[ic] = expf((float)hh[0]);  // TruncExp forward (custom_functions.py:165-167)
-            }
-            if constexpr (COLOR) {
-                const float dx = ok ? dirs[3 * (int64_t)ic] : 0.f, dy = ok ? dirs[3 * (int64_t)ic + 1] : 0.f,
-                            dz = ok ? dirs[3 * (int64_t)ic + 2] : 1.f;
-                float sh[4];
-                sh4_select(dx, dy, dz, g, sh);
-                const h8 cin = {(_Float16)sh[0], (_Float16)sh[1], (_Float16)sh[2], (_Float16)sh[3], hh[0], hh[1], hh[2], hh[3]};
-                h4 h3[4], h4v[4];
-                const h4 o = color_net(cin, sw, s, g, h3, h4v);
-                if (ok && g == 0) {
-                    rgbs[3 * (int64_t)ic] = sigmoid_h(o[0]);
-                    rgbs[3 * (int64_t)ic + 1] = sigmoid_h(o[1]);
-                    rgbs[3 * (int64_t)ic + 2] = sigmoid_h(o[2]);
-                }
-            }
-        }
-        NGP_FEM_PHASE(2);
-        __builtin_amdgcn_wave_barrier();  // this iteration's LDS reads before the next one's writes (in order per wave)
-    }
-}
-
 // ------------------------------ fused encode + MLP forward, register form
 // field_encode_mlp_kernel's arithmetic (bit-identical outputs) with two
 // changes in the structure:
@@ -705,6 +600,7 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
     float* __restrict__ rgbs, _Float16* __restrict__ h_out) {
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ LevelLds lv;
+    NGP_PROBE_BEGIN(NGP_P_FIELD_ENCODE_MLP);
     const int64_t N = n_dev ? *n_dev : n;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #if !NGP_FEM_REMAT
@@ -796,6 +692,7 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
             }
         }
     }
+    NGP_PROBE_END();
 }
 
 // Encode + MLPs of the 64-sample chunk [i0, i0 + cnt) on one wave (lane =
@@ -890,6 +787,7 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ LevelLds lv;
     __shared__ unsigned long long blk_eval;
+    NGP_PROBE_BEGIN(NGP_P_FIRST_CHUNK);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t NR = n_rows_dev ? *n_rows_dev : n_rows;
     const int64_t G = gridDim.x, stride = (int64_t)FEM2_WAVES * G;
@@ -935,102 +833,7 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
     if (lane == 0 && ev) atomicAdd(&blk_eval, (unsigned long long)ev);
     __syncthreads();
     if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
-}
-
-// Both chunked rounds in ONE launch, each block its own work queue in LDS.
-// The non-empty rows are dealt over every wave of the grid as in
-// field_first_chunk_kernel (a wave's first row, then every G x waves-th):
-// the wave evaluates the row's first chunk and the row's transmittance over
-// it, and if the row is still transparent pushes the row's remaining samples
-// as 64-sample items {first sample << 7 | count} onto its block's queue (LDS
-// atomic; past RQ_CAP items the wave evaluates the overflow itself).  After
-// one barrier the block's waves take the items (LDS ticket) until none is
-// left.  So a row past its first chunk is spread over the 8 waves of its
-// block (no serial chunk chain), round 2 starts per block as soon as that
-// block's round 1 is done (no list pass, no second launch, no grid-wide
-// tail between the rounds), and nothing waits on another block: no global
-// atomics, no polling (a device-wide queue, polled or CAS-claimed by
-// thousands of waves, saturated the memory channel holding its counters:
-// 0.43 ms / 6.3 ms per launch).
-constexpr int RQ_CAP = 1024;
-template <bool COLOR>
-__global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_block_kernel(
-    const float* __restrict__ xyzs, const float* __restrict__ dirs, const float* __restrict__ deltas,
-    const int64_t* __restrict__ rays_a, const int32_t* __restrict__ rows, const int64_t* __restrict__ n_rows_dev,
-    int64_t n_rows, int64_t n, float T_thr, GridArgs ga, const uint32_t* __restrict__ table,
-    const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm, float* __restrict__ sigmas,
-    float* __restrict__ rgbs, int64_t* __restrict__ evaluated) {
-    __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
-    __shared__ LevelLds lv;
-    __shared__ unsigned long long blk_eval;
-    __shared__ unsigned long long qi[RQ_CAP];
-    __shared__ uint32_t q_tail, q_head;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t NR = n_rows_dev ? *n_rows_dev : n_rows;
-    const int64_t G = gridDim.x, stride = (int64_t)FEM2_WAVES * G;
-    auto load_row = [&](int64_t j, int64_t& start, int64_t& N) {
-        const int64_t r = rows ? (int64_t)rows[j] : j;
-        start = rays_a[3 * r + 1];
-        N = rays_a[3 * r + 2];
-    };
-    int64_t j = (int64_t)wv * G + blockIdx.x;  // the wave's first row (wave-uniform)
-    int64_t start = 0, N = 0;
-    if (j < NR) load_row(j, start, N);  // (requested before the weight image is built)
-    if (threadIdx.x == 0) {
-        blk_eval = 0ull;
-        q_tail = q_head = 0u;
-    }
-    load_fwd_weights_direct(mlp, sw, COLOR);
-    load_levels(ga, lv);
-    __syncthreads();
-    int64_t ev = 0;
-    // ---- round 1: the wave's rows
-    for (; j < NR; j += stride) {
-        const int cnt = (int)(N < 64 ? N : 64);
-        uint32_t k = 0;
-        if (cnt > 0) {
-            const float dl = lane < cnt ? deltas[start + lane] : 0.f;
-            const float sg = encode_mlp_chunk<COLOR>(xyzs, dirs, start, cnt, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
-            const float om = 1.0f - (1.0f - __expf(-sg * dl));  // chunk_segments_kernel's expression
-            const ChunkT ct = chunk_transmittance(om, cnt, 1.0f, T_thr, lane);
-            if (!ct.hit && N > 64) k = (uint32_t)((N - 64 + 63) / 64);
-            ev += cnt;
-        }
-        if (k) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&q_tail, k);
-            base = rfl(__shfl(base, 0, 64));
-            for (uint32_t t = lane; t < k; t += 64) {
-                const int64_t i0 = start + 64 + 64 * (int64_t)t;
-                if (base + t < RQ_CAP) qi[base + t] = ((unsigned long long)i0 << 7) | (unsigned long long)min((int64_t)64, start + N - i0);
-            }
-            // (queue full: this wave evaluates the rest of its row itself)
-            for (uint32_t t = base < RQ_CAP ? RQ_CAP - base : 0u; t < k; ++t) {
-                const int64_t i0 = start + 64 + 64 * (int64_t)t;
-                const int c = (int)min((int64_t)64, start + N - i0);
-                encode_mlp_chunk<COLOR>(xyzs, dirs, i0, c, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
-                ev += c;
-            }
-        }
-        const int64_t jn = j + stride;
-        if (jn < NR) load_row(jn, start, N);
-    }
-    __syncthreads();  // every row of the block has pushed its items
-    // ---- round 2: the block's items
-    const uint32_t nq = min(q_tail, (uint32_t)RQ_CAP);
-    for (;;) {
-        uint32_t h = 0;
-        if (lane == 0) h = atomicAdd(&q_head, 1u);
-        h = rfl(__shfl(h, 0, 64));
-        if (h >= nq) break;
-        const unsigned long long it = qi[h];
-        const int c = (int)(it & 127ull);
-        encode_mlp_chunk<COLOR>(xyzs, dirs, (int64_t)(it >> 7), c, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
-        ev += c;
-    }
-    if (lane == 0 && ev) atomicAdd(&blk_eval, (unsigned long long)ev);
-    __syncthreads();
-    if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
+    NGP_PROBE_END();
 }
 
 // One level of the coarse (atomic) hash backward for the wave's 16 consecutive
@@ -1038,8 +841,11 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_rows_bl
 // receives w_c * gd (gd = dL/denc[s][2 l + f]); runs of equal corners along the
 // 16 samples (lanes 4 apart) are merged by segmented suffix sums, and each
 // run's head adds its sum with one memory-side fp32 atomic into dst.
-__device__ __forceinline__ void coarse_scatter_level(const float in[3], bool valid, float gd, int l, const LevelLds& lv,
-                                                     float* __restrict__ dst, int lane, int cx, int f) {
+// coarse_level_runs: the corner indices (idx[yz], level-offset included), the
+// run sums v[yz] and the run-head masks of one level; coarse_scatter_level
+// then adds each head's sum with a memory-side atomic.
+__device__ __forceinline__ void coarse_level_runs(const float in[3], bool valid, float gd, int l, const LevelLds& lv,
+                                                  int lane, int cx, uint32_t idx[4], float v[4], uint64_t heads[4]) {
     const float sc = lv.scale[l];
     const uint32_t res = lv.res[l], size = lv.size[l], off = lv.off[l];
     const bool dense = (lv.dense >> l) & 1u, pow2 = (lv.pow2 >> l) & 1u;
@@ -1055,9 +861,6 @@ __device__ __forceinline__ void coarse_scatter_level(const float in[3], bool val
     // corner c = cx | (cy<<1) | (cz<<2); weight product in tcnn's d order.
     // The four y/z corners are independent: their shuffles are issued
     // together (one LDS round trip per scan step, not four).
-    uint32_t idx[4];
-    float v[4];
-    uint64_t heads[4];
 #pragma unroll
     for (int yz = 0; yz < 4; ++yz) {
         const int cy = yz & 1, cz = yz >> 1;
@@ -1088,6 +891,14 @@ __device__ __forceinline__ void coarse_scatter_level(const float in[3], bool val
                 if (lane + o4 < 64 && (heads[yz] & span) == 0) v[yz] += ov[yz];
         }
     }
+}
+
+__device__ __forceinline__ void coarse_scatter_level(const float in[3], bool valid, float gd, int l, const LevelLds& lv,
+                                                     float* __restrict__ dst, int lane, int cx, int f) {
+    uint32_t idx[4];
+    float v[4];
+    uint64_t heads[4];
+    coarse_level_runs(in, valid, gd, l, lv, lane, cx, idx, v, heads);
 #pragma unroll
     for (int yz = 0; yz < 4; ++yz) {
         const bool head = (heads[yz] >> lane) & 1ull;
@@ -1379,37 +1190,17 @@ __device__ __forceinline__ void coop_dw(const _Float16* scr, int w, int s, int g
         if (t < n) acc[t] = part[t] * sc[t] + acc[t];
 }
 
-// The coarse (atomic) hash levels [0, hi) scattered by the MLP backward itself
-// (field_bwd_mlp_coop_kernel<true>): each wave adds its 16 samples' level
-// gradients straight from the registers that hold dL/denc, with
-// hash_bwd_kernel's arithmetic, run merging and replicas (coarse_scatter_level)
-// -- the atomics leave while the block's MFMA work goes on, instead of a launch
-// of their own beside the binned levels' record write.
-struct CoarseArgs {
-    const float* xyzs;
-    GridArgs ga;
-    float* grad;  // table gradient (entries x 2)
-    int hi;       // levels [0, hi)
-    float* rep;   // replicas of levels [0, rep_hi) (nullable)
-    int rep_hi;
-    uint32_t rep_stride;
-    int nrep;
-};
-
-template <bool COARSE>
 __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     const float* __restrict__ dirs, int64_t n, const int64_t* __restrict__ n_dev, const int32_t* __restrict__ sidx,
     const _Float16* __restrict__ enc, const _Float16* __restrict__ mlp, const float* __restrict__ dL_dsig,
-    const float* __restrict__ dL_drgb, float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride,
-    CoarseArgs ca) {
+    const float* __restrict__ dL_drgb, float* __restrict__ denc, float* __restrict__ grad_mlp, int64_t enc_pm_stride) {
     extern __shared__ __attribute__((aligned(16))) _Float16 smem[];
     // per-wave minima of the layers' per-sample exponents (double-buffered by iteration parity)
     __shared__ __attribute__((aligned(16))) int emin[2][5][CW];
-    __shared__ LevelLds lv;  // (COARSE)
-    float* const grep = COARSE && ca.rep ? ca.rep + (size_t)(blockIdx.x % ca.nrep) * ca.rep_stride : ca.grad;
     _Float16* sw = smem;
     _Float16* scr = smem + SCR;
     NGP_BWD_EDGE(0);
+    NGP_PROBE_BEGIN(NGP_P_MLP_BWD);
     const int64_t N = n_dev ? *n_dev : n;
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1423,10 +1214,6 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     struct In {
         h8 e;
         float dx, dy, dz, dsig, gr[3];
-        int32_t ii;  // (COARSE) the sample, -1 past the end
-        float px, py, pz;  // (COARSE) its position, loaded with the other inputs: a later load would
-                           // be younger than the previous iteration's atomics, and waiting for it would
-                           // wait for all of them (vmcnt counts in issue order)
     };
     // the sample of row jj (-1 past the end): listed rows' indices are loaded
     // two iterations ahead, so the dependent loads of the next iteration's
@@ -1448,14 +1235,6 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
             x.gr[0] = dL_drgb[3 * (int64_t)ii]; x.gr[1] = dL_drgb[3 * (int64_t)ii + 1];
             x.gr[2] = dL_drgb[3 * (int64_t)ii + 2];
         }
-        if constexpr (COARSE) {
-            x.ii = ii;
-            x.px = x.py = x.pz = 0.f;
-            if (ii >= 0) {
-                x.px = ca.xyzs[3 * (int64_t)ii]; x.py = ca.xyzs[3 * (int64_t)ii + 1];
-                x.pz = ca.xyzs[3 * (int64_t)ii + 2];
-            }
-        }
     };
     const int64_t stride = (int64_t)gridDim.x * CW * 16;
     const int64_t j0 = (int64_t)blockIdx.x * CW * 16 + 16 * wid + s;
@@ -1466,7 +1245,6 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     load_in(row_index(j0), cur);
     int32_t i_next = row_index(j0 + stride);
     load_bwd_weights_direct(mlp, sw);
-    if constexpr (COARSE) load_levels(ca.ga, lv);
     __syncthreads();
     NGP_BWD_EDGE(1);
     int par = 0;
@@ -1568,36 +1346,13 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         // ---- dL/denc = W1^T da1 (rows 16t + 4g + r of sample s), true units
         {
             const float r = ldexpf(1.0f, -E1);
-            f4 dco = z;  // (COARSE) rows 0-15: levels 0-7
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 f4 c = z;
 #pragma unroll
                 for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT1 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da1h[kt], c);
                 c = c * r;
-                if (t == 0) dco = c;
-                // (the coarse levels' rows are not stored when this kernel scatters them all)
-                if (valid && !(COARSE && t == 0 && ca.hi == 8)) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
-            }
-            if constexpr (COARSE) {
-                // lane = 4 s' + 2 cx + f takes sample s' = lane >> 2 (the wave's samples in row
-                // order, as hash_bwd_kernel groups them); dL/denc[s'][2 l + f] comes from lane
-                // (s', g = l >> 1), element 2 (l & 1) + f
-                const int sp = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1;
-                const int32_t isp = __shfl(cur.ii, sp, 64);
-                const bool vsp = isp >= 0;
-                const float xs[3] = {__shfl(cur.px, sp, 64), __shfl(cur.py, sp, 64), __shfl(cur.pz, sp, 64)};
-                float in[3];
-#pragma unroll
-                for (int d = 0; d < 3; ++d)  // load_x01's arithmetic (models/networks.py:104)
-                    in[d] = (xs[d] - ca.ga.g.xyz_min[d]) / (ca.ga.g.xyz_max[d] - ca.ga.g.xyz_min[d]);
-#pragma unroll 1
-                for (int l = 0; l < ca.hi; ++l) {
-                    const int src = 16 * (l >> 1) + sp;
-                    const float a = __shfl((l & 1) ? dco[2] : dco[0], src, 64);
-                    const float b = __shfl((l & 1) ? dco[3] : dco[1], src, 64);
-                    coarse_scatter_level(in, vsp, f ? b : a, l, lv, l < ca.rep_hi ? grep : ca.grad, lane, cx, f);
-                }
+                if (valid) *reinterpret_cast<f4*>(denc + j * 32 + 16 * t + 4 * g) = c;
             }
         }
         NGP_BWD_PHASE(2);
@@ -1687,6 +1442,7 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         atomicAdd(&grad_mlp[w], v);
     }
     NGP_BWD_EDGE(3);
+    NGP_PROBE_END();
 }
 
 
@@ -1717,6 +1473,7 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
     // the wave's 16 denc rows, staged once per iteration with coalesced 16-B
     // loads (one global round trip instead of one per level)
     __shared__ __attribute__((aligned(16))) float drow[4][16][36];
+    NGP_PROBE_BEGIN(NGP_P_HASH_BWD_COARSE);
     load_levels(ga, lv);
     __syncthreads();
     const int64_t N = n_dev ? *n_dev : n;
@@ -1747,9 +1504,132 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
         for (int l = lo; l < hi; ++l)
             coarse_scatter_level(in, valid, drow[wv][s][2 * l + f], l, lv, l < rep_hi ? grep : grad, lane, cx, f);
     }
+    NGP_PROBE_END();
 }
 
 constexpr unsigned HASH_BWD_BLOCKS = 8192;  // grid cap of hash_bwd_kernel (2048 measured slower)
+
+// The coarse levels' backward with the block's additions merged in LDS before
+// they leave the CU (SURVEY §7 step 5's LDS-privatised coarse accumulation).
+// hash_bwd_kernel merges runs of equal corners only inside a wave's 16
+// consecutive samples, so every wave instruction still sends ~6 memory-side
+// atomic requests per sample over levels 0-7 (one per 64-B line its run heads
+// touch): ~750 K requests per Lego step, which bound that kernel and slow the
+// record write beside it.  Here a block takes a tile of TW x 64 consecutive
+// gradient-carrying samples (wave w: TW groups of 16), computes the same run
+// heads, and adds each head's sum into an LDS table keyed by the 64-B line of
+// the gradient it belongs to (open addressing, CAS on the key, ds_add_f32 on
+// the line's 16 floats).  After the tile, the block flushes every line it
+// touched with one 16-lane add (one request per line): requests fall to the
+// distinct lines per tile -- 2.2-2.4x fewer on real Lego samples
+// (scripts/diag/coarse_requests.py on scripts/diag/active_dump.py's dump:
+// 874 K -> 367 K per step at 64-sample tiles of ... see DESIGN §6).
+// Lines of the replicated levels [0, rep_hi) go to this block's replica.
+// A head that finds no free slot in NS probes (table full) adds straight to
+// memory (still exact).  Addition order differs from hash_bwd_kernel's (fp32
+// sums in another order: atomic-order noise, as between two runs of either).
+constexpr uint32_t CT_EMPTY = 0xffffffffu;
+template <int NS>
+struct CoarseTable {
+    uint32_t key[NS];         // line index (float index >> 4) or CT_EMPTY
+    float val[NS * 16];       // the line's 16 floats
+    uint16_t used[NS];        // slots taken this tile, in taking order
+    uint32_t n_used;
+};
+template <int NS>
+__device__ __forceinline__ void table_add(CoarseTable<NS>& T, uint32_t fi, float v, float* __restrict__ gdst) {
+    const uint32_t key = fi >> 4;
+    uint32_t h = (key * 2654435761u) >> (32 - __builtin_ctz(NS));
+    for (int probe = 0; probe < 32; ++probe) {
+        uint32_t old = atomicCAS(&T.key[h], CT_EMPTY, key);
+        if (old == CT_EMPTY) {
+            T.used[atomicAdd(&T.n_used, 1u)] = (uint16_t)h;
+            old = key;
+        }
+        if (old == key) {
+            atomicAdd(&T.val[h * 16 + (fi & 15u)], v);
+            return;
+        }
+        h = (h + 1) & (NS - 1);
+    }
+    atomicAdd(gdst + fi, v);  // (table full around this key)
+}
+template <int NS, int TW>
+__global__ void __launch_bounds__(256) hash_bwd_lds_kernel(const float* __restrict__ xyzs, int64_t n,
+                                                           const int64_t* __restrict__ n_dev,
+                                                           const int32_t* __restrict__ sidx, GridArgs ga,
+                                                           const float* __restrict__ denc, float* __restrict__ grad,
+                                                           int lo, int hi, float* __restrict__ rep, int rep_hi,
+                                                           uint32_t rep_stride, int nrep) {
+    __shared__ LevelLds lv;
+    __shared__ __attribute__((aligned(16))) float drow[4][16][36];
+    __shared__ CoarseTable<NS> T;
+    NGP_PROBE_BEGIN(NGP_P_HASH_BWD_COARSE);
+    float* const grep = rep ? rep + (size_t)(blockIdx.x % nrep) * rep_stride : grad;
+    load_levels(ga, lv);
+    for (int i = threadIdx.x; i < NS; i += 256) T.key[i] = CT_EMPTY;
+    for (int i = threadIdx.x; i < NS * 16; i += 256) T.val[i] = 0.f;
+    if (threadIdx.x == 0) T.n_used = 0;
+    __syncthreads();
+    const uint32_t rep_fl = rep ? 2u * lv.off[rep_hi] : 0u;  // floats of the replicated levels
+    const int64_t N = n_dev ? *n_dev : n;
+    const int lane = threadIdx.x & 63, s = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1, wv = threadIdx.x >> 6;
+    const int64_t tiles = (N + 64 * TW - 1) / (64 * TW);
+    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+#pragma unroll 1
+        for (int it = 0; it < TW; ++it) {
+            const int64_t j = tile * (64 * TW) + (int64_t)(wv * TW + it) * 16 + s;  // compact position (denc row)
+            const bool valid = j < N;
+            const int64_t i = valid && sidx ? (int64_t)sidx[j] : j;
+            {
+                const int q = lane & 3;
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+                if (valid && 8 * q + 8 > 2 * lo && 8 * q < 2 * hi) {
+                    a = *reinterpret_cast<const float4*>(denc + j * 32 + 8 * q);
+                    b = *reinterpret_cast<const float4*>(denc + j * 32 + 8 * q + 4);
+                }
+                __builtin_amdgcn_wave_barrier();  // previous group's reads of drow are done (in order per wave)
+                *reinterpret_cast<float4*>(&drow[wv][s][8 * q]) = a;
+                *reinterpret_cast<float4*>(&drow[wv][s][8 * q + 4]) = b;
+            }
+            float in[3];
+            load_x01(xyzs, i, valid, ga, in);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+            for (int l = lo; l < hi; ++l) {
+                uint32_t idx[4];
+                float v[4];
+                uint64_t heads[4];
+                coarse_level_runs(in, valid, drow[wv][s][2 * l + f], l, lv, lane, cx, idx, v, heads);
+#pragma unroll
+                for (int yz = 0; yz < 4; ++yz)
+                    if (((heads[yz] >> lane) & 1ull) && valid) {
+                        const uint32_t fi = 2u * idx[yz] + f;
+                        table_add<NS>(T, fi, v[yz], fi < rep_fl ? grep : grad);
+                    }
+            }
+        }
+        __syncthreads();  // the tile's additions are in the table
+        // flush: 16 lanes per touched line, one memory-side request each
+        const uint32_t nu = T.n_used;
+        for (uint32_t u = threadIdx.x >> 4; u < nu; u += 16) {
+            const uint32_t h = T.used[u], key = T.key[h], e = threadIdx.x & 15u;
+            const float v = T.val[h * 16 + e];
+            const uint32_t fi = key * 16u + e;
+            if (v != 0.f) atomicAdd((fi < rep_fl ? grep : grad) + fi, v);
+            T.val[h * 16 + e] = 0.f;
+            if (e == 0) T.key[h] = CT_EMPTY;
+        }
+        __syncthreads();  // the table is clear
+        if (threadIdx.x == 0) T.n_used = 0;
+        // (the next tile's first additions follow the staging of its rows; the
+        // counter reset is ordered before them by the barrier below)
+        __syncthreads();
+    }
+    NGP_PROBE_END();
+}
 
 // grad[i] += sum_r rep[r][i]; rep[r][i] = 0 (i < n4 float4 groups), replicas
 // summed in order r = 0..nrep-1; all of a lane's loads are issued first
@@ -1774,24 +1654,23 @@ __global__ void __launch_bounds__(256) rep_reduce_kernel(float* __restrict__ gra
     }
 }
 
-template <bool COARSE>
 static int launch_bwd_mlp(const float* dirs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                           const void* enc_f16, int64_t enc_pm_stride, const void* mlp_f16, const float* dL_dsigmas,
-                          const float* dL_drgbs, float* denc_ws, float* grad_mlp, const CoarseArgs& ca, void* stream) {
+                          const float* dL_drgbs, float* denc_ws, float* grad_mlp, void* stream) {
     static bool attr_set = false;
     const size_t clds = (size_t)COOP_LDS_HALFS * sizeof(_Float16);
     if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)field_bwd_mlp_coop_kernel<COARSE>,
+        if (hipFuncSetAttribute((const void*)field_bwd_mlp_coop_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds) != hipSuccess)
             return NGP_ERANGE;
         attr_set = true;
     }
     hipStream_t s = as_stream(stream);
-    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel<COARSE>, 64 * CW, clds);
+    static const unsigned ccap = resident_blocks(field_bwd_mlp_coop_kernel, 64 * CW, clds);
     const unsigned cb = persistent_blocks(n, CW * 16, ccap);
-    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<COARSE><<<cb, 64 * CW, clds, s>>>(
+    NGP_TIMED(NGP_K_MLP_BWD, s, field_bwd_mlp_coop_kernel<<<cb, 64 * CW, clds, s>>>(
         dirs, n, n_dev, sample_idx, (const _Float16*)enc_f16, (const _Float16*)mlp_f16, dL_dsigmas, dL_drgbs, denc_ws,
-        grad_mlp, enc_pm_stride, ca));
+        grad_mlp, enc_pm_stride));
     return ngp_launch_status();
 }
 
@@ -1881,32 +1760,16 @@ int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const 
     NGP_CHECK_ARG(xyzs && table_f16 && mlp_f16 && sigmas && (dirs != nullptr) == (rgbs != nullptr));
     NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0);
     hipStream_t s = as_stream(stream);
-    // register form (default) or the LDS-parked form (NGP_FEM_LDS=1, A/B)
-    static const bool reg_form = !(getenv("NGP_FEM_LDS") && getenv("NGP_FEM_LDS")[0] == '1');
-    if (reg_form) {
-        // grid = every resident block (the chunks are dealt over the whole grid)
-        if (!dirs) {
-            static const unsigned capd = resident_blocks(field_encode_mlp_reg_kernel<false>, 64 * FEM2_WAVES, 0);
-            NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_reg_kernel<false><<<std::max(1u, std::min(capd, (unsigned)((n + 64 * FEM2_WAVES - 1) / (64 * FEM2_WAVES)))), 64 * FEM2_WAVES, 0, s>>>(
-                xyzs, nullptr, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16,
-                (_Float16*)enc_pm, sigmas, nullptr, (_Float16*)h_f16));
-            return ngp_launch_status();
-        }
-        static const unsigned capr = resident_blocks(field_encode_mlp_reg_kernel<true>, 64 * FEM2_WAVES, 0);
-        NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_reg_kernel<true><<<std::max(1u, std::min(capr, (unsigned)((n + 64 * FEM2_WAVES - 1) / (64 * FEM2_WAVES)))), 64 * FEM2_WAVES, 0, s>>>(
-            xyzs, dirs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16,
-            (_Float16*)enc_pm, sigmas, rgbs, (_Float16*)h_f16));
-        return ngp_launch_status();
-    }
+    // grid = every resident block (the chunks are dealt over the whole grid)
     if (!dirs) {
-        static const unsigned capd = resident_blocks(field_encode_mlp_kernel<false>, 64 * FEM_WAVES, 0);
-        NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_kernel<false><<<std::max(1u, std::min(capd, (unsigned)((n + 511) / 512))), 64 * FEM_WAVES, 0, s>>>(
+        static const unsigned capd = resident_blocks(field_encode_mlp_reg_kernel<false>, 64 * FEM2_WAVES, 0);
+        NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_reg_kernel<false><<<std::max(1u, std::min(capd, (unsigned)((n + 64 * FEM2_WAVES - 1) / (64 * FEM2_WAVES)))), 64 * FEM2_WAVES, 0, s>>>(
             xyzs, nullptr, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16,
             (_Float16*)enc_pm, sigmas, nullptr, (_Float16*)h_f16));
         return ngp_launch_status();
     }
-    static const unsigned cap = resident_blocks(field_encode_mlp_kernel<true>, 64 * FEM_WAVES, 0);
-    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_kernel<true><<<std::max(1u, std::min(cap, (unsigned)((n + 511) / 512))), 64 * FEM_WAVES, 0, s>>>(
+    static const unsigned capr = resident_blocks(field_encode_mlp_reg_kernel<true>, 64 * FEM2_WAVES, 0);
+    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_encode_mlp_reg_kernel<true><<<std::max(1u, std::min(capr, (unsigned)((n + 64 * FEM2_WAVES - 1) / (64 * FEM2_WAVES)))), 64 * FEM2_WAVES, 0, s>>>(
         xyzs, dirs, n, n_dev, sample_idx, ga, (const uint32_t*)table_f16, (const _Float16*)mlp_f16,
         (_Float16*)enc_pm, sigmas, rgbs, (_Float16*)h_f16));
     return ngp_launch_status();
@@ -1933,28 +1796,6 @@ int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* d
     NGP_TIMED(NGP_K_HASH_ENCODE, s, field_first_chunk_kernel<true><<<blocks, 64 * FEM2_WAVES, 0, s>>>(
         xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
         (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, list2, total2, evaluated));
-    return ngp_launch_status();
-}
-
-int ngp_field_forward_rows(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
-                           const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
-                           float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
-                           void* enc_pm, float* sigmas, float* rgbs, int64_t* evaluated, void* stream) {
-    GridArgs ga;
-    int st = grid_args(grid, ga);
-    if (st) return st;
-    NGP_CHECK_ARG(n_rows >= 0 && n >= 0 && n < (1ll << 50));
-    if (n_rows == 0) return NGP_OK;
-    NGP_CHECK_ARG(xyzs && dirs && deltas && rays_a && table_f16 && mlp_f16 && sigmas && rgbs);
-    NGP_CHECK_ARG(((uintptr_t)table_f16 & 15) == 0 && ((uintptr_t)mlp_f16 & 15) == 0 && ((uintptr_t)enc_pm & 7) == 0 &&
-                  ((uintptr_t)evaluated & 7) == 0);
-    hipStream_t s = as_stream(stream);
-    // grid = every resident block: the rows are dealt over all resident waves
-    static const unsigned cap = resident_blocks(field_rows_block_kernel<true>, 64 * FEM2_WAVES, 0);
-    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + FEM2_WAVES - 1) / FEM2_WAVES)));
-    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_rows_block_kernel<true><<<blocks, 64 * FEM2_WAVES, 0, s>>>(
-        xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
-        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, evaluated));
     return ngp_launch_status();
 }
 
@@ -1989,34 +1830,9 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
     if (n == 0) return NGP_OK;
     NGP_CHECK_ARG(dirs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp);
     NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
-    return launch_bwd_mlp<false>(dirs, n, n_dev, sample_idx, enc_f16, enc_pm_stride, mlp_f16, dL_dsigmas, dL_drgbs,
-                                 denc_ws, grad_mlp, CoarseArgs{}, stream);
+    return launch_bwd_mlp(dirs, n, n_dev, sample_idx, enc_f16, enc_pm_stride, mlp_f16, dL_dsigmas, dL_drgbs,
+                          denc_ws, grad_mlp, stream);
 }
-
-int ngp_field_backward_mlp_coarse(const float* dirs, const float* xyzs, int64_t n, const int64_t* n_dev,
-                                  const int32_t* sample_idx, const void* enc_f16, int64_t enc_pm_stride,
-                                  const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws,
-                                  float* grad_mlp, const ngp_hashgrid_t* grid, float* grad_table, int level_hi,
-                                  float* rep, int rep_levels, int n_rep, void* stream) {
-    CoarseArgs ca{};
-    int st = grid_args(grid, ca.ga);
-    if (st) return st;
-    NGP_CHECK_ARG(n >= 0 && 0 <= level_hi && level_hi <= L && 0 <= rep_levels && rep_levels <= level_hi);
-    if (n == 0) return NGP_OK;
-    NGP_CHECK_ARG(dirs && xyzs && enc_f16 && mlp_f16 && dL_dsigmas && dL_drgbs && denc_ws && grad_mlp && grad_table);
-    NGP_CHECK_ARG(((uintptr_t)mlp_f16 & 15) == 0);
-    if (rep && rep_levels > 0) NGP_CHECK_ARG(n_rep >= 1 && n_rep <= 64 && ((uintptr_t)rep & 15) == 0);
-    ca.xyzs = xyzs;
-    ca.grad = grad_table;
-    ca.hi = level_hi;
-    ca.rep = rep_levels > 0 ? rep : nullptr;
-    ca.rep_hi = ca.rep ? rep_levels : 0;
-    ca.rep_stride = 2u * grid->offsets[rep_levels];
-    ca.nrep = ca.rep ? n_rep : 1;
-    return launch_bwd_mlp<true>(dirs, n, n_dev, sample_idx, enc_f16, enc_pm_stride, mlp_f16, dL_dsigmas, dL_drgbs,
-                                denc_ws, grad_mlp, ca, stream);
-}
-
 
 int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                       const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* stream) {
@@ -2031,6 +1847,44 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
     return ngp_launch_status();
 }
 
+}  // extern "C"
+
+// the coarse levels' scatter: the LDS-merged kernel (NGP_COARSE_LDS=1: 64-sample tiles, 512-line
+// tables; 2: 128-sample tiles, 1024-line tables) or the wave-merged one (0)
+static int g_coarse_mode = -1;  // (ngp_hash_backward_coarse_mode; -1: NGP_COARSE_LDS or the default)
+static int coarse_mode() {
+    if (g_coarse_mode < 0) g_coarse_mode = getenv("NGP_COARSE_LDS") ? atoi(getenv("NGP_COARSE_LDS")) : 1;
+    return g_coarse_mode;
+}
+static void launch_coarse(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
+                          const GridArgs& ga, const float* denc, float* grad_table, int lo, int hi, float* rep,
+                          int rep_hi, uint32_t rep_stride, int nrep, hipStream_t s) {
+    const int mode = coarse_mode();
+    if (mode == 1) {
+        static const unsigned cap = resident_blocks(hash_bwd_lds_kernel<512, 1>, 256, 0);
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_lds_kernel<512, 1><<<persistent_blocks(n, 64, cap), 256, 0, s>>>(
+            xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
+    } else if (mode == 2) {
+        static const unsigned cap = resident_blocks(hash_bwd_lds_kernel<1024, 2>, 256, 0);
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_lds_kernel<1024, 2><<<persistent_blocks(n, 128, cap), 256, 0, s>>>(
+            xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
+    } else {
+        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<persistent_blocks(n, 64, HASH_BWD_BLOCKS), 256, 0, s>>>(
+            xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
+    }
+}
+
+extern "C" {
+
+int ngp_hash_backward_coarse_mode(int mode) {
+    const int prev = coarse_mode();
+    if (mode >= 0) {
+        if (mode > 2) return NGP_EINVAL;
+        g_coarse_mode = mode;
+    }
+    return prev;
+}
+
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
                              int level_hi, void* stream) {
@@ -2040,10 +1894,8 @@ int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev,
     NGP_CHECK_ARG(n >= 0 && 0 <= level_lo && level_lo <= level_hi && level_hi <= L);
     if (n == 0 || level_lo == level_hi) return NGP_OK;
     NGP_CHECK_ARG(xyzs && denc && grad_table && ((uintptr_t)denc & 15) == 0);
-    const unsigned blocks = persistent_blocks(n, 64, HASH_BWD_BLOCKS);
-    hipStream_t s = as_stream(stream);
-    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc,
-                                                                           grad_table, level_lo, level_hi));
+    launch_coarse(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi, nullptr, 0, 0, 1,
+                  as_stream(stream));
     return ngp_launch_status();
 }
 
@@ -2064,9 +1916,8 @@ int ngp_hash_backward_levels_rep(const float* xyzs, int64_t n, const int64_t* n_
     // replicas cover table entries [0, offsets[rep_levels]) (x 2 features)
     const uint32_t nfl = 2u * grid->offsets[rep_levels];
     NGP_CHECK_ARG(nfl % 4 == 0);
-    const unsigned blocks = persistent_blocks(n, 64, HASH_BWD_BLOCKS);
     hipStream_t s = as_stream(stream);
-    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<blocks, 256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi, rep, rep_levels, nfl, n_rep));
+    launch_coarse(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, level_lo, level_hi, rep, rep_levels, nfl, n_rep, s);
     if (!fold) return ngp_launch_status();  // the caller folds them (ngp_adam_step_dev_rep)
     const uint32_t n4 = nfl / 4;
     const unsigned rb = std::min(2048u, (n4 + 255) / 256);

@@ -183,6 +183,7 @@ __global__ void __launch_bounds__(256) hash_count_kernel(const float* __restrict
                                                          BinWs ws) {
     __shared__ LevelLds lv;
     __shared__ uint32_t cnt[NSLOT];
+    NGP_PROBE_BEGIN(NGP_P_HASH_COUNT);
     load_levels(ga, lv);
     const int64_t N = n_dev ? *n_dev : n;
     const int64_t ntiles = min((N + TILE - 1) / TILE, ba.tiles_cap);
@@ -218,6 +219,7 @@ __global__ void __launch_bounds__(256) hash_count_kernel(const float* __restrict
         for (int i = t; i < NSLOT; i += 256) ws.ofs[(size_t)i * ba.tiles_cap + tile] = cnt[i];
         __syncthreads();
     }
+    NGP_PROBE_END();
 }
 
 // one workgroup per (level, bucket) slot: exclusive prefix over tiles in place
@@ -299,6 +301,7 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
     // does not wait at every level for the block's slowest wave
     uint32_t* const hall = reinterpret_cast<uint32_t*>(stage);
     static_assert(sizeof(stage) >= NSLOT * sizeof(uint32_t), "stage[] holds the per-level counters");
+    NGP_PROBE_BEGIN(NGP_P_HASH_WRITE);
     load_levels(ga, lv);
     const int64_t N = n_dev ? *n_dev : n;
     const int64_t ntiles = (N + TILE - 1) / TILE;
@@ -451,6 +454,7 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
         }
         __syncthreads();
     }
+    NGP_PROBE_END();
 }
 
 // A bucket whose summed gradient one workgroup owns: a single chunk, no
@@ -502,6 +506,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
                                                           uint32_t b_lo, uint32_t b_hi) {
     // buckets [b_lo, b_hi) (a level range; all buckets: 0, nbt)
     extern __shared__ __attribute__((aligned(16))) double img[];  // [2][BENT]: feature-major, 8-byte stride
+    NGP_PROBE_BEGIN(NGP_P_HASH_ACCUM);
     const uint32_t total = ws.items[b_hi];
     const int t = threadIdx.x, lane = t & 63;
     const bool overflow = ws.fb[MAXB] != 0;
@@ -679,20 +684,18 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
             }
         }
     }
+    NGP_PROBE_END();
 }
 
 // Adam (+ gradient zeroing) of the binned buckets the fused accumulation did
 // not step: one workgroup per bucket, from the gradient in memory.
 __global__ void __launch_bounds__(256) hash_adam_residual_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
                                                                   float* __restrict__ grad, BinWs ws, AdamArgs adam,
-                                                                  uint32_t b_lo, StepTicket ticket) {
+                                                                  uint32_t b_lo) {
     const uint32_t b = b_lo + blockIdx.x;
     const bool mine = b < nbt && !fused_bucket(ws, b, ws.fb[MAXB] != 0);  // (block-uniform)
     float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
     if (mine) adam_bias(adam.lr_dev, adam.step_dev, adam.b1, adam.b2, lr, bc1, bc2);
-    // (after the block's counter reads -- and the accumulation launch before it is done reading
-    // too -- not after its stores, which the arrival's vmcnt(0) would wait for)
-    step_ticket_arrive(ticket);
     if (mine) {
         const uint32_t l = bucket_level(ba, b), lb = b - ba.bbase[l];
         const uint32_t ne = min((uint32_t)BENT, ga.g.sizes[l] - (lb << BSHIFT));
@@ -791,8 +794,7 @@ static int hash_binned(const float* xyzs, int64_t n, const int64_t* n_dev, const
         if (adam) {
             NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<true><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, *adam, b_lo, b_hi));
             if (b_hi > b_lo)
-                NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<b_hi - b_lo, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam, b_lo,
-                                                                                             ngp_step_ticket_next()));
+                NGP_TIMED(NGP_K_ADAM, s, hash_adam_residual_kernel<<<b_hi - b_lo, 256, 0, s>>>(ga, ba, nbt, grad_table, ws, *adam, b_lo));
         } else {
             NGP_TIMED(NGP_K_HASH_ACCUM, s, hash_accum_kernel<false><<<capB, ACC_T, lds, s>>>(ga, ba, nbt, grad_table, ws, AdamArgs{}, b_lo, b_hi));
         }

@@ -29,33 +29,20 @@ void ngp_timing_mark(int id, int end, hipStream_t s) {
                                   ((int64_t)id * g_per + i) * 2 + (end ? 1 : 0));
 }
 
-static ngp::StepTicket g_ticket{nullptr, nullptr, 0, 0, 0};
-static int g_ticket_next = 0;
+// device probes: every translation unit registers the setter of its copy of
+// the control symbol (common.h) at load time
+static void (*g_probe_setters[16])(const ProbeCtl&);
+static int g_n_probe_setters = 0;
+void ngp_probe_register(void (*set)(const ProbeCtl&)) {
+    if (g_n_probe_setters < 16) g_probe_setters[g_n_probe_setters++] = set;
+}
 
-ngp::StepTicket ngp::ngp_step_ticket_next() {
-    if (!g_ticket.ws) return StepTicket{nullptr, nullptr, 0, 0, 0};
-    StepTicket t = g_ticket;
-    t.party = g_ticket_next++;
-    if (t.party >= t.parties) t.ws = nullptr;  // (more launches than declared: checked by the setter's caller)
-    return t;
+// a kernel whose only purpose is its name in a dispatch trace (ngp_trace_marker)
+__global__ void trace_marker_kernel(int tag) {
+    if (tag < 0) __builtin_trap();  // (never: keeps the argument live)
 }
 
 extern "C" {
-
-int ngp_step_ticket_set(void* ws, int64_t* counters, int n_counters, int parties) {
-    if (ws && (!counters || n_counters < 1 || n_counters > 8 || parties < 1 || parties > 8 ||
-               ((uintptr_t)ws & 3) != 0))
-        return NGP_EINVAL;
-    const int used = g_ticket_next;
-    const bool was = g_ticket.ws != nullptr;
-    const int declared = g_ticket.parties;
-    g_ticket = ngp::StepTicket{(uint32_t*)ws, ws ? counters : nullptr, ws ? n_counters : 0, ws ? parties : 0, 0};
-    g_ticket_next = 0;
-    // clearing after a capture: exactly `parties` launches must have taken a ticket
-    return (was && !ws && used != declared) ? NGP_ERANGE : NGP_OK;
-}
-
-size_t ngp_step_ticket_workspace(void) { return 64; }
 
 const char* ngp_version(void) { return "ngp_amd 0.2 gfx950"; }
 
@@ -71,6 +58,22 @@ int ngp_timing_set(uint64_t* stamps, const int64_t* step_dev, int64_t ring, int 
     g_end = end_mask;
     for (int i = 0; i < 64; ++i) g_count[i] = 0;
     return NGP_OK;
+}
+
+int ngp_probe_set(uint64_t* buf, const int64_t* step_dev, int64_t ring) {
+    if (buf && (!step_dev || ring < 1)) return NGP_EINVAL;
+    const ProbeCtl c{(unsigned long long*)buf, buf ? step_dev : nullptr, buf ? ring : 0};
+    for (int i = 0; i < g_n_probe_setters; ++i) g_probe_setters[i](c);
+    const hipError_t e = hipDeviceSynchronize();
+    return e == hipSuccess ? NGP_OK : (int)e;
+}
+
+int ngp_probe_count(void) { return NGP_P_COUNT; }
+
+int ngp_trace_marker(int tag, void* stream) {
+    NGP_CHECK_ARG(tag >= 0);
+    trace_marker_kernel<<<1, 64, 0, as_stream(stream)>>>(tag);
+    return ngp_launch_status();
 }
 
 int ngp_timing_counts(int32_t* counts, int n_ids) {

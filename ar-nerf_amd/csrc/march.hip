@@ -403,6 +403,7 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
     extern __shared__ uint32_t ssum[];
     __shared__ LatSeg segs[4];
     WordCache wc;
+    NGP_PROBE_BEGIN(NGP_P_MARCH);
     wc.sum = load_summary(p, ssum);
     wc.dil = wc.sum ? wc.sum + p.n_sum32 : nullptr;
     __syncthreads();
@@ -525,6 +526,7 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
         }
         if (lane == 0) counts[r] = N;
     }
+    NGP_PROBE_END();
 }
 
 // Dense ray-ordered outputs from the slots: one wave per ray, lanes over the

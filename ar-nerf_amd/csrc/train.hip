@@ -335,6 +335,7 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
     __shared__ unsigned long long blk[3];
     __shared__ int64_t s_na[4];
     __shared__ unsigned long long s_base;
+    NGP_PROBE_BEGIN(NGP_P_COMPOSITE);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x < 3) blk[threadIdx.x] = 0;
     __syncthreads();
@@ -386,6 +387,7 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
             }
         }
     }
+    NGP_PROBE_END();
 }
 
 // ------------------------------------------------------------------ Adam
@@ -404,12 +406,9 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    float grad_scale, int zero_grad, const float* __restrict__ lr_dev,
                                                    const int64_t* __restrict__ step_dev, float* __restrict__ rep = nullptr,
                                                    int64_t rep_lo4 = 0, int64_t rep4 = 0, int nrep = 0,
-                                                   StepTicket ticket = StepTicket{nullptr, nullptr, 0, 0, 0},
                                                    float* __restrict__ zero = nullptr, int64_t zero4 = 0) {
+    NGP_PROBE_BEGIN(NGP_P_ADAM);
     adam_bias(lr_dev, step_dev, b1, b2, lr, bc1, bc2);
-    // (the block's counter reads are done: it arrives now, not after its stores, which the
-    // arrival's vmcnt(0) would otherwise wait for)
-    step_ticket_arrive(ticket);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         float4 P = reinterpret_cast<float4*>(p)[i], Gd = reinterpret_cast<float4*>(grad)[i];
@@ -452,6 +451,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
     // (ngp_adam_step_dev_zero) a second range cleared by the same launch
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < zero4; i += stride)
         reinterpret_cast<float4*>(zero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    NGP_PROBE_END();
 }
 
 // --------------------------------------------------- occupancy grid update
@@ -1298,7 +1298,7 @@ int ngp_adam_step_dev(float* params, float* grads, float* exp_avg, float* exp_av
     NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
                                                                  1.f, grad_scale, zero_grad, lr_dev, step_dev, nullptr, 0,
-                                                                 0, 0, ngp_step_ticket_next()));
+                                                                 0, 0));
     return ngp_launch_status();
 }
 
@@ -1316,7 +1316,7 @@ int ngp_adam_step_dev_zero(float* params, float* grads, float* exp_avg, float* e
     NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
                                                                  1.f, grad_scale, zero_grad, lr_dev, step_dev, nullptr, 0,
-                                                                 0, 0, StepTicket{nullptr, nullptr, 0, 0, 0}, zero, z4));
+                                                                 0, 0, zero, z4));
     return ngp_launch_status();
 }
 
@@ -1337,7 +1337,7 @@ int ngp_adam_step_dev_rep(float* params, float* grads, float* exp_avg, float* ex
     NGP_TIMED(NGP_K_ADAM, as_stream(stream), adam_kernel<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(params, grads, exp_avg, exp_avg_sq,
                                                                  (_Float16*)params_f16, n4, 0.f, beta1, beta2, eps, 1.f,
                                                                  1.f, grad_scale, zero_grad, lr_dev, step_dev, rep,
-                                                                 rep_offset / 4, rep_n / 4, n_rep, ngp_step_ticket_next()));
+                                                                 rep_offset / 4, rep_n / 4, n_rep));
     return ngp_launch_status();
 }
 

@@ -6,8 +6,8 @@ batches (train.py:288): gradients all-reduced every step, buffers broadcast
 from rank 0 every forward (SURVEY.md §2 "Collective call sites").  Here:
   * ZeRO-1 over the flat parameter vector: the fp32 gradient is
     reduce-scattered (SUM) in 1 + K buckets -- [MLP | coarse hash levels],
-    then the binned levels in K level ranges (level_cuts, K = 4 by
-    default) -- each rank
+    then the binned levels in K level ranges (level_cuts; K =
+    the trainer's dp_fine_buckets, 2 by default) -- each rank
     runs FusedAdam on its 1/world shard of every bucket only (fp32 master,
     moments; the 1/world mean is folded into Adam), and the updated fp16
     shadow the kernels read is all-gathered; a bucket's reduce-scatter, Adam
@@ -29,6 +29,17 @@ host memory.
 """
 import torch
 import torch.distributed as dist
+
+
+# (tests) run the collectives through the process group even at world size 1 -- a world-1
+# RCCL group then executes the real reduce_scatter_tensor / all_gather_into_tensor calls
+# of the data-parallel step (tests/test_ddp_gpu.py), not the world-1 copies
+FORCE_COLLECTIVES = False
+
+
+def comm_active(group=None):
+    """True when the collectives below go through the process group."""
+    return world_info(group)[1] > 1 or (FORCE_COLLECTIVES and dist.is_available() and dist.is_initialized())
 
 
 def world_info(group=None):
@@ -76,7 +87,7 @@ def _gloo(group):
 
 def reduce_scatter_(full, out, group=None):
     """out (len/world) = this rank's shard of SUM over ranks of full (len)."""
-    if world_info(group)[1] == 1:
+    if not comm_active(group):
         out.copy_(full)
         return out
     if _gloo(group) and full.is_cuda:
@@ -90,7 +101,7 @@ def reduce_scatter_(full, out, group=None):
 
 def all_gather_(full, shard, group=None):
     """full (len) = concatenation over ranks of shard (len/world)."""
-    if world_info(group)[1] == 1:
+    if not comm_active(group):
         full.copy_(shard)
         return full
     if _gloo(group) and full.is_cuda:

@@ -45,14 +45,10 @@ def _lib():
         L.ngp_density_input_grad.argtypes = [vp, c_int64, P, vp, vp, vp, vp, vp]
         L.ngp_field_backward.argtypes = [vp, vp, c_int64, vp, P, vp, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_backward_mlp.argtypes = [vp, c_int64, vp, vp, vp, c_int64, vp, vp, vp, vp, vp, vp]
-        L.ngp_field_backward_mlp_coarse.argtypes = [vp, vp, c_int64, vp, vp, vp, c_int64, vp, vp, vp, vp, vp, P, vp,
-                                                    c_int, vp, c_int, c_int, vp]
         L.ngp_hash_encode.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
         L.ngp_field_forward_indexed.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp]
         L.ngp_field_mlp_forward.argtypes = [vp, vp, c_int64, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_encode_mlp.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp, vp]
-        L.ngp_field_forward_rows.argtypes = [vp, vp, vp, vp, vp, vp, c_int64, c_int64, c_float, P, vp, vp, vp, vp, vp, vp,
-                                             vp]
         L.ngp_field_forward_first.argtypes = [vp, vp, vp, vp, vp, vp, c_int64, c_int64, c_float, P, vp, vp, vp, vp, vp,
                                               vp, vp, vp, vp, vp]
         L.ngp_hash_backward.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
@@ -60,6 +56,8 @@ def _lib():
         L.ngp_hash_backward_levels.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp]
         L.ngp_hash_backward_levels_rep.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp, c_int, c_int, c_int,
                                                    vp]
+        L.ngp_hash_backward_coarse_mode.argtypes = [c_int]
+        L.ngp_hash_backward_coarse_mode.restype = c_int
         L.ngp_hash_backward_rep_floats.argtypes = [P, c_int, c_int]
         L.ngp_hash_backward_rep_floats.restype = ctypes.c_size_t
         L.ngp_hash_binned_plan.argtypes = [vp, c_int64, vp, vp, P, vp, c_int64, c_int, c_int, vp]
@@ -74,7 +72,6 @@ def _lib():
         L.ngp_hash_backward_binned_workspace.argtypes = [c_int64]
         L.ngp_hash_backward_binned_workspace.restype = ctypes.c_size_t
         for f in (L.ngp_field_forward, L.ngp_density_forward, L.ngp_density_input_grad, L.ngp_field_backward, L.ngp_field_backward_mlp,
-                  L.ngp_field_backward_mlp_coarse,
                   L.ngp_hash_encode, L.ngp_field_mlp_forward, L.ngp_field_forward_indexed, L.ngp_field_encode_mlp,
                   L.ngp_hash_backward, L.ngp_hash_backward_binned, L.ngp_hash_backward_levels,
                   L.ngp_hash_backward_levels_rep,

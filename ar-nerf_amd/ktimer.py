@@ -119,3 +119,61 @@ class KernelTimer:
         """{kernel: (avg ms per launch, launches per step)} over the steps recorded"""
         n = max(1, self.steps())
         return {k: (sum(v) / len(v), len(v) / n) for k, v in self.read().items()}
+
+
+# include/ngp_amd.h NGP_P_* order
+PROBES = ["march", "first_chunk", "field_encode_mlp", "composite_loss", "mlp_bwd", "hash_bwd_coarse", "hash_count",
+          "hash_write", "hash_accum", "adam"]
+
+
+class ProbeTimer:
+    """Execution spans of the probed kernels (ngp_probe_set: lane 0 of each
+    wave of a probed kernel stores its start and end time into its own slot
+    of a row chosen by the device step counter; the span = min start .. max
+    end).  No graph node is added, so the graphs already captured replay
+    unchanged with the probes on: the spans are those of the product step,
+    comparable launch for launch with a rocprofv3 kernel trace of the same
+    replays.  rows: steps kept (row = step % rows: a window longer than rows
+    keeps its last `rows` steps).  Usage: arm(); run steps; disarm();
+    summary(skip_rows=...)."""
+
+    WAVES = 65536  # NGP_PROBE_WAVES
+
+    def __init__(self, step_counter, rows=32, device="cuda"):
+        assert _lib().ngp_probe_count() == len(PROBES)
+        self.step = step_counter
+        self.rows = rows
+        self.buf = torch.zeros(rows, len(PROBES), self.WAVES, 2, dtype=torch.int64, device=device)
+        self.tick_ns = _lib().ngp_timing_tick_ns()
+
+    def reset(self):
+        self.buf.zero_()
+
+    def arm(self):
+        torch.cuda.synchronize()
+        self.reset()
+        vren._ok(_lib().ngp_probe_set(self.buf.data_ptr(), self.step.data_ptr(), self.rows), "probe_set")
+
+    def disarm(self):
+        torch.cuda.synchronize()
+        vren._ok(_lib().ngp_probe_set(None, None, 0), "probe_set")
+
+    def spans(self, skip_rows=()):
+        """{probe: [(row, ms), ...]} for every row where the probe ran, rows in skip_rows excluded"""
+        b = self.buf
+        big = torch.iinfo(torch.int64).max
+        st = torch.where(b[..., 0] > 0, b[..., 0], torch.full_like(b[..., 0], big)).min(-1).values.cpu()
+        en = b[..., 1].max(-1).values.cpu()
+        ok = (en > 0) & (st < big) & (en >= st)
+        ms = (en - st).double() * self.tick_ns * 1e-6
+        skip = set(skip_rows)
+        out = {}
+        for k, n in enumerate(PROBES):
+            rows = [r for r in torch.nonzero(ok[:, k]).flatten().tolist() if r not in skip]
+            if rows:
+                out[n] = [(r, float(ms[r, k])) for r in rows]
+        return out
+
+    def summary(self, skip_rows=()):
+        """{probe: (avg ms per launch, launches counted)}"""
+        return {k: (sum(m for _, m in v) / len(v), len(v)) for k, v in self.spans(skip_rows).items()}

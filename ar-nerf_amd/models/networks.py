@@ -67,6 +67,8 @@ class NGP(nn.Module):
         self.grid = HG.HashGrid(scale, L, log2_T, N_min, float(b))
         self.params = nn.Parameter(HG.init_params(self.grid, seed=seed, device="cpu"))
         self._shadow = HG.FP16Shadow(self.params)
+        # optimizers.FusedAdam writes this shadow in its Adam launch (no re-cast before the next forward)
+        self.params._ngp_shadow = self._shadow
 
     # -------------------------------------------------- tcnn param mapping
     def tcnn_params(self):

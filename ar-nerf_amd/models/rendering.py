@@ -35,6 +35,11 @@ def render(model, rays_o, rays_d, **kwargs):
     return results
 
 
+# BASELINE.json's north_star names the drop-in surface models.rendering.render_rays;
+# the reference module's entry point is render() (rendering.py:13), so both names bind it
+render_rays = render
+
+
 def _background(kwargs, rays_d, default):
     if kwargs.get('SH_bkg', None) is not None:
         raise NotImplementedError("SH_bkg belongs to the AR-insertion app (insert/), out of scope")

@@ -212,10 +212,10 @@ class NGPTrainer:
         # row forward (NGP_ROW_FWD=1, the default since round 4: +2 %, 9 of 9 alternating pairs,
         # profiles/r04/ab/row_forward_variants.txt): round 1 one wave per non-empty row with the
         # row's transmittance in its epilogue, which appends the row's round-2 samples to the
-        # round-2 list itself (ngp_field_forward_first: no list launch); NGP_ROW_FWD=2: both
-        # rounds in one launch, each workgroup queueing its rows' round-2 chunks in LDS for its
-        # own waves (ngp_field_forward_rows); 0: the two-round lists below
+        # round-2 list itself (ngp_field_forward_first: no list launch); NGP_ROW_FWD=0: the
+        # two-round lists below
         self.row_forward = int(os.environ.get("NGP_ROW_FWD", "1"))
+        assert self.row_forward in (0, 1)
         # where the next batch's march forks off the step: after the row forward's round 1 on the
         # single-cascade (Lego-shaped) scenes (round 1 runs alone, the march beside round 2 /
         # composite / MLP backward: +2.1 %, 6 of 6 pairs, profiles/r04/ab/march_fork_position.txt);
@@ -274,23 +274,9 @@ class NGPTrainer:
         # device step counters: [0] Adam steps taken, [1] batches drawn (RNG
         # counter), [2] device-sampled occupancy updates (their RNG counter)
         self.dctr = torch.zeros(3, dtype=torch.int64, device=dev)
-        # (opt-in, NGP_STEP_TICKET=1) steady-state graphs of the fused single-process step: the
-        # step's two Adam launches (MLP + coarse levels on the side stream, the binned levels'
-        # residual Adam on the main stream) advance dctr[0:2] themselves through a completion
-        # ticket (ngp_step_ticket_set) instead of an increment launch joining the step's streams
-        # -- measured 2-4 % slower: the next forward then waits on three queues directly and the
-        # side Adam on the march queue (cross-queue edges cost ~13 us each inside a replayed
-        # graph, scripts/diag/graph_split_cost.py; profiles/r04/ab/ab_r4d.txt)
-        self._ticket_ws = torch.zeros((vren.lib().ngp_step_ticket_workspace() + 3) // 4, dtype=torch.int32,
-                                      device=dev)
-        self.step_ticket = os.environ.get("NGP_STEP_TICKET", "0") == "1"
-        self._ticket_active = False
-        # (opt-in, NGP_FUSED_COARSE=1) single-process hybrid steps: the coarse (atomic) hash levels
-        # scattered by the MLP backward launch itself (ngp_field_backward_mlp_coarse) instead of a
-        # launch of their own beside the binned levels' record write -- measured 4 % slower end to
-        # end (the MLP backward 60 -> 135-147 us: its waves stall behind their outstanding atomics;
-        # profiles/r04/ab/ab_r4b.txt)
-        self.fused_coarse = os.environ.get("NGP_FUSED_COARSE", "0") == "1"
+        # (Measured and removed in round 5's clean-up, DESIGN.md §9: a completion ticket by which
+        # the step's Adam launches advanced dctr themselves, -2..-4 %; the coarse levels scattered
+        # by the MLP backward launch, -4 %.)
         self._updated_for = -1  # global step whose occupancy update already ran (end of the previous graph)
         self.lr_dev = torch.full((1,), float(lr), device=dev)
         self._lr_set = float(lr)
@@ -669,6 +655,10 @@ class NGPTrainer:
                 comm.wait_stream(self.bwd_stream)
                 self._bucket_update(0)
                 nr = len(self.bin_cuts) - 1
+                if nr <= 0:  # every level atomic (bin_level_lo == n_levels): the buckets past the
+                    # alignment cut hold the last params, complete once the coarse segment is
+                    for j in range(1, len(self.buckets)):
+                        self._bucket_update(j)
                 for r in range(nr):
                     self._run_graph(key + ("apply", r), lambda r=r: self._segment_apply(r))
                     comm.wait_stream(cs)
@@ -803,12 +793,13 @@ class NGPTrainer:
         h = self._bucket_host()[i]
         cs = self.comm_stream
         with torch.cuda.stream(cs):
-            if self.world == 1:  # (emulation: this rank's shard of the local gradient)
+            comm = ddp.comm_active(self.pg)
+            if not comm:  # (emulation: this rank's shard of the local gradient)
                 h["shard"].copy_(h["src"])
             else:
                 ddp.reduce_scatter_(h["full"], h["shard"], self.pg)
             self._adam_shard(i, HG.c_void_p(cs.cuda_stream), zero=True)
-            if self.world > 1:
+            if comm:
                 ddp.all_gather_(h["p16full"], h["p16shard"], self.pg)
 
     def _bucket_host(self):
@@ -828,22 +819,15 @@ class NGPTrainer:
 
     def _rs(self, i):
         (a, b), (lo, hi), gs = self.buckets[i], self.shards[i], self._gshard[i]
-        if self.world == 1:  # (emulation: this rank's shard of the local gradient)
+        if not ddp.comm_active(self.pg):  # (emulation: this rank's shard of the local gradient)
             gs.copy_(self._gbuf[lo:hi])
         else:
             ddp.reduce_scatter_(self._gbuf[a:b], gs, self.pg)
 
     def _ag(self, i):
         (a, b), (lo, hi) = self.buckets[i], self.shards[i]
-        if self.world > 1:  # (emulation: the shard's shadow is in place already)
+        if ddp.comm_active(self.pg):  # (emulation: the shard's shadow is in place already)
             ddp.all_gather_(self._p16buf[a:b], self._p16buf[lo:hi], self.pg)
-
-    def _ticket_ok(self):
-        """The step's counters advanced by its two Adam launches (fused
-        single-process hybrid step, no measurement stamps, which index their
-        rows by the counter)."""
-        return (self.step_ticket and self.fused_adam and not self.dp and self.hash_backward != "atomic"
-                and self.timer is None)
 
     def _graph_body(self, k, gt, directions, poses, update_after=False):
         self.cur = k
@@ -854,16 +838,6 @@ class NGPTrainer:
                 self.march_stream.wait_stream(cs)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
 
-            if self._ticket_ok():
-                vren._ok(self.L.ngp_step_ticket_set(_p(self._ticket_ws), _p(self.dctr), 2, 2), "step_ticket")
-                self._ticket_active = True
-                try:
-                    self._compute(self.rgb_gt, True, fork)
-                finally:
-                    self._ticket_active = False
-                    vren._ok(self.L.ngp_step_ticket_set(None, None, 0, 0), "step_ticket (launches != parties)")
-                cs.wait_stream(self.march_stream)
-                return
             self._compute(self.rgb_gt, True, fork)
             cs.wait_stream(self.march_stream)
             vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
@@ -922,24 +896,16 @@ class NGPTrainer:
             # deciding the row's round 2, whose samples it appends to the round-2 list itself (no
             # list pass); round 2: the field over that list
             self._ev("hash_encode", 0)
-            if self.row_forward == 2:  # both rounds, one launch (per-workgroup LDS queues)
-                vren._ok(HGL.ngp_field_forward_rows(
-                    _p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a), _p(self.rows_ne),
-                    _p(self.n_rows_ne), R, self.cap, ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
-                    _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc), _p(self.sigmas),
-                    _p(self.rgbs), _p(self.eval_stats), s), "field_forward_rows")
-                self._ev("hash_encode", 1)
-            else:
-                vren._ok(HGL.ngp_field_forward_first(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a),
-                                                     _p(self.rows_ne), _p(self.n_rows_ne), R, self.cap,
-                                                     ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
-                                                     _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc),
-                                                     _p(self.sigmas), _p(self.rgbs), None, _p(self.eval_idx),
-                                                     _p(self.eval_total2), _p(self.eval_stats), s), "field_forward_first")
-                self._ev("hash_encode", 1)
-                if fork is not None and at == "r1":
-                    fork()
-                self._field_indexed(s, self.eval_idx, self.eval_total2)
+            vren._ok(HGL.ngp_field_forward_first(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a),
+                                                 _p(self.rows_ne), _p(self.n_rows_ne), R, self.cap,
+                                                 ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
+                                                 _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16), _p(self.enc),
+                                                 _p(self.sigmas), _p(self.rgbs), None, _p(self.eval_idx),
+                                                 _p(self.eval_total2), _p(self.eval_stats), s), "field_forward_first")
+            self._ev("hash_encode", 1)
+            if fork is not None and at == "r1":
+                fork()
+            self._field_indexed(s, self.eval_idx, self.eval_total2)
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
             if self.eval1_K == K:  # built by this batch's march
@@ -1003,20 +969,9 @@ class NGPTrainer:
                 planned = torch.cuda.Event()
                 planned.record(bs)
         self._ev("mlp_bwd", 0)
-        # the coarse levels inside the MLP backward: single-process hybrid steps with Adam, whose
-        # coarse Adam folds the gradient replicas (otherwise the separate launch below)
-        fuse_coarse = (hybrid and self.fused_coarse and apply_adam and not self.dp and self.bin_level_lo > 0
-                       and self.rep_buf is not None)
-        if fuse_coarse:
-            vren._ok(HGL.ngp_field_backward_mlp_coarse(
-                _p(self.dirs), _p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx), _p(self.enc),
-                self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb), _p(self.denc), _p(self.grad),
-                HG.ctypes.byref(self.grid.desc), _p(self.grad[HG.MLP_PARAMS:]), self.bin_level_lo, _p(self.rep_buf),
-                self.coarse_rep_levels, max(1, self.coarse_rep), s), "field_backward_mlp_coarse")
-        else:
-            vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                                                _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
-                                                _p(self.denc), _p(self.grad), s), "field_backward_mlp")
+        vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                                            _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
+                                            _p(self.denc), _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
         if fork is not None and at == "mlp":
             fork()
@@ -1041,15 +996,10 @@ class NGPTrainer:
             fold_in_adam = adam_split and self.rep_buf is not None
             bs.wait_stream(cs)
             with torch.cuda.stream(bs):
-                if not fuse_coarse:
-                    self._ev("hash_bwd_coarse", 0)
-                    self._coarse_levels(fold=not fold_in_adam)
-                    self._ev("hash_bwd_coarse", 1)
+                self._ev("hash_bwd_coarse", 0)
+                self._coarse_levels(fold=not fold_in_adam)
+                self._ev("hash_bwd_coarse", 1)
                 if adam_split:
-                    if self._ticket_active:
-                        # the ticketed Adam launches advance the batch counter: the next batch's
-                        # draw (march stream, forked at the step start) reads it first
-                        bs.wait_stream(self.march_stream)
                     self._adam(0, split, vren._stream(), rep=fold_in_adam)
             cs.wait_event(planned)
             self._ev("hash_binned_apply", 0)

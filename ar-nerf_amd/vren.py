@@ -49,7 +49,6 @@ def _declare(L):
         "ngp_adam_step_dev_rep": [vp, vp, vp, vp, vp, c_int64, vp, c_float, c_float, c_float, vp, c_float, c_int, vp,
                                   c_int64, c_int64, c_int, vp],
         "ngp_counters_inc": [vp, c_int, vp],
-        "ngp_step_ticket_set": [vp, vp, c_int, c_int],
         "ngp_random_bg": [ctypes.c_uint64, vp, c_int64, vp, vp],
         "ngp_occupied_cells": [vp, c_int64, c_float, vp, vp, vp, vp],
         "ngp_occupancy_samples": [ctypes.c_uint64, vp, c_int, c_int, c_int64, c_float, c_float, vp, vp, c_int64,
@@ -108,8 +107,6 @@ def _declare(L):
     L.ngp_chunk_segments_workspace.restype = ctypes.c_size_t
     L.ngp_render_test_capacity.argtypes = [c_int64, c_int]
     L.ngp_render_test_capacity.restype = c_int64
-    L.ngp_step_ticket_workspace.argtypes = []
-    L.ngp_step_ticket_workspace.restype = ctypes.c_size_t
     L.ngp_guard_hits.argtypes = []
     L.ngp_guard_hits.restype = ctypes.c_ulonglong
     # measurement hook (ktimer.py)
@@ -119,6 +116,12 @@ def _declare(L):
     L.ngp_timing_counts.restype = c_int
     L.ngp_timing_tick_ns.argtypes = []
     L.ngp_timing_tick_ns.restype = ctypes.c_double
+    L.ngp_probe_set.argtypes = [vp, vp, c_int64]
+    L.ngp_probe_set.restype = c_int
+    L.ngp_probe_count.argtypes = []
+    L.ngp_probe_count.restype = c_int
+    L.ngp_trace_marker.argtypes = [c_int, vp]
+    L.ngp_trace_marker.restype = c_int
 
 
 def lib():

@@ -34,58 +34,54 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import ktimer as KT  # noqa: E402
+import vren  # noqa: E402
 import synthetic as S  # noqa: E402
 from trainer import NGPTrainer  # noqa: E402
 
 with open(os.path.join(ROOT, "BASELINE.json")) as f:
     BASELINE = json.load(f)
 
-# Algorithmic work per unit, per kernel of the step (SURVEY.md
-# §8(d)).  Units: "marched" / "evaluated" (field-evaluated) / "composited" /
+# Algorithmic work per unit, per op of the step (DESIGN.md
+# §6-7).  Units: "marched" / "evaluated" (field-evaluated) / "composited" /
 # "active" (gradient-carrying) samples of the step, "params" of the model.
 # bound: "hbm" (algorithmic bytes vs 8 TB/s), "mfma" (dense fp16 FLOPs vs
 # 2.5 PFLOP/s), "atomic" (bytes added by memory-side float atomics vs the
-# chip-wide ~1.3 TB/s of MI355X_MICROARCH.md "Global float atomics"),
-# "latency" (small scans / list builders: time only).
-#  hash_encode: 16 levels x 8 corners x fp16x2 gathered (512 B) + xyz 12 B +
-#      list index 4 B read + fp16 encoding 64 B written            -> 592 B
-#  field_mlp: density 32-64-16 + colour 32-64-64-16 forward       -> 20,480 FLOP
+# chip-wide ~1.3 TB/s of MI355X_MICROARCH.md "Global float atomics").
+# Members are device-probe names (ktimer.PROBES): an op's time is the sum of
+# its kernels' execution spans, as a rocprofv3 kernel trace measures them.
+#  hash_encode (both forward rounds): 16 levels x 8 corners x 2 feats x 2 B
+#      gathered (512 B) + xyz 12 B + fp16 features 64 B (§8(d))   -> 588 B
+#      (+ the fused MLP forward, density 32-64-16 + colour 32-64-64-16:
+#      20,480 FLOP, noted beside it)
 #  mlp_bwd: forward recompute + dX + dW of both MLPs               -> 59,392 FLOP
-#  hash_bwd_coarse (levels 0-7, atomic): 8 x 8 corners x 2 fp32 gradients
-#      added (512 B of atomics per sample)                         -> 512 B
-#  hash_bwd_fine = hash_write + hash_accum (levels 8-15, counting sort +
-#      LDS accumulation): xyz + index 16 B + dL/denc 64 B read + read-modify-
-#      write of 8 x 8 x 2 fp32 table gradients (2 x 512 B)         -> 1,104 B
-#  march + march_compact: xyz, dir, t, dt written (32 B / marched sample)
+#  hash_bwd_coarse (levels 0-7, memory-side atomics): 8 levels x 8 corners
+#      x 2 fp32 gradients added                                    -> 512 B
+#  hash_bwd_fine = hash_write + hash_accum (levels 8-15, §8(d)'s hash
+#      backward restricted to them): dL/dfeat 32 B + xyz 12 B + read-modify-
+#      write of 8 x 8 x 2 fp16-sized table gradients (2 x 256 B)  -> 556 B,
+#      plus, with the binned levels' Adam fused into the accumulation, their
+#      Adam state: p, m, v read and written + the fp16 shadow     -> 26 B / param
+#      (the counting sort's records are implementation traffic: roofline.traffic)
+#  march: xyz, dir, t, dt written (32 B / marched sample)
 #  composite_loss: fwd 28 B + bwd 48 B per composited sample      -> 76 B
 #  adam: p, g, m, v read; p, m, v, fp16 p written, g zeroed        -> 34 B / param
 _MLP_FWD = 2 * (32 * 64 + 64 * 16) + 2 * (32 * 64 + 64 * 64 + 64 * 16)
 _MLP_BWD = (2 * (32 * 64 + 64 * 16 + 32 * 64 + 64 * 64 + 64 * 16)
             + 2 * (16 * 64 + 64 * 64 + 64 * 16 + 16 * 64 + 64 * 32)
             + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32))
-KERNEL_WORK = {  # name: (bound, [(work per unit, unit basis), ...], member kernels)
-    "hash_encode": ("hbm", [(16 * 8 * 4 + 12 + 4 + 64, "evaluated")], ["hash_encode"]),
-    "field_mlp": ("mfma", [(_MLP_FWD, "evaluated")], ["field_mlp"]),
+KERNEL_WORK = {  # name: (bound, [(work per unit, unit basis), ...], member probes)
+    "hash_encode": ("hbm", [(16 * 8 * 2 * 2 + 12 + 64, "evaluated")], ["first_chunk", "field_encode_mlp"]),
     "mlp_bwd": ("mfma", [(_MLP_BWD, "active")], ["mlp_bwd"]),
     "hash_bwd_coarse": ("atomic", [(8 * 8 * 2 * 4, "active")], ["hash_bwd_coarse"]),
-    # records written + read (1104 B / active sample) and, when the binned
-    # levels' Adam is fused into the accumulation, their Adam state: p, m, v
-    # read and written + the fp16 shadow (26 B / param; no gradient traffic)
-    "hash_bwd_fine": ("hbm", [(16 + 64 + 2 * 8 * 8 * 2 * 4, "active"), (26, "fused_params")],
+    "hash_bwd_fine": ("hbm", [(32 + 12 + 2 * 8 * 8 * 2 * 2, "active"), (26, "fused_params")],
                       ["hash_write", "hash_accum"]),
-    "march": ("hbm", [(32, "marched")], ["march", "march_compact"]),
+    "march": ("hbm", [(32, "marched")], ["march"]),
     "composite_loss": ("hbm", [(76, "composited")], ["composite_loss"]),
     "adam": ("hbm", [(34, "adam_params")], ["adam"]),  # params the Adam launches step
 }
-
-
-def active_work(trainer):
-    """KERNEL_WORK for the trainer's configuration: the training forward is
-    fused (ngp_field_encode_mlp), so the MLP forward runs inside the encode
-    launches and has no op of its own (its FLOPs are noted on hash_encode)."""
-    kw = dict(KERNEL_WORK)
-    kw.pop("field_mlp")
-    return kw
+# PMC traffic (profiles/pmc_traffic.json) keys of each op's kernels
+PMC_KEYS = {"hash_bwd_fine": ["hash_write", "hash_accum"], "hash_encode": ["hash_encode_first", "hash_encode"],
+            "mlp_bwd": ["mlp_bwd"], "adam": ["adam"]}
 
 
 PEAK = {"hbm": (8000.0, "GB/s"), "mfma": (2500.0, "TFLOP/s"), "atomic": (1300.0, "GB/s")}
@@ -140,6 +136,8 @@ def parse():
                          "2000 steps of the reference's schedule on a small problem, product defaults and exact mode)")
     ap.add_argument("--infer-frames", type=int, default=20, help="timed full-frame test renders (0: skip)")
     ap.add_argument("--infer-res", type=int, default=800)
+    ap.add_argument("--dropin-steps", type=int, default=50,
+                    help="timed steps of the reference's loop on the drop-in surface (DropinLoop; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="world > 1 process group (nccl = RCCL; gloo only to rehearse the path with ranks sharing a GPU)")
     return ap.parse_args()
@@ -235,6 +233,85 @@ def inference_bench(trainer, res, frames, world, rank):
                         "iteration in HIP graphs (16 iterations, then 8 per replay while rays remain), one host sync per graph"}
 
 
+class DropinLoop:
+    """The reference's training loop on the drop-in surface, as a user who
+    swaps the package in behind train.py gets it: NeRFSystem.forward
+    (train.py:84-108: poses / directions gathered per ray, get_rays,
+    models.rendering.render_rays) + training_step (train.py:158-200:
+    update_density_grid every 16 steps, NeRFLoss, loss = sum of means) +
+    Lightning's backward + FusedAdam (train.py:146-152, optimizers.FusedAdam)
+    on models.networks.NGP.  Batches are drawn as the reference's dataset
+    draws them (a random image and pixel per ray, datasets/base.py:22-35) but
+    with the indices drawn on the device and the images resident in HBM.
+    Starts from `trainer`'s state (parameters, occupancy grid, Adam moments
+    and step)."""
+
+    def __init__(self, trainer, gt_images, directions, poses, batch, seed=7):
+        from datasets.ray_utils import get_rays
+        from losses import NeRFLoss
+        from models.networks import NGP
+        from models.rendering import render_rays
+        from optimizers import FusedAdam
+        dev = trainer.dev
+        self.get_rays, self.render_rays = get_rays, render_rays
+        m = NGP(trainer.scale).to(dev)
+        with torch.no_grad():
+            m.params.copy_(trainer.params)
+        m.density_bitfield.copy_(trainer.density_bitfield)
+        m.register_buffer("density_grid", trainer.density_grid.clone())  # train.py:78-80
+        m.register_buffer("grid_coords", trainer.grid_coords.clone())
+        self.model = m
+        self.opt = FusedAdam([m.params], trainer.lr(), eps=1e-15)
+        st = self.opt.state[m.params]
+        st["step"] = int(trainer.dctr[0].item())
+        st["exp_avg"], st["exp_avg_sq"] = trainer.exp_avg.clone(), trainer.exp_avg_sq.clone()
+        self.loss = NeRFLoss(30, "raw", trainer.scale, 0.0, lambda_distortion=0.0)
+        self.gt, self.directions, self.poses, self.batch = gt_images, directions, poses, batch
+        self.global_step = trainer.global_step
+        self.gen = torch.Generator(device=dev).manual_seed(seed)
+        self.kw = {"exp_step_factor": 1 / 256} if trainer.scale > 0.5 else {}
+
+    def step(self):
+        m, B = self.model, self.batch
+        if self.global_step % 16 == 0:
+            m.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
+        img = torch.randint(self.gt.shape[0], (B,), device=self.gt.device, generator=self.gen)
+        pix = torch.randint(self.gt.shape[1], (B,), device=self.gt.device, generator=self.gen)
+        rays_o, rays_d = self.get_rays(self.directions[pix], self.poses[img])
+        results = self.render_rays(m, rays_o, rays_d, test_time=False, random_bg=False, **self.kw)
+        rgb = self.gt[img, pix].float() / 255
+        loss_d = self.loss(results, {"rgb": rgb}, step=self.global_step)
+        loss = sum(lo.mean() for lo in loss_d.values())
+        loss.backward()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=False)
+        self.global_step += 1
+        return loss, results
+
+
+def dropin_bench(trainer, gt_images, directions, poses, batch, steps, warmup=5):
+    """rays/s of DropinLoop (the reference's loop on the drop-in surface),
+    `steps` timed after `warmup`; same trained state as the product line."""
+    loop = DropinLoop(trainer, gt_images, directions, poses, batch)
+    for _ in range(warmup):
+        loop.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rm = vr = 0
+    for _ in range(steps):
+        loss, res = loop.step()
+        rm += res["rm_samples"]
+        vr += res["vr_samples"]
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    return {"value": round(batch * steps / t, 1), "unit": "rays/s", "steps": steps, "warmup": warmup,
+            "ms_per_step": round(t / steps * 1e3, 3), "rm_samples_per_ray": round(float(rm) / (steps * batch), 2),
+            "vr_samples_per_ray": round(float(vr) / (steps * batch), 2), "last_loss": round(float(loss), 5),
+            "loop": "models.rendering.render_rays + losses.NeRFLoss + loss.backward() + optimizers.FusedAdam on "
+                    "models.networks.NGP, update_density_grid every 16 steps (train.py:84-200), eager, from the "
+                    "product run's trained state"}
+
+
 def oracle_quality():
     """J1 (north_star "PSNR within 0.2 dB of reference"): the product trained
     on the fp32-oracle fixture problem (tests/golden/make_quality.py: the
@@ -316,9 +393,9 @@ def cpu_baseline(trainer, scene, gt_images, batch, warm=3, timed=20):
                       f"{sum(times):.1f} s timed"}
 
 
-def pmc_traffic(members, launches):
-    """HBM bytes per step of the op made of kernels `members` (launches per
-    step from the breakdown), from the committed PMC summary
+def pmc_traffic(members):
+    """HBM bytes per step of the op made of kernels `members` (PMC keys, one
+    launch per step each), from the committed PMC summary
     (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py from
     separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
     corrected per MI355X_MICROARCH.md "HBM"), or None if not measured."""
@@ -328,9 +405,9 @@ def pmc_traffic(members, launches):
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if not all(m in t and m in launches for m in members):
+    if not members or not all(m in t for m in members):
         return None
-    return round(sum(t[m]["bytes_per_launch"] * launches[m][1] for m in members))
+    return round(sum(t[m]["bytes_per_launch"] for m in members))
 
 
 def main():
@@ -349,7 +426,7 @@ def main():
                          **({} if args.dp_fine_buckets is None else {"dp_fine_buckets": args.dp_fine_buckets}),
                          **({} if args.chunk_first is None else {"chunk_first": args.chunk_first}))
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
-    WORK = active_work(trainer)
+    WORK = KERNEL_WORK
     R = args.batch
 
     def run(n):
@@ -400,8 +477,10 @@ def main():
                 "active": active_bd / nb, **pw}
 
     def op_row(name, summary, units):
+        """summary: {probe: (avg ms per launch, launches counted)}; every
+        member is launched once per step in the rows counted"""
         bound, terms, members = WORK[name]
-        ms = sum(summary[m][0] * summary[m][1] for m in members if m in summary)  # per step
+        ms = sum(summary[m][0] for m in members if m in summary)  # per step
         if ms <= 0:
             return None
         work = sum(units[basis] * per_unit for per_unit, basis in terms)  # per step
@@ -410,25 +489,9 @@ def main():
         return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 4), "ms_per_step": round(ms, 4),
                 "work_per_step": round(work), "work_terms": [[pu, b, round(units[b], 1)] for pu, b in terms if units[b]],
-                "kernels": members}
+                "kernels": members, "kernel_ms": {m: round(summary[m][0], 4) for m in members if m in summary},
+                "launches_timed": min((summary[m][1] for m in members if m in summary), default=0)}
 
-    ops = {k: r for k in WORK if (r := op_row(k, bd_summary, units_bd)) is not None}
-    if "hash_encode" in ops:
-        # the encode's real limit is the lane-gather issue rate: 4 loads per level on dense levels,
-        # 4 + 1/4 on hashed ones; scripts/diag/gather_diag.py measured 265 G lane-gathers/s for
-        # random 4-16 B gathers from an L2-resident table, 72 G/s from a 24 MB one
-        # (profiles/r02/gather_microbench.json)
-        sizes = list(trainer.grid.desc.sizes)[:trainer.grid.n_levels]
-        n_hashed = sum(1 for z in sizes if z == 1 << trainer.grid.log2_T)
-        per_sample = 4 * (len(sizes) - n_hashed) + 5 * n_hashed
-        ge = units_bd["evaluated"] * per_sample / (ops["hash_encode"]["ms_per_step"] * 1e-3)
-        ops["hash_encode"]["lane_gathers_per_sample"] = per_sample
-        ops["hash_encode"]["G_lane_gathers_per_s"] = round(ge / 1e9, 1)
-        ops["hash_encode"]["gather_peak_note"] = ("random-gather rate 265 G/s L2-resident, 72 G/s from a 24 MB "
-                                                  "table (profiles/r02/gather_microbench.json)")
-        if "field_mlp" not in WORK:
-            ops["hash_encode"]["fused_mlp_forward_flop_per_sample"] = _MLP_FWD
-    dominant = max(ops, key=lambda k: ops[k]["ms_per_step"])
     kernels = {k: {"avg_launch_ms": round(v[0], 4), "launches_per_step": round(v[1], 2),
                    "ms_per_step": round(v[0] * v[1], 4)} for k, v in sorted(bd_summary.items(), key=lambda kv: -kv[1][0] * kv[1][1])}
     # ---- timed region: plain graph replays (no instrumentation: even two
@@ -451,30 +514,53 @@ def main():
     if ran_timed != args.steps:
         raise RuntimeError(f"timed window ran {ran_timed} steps, expected {args.steps}")
     marched, composited, active, evaluated = trainer.stat_totals()
-    # ---- roofline region: the same number of graph-replayed steps again, with
-    # one stamp before the dominant op's first kernel and one after its last
-    # (consecutive on the main stream)
-    members = WORK[dominant][2]
-    dom = KT.KernelTimer(trainer.dctr, rows=max(4096, 2 * args.steps), span=(members[0], members[-1]))
-    trainer.timer = dom
-    run(64)  # capture this timer's graph variants
-    torch.cuda.synchronize()
-    dom.reset()
+    # ---- roofline region: the same number of steps again, replaying the SAME
+    # graphs as the timed window with the device probes armed (ktimer.ProbeTimer:
+    # each probed kernel's execution span, no extra graph node); the steps that
+    # open with an occupancy update (which launches field / march kernels a
+    # second time in that step's row) are left out
+    n_rf = min(args.steps, 32)  # (one probe row per step: 335 MB of slots)
+    probes = KT.ProbeTimer(trainer.dctr, rows=n_rf)
     trainer.reset_stats()
     s_rf = adam_steps()
+    probes.arm()
+    vren._ok(vren.lib().ngp_trace_marker(1, vren._stream()), "trace_marker")  # window start (kernel traces)
     t_rf = time.perf_counter()
-    run(args.steps)
+    run(n_rf)
+    vren._ok(vren.lib().ngp_trace_marker(2, vren._stream()), "trace_marker")  # window end
     torch.cuda.synchronize()
-    t_rf = (time.perf_counter() - t_rf) / args.steps
+    t_rf = (time.perf_counter() - t_rf) / n_rf
+    probes.disarm()
     ran_rf = adam_steps() - s_rf
-    trainer.timer = None
-    span = dom.read_span()
-    dom_summary = {members[0]: (sum(span) / len(span), 1.0)} if span else bd_summary
+    ui = trainer.update_interval
+    # (rows hold step % rows; a step whose number is a multiple of the update interval opens with
+    # an occupancy update)
+    skip = [r for r in range(probes.rows) if any(st % ui == 0 for st in range(s_rf, s_rf + ran_rf)
+                                                 if st % probes.rows == r)]
+    pr_summary = probes.summary(skip_rows=skip)
     m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         e_rf = m_rf
     nr = max(1, ran_rf)
     units_rf = {"marched": m_rf / nr, "evaluated": e_rf / nr, "composited": c_rf / nr, "active": a_rf / nr, **pw}
+    ops = {k: r for k in WORK if (r := op_row(k, pr_summary, units_rf)) is not None}
+    if "hash_encode" in ops:
+        # the encode's real limit is the lane-gather issue rate: 4 loads per level on dense levels,
+        # 4 + 1/4 on hashed ones; scripts/diag/gather_diag.py measured 265 G lane-gathers/s for
+        # random 4-16 B gathers from an L2-resident table, 72 G/s from a 24 MB one
+        # (profiles/r02/gather_microbench.json)
+        sizes = list(trainer.grid.desc.sizes)[:trainer.grid.n_levels]
+        n_hashed = sum(1 for z in sizes if z == 1 << trainer.grid.log2_T)
+        per_sample = 4 * (len(sizes) - n_hashed) + 5 * n_hashed
+        ge = units_rf["evaluated"] * per_sample / (ops["hash_encode"]["ms_per_step"] * 1e-3)
+        ops["hash_encode"]["lane_gathers_per_sample"] = per_sample
+        ops["hash_encode"]["G_lane_gathers_per_s"] = round(ge / 1e9, 1)
+        ops["hash_encode"]["gather_peak_note"] = ("random-gather rate 265 G/s L2-resident, 72 G/s from a 24 MB "
+                                                  "table (profiles/r02/gather_microbench.json)")
+        ops["hash_encode"]["fused_mlp_forward_flop_per_sample"] = _MLP_FWD
+    for k, r in ops.items():
+        r["traffic"] = pmc_traffic(PMC_KEYS.get(k, []))
+    dominant = max(ops, key=lambda k: ops[k]["ms_per_step"])
     t_max = torch.tensor([t_el], device=dev)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -487,7 +573,7 @@ def main():
              "composited": composited / args.steps, "active": active / args.steps, **pw}
     rm_s, vr_s, ev_s = units["marched"] / R, units["composited"] / R, units["evaluated"] / R
     # units per step of each window: every window's own counters over exactly its own steps
-    # (the roofline's units and its stamps cover the same replays).  Within a window the counts
+    # (the roofline's units and its probes cover the same replays).  Within a window the counts
     # must nest -- gradient-carrying <= field-evaluated <= marched, composited <= marched,
     # gradient-carrying <= composited + one per ray (the terminating sample); ACROSS windows they
     # differ with the training state: on this workload the per-step composited samples swing
@@ -500,25 +586,26 @@ def main():
     nested = all(w["active"] <= w["evaluated"] + 0.5 and w["evaluated"] <= w["marched"] + 0.5
                  and w["composited"] <= w["marched"] + 0.5 and w["active"] <= w["composited"] + R + 0.5
                  for w in wins.values())
-    steps_ok = ran_rf == args.steps and ran_bd == n_bd and ran_timed == args.steps
+    steps_ok = ran_rf == n_rf and ran_bd == n_bd and ran_timed == args.steps
     vals = [w["composited"] for w in wins.values() if w["composited"] > 0]
     units_check["drift_composited_max_over_min"] = round(max(vals) / min(vals), 3) if vals else None
     units_check["ok"] = bool(nested and steps_ok)
     if not units_check["ok"]:
         print(f"[bench] WARNING: a window's unit counts do not nest or its step count is off: {units_check}",
               file=sys.stderr)
-    roof = op_row(dominant, dom_summary, units_rf)
-    roof = dict(op=dominant, traffic=pmc_traffic(members, bd_summary), traffic_unit="bytes per step", **roof,
-                units_check=units_check,
-                measured=f"device wall-clock stamps before / after the op inside the captured graphs of "
-                         f"{args.steps} graph-replayed steps run right after the timed ones "
-                         f"({t_rf * 1e3:.4f} ms/step with the 2 stamps; ktimer)")
+    roof = dict(op=dominant, traffic_unit="bytes per step", **ops[dominant], units_check=units_check,
+                measured=f"sum of the op's kernels' execution spans (earliest wave start to latest wave end, "
+                         f"device probes inside the kernels, ktimer.ProbeTimer) averaged over the "
+                         f"{ops[dominant]['launches_timed']} steps of a {n_rf}-step window of the same "
+                         f"graph replays as the timed one, steps opening with an occupancy update left out "
+                         f"({t_rf * 1e3:.4f} ms/step in that window); rocprofv3 kernel-trace durations of the "
+                         f"same command: scripts/roofline_check.py")
     # step-level bound: every op's algorithmic bytes at HBM peak + MLP FLOPs at MFMA peak
     def op_work(k):
         return sum(units[b] * pu for pu, b in KERNEL_WORK[k][1])
     # (all ops' work, the fused MLP forward's FLOPs included)
     hbm_bytes = sum(op_work(k) for k in KERNEL_WORK if KERNEL_WORK[k][0] != "mfma")
-    flops = sum(op_work(k) for k in KERNEL_WORK if KERNEL_WORK[k][0] == "mfma")
+    flops = sum(op_work(k) for k in KERNEL_WORK if KERNEL_WORK[k][0] == "mfma") + units["evaluated"] * _MLP_FWD
     bound_ms = hbm_bytes / 8000e9 * 1e3 + flops / 2500e12 * 1e3
     adam_ms = units["params"] * 34 / 8000e9 * 1e3
     step_bound = {"hbm_bytes_per_step": round(hbm_bytes), "mlp_flops_per_step": round(flops),
@@ -532,6 +619,9 @@ def main():
     loss = float(trainer.out_loss.sum().item())
     psnr = psnr_eval(trainer, scene, args.psnr_views, args.psnr_res) if (rank == 0 and args.psnr_views > 0) else None
     infer = inference_bench(trainer, args.infer_res, args.infer_frames, world, rank) if args.infer_frames > 0 else None
+    dropin = None
+    if rank == 0 and world == 1 and args.dropin_steps > 0:
+        dropin = dropin_bench(trainer, gt_images, directions, poses, R, args.dropin_steps)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(trainer, scene, gt_images, R)
@@ -581,6 +671,7 @@ def main():
             "quality": quality,
             "quality_vs_fp32_oracle": oracle_q,
             "inference": infer,
+            "dropin": dropin,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -58,6 +58,28 @@ int ngp_timing_set(uint64_t* stamps, const int64_t* step_dev, int64_t ring, int 
 int ngp_timing_counts(int32_t* counts, int n_ids);
 double ngp_timing_tick_ns(void);
 
+/* Device probes (bench.py's roofline window): lane 0 of every wave of the
+ * probed kernels below stores its start and its end (GPU wall-clock ticks)
+ * into buf[(((*step_dev % ring) * NGP_P_COUNT + id) * NGP_PROBE_WAVES + wave %
+ * NGP_PROBE_WAVES) * 2 + {0, 1}] (plain stores; the caller zeroes buf and
+ * takes the min start / max end of the nonzero slots) -- a kernel's
+ * execution span as a dispatch trace (rocprofv3 --kernel-trace) measures it,
+ * without extra graph nodes: the control block is a device symbol the kernels
+ * read at run time, so graphs captured with the probes off replay with them
+ * on.  buf == NULL disables.  A kernel launched twice in one step row leaves
+ * the slots of both (the caller discards such rows).  Host-side global state. */
+#define NGP_PROBE_WAVES 65536
+enum {
+    NGP_P_MARCH = 0, NGP_P_FIRST_CHUNK, NGP_P_FIELD_ENCODE_MLP, NGP_P_COMPOSITE, NGP_P_MLP_BWD, NGP_P_HASH_BWD_COARSE,
+    NGP_P_HASH_COUNT, NGP_P_HASH_WRITE, NGP_P_HASH_ACCUM, NGP_P_ADAM,
+    NGP_P_COUNT
+};
+int ngp_probe_set(uint64_t* buf, const int64_t* step_dev, int64_t ring);
+int ngp_probe_count(void);
+/* Launches an empty kernel named trace_marker_kernel (tag >= 0) on `stream`:
+ * brackets a window of a rocprofv3 dispatch trace (scripts/roofline_check.py). */
+int ngp_trace_marker(int tag, void* stream);
+
 /* ---------------------------------------------------------------- rays */
 /* Replaces vren.ray_aabb_intersect (binding.cpp:9-20 -> intersection.cu:59-100).
  * rays_o/rays_d (n_rays,3) f32; centers/half_sizes (n_voxels,3) f32.
@@ -342,20 +364,6 @@ int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const 
  * of a batch of rays, built beside the previous step). */
 int ngp_rays_nonempty(const int64_t* rays_a, int64_t n_rays, int32_t* rows, int64_t* n_rows, int32_t* rest,
                       int64_t* zero, void* stream);
-/* Both chunked rounds of the training forward in ONE launch: for the rows
- * rows[j], j < *n_rows_dev (rows NULL: 0..n_rows-1; n_rows_dev NULL: n_rows)
- * of rays_a, the first min(N, 64) samples, then -- for the rows whose
- * transmittance is still above T_threshold after them -- every later
- * sample, in 64-sample items each workgroup queues in LDS for its own waves.
- * Evaluates exactly ngp_field_forward_first's samples + its round-2 list's
- * (ngp_field_encode_mlp's values bit for bit; no other sample touched).
- * *evaluated (nullable) += the evaluated samples.  Replaces, for the
- * model(xyzs, dirs) call of __render_rays_train (models/rendering.py:278),
- * both rounds' field launches and the round-2 list launch. */
-int ngp_field_forward_rows(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
-                           const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
-                           float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
-                           void* enc_pm, float* sigmas, float* rgbs, int64_t* evaluated, void* stream);
 /* Round 1 of the chunked training forward with the round-2 counts: for the
  * rows rows[j], j < *n_rows_dev (rows NULL: rows 0..n_rows-1; n_rows_dev
  * NULL: n_rows) of rays_a (ray, start, N), the first min(N, 64) samples
@@ -402,19 +410,6 @@ int ngp_field_backward_mlp(const float* dirs, int64_t n, const int64_t* n_dev, c
                            const void* enc_f16, int64_t enc_pm_stride, const void* mlp_f16,
                            const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws, float* grad_mlp,
                            void* stream);
-/* ngp_field_backward_mlp that also scatters the coarse hash levels [0,
- * level_hi) into grad_table (entries x 2 fp32) -- ngp_hash_backward_levels_rep
- * with fold = 0 (levels below rep_levels into the n_rep replicas at rep,
- * folded later by ngp_adam_step_dev_rep) -- from the registers that hold
- * dL/denc, with that function's arithmetic: one launch where the hybrid
- * backward had two.  xyzs (n, 3) are the samples' positions.  With level_hi
- * == 8 the denc rows of levels 0-7 are not written (nothing else reads them:
- * the binned levels start at 8). */
-int ngp_field_backward_mlp_coarse(const float* dirs, const float* xyzs, int64_t n, const int64_t* n_dev,
-                                  const int32_t* sample_idx, const void* enc_f16, int64_t enc_pm_stride,
-                                  const void* mlp_f16, const float* dL_dsigmas, const float* dL_drgbs, float* denc_ws,
-                                  float* grad_mlp, const ngp_hashgrid_t* grid, float* grad_table, int level_hi,
-                                  float* rep, int rep_levels, int n_rep, void* stream);
 int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                       const ngp_hashgrid_t* grid, const float* denc, float* grad_table, void* stream);
 
@@ -481,7 +476,15 @@ int ngp_hash_binned_accum_adam(const ngp_hashgrid_t* grid, float* grad_table, vo
                                int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
                                void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
                                const int64_t* step_dev, float grad_scale, void* stream);
-/* ngp_hash_backward restricted to levels [level_lo, level_hi). */
+/* ngp_hash_backward restricted to levels [level_lo, level_hi).  The levels'
+ * scatter merges each workgroup's additions in LDS first (tiles of 64
+ * consecutive samples, their run heads summed per 64-B gradient line in an LDS
+ * table, one memory-side add per touched line: ~2.3x fewer atomic requests
+ * than merging runs per wave) -- ngp_hash_backward_coarse_mode selects it
+ * (1, default; 2: 128-sample tiles) or the per-wave merge (0) for the
+ * ngp_hash_backward_levels* calls that follow and returns the previous mode
+ * (mode < 0: query only).  Same sums in every mode up to fp32 order. */
+int ngp_hash_backward_coarse_mode(int mode);
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
                              int level_hi, void* stream);
@@ -582,20 +585,6 @@ int ngp_ray_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_row
 int ngp_ray_segments_capped(const int64_t* rays_a, int64_t n_rows, int cap, int64_t* start_ws, int64_t* total,
                             int64_t* total_acc, int32_t* sample_idx, void* stream);
 
-/* Step completion ticket.  Between ngp_step_ticket_set(ws, counters, n,
- * parties) and ngp_step_ticket_set(NULL, ...), the next `parties` launches of
- * the Adam kernels (ngp_adam_step_dev / _dev_rep; the residual Adam of
- * ngp_hash_binned_apply_adam / _accum_adam) take a ticket: when every block
- * of every one of them has finished, the last one adds 1 to counters[0..n)
- * (device-scope atomics) -- a step's Adam launches advance the step counters
- * themselves, without a separate increment launch joined after them (the
- * caller must order every other reader of the counters before those
- * launches).  ws: ngp_step_ticket_workspace() bytes, 4-byte aligned, zeroed
- * once, owned by the call site.  Clearing returns NGP_ERANGE if the number
- * of launches that took a ticket differs from `parties`.  Host-side state of
- * the library (like ngp_timing_set): set it around one capture at a time. */
-int ngp_step_ticket_set(void* ws, int64_t* counters, int n_counters, int parties);
-size_t ngp_step_ticket_workspace(void);
 
 /* apex FusedAdam step (train.py:146; weight decay 0) over n (multiple of 4)
  * fp32 params with grad *= grad_scale, bias corrections for `step` (1-based);

@@ -155,11 +155,11 @@ def _patch_f32_outputs(O):
     the reference the gradients the glue hands back to them -- dL/dh from
     TruncExp (custom_functions.py:162-173, computed in fp32 under autocast and
     cast back across the fp16 output) and dL/drgb from VolumeRenderer -- are
-    rounded to fp16 without a loss scale (tcnn applies its scale inside its
-    own backward), flushing magnitudes below 2^-24 to zero.  This variant
+    rounded to fp16 (at the GradScaler's loss scale under Lightning's
+    precision=16, train.py:291: the reference-precision fixtures model that
+    scaler, see the GradScaler model further down).  This variant -- the "fp32 boundary" fixture --
     returns the same VALUES (fp16-rounded) as fp32 tensors, so those
-    gradients stay fp32: the precision the product's MLP backward keeps
-    (per-sample scaled fp16).  On the CPU (no autocast) TruncExp then also
+    gradients stay fp32 and no rounding happens at the boundary at all.  On the CPU (no autocast) TruncExp then also
     runs in fp32, as it does on the GPU."""
     T = O.tcnn_stub
 

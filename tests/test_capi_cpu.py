@@ -120,7 +120,7 @@ def test_gradient_replica_entry_points_check_arguments_without_launching():
 
 
 def test_row_forward_entry_points_check_arguments_without_launching():
-    """ngp_field_forward_first / ngp_field_forward_rows / ngp_rays_nonempty
+    """ngp_field_forward_first / ngp_rays_nonempty
     (round 4): argument checks on the host, before any launch (NGP_EINVAL =
     -1); zero rows are a no-op."""
     import ctypes as C
@@ -140,12 +140,6 @@ def test_row_forward_entry_points_check_arguments_without_launching():
                                      None, None, None, None, None) == -1
     assert L.ngp_field_forward_first(None, None, None, None, None, None, 0, 64, f, d, None, None, None, None, None,
                                      None, None, None, None, None) == 0
-    # missing inputs; a misaligned table
-    assert L.ngp_field_forward_rows(None, p, p, p, None, None, 8, 64, f, d, p, p, p, p, p, None, None) == -1
-    assert L.ngp_field_forward_rows(p, p, p, p, None, None, 8, 64, f, d, C.c_void_p(258), p, p, p, p, None,
-                                    None) == -1
-    assert L.ngp_field_forward_rows(None, None, None, None, None, None, 0, 64, f, d, None, None, None, None, None,
-                                    None, None) == 0
     assert Lv.ngp_rays_nonempty(p, 8, None, p, None, None, None) == -1
     assert Lv.ngp_rays_nonempty(p, -1, p, p, None, None, None) == -1
     assert Lv.ngp_rays_nonempty(p, 8, p, None, None, None, None) == -1

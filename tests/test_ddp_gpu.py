@@ -333,3 +333,64 @@ def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k):
         worst = max(worst, float((dA[a:b].double() - ref).norm() / ref.norm()))
     print(f"segmented (emulated world 1, {len(buckets)} buckets) vs unsegmented step: worst bucket update rel L2 {worst:.2e}")
     assert worst < 2e-2
+
+
+@pytest.mark.parametrize("k", [2])
+def test_rccl_world1_segmented_replay_matches_the_unsegmented_step(k):
+    """the data-parallel step's collectives through RCCL itself.
+    One process, a world-1 `nccl` (= RCCL) process group and
+    ddp.FORCE_COLLECTIVES past the world-1 shortcut: every bucket's
+    reduce_scatter_tensor and all_gather_into_tensor run as RCCL calls on the
+    comm stream between the replayed graph segments (and the unsegmented
+    eager path's own reduce-scatters / all-gathers), on the trainer's real
+    buffers.  The segmented replay's per-bucket updates equal the unsegmented
+    step's to the fp32 atomic-order noise of the gradient, the fp16 shadow is
+    gathered in full, and the process group saw the calls (RCCL ran)."""
+    import ddp
+    assert not dist.is_initialized()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    calls = {"rs": 0, "ag": 0}
+    rs0, ag0 = dist.reduce_scatter_tensor, dist.all_gather_into_tensor
+
+    def rs(*a, **kw):
+        calls["rs"] += 1
+        return rs0(*a, **kw)
+
+    def ag(*a, **kw):
+        calls["ag"] += 1
+        return ag0(*a, **kw)
+    ddp.FORCE_COLLECTIVES = True
+    dist.reduce_scatter_tensor, dist.all_gather_into_tensor = rs, ag
+    try:
+        assert dist.get_backend() == "nccl" and ddp.comm_active()
+        runs = []
+        for graphs in (True, False):
+            tr, sc = _emu_trainer(graphs, k)
+            assert tr.world == 1 and tr.dp
+            p0 = tr.params.clone()
+            gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
+            for _ in range(3):
+                tr.train_step(gt, dirs, poses)
+            tr.drain()
+            torch.cuda.synchronize()
+            runs.append(((tr.params - p0).cpu(), tr.buckets,
+                         (tr.params16.float() - tr.params.half().float()).abs().max()))
+        nb = len(runs[0][1])
+        assert calls["rs"] >= 2 * 3 * nb and calls["ag"] >= 2 * 3 * nb, calls  # both paths, 3 steps, every bucket
+    finally:
+        dist.reduce_scatter_tensor, dist.all_gather_into_tensor = rs0, ag0
+        ddp.FORCE_COLLECTIVES = False
+        dist.destroy_process_group()
+    (dA, buckets, s16a), (dB, _, s16b) = runs
+    assert float(s16a) == 0.0 and float(s16b) == 0.0
+    worst = 0.0
+    for a, b in buckets:
+        b = min(b, dA.numel())
+        ref = dB[a:b].double()
+        if float(ref.norm()) == 0:
+            continue
+        worst = max(worst, float((dA[a:b].double() - ref).norm() / ref.norm()))
+    print(f"RCCL world-1 segmented vs unsegmented step ({len(buckets)} buckets, {calls}): worst rel L2 {worst:.2e}")
+    assert worst < 2e-2

@@ -306,6 +306,62 @@ def test_hash_backward_binned_matches_atomic(scale, level_cap, level_lo, merge_h
     torch.testing.assert_close(out.cpu(), ref.cpu(), rtol=1e-4, atol=1e-6 * float(d_ref.abs().max()))
 
 
+@pytest.mark.parametrize("layout", ["rays", "scattered"])
+def test_coarse_scatter_modes_match_oracle(layout):
+    """ngp_hash_backward_levels(_rep) over levels 0-7 in every coarse mode --
+    0: runs merged per wave, memory-side atomics per head; 1 / 2: the block's
+    heads merged per 64-B gradient line in an LDS table, one add per touched
+    line (64- / 128-sample tiles) -- against the oracle's hash backward
+    (oracle.hash_encode_bwd, tcnn's scatter restated in C) on the same
+    samples: rel-L2 per level <= 1e-5 (fp32 summation order only).
+    "scattered": uncorrelated positions, so a tile touches more lines than the
+    LDS table holds and the table-full path (direct adds) runs too; the
+    replicated call must leave its replicas zero."""
+    if layout == "rays":
+        x = _ray_points(600, 120, 0.5, seed=11)
+    else:  # marched samples in random order: no two consecutive ones on one ray
+        x = _points(60000, 0.5, seed=11)[0]
+        x = x[torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(12))].contiguous()
+    n = x.shape[0]
+    grid = HG.HashGrid(0.5)
+    g = torch.Generator().manual_seed(13)
+    sidx = torch.randperm(n, generator=g)[: n * 3 // 4].sort().values.to(torch.int32)
+    m = sidx.numel()
+    denc = torch.randn(m, 32, generator=g) * 1e-2
+    denc[:, 16:] = 0  # levels 8-15 are not scattered here
+    spec = O.HashGridSpec(scale=0.5)
+    ref = O.hash_encode_bwd(spec, x[sidx.long()], -0.5 * torch.ones(3), 0.5 * torch.ones(3), denc).double()
+    L = HG._lib()
+    p = lambda t: vren.c_void_p(t.data_ptr())  # noqa: E731
+    desc = HG.ctypes.byref(grid.desc)
+    xd, sd, dd = x.to(DEV), sidx.to(DEV), denc.to(DEV)
+    n_dev = torch.tensor([m], dtype=torch.int64, device=DEV)
+    rep = torch.zeros(L.ngp_hash_backward_rep_floats(desc, 4, 8), device=DEV)
+    prev = L.ngp_hash_backward_coarse_mode(-1)
+    try:
+        for mode in (0, 1, 2):
+            assert L.ngp_hash_backward_coarse_mode(mode) >= 0
+            for replicated in (False, True):
+                out = torch.zeros(grid.n_entries * 2, device=DEV)
+                if replicated:
+                    vren._ok(L.ngp_hash_backward_levels_rep(p(xd), n, p(n_dev), p(sd), desc, p(dd), p(out), 0, 8,
+                                                            p(rep), 4, 8, 1, vren._stream()), "levels_rep")
+                else:
+                    vren._ok(L.ngp_hash_backward_levels(p(xd), n, p(n_dev), p(sd), desc, p(dd), p(out), 0, 8,
+                                                        vren._stream()), "levels")
+                torch.cuda.synchronize()
+                assert float(rep.abs().max()) == 0.0
+                got = out.cpu().double()
+                for lv in range(8):
+                    a, b = 2 * int(grid.offsets[lv]), 2 * int(grid.offsets[lv + 1])
+                    assert float(ref[a:b].abs().max()) > 0
+                    assert _rel(got[a:b], ref[a:b]) < 1e-5, (mode, replicated, lv, _rel(got[a:b], ref[a:b]))
+                assert float(got[2 * int(grid.offsets[8]):].abs().max()) == 0.0  # nothing outside levels 0-7
+    finally:
+        L.ngp_hash_backward_coarse_mode(prev)
+    assert L.ngp_hash_backward_coarse_mode(3) < 0
+
+
 @pytest.mark.parametrize("rep_levels,n_rep", [(4, 8), (8, 16), (2, 1)])
 def test_hash_backward_levels_replicated(rep_levels, n_rep):
     """ngp_hash_backward_levels_rep (levels < rep_levels into n_rep replicas,
@@ -355,9 +411,7 @@ def test_forward_first_chunk_matches_encode_mlp_and_chunk_counts(scale):
     ngp_field_encode_mlp, no other sample touched; rest = the counts
     ngp_chunk_counts_range(first 64) gives from the full forward's sigmas; and
     with ngp_rays_nonempty's row list, the appended round-2 list holds exactly
-    ngp_ray_segments' samples (each row's run contiguous and ascending); and
-    ngp_field_forward_rows (both rounds, one launch) evaluates exactly those
-    samples."""
+    ngp_ray_segments' samples (each row's run contiguous and ascending)."""
     import ctypes
     _, flat = _oracle_and_params(scale=scale)
     x, d = _points(20000, scale)
@@ -425,20 +479,3 @@ def test_forward_first_chunk_matches_encode_mlp_and_chunk_counts(scale):
     # runs of a row are contiguous and ascending: every step inside the list is +1 or a jump to another row's start
     steps = got[1:] - got[:-1]
     assert int((steps == 1).sum()) == T - int((cnt_ref > 0).sum())
-    # 3) both rounds in one launch (ngp_field_forward_rows, per-workgroup LDS queues): exactly the first chunks +
-    # the round-2 list evaluated, same values, nothing else touched; with and without the row list
-    both = torch.zeros(n, dtype=torch.bool, device=DEV)
-    both[first] = True
-    both[got] = True
-    for it in range(2):
-        enc_pm.fill_(7.0); sig2.fill_(-1.0); rgb2.fill_(-1.0); ev.zero_()
-        vren._ok(L.ngp_field_forward_rows(vp(x), vp(d), vp(deltas), vp(rays_a), vp(rows) if it else None,
-                                          vp(n_ne) if it else None, R, n, ctypes.c_float(1e-4), ctypes.byref(grid.desc),
-                                          vp(p16[HG.MLP_PARAMS:]), vp(p16), vp(enc_pm), vp(sig2), vp(rgb2),
-                                          vp(ev), vren._stream()), "forward_rows")
-        torch.cuda.synchronize()
-        rows_enc = enc_pm.permute(1, 0, 2).reshape(n, 32)
-        assert torch.equal(rows_enc[both].view(torch.int16), enc[both].view(torch.int16))
-        assert torch.equal(sig2[both], sig[both]) and torch.equal(rgb2[both], rgb[both])
-        assert bool((sig2[~both] == -1.0).all()) and bool((rows_enc[~both] == 7.0).all())
-        assert int(ev) == int(both.sum())

@@ -178,13 +178,12 @@ def test_chunked_forward_matches_full(first, table_init):
         assert ev1 < n1
 
 
-@pytest.mark.parametrize("table_init,mode", [(0.2, 1), (2.0, 1), (0.2, 2), (2.0, 2)])
+@pytest.mark.parametrize("table_init,mode", [(0.2, 1), (2.0, 1)])
 def test_row_forward_matches_two_rounds_and_full(table_init, mode):
-    """The row forward -- mode 1: round 1 a wave per non-empty row from
+    """The row forward -- round 1 a wave per non-empty row from
     ngp_rays_nonempty with the row's transmittance in its epilogue, which
     appends the round-2 list (ngp_field_forward_first), then the field over
-    that list; mode 2: both rounds in one launch, per-workgroup LDS queues of
-    round-2 chunks (ngp_field_forward_rows) -- gives the full forward's step
+    that list -- gives the full forward's step
     exactly as the two chunked rounds do: loss and per-ray outputs
     bit-identical, gradients equal up to atomic summation order, the same
     samples evaluated; and a second step repeats it bit for bit."""
@@ -362,52 +361,21 @@ def test_pair_step_replays_match_single_steps():
     assert abs(lp - la) <= 0.1 * abs(la) + 3 * abs(lb - la)
 
 
-def test_step_ticket_replays_match_the_increment_launch():
-    """Steady-state graphs advance the device step / batch counters from the
-    step's two Adam launches (ngp_step_ticket_set: the last block of the last
-    of them adds 1) instead of a separate increment launch joined after both:
-    after the same schedule from the same seed the counters end at the same
-    values, the ticket workspace is back to zero, the losses agree, and the
-    parameters differ from an
-    increment-launch run no more than two increment-launch runs differ from
-    each other (float-atomic order noise)."""
-    sc = S.AnalyticScene(W=100, H=100, n_images=10)
-    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
-    gt_img = sc.gt_images(device=DEV)
-    outs = []
-    for ticket in (False, False, True):  # (opt-in path, NGP_STEP_TICKET=1)
-        tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, warmup_steps=16)
-        tr.step_ticket = ticket
-        tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
-        losses = []
-        for _ in range(120):
-            losses.append(float(tr.train_step(gt_img, dirs, poses).mean()))
-        tr.drain()
-        torch.cuda.synchronize()
-        outs.append((tr.params.clone(), losses, tr.dctr.clone(), int(tr._ticket_ws.abs().sum()), len(tr._graphs)))
-    (pa, la, ca, _, ga), (pb, lb, cb, _, _), (pt, lt, ct, wt, gt_) = outs
-    assert ga >= 1 and gt_ >= 1  # graph replays ran
-    assert torch.equal(ct, ca) and torch.equal(ca, cb) and int(ca[0]) == 120, (ca, ct)
-    assert wt == 0
-    assert lt[0] == la[0]  # (same first batch; later losses carry float-atomic order noise)
-    assert abs(sum(lt[-20:]) - sum(la[-20:])) <= 0.1 * abs(sum(la[-20:])) + 3 * abs(sum(lb[-20:]) - sum(la[-20:]))
-    noise = float((pb - pa).norm())
-    print(f"ticket vs increment launch {float((pt - pa).norm()):.3f}, increment vs increment {noise:.3f}")
-    assert float((pt - pa).norm()) <= 3 * noise + 1e-3 * float(pa.norm())
-
-
-def test_fused_coarse_scatter_matches_the_separate_launch():
-    """The coarse (atomic) hash levels scattered by the MLP backward launch
-    (ngp_field_backward_mlp_coarse: the single-process step's default) add
-    the same gradient as the separate hash_bwd launch it replaces: the same
-    step from the same state, the MLP + coarse-level gradient the coarse Adam
-    launch consumes (gradient + its folded replicas) agrees per parameter
-    group to fp32 atomic-order noise."""
+@pytest.mark.parametrize("mode", [1, 2])
+def test_lds_merged_coarse_scatter_matches_the_wave_merged_one(mode):
+    """The coarse (atomic) hash levels scattered with the block's additions
+    merged per 64-B gradient line in LDS (ngp_hash_backward_coarse_mode 1 / 2:
+    64- / 128-sample tiles) add the same gradient as the per-wave run merge
+    (mode 0): the same training step from the same state, the MLP +
+    coarse-level gradient the coarse Adam launch consumes (gradient + its
+    folded replicas) agrees per parameter group to fp32 atomic-order noise."""
     import hashgrid as HG
     grads = []
-    for fused in (False, True):
+    L = HG._lib()
+    prev = L.ngp_hash_backward_coarse_mode(-1)
+    for m in (0, mode):
+        L.ngp_hash_backward_coarse_mode(m)
         sc, tr, img, pix, noise = _setup(table_init=0.2)
-        tr.fused_coarse = fused
         seen = {}
         orig = tr._adam
 
@@ -426,6 +394,7 @@ def test_fused_coarse_scatter_matches_the_separate_launch():
         tr.step(img.to(DEV), pix.to(DEV), gt, dirs, poses, noise=noise.to(DEV))
         torch.cuda.synchronize()
         grads.append((seen["g"].cpu(), tr))
+    L.ngp_hash_backward_coarse_mode(prev)
     (ga, tra), (gb, _) = grads
     offs = [0, 3072, HG.MLP_PARAMS] + [HG.MLP_PARAMS + 2 * int(tra.grid.offsets[l]) for l in range(1, tra.bin_level_lo + 1)]
     worst = 0.0
@@ -434,5 +403,5 @@ def test_fused_coarse_scatter_matches_the_separate_launch():
         if float(ref.norm()) == 0:
             continue
         worst = max(worst, float((gb[a:b].double() - ref).norm() / ref.norm()))
-    print(f"fused coarse scatter vs separate launch: worst group relative L2 {worst:.2e}")
+    print(f"LDS-merged coarse scatter (mode {mode}) vs wave-merged: worst group relative L2 {worst:.2e}")
     assert worst < 1e-5
