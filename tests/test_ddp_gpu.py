@@ -298,8 +298,8 @@ def _emu_trainer(use_graphs, k=2):
     return tr, sc
 
 
-@pytest.mark.parametrize("k", [2, 4])
-def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k):
+@pytest.mark.parametrize("k,capture", [(2, True), (4, True), (2, False)])
+def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k, capture, monkeypatch):
     """the world > 1 step's per-bucket pipeline (graph segments,
     reduce-scatter / sharded Adam / all-gather of each bucket on the comm
     stream while the next level range accumulates on the main stream) run in
@@ -309,7 +309,10 @@ def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k):
     the same steps through the unsegmented eager path (_reduce_grads, Adam on
     the shards, all-gather of the shadow, one stream).  Same state, same
     device-drawn batches: every bucket's parameter update agrees to the fp32
-    atomic-order noise of the MLP and coarse-level gradients."""
+    atomic-order noise of the MLP and coarse-level gradients.  capture: the
+    whole step incl. the comm stream's chains as ONE graph (the default), else
+    the graph segments with the collectives between them (NGP_DP_CAPTURE=0)."""
+    monkeypatch.setenv("NGP_DP_CAPTURE", "1" if capture else "0")
     runs = []
     for graphs in (True, False):
         tr, sc = _emu_trainer(graphs, k)
@@ -320,7 +323,8 @@ def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k):
         tr.drain()
         torch.cuda.synchronize()
         if graphs:
-            assert any("compute" in g for g in tr._graphs) and len(tr.bin_cuts) == k + 1  # replayed; 1 + k buckets
+            assert any(("whole" if capture else "compute") in g for g in tr._graphs)  # replayed
+            assert len(tr.bin_cuts) == k + 1  # 1 + k buckets
         runs.append(((tr.params - p0).cpu(), tr.buckets, (tr.params16.float() - tr.params.half().float()).abs().max()))
     (dA, buckets, s16a), (dB, _, s16b) = runs
     assert float(s16a) == 0.0 and float(s16b) == 0.0  # every rank's shadow all-gathered in full
@@ -368,7 +372,7 @@ def test_rccl_world1_segmented_replay_matches_the_unsegmented_step(k):
         runs = []
         for graphs in (True, False):
             tr, sc = _emu_trainer(graphs, k)
-            assert tr.world == 1 and tr.dp
+            assert tr.world == 1 and tr.dp and tr._capture_comm()  # RCCL calls captured into the step graph
             p0 = tr.params.clone()
             gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
             for _ in range(3):
@@ -378,7 +382,9 @@ def test_rccl_world1_segmented_replay_matches_the_unsegmented_step(k):
             runs.append(((tr.params - p0).cpu(), tr.buckets,
                          (tr.params16.float() - tr.params.half().float()).abs().max()))
         nb = len(runs[0][1])
-        assert calls["rs"] >= 2 * 3 * nb and calls["ag"] >= 2 * 3 * nb, calls  # both paths, 3 steps, every bucket
+        # every bucket's collectives went through RCCL: the eager path's 3 steps, and the graph path's eager
+        # first step and its capture (the replays re-run the captured RCCL kernels without Python calls)
+        assert calls["rs"] >= 4 * nb and calls["ag"] >= 4 * nb, calls
     finally:
         dist.reduce_scatter_tensor, dist.all_gather_into_tensor = rs0, ag0
         ddp.FORCE_COLLECTIVES = False
@@ -392,5 +398,5 @@ def test_rccl_world1_segmented_replay_matches_the_unsegmented_step(k):
         if float(ref.norm()) == 0:
             continue
         worst = max(worst, float((dA[a:b].double() - ref).norm() / ref.norm()))
-    print(f"RCCL world-1 segmented vs unsegmented step ({len(buckets)} buckets, {calls}): worst rel L2 {worst:.2e}")
+    print(f"RCCL world-1 captured step vs unsegmented step ({len(buckets)} buckets, {calls}): worst rel L2 {worst:.2e}")
     assert worst < 2e-2
