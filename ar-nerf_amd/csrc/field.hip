@@ -1571,128 +1571,6 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
 
 constexpr unsigned HASH_BWD_BLOCKS = 8192;  // grid cap of hash_bwd_kernel (2048 measured slower)
 
-// The coarse levels' backward with the block's additions merged in LDS before
-// they leave the CU (SURVEY §7 step 5's LDS-privatised coarse accumulation).
-// hash_bwd_kernel merges runs of equal corners only inside a wave's 16
-// consecutive samples, so every wave instruction still sends ~6 memory-side
-// atomic requests per sample over levels 0-7 (one per 64-B line its run heads
-// touch): ~750 K requests per Lego step, which bound that kernel and slow the
-// record write beside it.  Here a block takes a tile of TW x 64 consecutive
-// gradient-carrying samples (wave w: TW groups of 16), computes the same run
-// heads, and adds each head's sum into an LDS table keyed by the 64-B line of
-// the gradient it belongs to (open addressing, CAS on the key, ds_add_f32 on
-// the line's 16 floats).  After the tile, the block flushes every line it
-// touched with one 16-lane add (one request per line): requests fall to the
-// distinct lines per tile -- 2.2-2.4x fewer on real Lego samples
-// (scripts/diag/coarse_requests.py on scripts/diag/active_dump.py's dump:
-// 874 K -> 367 K per step at 64-sample tiles of ... see DESIGN §6).
-// Lines of the replicated levels [0, rep_hi) go to this block's replica.
-// A head that finds no free slot in NS probes (table full) adds straight to
-// memory (still exact).  Addition order differs from hash_bwd_kernel's (fp32
-// sums in another order: atomic-order noise, as between two runs of either).
-constexpr uint32_t CT_EMPTY = 0xffffffffu;
-template <int NS>
-struct CoarseTable {
-    uint32_t key[NS];         // line index (float index >> 4) or CT_EMPTY
-    float val[NS * 16];       // the line's 16 floats
-    uint16_t used[NS];        // slots taken this tile, in taking order
-    uint32_t n_used;
-};
-template <int NS>
-__device__ __forceinline__ void table_add(CoarseTable<NS>& T, uint32_t fi, float v, float* __restrict__ gdst) {
-    const uint32_t key = fi >> 4;
-    uint32_t h = (key * 2654435761u) >> (32 - __builtin_ctz(NS));
-    for (int probe = 0; probe < 32; ++probe) {
-        uint32_t old = atomicCAS(&T.key[h], CT_EMPTY, key);
-        if (old == CT_EMPTY) {
-            T.used[atomicAdd(&T.n_used, 1u)] = (uint16_t)h;
-            old = key;
-        }
-        if (old == key) {
-            atomicAdd(&T.val[h * 16 + (fi & 15u)], v);
-            return;
-        }
-        h = (h + 1) & (NS - 1);
-    }
-    atomicAdd(gdst + fi, v);  // (table full around this key)
-}
-template <int NS, int TW>
-__global__ void __launch_bounds__(256) hash_bwd_lds_kernel(const float* __restrict__ xyzs, int64_t n,
-                                                           const int64_t* __restrict__ n_dev,
-                                                           const int32_t* __restrict__ sidx, GridArgs ga,
-                                                           const float* __restrict__ denc, float* __restrict__ grad,
-                                                           int lo, int hi, float* __restrict__ rep, int rep_hi,
-                                                           uint32_t rep_stride, int nrep) {
-    __shared__ LevelLds lv;
-    __shared__ __attribute__((aligned(16))) float drow[4][16][36];
-    __shared__ CoarseTable<NS> T;
-    NGP_PROBE_BEGIN(NGP_P_HASH_BWD_COARSE);
-    float* const grep = rep ? rep + (size_t)(blockIdx.x % nrep) * rep_stride : grad;
-    load_levels(ga, lv);
-    for (int i = threadIdx.x; i < NS; i += 256) T.key[i] = CT_EMPTY;
-    for (int i = threadIdx.x; i < NS * 16; i += 256) T.val[i] = 0.f;
-    if (threadIdx.x == 0) T.n_used = 0;
-    __syncthreads();
-    const uint32_t rep_fl = rep ? 2u * lv.off[rep_hi] : 0u;  // floats of the replicated levels
-    const int64_t N = n_dev ? *n_dev : n;
-    const int lane = threadIdx.x & 63, s = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1, wv = threadIdx.x >> 6;
-    const int64_t tiles = (N + 64 * TW - 1) / (64 * TW);
-    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-#pragma unroll 1
-        for (int it = 0; it < TW; ++it) {
-            const int64_t j = tile * (64 * TW) + (int64_t)(wv * TW + it) * 16 + s;  // compact position (denc row)
-            const bool valid = j < N;
-            const int64_t i = valid && sidx ? (int64_t)sidx[j] : j;
-            {
-                const int q = lane & 3;
-                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-                if (valid && 8 * q + 8 > 2 * lo && 8 * q < 2 * hi) {
-                    a = *reinterpret_cast<const float4*>(denc + j * 32 + 8 * q);
-                    b = *reinterpret_cast<const float4*>(denc + j * 32 + 8 * q + 4);
-                }
-                __builtin_amdgcn_wave_barrier();  // previous group's reads of drow are done (in order per wave)
-                *reinterpret_cast<float4*>(&drow[wv][s][8 * q]) = a;
-                *reinterpret_cast<float4*>(&drow[wv][s][8 * q + 4]) = b;
-            }
-            float in[3];
-            load_x01(xyzs, i, valid, ga, in);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 1
-            for (int l = lo; l < hi; ++l) {
-                uint32_t idx[4];
-                float v[4];
-                uint64_t heads[4];
-                coarse_level_runs(in, valid, drow[wv][s][2 * l + f], l, lv, lane, cx, idx, v, heads);
-#pragma unroll
-                for (int yz = 0; yz < 4; ++yz)
-                    if (((heads[yz] >> lane) & 1ull) && valid) {
-                        const uint32_t fi = 2u * idx[yz] + f;
-                        table_add<NS>(T, fi, v[yz], fi < rep_fl ? grep : grad);
-                    }
-            }
-        }
-        __syncthreads();  // the tile's additions are in the table
-        // flush: 16 lanes per touched line, one memory-side request each
-        const uint32_t nu = T.n_used;
-        for (uint32_t u = threadIdx.x >> 4; u < nu; u += 16) {
-            const uint32_t h = T.used[u], key = T.key[h], e = threadIdx.x & 15u;
-            const float v = T.val[h * 16 + e];
-            const uint32_t fi = key * 16u + e;
-            if (v != 0.f) atomicAdd((fi < rep_fl ? grep : grad) + fi, v);
-            T.val[h * 16 + e] = 0.f;
-            if (e == 0) T.key[h] = CT_EMPTY;
-        }
-        __syncthreads();  // the table is clear
-        if (threadIdx.x == 0) T.n_used = 0;
-        // (the next tile's first additions follow the staging of its rows; the
-        // counter reset is ordered before them by the barrier below)
-        __syncthreads();
-    }
-    NGP_PROBE_END();
-}
-
 // grad[i] += sum_r rep[r][i]; rep[r][i] = 0 (i < n4 float4 groups), replicas
 // summed in order r = 0..nrep-1; all of a lane's loads are issued first
 template <int MAXR>
@@ -1940,41 +1818,14 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
 
 }  // extern "C"
 
-// the coarse levels' scatter: the LDS-merged kernel (NGP_COARSE_LDS=1: 64-sample tiles, 512-line
-// tables; 2: 128-sample tiles, 1024-line tables) or the wave-merged one (0)
-static int g_coarse_mode = -1;  // (ngp_hash_backward_coarse_mode; -1: NGP_COARSE_LDS or the default)
-static int coarse_mode() {
-    if (g_coarse_mode < 0) g_coarse_mode = getenv("NGP_COARSE_LDS") ? atoi(getenv("NGP_COARSE_LDS")) : 1;
-    return g_coarse_mode;
-}
 static void launch_coarse(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                           const GridArgs& ga, const float* denc, float* grad_table, int lo, int hi, float* rep,
                           int rep_hi, uint32_t rep_stride, int nrep, hipStream_t s) {
-    const int mode = coarse_mode();
-    if (mode == 1) {
-        static const unsigned cap = resident_blocks(hash_bwd_lds_kernel<512, 1>, 256, 0);
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_lds_kernel<512, 1><<<persistent_blocks(n, 64, cap), 256, 0, s>>>(
-            xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
-    } else if (mode == 2) {
-        static const unsigned cap = resident_blocks(hash_bwd_lds_kernel<1024, 2>, 256, 0);
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_lds_kernel<1024, 2><<<persistent_blocks(n, 128, cap), 256, 0, s>>>(
-            xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
-    } else {
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<persistent_blocks(n, 64, HASH_BWD_BLOCKS), 256, 0, s>>>(
-            xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
-    }
+    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<persistent_blocks(n, 64, HASH_BWD_BLOCKS), 256, 0, s>>>(
+        xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
 }
 
 extern "C" {
-
-int ngp_hash_backward_coarse_mode(int mode) {
-    const int prev = coarse_mode();
-    if (mode >= 0) {
-        if (mode > 2) return NGP_EINVAL;
-        g_coarse_mode = mode;
-    }
-    return prev;
-}
 
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,

@@ -257,6 +257,7 @@ __global__ void __launch_bounds__(256) hash_scan_kernel(const int64_t* __restric
 // bucket regions + chunk items (one workgroup of MAXB / 2 threads, two buckets each)
 __global__ void __launch_bounds__(MAXB / 2) hash_plan_kernel(uint32_t nbt, BinWs ws) {
     __shared__ uint32_t a[MAXB / 2], c[MAXB / 2];
+    NGP_PROBE_BEGIN(NGP_P_HASH_PLAN);
     const uint32_t t = threadIdx.x, b0 = 2 * t, b1 = 2 * t + 1;
     const uint32_t t0 = b0 < nbt ? ws.tot[b0] : 0u, t1 = b1 < nbt ? ws.tot[b1] : 0u;
     const uint32_t c0 = (t0 + CH - 1) / CH, c1 = (t1 + CH - 1) / CH;
@@ -278,6 +279,7 @@ __global__ void __launch_bounds__(MAXB / 2) hash_plan_kernel(uint32_t nbt, BinWs
     // item -> bucket table (one entry per chunk; usually one chunk per bucket)
     for (uint32_t it = c[t] - c1 - c0; it < c[t] - c1 && it < IB_CAP; ++it) ws.ib[it] = b0;
     for (uint32_t it = c[t] - c1; it < c[t] && it < IB_CAP; ++it) ws.ib[it] = b1;
+    NGP_PROBE_END();
 }
 
 // MODE bits: 2 = store each record from registers at its rank (the product
@@ -692,6 +694,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
 __global__ void __launch_bounds__(256) hash_adam_residual_kernel(GridArgs ga, BinArgs ba, uint32_t nbt,
                                                                   float* __restrict__ grad, BinWs ws, AdamArgs adam,
                                                                   uint32_t b_lo) {
+    NGP_PROBE_BEGIN(NGP_P_RESIDUAL);
     const uint32_t b = b_lo + blockIdx.x;
     const bool mine = b < nbt && !fused_bucket(ws, b, ws.fb[MAXB] != 0);  // (block-uniform)
     float lr = 0.f, bc1 = 1.f, bc2 = 1.f;
@@ -708,6 +711,7 @@ __global__ void __launch_bounds__(256) hash_adam_residual_kernel(GridArgs ga, Bi
             g4[e] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
+    NGP_PROBE_END();
 }
 
 static int bin_args(const ngp_hashgrid_t* grid, int64_t tiles_cap, int lo, int merge_hi, BinArgs& ba,

@@ -129,6 +129,7 @@ __global__ void __launch_bounds__(256) sample_batch_kernel(
     const float* __restrict__ center, const float* __restrict__ half_size, float near, int64_t* __restrict__ img_idx,
     int64_t* __restrict__ pix_idx, float* __restrict__ rgb_gt, float* __restrict__ noise,
     float* __restrict__ rays_o, float* __restrict__ rays_d, float* __restrict__ hits_t) {
+    NGP_PROBE_BEGIN(NGP_P_SAMPLE_BATCH);
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_rays) return;
     if (step_dev) step += (uint64_t)*step_dev;  // device counter + offset (graph replays)
@@ -149,6 +150,7 @@ __global__ void __launch_bounds__(256) sample_batch_kernel(
     }
     gen_ray(poses + img * 12, directions + pix * 3, center, half_size, near, rays_o + 3 * r, rays_d + 3 * r,
             hits_t + 2 * r);
+    NGP_PROBE_END();
 }
 
 // random_bg (models/rendering.py:287-288: rgb_bg = torch.rand(3) per batch),
@@ -539,6 +541,7 @@ __global__ void __launch_bounds__(256) march_compact_kernel(const float* __restr
                                                             const float* __restrict__ slot_dt, int max_samples,
                                                             float* __restrict__ xyzs, float* __restrict__ dirs,
                                                             float* __restrict__ deltas, float* __restrict__ ts) {
+    NGP_PROBE_BEGIN(NGP_P_COMPACT);
     const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (r >= n_rays) return;
@@ -556,6 +559,7 @@ __global__ void __launch_bounds__(256) march_compact_kernel(const float* __restr
         ts[s] = t;
         deltas[s] = sd[k];
     }
+    NGP_PROBE_END();
 }
 
 // raymarching.cu:335-404 (test time), zero-filling unused slots itself.

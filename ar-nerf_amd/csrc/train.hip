@@ -873,6 +873,7 @@ __global__ void __launch_bounds__(SEG_THREADS) segments_kernel(const int32_t* __
     __shared__ int64_t red[SEG_THREADS / 64];
     __shared__ int32_t lofs[SEG_ROWS + 1];
     __shared__ int64_t src[SEG_ROWS];
+    NGP_PROBE_BEGIN(NGP_P_SEGMENTS);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int64_t r0 = (int64_t)blockIdx.x * SEG_ROWS, r1 = min(r0 + SEG_ROWS, n_rows);
     auto count = [&](int64_t r) -> int64_t {
@@ -927,6 +928,7 @@ __global__ void __launch_bounds__(SEG_THREADS) segments_kernel(const int32_t* __
         }
         sample_idx[prefix + q] = (int32_t)(src[lo] + (q - lofs[lo]));
     }
+    NGP_PROBE_END();
 }
 
 static void launch_segments(const int32_t* counts, const int64_t* rays_a, int64_t n_rows, int cap, int first,
@@ -993,6 +995,7 @@ __global__ void __launch_bounds__(1024) rays_nonempty_kernel(const int64_t* __re
                                                              int32_t* __restrict__ rest, int64_t* __restrict__ zero) {
     __shared__ int32_t wave_sums[16];
     __shared__ int64_t carry_s;
+    NGP_PROBE_BEGIN(NGP_P_NONEMPTY);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     if (tid == 0) carry_s = 0;
     __syncthreads();
@@ -1040,6 +1043,7 @@ __global__ void __launch_bounds__(1024) rays_nonempty_kernel(const int64_t* __re
         *n_out = carry_s;
         if (zero) *zero = 0;
     }
+    NGP_PROBE_END();
 }
 
 // Round-2 list in one launch: chunk_rest_kernel's counts + the exclusive scan
@@ -1344,7 +1348,9 @@ int ngp_adam_step_dev_rep(float* params, float* grads, float* exp_avg, float* ex
 // counters[i] += 1 for i < n (the per-step device counters a replayed graph
 // advances at its end: Adam's step count, the batch RNG counter)
 __global__ void counters_inc_kernel(int64_t* __restrict__ c, int n) {
+    NGP_PROBE_BEGIN(NGP_P_COUNTERS);  // (the row of the step the increment closes: read before it)
     if ((int)threadIdx.x < n) c[threadIdx.x] += 1;
+    NGP_PROBE_END();
 }
 
 int ngp_counters_inc(int64_t* counters, int n, void* stream) {

@@ -59,8 +59,6 @@ def _lib():
         L.ngp_hash_backward_levels.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp]
         L.ngp_hash_backward_levels_rep.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp, c_int, c_int, c_int,
                                                    vp]
-        L.ngp_hash_backward_coarse_mode.argtypes = [c_int]
-        L.ngp_hash_backward_coarse_mode.restype = c_int
         L.ngp_hash_backward_rep_floats.argtypes = [P, c_int, c_int]
         L.ngp_hash_backward_rep_floats.restype = ctypes.c_size_t
         L.ngp_hash_binned_plan.argtypes = [vp, c_int64, vp, vp, P, vp, c_int64, c_int, c_int, vp]

@@ -123,7 +123,8 @@ class KernelTimer:
 
 # include/ngp_amd.h NGP_P_* order
 PROBES = ["march", "first_chunk", "field_encode_mlp", "composite_loss", "mlp_bwd", "hash_bwd_coarse", "hash_count",
-          "hash_write", "hash_accum", "adam"]
+          "hash_write", "hash_accum", "adam", "segments", "rays_nonempty", "counters_inc", "hash_plan", "adam_residual",
+          "march_compact", "sample_batch"]
 
 
 class ProbeTimer:
@@ -177,3 +178,23 @@ class ProbeTimer:
     def summary(self, skip_rows=()):
         """{probe: (avg ms per launch, launches counted)}"""
         return {k: (sum(m for _, m in v) / len(v), len(v)) for k, v in self.spans(skip_rows).items()}
+
+    def timeline(self, skip_rows=(), origin="first_chunk"):
+        """{probe: (avg start us, avg end us)} relative to the start of `origin`
+        in the same step row: the step's schedule as the kernels ran (no
+        stamp kernels in the graph), over the rows where both ran"""
+        b = self.buf
+        big = torch.iinfo(torch.int64).max
+        st = torch.where(b[..., 0] > 0, b[..., 0], torch.full_like(b[..., 0], big)).min(-1).values.cpu()
+        en = b[..., 1].max(-1).values.cpu()
+        o = PROBES.index(origin)
+        skip = set(skip_rows)
+        out = {}
+        for k, n in enumerate(PROBES):
+            rows = [r for r in range(self.rows) if r not in skip and en[r, k] > 0 and st[r, k] < big
+                    and en[r, o] > 0 and st[r, o] < big]
+            if rows:
+                s0 = sum(float(st[r, k] - st[r, o]) for r in rows) / len(rows) * self.tick_ns * 1e-3
+                e0 = sum(float(en[r, k] - st[r, o]) for r in rows) / len(rows) * self.tick_ns * 1e-3
+                out[n] = (round(s0, 1), round(e0, 1))
+        return dict(sorted(out.items(), key=lambda kv: kv[1][0]))

@@ -538,6 +538,7 @@ def main():
     skip = [r for r in range(probes.rows) if any(st % ui == 0 for st in range(s_rf, s_rf + ran_rf)
                                                  if st % probes.rows == r)]
     pr_summary = probes.summary(skip_rows=skip)
+    pr_timeline = probes.timeline(skip_rows=skip)
     m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         e_rf = m_rf
@@ -661,6 +662,7 @@ def main():
             "ops": ops,
             "kernels": kernels,
             "timeline_us": bd_timeline,
+            "probe_timeline_us": pr_timeline,
             "step_bound": step_bound,
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "breakdown_note": (f"ops / kernels: wall-clock stamps around every kernel inside the captured graphs "

@@ -71,7 +71,8 @@ double ngp_timing_tick_ns(void);
 #define NGP_PROBE_WAVES 65536
 enum {
     NGP_P_MARCH = 0, NGP_P_FIRST_CHUNK, NGP_P_FIELD_ENCODE_MLP, NGP_P_COMPOSITE, NGP_P_MLP_BWD, NGP_P_HASH_BWD_COARSE,
-    NGP_P_HASH_COUNT, NGP_P_HASH_WRITE, NGP_P_HASH_ACCUM, NGP_P_ADAM,
+    NGP_P_HASH_COUNT, NGP_P_HASH_WRITE, NGP_P_HASH_ACCUM, NGP_P_ADAM, NGP_P_SEGMENTS, NGP_P_NONEMPTY, NGP_P_COUNTERS,
+    NGP_P_HASH_PLAN, NGP_P_RESIDUAL, NGP_P_COMPACT, NGP_P_SAMPLE_BATCH,
     NGP_P_COUNT
 };
 int ngp_probe_set(uint64_t* buf, const int64_t* step_dev, int64_t ring);
@@ -493,15 +494,7 @@ int ngp_hash_binned_accum_adam(const ngp_hashgrid_t* grid, float* grad_table, vo
                                int level_lo, int merge_hi, float* params, float* exp_avg, float* exp_avg_sq,
                                void* params_f16, const float* lr_dev, float beta1, float beta2, float eps,
                                const int64_t* step_dev, float grad_scale, void* stream);
-/* ngp_hash_backward restricted to levels [level_lo, level_hi).  The levels'
- * scatter merges each workgroup's additions in LDS first (tiles of 64
- * consecutive samples, their run heads summed per 64-B gradient line in an LDS
- * table, one memory-side add per touched line: ~2.3x fewer atomic requests
- * than merging runs per wave) -- ngp_hash_backward_coarse_mode selects it
- * (1, default; 2: 128-sample tiles) or the per-wave merge (0) for the
- * ngp_hash_backward_levels* calls that follow and returns the previous mode
- * (mode < 0: query only).  Same sums in every mode up to fp32 order. */
-int ngp_hash_backward_coarse_mode(int mode);
+/* ngp_hash_backward restricted to levels [level_lo, level_hi). */
 int ngp_hash_backward_levels(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                              const ngp_hashgrid_t* grid, const float* denc, float* grad_table, int level_lo,
                              int level_hi, void* stream);

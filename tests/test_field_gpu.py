@@ -364,16 +364,13 @@ def test_forward_first_with_preencoded_coarse_levels_is_bit_identical():
 
 
 @pytest.mark.parametrize("layout", ["rays", "scattered"])
-def test_coarse_scatter_modes_match_oracle(layout):
-    """ngp_hash_backward_levels(_rep) over levels 0-7 in every coarse mode --
-    0: runs merged per wave, memory-side atomics per head; 1 / 2: the block's
-    heads merged per 64-B gradient line in an LDS table, one add per touched
-    line (64- / 128-sample tiles) -- against the oracle's hash backward
-    (oracle.hash_encode_bwd, tcnn's scatter restated in C) on the same
-    samples: rel-L2 per level <= 1e-5 (fp32 summation order only).
-    "scattered": uncorrelated positions, so a tile touches more lines than the
-    LDS table holds and the table-full path (direct adds) runs too; the
-    replicated call must leave its replicas zero."""
+def test_coarse_scatter_matches_oracle(layout):
+    """ngp_hash_backward_levels(_rep) over levels 0-7 (runs merged per wave,
+    memory-side atomics per run head; levels 0-3 into 8 replicas in the _rep
+    form) against the oracle's hash backward (oracle.hash_encode_bwd, tcnn's
+    scatter restated in C) on the same samples: rel-L2 per level <= 1e-5
+    (fp32 summation order only); "scattered": no runs to merge; the replicated
+    call leaves its replicas zero and nothing outside levels 0-7 is touched."""
     if layout == "rays":
         x = _ray_points(600, 120, 0.5, seed=11)
     else:  # marched samples in random order: no two consecutive ones on one ray
@@ -394,29 +391,22 @@ def test_coarse_scatter_modes_match_oracle(layout):
     xd, sd, dd = x.to(DEV), sidx.to(DEV), denc.to(DEV)
     n_dev = torch.tensor([m], dtype=torch.int64, device=DEV)
     rep = torch.zeros(L.ngp_hash_backward_rep_floats(desc, 4, 8), device=DEV)
-    prev = L.ngp_hash_backward_coarse_mode(-1)
-    try:
-        for mode in (0, 1, 2):
-            assert L.ngp_hash_backward_coarse_mode(mode) >= 0
-            for replicated in (False, True):
-                out = torch.zeros(grid.n_entries * 2, device=DEV)
-                if replicated:
-                    vren._ok(L.ngp_hash_backward_levels_rep(p(xd), n, p(n_dev), p(sd), desc, p(dd), p(out), 0, 8,
-                                                            p(rep), 4, 8, 1, vren._stream()), "levels_rep")
-                else:
-                    vren._ok(L.ngp_hash_backward_levels(p(xd), n, p(n_dev), p(sd), desc, p(dd), p(out), 0, 8,
-                                                        vren._stream()), "levels")
-                torch.cuda.synchronize()
-                assert float(rep.abs().max()) == 0.0
-                got = out.cpu().double()
-                for lv in range(8):
-                    a, b = 2 * int(grid.offsets[lv]), 2 * int(grid.offsets[lv + 1])
-                    assert float(ref[a:b].abs().max()) > 0
-                    assert _rel(got[a:b], ref[a:b]) < 1e-5, (mode, replicated, lv, _rel(got[a:b], ref[a:b]))
-                assert float(got[2 * int(grid.offsets[8]):].abs().max()) == 0.0  # nothing outside levels 0-7
-    finally:
-        L.ngp_hash_backward_coarse_mode(prev)
-    assert L.ngp_hash_backward_coarse_mode(3) < 0
+    for replicated in (False, True):
+        out = torch.zeros(grid.n_entries * 2, device=DEV)
+        if replicated:
+            vren._ok(L.ngp_hash_backward_levels_rep(p(xd), n, p(n_dev), p(sd), desc, p(dd), p(out), 0, 8,
+                                                    p(rep), 4, 8, 1, vren._stream()), "levels_rep")
+        else:
+            vren._ok(L.ngp_hash_backward_levels(p(xd), n, p(n_dev), p(sd), desc, p(dd), p(out), 0, 8,
+                                                vren._stream()), "levels")
+        torch.cuda.synchronize()
+        assert float(rep.abs().max()) == 0.0
+        got = out.cpu().double()
+        for lv in range(8):
+            a, b = 2 * int(grid.offsets[lv]), 2 * int(grid.offsets[lv + 1])
+            assert float(ref[a:b].abs().max()) > 0
+            assert _rel(got[a:b], ref[a:b]) < 1e-5, (replicated, lv, _rel(got[a:b], ref[a:b]))
+        assert float(got[2 * int(grid.offsets[8]):].abs().max()) == 0.0  # nothing outside levels 0-7
 
 
 @pytest.mark.parametrize("rep_levels,n_rep", [(4, 8), (8, 16), (2, 1)])

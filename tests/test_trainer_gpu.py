@@ -361,52 +361,6 @@ def test_pair_step_replays_match_single_steps():
     assert abs(lp - la) <= 0.1 * abs(la) + 3 * abs(lb - la)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-def test_lds_merged_coarse_scatter_matches_the_wave_merged_one(mode):
-    """The coarse (atomic) hash levels scattered with the block's additions
-    merged per 64-B gradient line in LDS (ngp_hash_backward_coarse_mode 1 / 2:
-    64- / 128-sample tiles) add the same gradient as the per-wave run merge
-    (mode 0): the same training step from the same state, the MLP +
-    coarse-level gradient the coarse Adam launch consumes (gradient + its
-    folded replicas) agrees per parameter group to fp32 atomic-order noise."""
-    import hashgrid as HG
-    grads = []
-    L = HG._lib()
-    prev = L.ngp_hash_backward_coarse_mode(-1)
-    for m in (0, mode):
-        L.ngp_hash_backward_coarse_mode(m)
-        sc, tr, img, pix, noise = _setup(table_init=0.2)
-        seen = {}
-        orig = tr._adam
-
-        def spy(lo, hi, s, rep=False, tr=tr, seen=seen, orig=orig):
-            if lo == 0:  # the MLP + coarse levels' Adam: its gradient incl. the unfolded replicas
-                g = tr.grad[lo:hi].clone()
-                if rep:
-                    n = 2 * int(tr.grid.offsets[tr.coarse_rep_levels])
-                    g[HG.MLP_PARAMS:HG.MLP_PARAMS + n] += tr.rep_buf.view(tr.coarse_rep, n).sum(0)
-                seen["g"] = g
-            orig(lo, hi, s, rep)
-        tr._adam = spy
-        dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
-        o, d = sc.rays(img, pix)
-        gt = sc.gt_rgb_rays(o, d).to(DEV)
-        tr.step(img.to(DEV), pix.to(DEV), gt, dirs, poses, noise=noise.to(DEV))
-        torch.cuda.synchronize()
-        grads.append((seen["g"].cpu(), tr))
-    L.ngp_hash_backward_coarse_mode(prev)
-    (ga, tra), (gb, _) = grads
-    offs = [0, 3072, HG.MLP_PARAMS] + [HG.MLP_PARAMS + 2 * int(tra.grid.offsets[l]) for l in range(1, tra.bin_level_lo + 1)]
-    worst = 0.0
-    for a, b in zip(offs[:-1], offs[1:]):
-        ref = ga[a:b].double()
-        if float(ref.norm()) == 0:
-            continue
-        worst = max(worst, float((gb[a:b].double() - ref).norm() / ref.norm()))
-    print(f"LDS-merged coarse scatter (mode {mode}) vs wave-merged: worst group relative L2 {worst:.2e}")
-    assert worst < 1e-5
-
-
 def test_preencoded_round1_trains_like_the_plain_forward():
     """Round 1's coarse levels encoded ahead beside the previous step's
     accumulation (NGPTrainer.pre_coarse, the default) train like the plain
