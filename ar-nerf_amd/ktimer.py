@@ -179,6 +179,21 @@ class ProbeTimer:
         """{probe: (avg ms per launch, launches counted)}"""
         return {k: (sum(m for _, m in v) / len(v), len(v)) for k, v in self.spans(skip_rows).items()}
 
+    def step_gaps(self, first="first_chunk", last="counters_inc"):
+        """[(row, us)]: from the end of row r's `last` kernel to the start of
+        row r + 1's `first` (the step boundary: inside a two-step graph, or
+        between two graph replays), over consecutive rows where both ran"""
+        b = self.buf
+        big = torch.iinfo(torch.int64).max
+        st = torch.where(b[..., 0] > 0, b[..., 0], torch.full_like(b[..., 0], big)).min(-1).values.cpu()
+        en = b[..., 1].max(-1).values.cpu()
+        f, l = PROBES.index(first), PROBES.index(last)
+        out = []
+        for r in range(self.rows - 1):
+            if en[r, l] > 0 and st[r + 1, f] < big:
+                out.append((r, round(float(st[r + 1, f] - en[r, l]) * self.tick_ns * 1e-3, 1)))
+        return out
+
     def timeline(self, skip_rows=(), origin="first_chunk"):
         """{probe: (avg start us, avg end us)} relative to the start of `origin`
         in the same step row: the step's schedule as the kernels ran (no

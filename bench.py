@@ -539,6 +539,7 @@ def main():
                                                  if st % probes.rows == r)]
     pr_summary = probes.summary(skip_rows=skip)
     pr_timeline = probes.timeline(skip_rows=skip)
+    pr_gaps = probes.step_gaps()
     m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         e_rf = m_rf
@@ -663,6 +664,11 @@ def main():
             "kernels": kernels,
             "timeline_us": bd_timeline,
             "probe_timeline_us": pr_timeline,
+            "probe_step_gaps_us": {"gaps": [g for _, g in pr_gaps],
+                                   "mean": round(sum(g for _, g in pr_gaps) / max(1, len(pr_gaps)), 1),
+                                   "note": "end of a step's counters_inc to the next step's round 1, per "
+                                           "consecutive step pair of the probe window (two steps per graph "
+                                           "replay: alternately inside a graph and across a replay boundary)"},
             "step_bound": step_bound,
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "breakdown_note": (f"ops / kernels: wall-clock stamps around every kernel inside the captured graphs "

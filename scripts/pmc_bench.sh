@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 RE=${1:-field_fwd}
 OUT=gpurun_out/pmc_${2:-run}
 mkdir -p "$OUT"
-BENCH="python3 bench.py --steps 10 --warmup 2 --psnr-views 0 --no-cpu-baseline --infer-frames 0 --quality-steps 0 --no-oracle-quality"
+BENCH="python3 bench.py --steps 10 --warmup 2 --psnr-views 0 --no-cpu-baseline --infer-frames 0 --quality-steps 0 --no-oracle-quality --dropin-steps 0"
 pass() {
     name=$1; shift
     timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$RE" -d "$OUT/$name" -o run -f csv -- $BENCH > "$OUT/$name.log" 2>&1
