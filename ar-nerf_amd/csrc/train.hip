@@ -739,6 +739,93 @@ __global__ void __launch_bounds__(OSC_T) occ_sample_sorted_kernel(
     }
 }
 
+// The occupancy samples whose sigma survives density_grid_tmp[c, idx] =
+// sigma's last-write-wins (networks.py:268): of the sorted 2M-sample list
+// (each half ascending, ngp_occupancy_samples_sorted), position i is kept iff
+// no later position holds its cell -- the last of its run within its half
+// (duplicates are adjacent there), and, in the uniform half, only if the
+// occupied half does not draw the cell at all.  Only kept positions need a
+// density evaluation: the others' sigmas would be overwritten.
+// occ_mark_kernel: byte per cell, set for every occupied-half cell (plain
+// byte stores of one value: no atomics); occ_keep_kernel: the kept positions
+// of [lo, hi), compacted per 8192-position block (one reservation per block).
+__global__ void __launch_bounds__(256) zero_u4_kernel(uint4* __restrict__ p, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+__global__ void __launch_bounds__(256) occ_mark_kernel(const int64_t* __restrict__ flat, int64_t M, int64_t cell_base,
+                                                       int64_t n_cells, uint8_t* __restrict__ mark) {
+    const int64_t i = M + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= 2 * M) return;
+    const int64_t c = flat[i] - cell_base;
+    if (c >= 0 && c < n_cells) mark[c] = 1;
+}
+
+constexpr int KEEP_T = 1024, KEEP_PER = 8;
+__global__ void __launch_bounds__(KEEP_T) occ_keep_kernel(const int64_t* __restrict__ flat, int64_t M,
+                                                          int64_t cell_base, int64_t n_cells,
+                                                          const uint8_t* __restrict__ mark, int64_t lo, int64_t hi,
+                                                          int32_t* __restrict__ list,
+                                                          unsigned long long* __restrict__ count) {
+    __shared__ uint32_t wcnt[KEEP_T / 64];
+    __shared__ unsigned long long base;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int64_t i0 = lo + ((int64_t)blockIdx.x * KEEP_T + tid) * KEEP_PER;
+    bool keep[KEEP_PER];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < KEEP_PER; ++k) {
+        const int64_t i = i0 + k;
+        bool kp = false;
+        if (i < hi) {
+            const int64_t f = flat[i];
+            const int64_t end = i < M ? M : 2 * M;  // the end of i's half
+            kp = f >= 0 && (i + 1 == end || flat[i + 1] != f);
+            if (kp && i < M) {
+                const int64_t c = f - cell_base;
+                kp = !(c >= 0 && c < n_cells && mark[c]);
+            }
+        }
+        keep[k] = kp;
+        mine += kp;
+    }
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wcnt[wid] = incl;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < KEEP_T / 64; ++w) { const uint32_t v = wcnt[w]; wcnt[w] = tot; tot += v; }
+        base = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    int64_t pos = (int64_t)base + wcnt[wid] + incl - mine;
+#pragma unroll
+    for (int k = 0; k < KEEP_PER; ++k)
+        if (keep[k]) list[pos++] = (int32_t)(i0 + k);
+}
+
+// scatter_last_kernel over the kept positions list[j], j < *count: sample i =
+// list[j] (list position pos_base + i) with its cell flat[i] and sigma sig[i]
+__global__ void __launch_bounds__(256) scatter_kept_kernel(const int32_t* __restrict__ list,
+                                                           const int64_t* __restrict__ count, int64_t n_max,
+                                                           const int64_t* __restrict__ flat,
+                                                           const float* __restrict__ sig, int64_t pos_base,
+                                                           unsigned long long* __restrict__ key) {
+    const int64_t nk = min(*count, n_max);
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nk; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = list[j];
+        const int64_t c = flat[i];
+        if (c < 0) continue;
+        const unsigned long long k = ((unsigned long long)(pos_base + i + 1) << 32) | __float_as_uint(fmaxf(sig[i], 0.f));
+        atomicMax(key + c, k);
+    }
+}
+
 // models/networks.py:270-278: grid = where(grid<0, grid, max(grid*decay, tmp)),
 // decay per cell when decay_cells != nullptr (erode, networks.py:270-272:
 // clamp(decay**(1/count_grid), 0.1, 0.95), evaluated once per count grid by the
@@ -1425,6 +1512,36 @@ int ngp_occupancy_samples_sorted(uint64_t seed, const int64_t* counter_dev, int 
                                                                  s_minus_hgs, hgs, occ_list,
                                                                  (const unsigned long long*)occ_count, sums, lo, hi,
                                                                  xyzs, flat_idx);
+    return ngp_launch_status();
+}
+
+int ngp_occupancy_keep(const int64_t* flat_idx, int64_t M, int64_t cell_base, int64_t n_cells, int64_t lo, int64_t hi,
+                       void* mark_ws, int32_t* list, int64_t* count, void* stream) {
+    NGP_CHECK_ARG(M >= 0 && n_cells > 0 && cell_base >= 0 && lo >= 0 && lo <= hi && hi <= 2 * M &&
+                  hi < (1ll << 31) && flat_idx && mark_ws && list && count && ((uintptr_t)count & 7) == 0);
+    NGP_CHECK_ARG(((uintptr_t)mark_ws & 15) == 0);
+    hipStream_t s = as_stream(stream);
+    zero_words_kernel<<<1, 64, 0, s>>>((unsigned long long*)count, 1);  // (kernel nodes, not memsets: see above)
+    if (hi == lo) return ngp_launch_status();
+    const int64_t n16 = (n_cells + 15) / 16;
+    zero_u4_kernel<<<(unsigned)((n16 + 255) / 256), 256, 0, s>>>((uint4*)mark_ws, n16);
+    if (M > 0)
+        occ_mark_kernel<<<(unsigned)((M + 255) / 256), 256, 0, s>>>(flat_idx, M, cell_base, n_cells, (uint8_t*)mark_ws);
+    const int64_t per_blk = (int64_t)KEEP_T * KEEP_PER;
+    occ_keep_kernel<<<(unsigned)((hi - lo + per_blk - 1) / per_blk), KEEP_T, 0, s>>>(
+        flat_idx, M, cell_base, n_cells, (const uint8_t*)mark_ws, lo, hi, list, (unsigned long long*)count);
+    return ngp_launch_status();
+}
+
+int ngp_density_scatter_kept(const int32_t* list, const int64_t* count, int64_t n_max, const int64_t* indices,
+                             const float* sigmas, int64_t pos_base, uint64_t* grid_key, void* stream) {
+    NGP_CHECK_ARG(n_max >= 0 && pos_base >= 0 && pos_base + n_max < (1ll << 31));
+    if (n_max == 0) return NGP_OK;
+    NGP_CHECK_ARG(list && count && indices && sigmas && grid_key && ((uintptr_t)grid_key & 7) == 0);
+    static const unsigned cap = resident_blocks(scatter_kept_kernel, 256, 0);
+    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_max + 255) / 256)));
+    scatter_kept_kernel<<<blocks, 256, 0, as_stream(stream)>>>(list, count, n_max, indices, sigmas, pos_base,
+                                                              reinterpret_cast<unsigned long long*>(grid_key));
     return ngp_launch_status();
 }
 

@@ -83,6 +83,8 @@ def _declare(L):
         "ngp_adam_step": [vp, vp, vp, vp, vp, c_int64, c_float, c_float, c_float, c_float, c_int64, c_float, c_int,
                           vp],
         "ngp_density_scatter_last": [vp, vp, c_int64, c_int64, vp, vp],
+        "ngp_occupancy_keep": [vp, c_int64, c_int64, c_int64, c_int64, c_int64, vp, vp, vp, vp],
+        "ngp_density_scatter_kept": [vp, vp, c_int64, vp, vp, c_int64, vp, vp],
         "ngp_density_grid_ema": [vp, vp, c_int64, c_float, vp, c_float, vp, vp, vp],
         "ngp_distortion_loss_fw": [vp, vp, vp, vp, c_int64, vp, vp, vp, vp],
         "ngp_distortion_loss_bw": [vp, vp, vp, vp, vp, vp, vp, c_int64, vp, vp],

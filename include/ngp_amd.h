@@ -389,23 +389,6 @@ int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* d
                             float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
                             void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int32_t* list2,
                             int64_t* total2, int64_t* evaluated, void* stream);
-/* ngp_field_forward_first whose levels [0, pre_levels) (pre_levels 0 or 8) are
- * already in enc_pm for the first-chunk samples (ngp_field_encode_first_coarse
- * with the same rows and parameters): read back instead of gathered, and not
- * rewritten.  Same outputs bit for bit. */
-int ngp_field_forward_first_pre(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
-                                const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
-                                float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16,
-                                const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs, int32_t* rest,
-                                int32_t* list2, int64_t* total2, int64_t* evaluated, int pre_levels, void* stream);
-/* The coarse levels 0-7 of ngp_field_forward_first's encoding, ahead of time:
- * for the rows rows[j], j < *n_rows_dev (as there), the first min(N, 64)
- * samples' level features written to enc_pm pairs 0-3 (plane stride n).  The
- * training step runs it for the NEXT batch once the coarse levels' Adam has
- * run, beside the binned levels' accumulation. */
-int ngp_field_encode_first_coarse(const float* xyzs, const int64_t* rays_a, const int32_t* rows,
-                                  const int64_t* n_rows_dev, int64_t n_rows, int64_t n, const ngp_hashgrid_t* grid,
-                                  const void* table_f16, void* enc_pm, void* stream);
 int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev,
                           const int32_t* sample_idx, const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16,
                           void* stream);
@@ -684,6 +667,25 @@ int ngp_occupancy_samples_sorted(uint64_t seed, const int64_t* counter_dev, int 
                                  float s_minus_hgs, float hgs, const int32_t* occ_list, const int64_t* occ_count,
                                  int64_t lo, int64_t hi, void* workspace, float* xyzs, int64_t* flat_idx,
                                  void* stream);
+/* The samples of ngp_occupancy_samples_sorted's full list (positions [0, 2M),
+ * flat_idx; each half ascending) whose sigma the update keeps: position i
+ * survives density_grid_tmp[c, idx] = sigma's last-write-wins
+ * (networks.py:268; ngp_density_scatter_last's rule) iff no later position
+ * holds its cell -- the last of its run in its half, and in the uniform half
+ * only a cell the occupied half does not draw.  Lists the kept positions of
+ * [lo, hi) (ascending within each 8192-position block, blocks in any order)
+ * and *count = their number (device, 8-byte aligned).  cell_base = cascade *
+ * n_cells; mark_ws: n_cells bytes of scratch, 16-byte aligned.  Evaluating
+ * only these (ngp_field_encode_mlp with sample_idx = list) and scattering them
+ * with ngp_density_scatter_kept leaves the same key grid as evaluating and
+ * scattering all of [lo, hi). */
+int ngp_occupancy_keep(const int64_t* flat_idx, int64_t M, int64_t cell_base, int64_t n_cells, int64_t lo,
+                       int64_t hi, void* mark_ws, int32_t* list, int64_t* count, void* stream);
+/* ngp_density_scatter_last over the listed positions i = list[j], j <
+ * min(*count, n_max): key of cell indices[i] max= (pos_base + i + 1) << 32 |
+ * sigma bits of sigmas[i]. */
+int ngp_density_scatter_kept(const int32_t* list, const int64_t* count, int64_t n_max, const int64_t* indices,
+                             const float* sigmas, int64_t pos_base, uint64_t* grid_key, void* stream);
 
 #ifdef __cplusplus
 }

@@ -272,3 +272,85 @@ def test_sampled_update_matches_reference_glue():
     b = torch.maximum(_warm_bounds(fm, cells, jits), _sampled_bounds(fm, cells, log2, occupied))
     _check_flips(cells, m.density_grid, b, "sampled update")
     assert abs(int(np.unpackbits(got).sum()) - int(fx["upd_popcount"])) <= cells.numel()
+
+
+@pytest.mark.parametrize("lo_hi", ["all", "head", "tail", "empty"])
+def test_occupancy_keep_lists_each_cells_last_draw(lo_hi):
+    """ngp_occupancy_keep: of a 2M-sample list shaped as the sorted sampler
+    emits it (each half ascending, duplicates adjacent, some cells in both
+    halves, empty-list markers -1), exactly the positions in [lo, hi) that no
+    later position repeats -- the samples density_grid_tmp's last-write-wins
+    keeps (networks.py:268) -- with their count; then ngp_density_scatter_kept
+    over the shards [0, lo), [lo, hi), [hi, 2M) leaves the key grid
+    ngp_density_scatter_last leaves over the whole list."""
+    g = torch.Generator().manual_seed(7)
+    G3, M, cascade = 4096, 3000, 1
+    base = cascade * G3
+    uni = torch.sort(torch.randint(0, G3, (M,), generator=g)).values
+    occ_cells = torch.sort(torch.randperm(G3, generator=g)[:300]).values
+    occ = torch.sort(occ_cells[torch.randint(0, 300, (M,), generator=g)]).values
+    flat = torch.cat([uni, occ]).to(torch.int64) + base
+    flat[2 * M - 5:] = -1  # (markers: skipped)
+    lo, hi = {"all": (0, 2 * M), "head": (0, M + 7), "tail": (M - 5, 2 * M), "empty": (1234, 1234)}[lo_hi]
+    last = {}
+    for i, f in enumerate(flat.tolist()):
+        if f >= 0:
+            last[f] = i
+    want = sorted(i for i in last.values() if lo <= i < hi)
+    L = vren.lib()
+    dflat = flat.to(DEV)
+    mark = torch.empty(G3 // 4, dtype=torch.int32, device=DEV)
+    kept = torch.full((2 * M,), -7, dtype=torch.int32, device=DEV)
+    cnt = torch.full((1,), 99, dtype=torch.int64, device=DEV)
+    vren._ok(L.ngp_occupancy_keep(dflat.data_ptr(), M, base, G3, lo, hi, mark.data_ptr(), kept.data_ptr(),
+                                  cnt.data_ptr(), vren._stream()), "occupancy_keep")
+    torch.cuda.synchronize()
+    n = int(cnt.item())
+    assert n == len(want)
+    assert sorted(kept[:n].cpu().tolist()) == want
+    # scatter: the kept samples of [0, lo), [lo, hi), [hi, 2M) (three ranks' shards, MAX-combined by
+    # scattering into one key grid) == every sample of the list (the last position wins)
+    sig = torch.rand(2 * M, generator=g).to(DEV)
+    k_all = torch.zeros(2 * G3, dtype=torch.int64, device=DEV)
+    k_kept = torch.zeros_like(k_all)
+    vren._ok(L.ngp_density_scatter_last(dflat.data_ptr(), sig.data_ptr(), 2 * M, 0, k_all.data_ptr(),
+                                        vren._stream()), "scatter_last")
+    for a, b in ((0, lo), (lo, hi), (hi, 2 * M)):
+        vren._ok(L.ngp_occupancy_keep(dflat.data_ptr(), M, base, G3, a, b, mark.data_ptr(), kept.data_ptr(),
+                                      cnt.data_ptr(), vren._stream()), "occupancy_keep")
+        vren._ok(L.ngp_density_scatter_kept(kept.data_ptr(), cnt.data_ptr(), b - a, dflat.data_ptr(),
+                                            sig.data_ptr(), 0, k_kept.data_ptr(), vren._stream()), "scatter_kept")
+    torch.cuda.synchronize()
+    assert torch.equal(k_all, k_kept)
+
+
+def test_trainer_update_with_kept_samples_is_bit_identical():
+    """NGPTrainer's sampled occupancy update evaluating only the kept samples
+    (occ_keep, the default) leaves the density grid, threshold and bitfield
+    bit for bit as evaluating all 2M samples, from the same trained state."""
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, warmup_steps=16)
+    tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
+    for _ in range(60):
+        tr.train_step(gt_img, dirs, poses)
+    tr.drain()
+    torch.cuda.synchronize()
+    state = [t.clone() for t in (tr.density_grid, tr.density_bitfield, tr.dctr, tr.threshold)]
+    outs = []
+    for keep in (False, True):
+        for t, v in zip((tr.density_grid, tr.density_bitfield, tr.dctr, tr.threshold), state):
+            t.copy_(v)
+        tr.occ_keep = keep
+        tr.update_density_grid(THR, warmup=False)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (tr.density_grid, tr.density_bitfield, tr.threshold)])
+        if keep:
+            n_kept = int(tr._occ_kept_n.item())
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    M2 = 2 * (tr.G ** 3 // 4)
+    print(f"kept {n_kept} of {M2} samples ({n_kept / M2:.3f})")
+    assert 0 < n_kept < M2
+    assert not torch.equal(outs[0][0], state[0])  # (the update did change the grid)
