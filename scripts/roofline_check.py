@@ -25,7 +25,7 @@ KERNEL_OF = {
     "field_encode_mlp": ("field_encode_mlp_reg_kernel", ("ILb1E", "<true>")),
     "composite_loss": "composite_loss_wave_kernel",
     "mlp_bwd": "field_bwd_mlp_coop_kernel",
-    "hash_bwd_coarse": "hash_bwd_kernel",
+    "hash_bwd_coarse": ("hash_bwd_", ("hash_bwd_kernel", "hash_bwd_wide_kernel")),
     "hash_count": "hash_count_kernel",
     "hash_write": "hash_write_kernel",
     "hash_accum": "hash_accum_kernel",
@@ -72,6 +72,14 @@ def main():
             frac = ach / r["peak"]
             out.append((op, r["frac"], frac, r["ms_per_step"], ms, n))
             continue
+    for op, r in line["ops"].items():  # per member kernel: probe span vs dispatch duration
+        for probe in r["kernels"]:
+            ds = [d for k, v in per.items() if matches(probe, k) for d in v]
+            pm = r.get("kernel_ms", {}).get(probe)
+            if ds and pm:
+                td = sum(ds) / len(ds)
+                print(f"  {op:16s} {probe:18s} probe {pm * 1e3:8.1f} us | trace {td:8.1f} us | trace - probe "
+                      f"{td - pm * 1e3:6.1f} us")
     for op, fp, ft, mp, mt, n in out:
         print(f"{op:16s} probes: {mp * 1e3:8.1f} us/step frac {fp:.4f} | trace: {mt * 1e3:8.1f} us/step frac {ft:.4f} "
               f"(launches {n}) | ratio {ft / fp:.3f}")

@@ -282,13 +282,14 @@ def test_segmented_replay_reduces_the_whole_gradient_when_every_level_is_binned(
     assert worst < 1e-3
 
 
-def _emu_trainer(use_graphs, k=2):
+def _emu_trainer(use_graphs, k=2, lo=None):
     import synthetic as S
     from trainer import NGPTrainer
     sc = S.AnalyticScene(W=100, H=100, n_images=10)
     dev = torch.device("cuda", 0)
     tr = NGPTrainer(scale=0.5, batch_size=R, device=dev, seed=3, warmup_steps=0, update_interval=10 ** 6,
-                    emulate_dp=1, use_graphs=use_graphs, dp_fine_buckets=k)
+                    emulate_dp=1, use_graphs=use_graphs, dp_fine_buckets=k,
+                    **({} if lo is None else {"bin_level_lo": lo}))
     with torch.no_grad():
         g = torch.Generator().manual_seed(11)
         tr.params[10240:] = ((torch.rand(tr.n_params - 10240, generator=g) * 2 - 1) * 0.5).to(dev)
@@ -298,8 +299,9 @@ def _emu_trainer(use_graphs, k=2):
     return tr, sc
 
 
-@pytest.mark.parametrize("k,capture", [(2, True), (4, True), (2, False)])
-def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k, capture, monkeypatch):
+@pytest.mark.parametrize("k,capture,lo", [(2, True, None), (4, True, None), (2, False, None), (2, True, 16),
+                                          (2, False, 16)])
+def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k, capture, lo, monkeypatch):
     """the world > 1 step's per-bucket pipeline (graph segments,
     reduce-scatter / sharded Adam / all-gather of each bucket on the comm
     stream while the next level range accumulates on the main stream) run in
@@ -311,11 +313,13 @@ def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k, capture
     device-drawn batches: every bucket's parameter update agrees to the fp32
     atomic-order noise of the MLP and coarse-level gradients.  capture: the
     whole step incl. the comm stream's chains as ONE graph (the default), else
-    the graph segments with the collectives between them (NGP_DP_CAPTURE=0)."""
+    the graph segments with the collectives between them (NGP_DP_CAPTURE=0).
+    lo = 16: every hash level atomic -- no binned range, so the buckets
+    past the alignment cut must still be reduced, stepped and gathered."""
     monkeypatch.setenv("NGP_DP_CAPTURE", "1" if capture else "0")
     runs = []
     for graphs in (True, False):
-        tr, sc = _emu_trainer(graphs, k)
+        tr, sc = _emu_trainer(graphs, k, lo)
         p0 = tr.params.clone()
         gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
         for _ in range(3):
@@ -324,7 +328,7 @@ def test_segmented_replay_matches_the_unsegmented_step_in_one_process(k, capture
         torch.cuda.synchronize()
         if graphs:
             assert any(("whole" if capture else "compute") in g for g in tr._graphs)  # replayed
-            assert len(tr.bin_cuts) == k + 1  # 1 + k buckets
+            assert len(tr.bin_cuts) == (k + 1 if lo is None else 0)  # 1 + k buckets (none binned: no cuts)
         runs.append(((tr.params - p0).cpu(), tr.buckets, (tr.params16.float() - tr.params.half().float()).abs().max()))
     (dA, buckets, s16a), (dB, _, s16b) = runs
     assert float(s16a) == 0.0 and float(s16b) == 0.0  # every rank's shadow all-gathered in full

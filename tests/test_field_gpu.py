@@ -127,6 +127,45 @@ def test_split_encode_mlp_equals_fused(scale):
     assert torch.equal(sig3, HG.density_forward(x, grid, p16)[0])
 
 
+def test_encoding_outside_the_box_wraps_like_tcnn():
+    """Inputs outside the grid's box (negative or past-the-end cell coordinates:
+    the API takes arbitrary points) index every level modulo its size, as tcnn's
+    grid_index does -- each forward kernel (fused field, split encode, the
+    trainer's one-launch encode + MLPs) gives the oracle's encoding bit for bit,
+    with no read outside the table."""
+    import ctypes
+    f, flat = _oracle_and_params(0.5)
+    g = torch.Generator().manual_seed(21)
+    x = (torch.rand(8192, 3, generator=g) * 2 - 1) * 1.5  # up to 3x the box half-size, every octant
+    x[:6] = torch.tensor([[-40.0, 0, 0], [0, 55.0, 0], [0, 0, -70.0], [1e3, -1e3, 1e3], [0.5, 0.5, 0.5],
+                          [-0.5, -0.5, -0.5]])
+    d = torch.randn(8192, 3, generator=g)
+    n = x.shape[0]
+    grid = HG.HashGrid(0.5)
+    p16 = flat.to(DEV).half()
+    xd, dd = x.to(DEV), d.to(DEV)
+    enc_ref = O.hash_encode_fwd(f.spec, x, f.xyz_min, f.xyz_max, f.xyz_params.detach()[f.n_dens:])
+    _, _, enc, _ = HG.field_forward(xd, dd, grid, p16)
+    assert torch.equal(enc.cpu().view(torch.int16), enc_ref.view(torch.int16))
+    L = HG._lib()
+    vp = ctypes.c_void_p
+    for fused in (False, True):
+        enc_pm = torch.empty(8, n, 4, dtype=torch.float16, device=DEV)
+        if fused:
+            sig, rgb = torch.empty(n, device=DEV), torch.empty(n, 3, device=DEV)
+            vren._ok(L.ngp_field_encode_mlp(vp(xd.data_ptr()), vp(dd.data_ptr()), n, None, None, ctypes.byref(grid.desc),
+                                            vp(p16[HG.MLP_PARAMS:].data_ptr()), vp(p16.data_ptr()),
+                                            vp(enc_pm.data_ptr()), vp(sig.data_ptr()), vp(rgb.data_ptr()), None,
+                                            vren._stream()), "encode_mlp")
+        else:
+            vren._ok(L.ngp_hash_encode(vp(xd.data_ptr()), n, None, None, ctypes.byref(grid.desc),
+                                       vp(p16[HG.MLP_PARAMS:].data_ptr()), vp(enc_pm.data_ptr()), vren._stream()),
+                     "hash_encode")
+        torch.cuda.synchronize()
+        got = enc_pm.permute(1, 0, 2).reshape(n, 32).cpu()
+        assert torch.equal(got.view(torch.int16), enc_ref.view(torch.int16)), fused
+
+
 @pytest.mark.parametrize("scale", [0.5, 16.0])
 def test_field_forward_parity(scale):
     f, flat = _oracle_and_params(scale)
