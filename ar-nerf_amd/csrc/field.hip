@@ -1512,97 +1512,6 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
     NGP_PROBE_END();
 }
 
-// hash_bwd_kernel with the run merging widened from one 16-sample group to NG
-// consecutive groups (16 NG samples per wave): a group's last run is not added
-// at its head but carried -- its index and sum moved to every lane of its
-// (cx, f) column -- into the next group, where it joins that group's first run
-// if the corner is the same (else the carry is added then, by the s = 0
-// lane).  Runs of a ray no longer break every 16 samples, so fewer
-// memory-side atomics leave the wave.  Work item = (16 NG samples, LPW
-// levels): the levels of one sample range are spread over 8 / LPW waves, so
-// the longer merge window does not cost parallelism.  Levels [0, hi), hi <= 8;
-// the lane's dL/denc values are read straight into registers.
-template <int NG, int LPW>
-__global__ void __launch_bounds__(256) hash_bwd_wide_kernel(const float* __restrict__ xyzs, int64_t n,
-                                                            const int64_t* __restrict__ n_dev,
-                                                            const int32_t* __restrict__ sidx, GridArgs ga,
-                                                            const float* __restrict__ denc, float* __restrict__ grad,
-                                                            int hi, float* __restrict__ rep, int rep_hi,
-                                                            uint32_t rep_stride, int nrep) {
-    constexpr int NLG = 8 / LPW;  // level groups
-    float* const grep = rep ? rep + (size_t)(blockIdx.x % nrep) * rep_stride : grad;
-    __shared__ LevelLds lv;
-    NGP_PROBE_BEGIN(NGP_P_HASH_BWD_COARSE);
-    load_levels(ga, lv);
-    __syncthreads();
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
-    const int lane = threadIdx.x & 63, s = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1, q = lane & 3;
-    const uint64_t colmask = 0x1111111111111111ull << q;  // the lanes of this lane's (cx, f) column
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const int64_t items = (N + 16 * NG - 1) / (16 * NG) * NLG;
-    for (int64_t it = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); it < items; it += nw) {
-        const int64_t base = it / NLG * (16 * NG);
-        const int l0 = (int)(it % NLG) * LPW;
-        if (l0 >= hi) continue;
-        struct GIn {
-            float in[3], gd[LPW];
-            bool valid;
-        };
-        // the group's inputs, one group ahead of its runs (two in registers, not NG)
-        auto load_group = [&](int g, GIn& x) {
-            const int64_t j = base + 16 * g + s;
-            x.valid = g < NG && j < N;
-            const int64_t i = x.valid && sidx ? (int64_t)sidx[j] : j;
-#pragma unroll
-            for (int u = 0; u < LPW; ++u) x.gd[u] = x.valid && l0 + u < hi ? denc[j * 32 + 2 * (l0 + u) + f] : 0.f;
-            load_x01(xyzs, i, x.valid, ga, x.in);
-        };
-        uint32_t cidx[LPW][4];
-        float cv[LPW][4];
-#pragma unroll
-        for (int u = 0; u < LPW; ++u)
-#pragma unroll
-            for (int yz = 0; yz < 4; ++yz) { cidx[u][yz] = 0xffffffffu; cv[u][yz] = 0.f; }
-        GIn cur;
-        load_group(0, cur);
-#pragma unroll 1
-        for (int g = 0; g < NG; ++g) {
-            GIn nxt;
-            load_group(g + 1, nxt);
-            const bool carry = g < NG - 1;
-#pragma unroll
-            for (int u = 0; u < LPW; ++u) {
-                const int l = l0 + u;
-                if (l >= hi) break;
-                float* const dst = l < rep_hi ? grep : grad;
-                uint32_t idx[4];
-                float v[4];
-                uint64_t heads[4];
-                coarse_level_runs(cur.in, cur.valid, cur.gd[u], l, lv, lane, cx, idx, v, heads);
-#pragma unroll
-                for (int yz = 0; yz < 4; ++yz) {
-                    // the carried run: joins this group's first run (head s = 0: its total) or is added now
-                    if (s == 0 && cidx[u][yz] != 0xffffffffu) {
-                        if (cidx[u][yz] == idx[yz]) v[yz] += cv[u][yz];
-                        else atomicAdd(&dst[2 * (size_t)cidx[u][yz] + f], cv[u][yz]);
-                    }
-                    const uint64_t hm = heads[yz] & colmask;
-                    const int hl = 63 - __builtin_clzll(hm);  // the head of the column's last run
-                    const bool head = (hm >> lane) & 1ull;
-                    if (head && cur.valid && !(carry && lane == hl)) atomicAdd(&dst[2 * (size_t)idx[yz] + f], v[yz]);
-                    if (carry) {
-                        cv[u][yz] = __shfl(v[yz], hl, 64);
-                        const uint32_t ci = __shfl(idx[yz], hl, 64);
-                        cidx[u][yz] = __shfl(cur.valid ? 1 : 0, hl, 64) ? ci : 0xffffffffu;
-                    }
-                }
-            }
-            cur = nxt;
-        }
-    }
-    NGP_PROBE_END();
-}
-
 constexpr unsigned HASH_BWD_BLOCKS = 8192;  // grid cap of hash_bwd_kernel (2048 measured slower)
 
 // grad[i] += sum_r rep[r][i]; rep[r][i] = 0 (i < n4 float4 groups), replicas
@@ -1826,20 +1735,6 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
 static void launch_coarse(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                           const GridArgs& ga, const float* denc, float* grad_table, int lo, int hi, float* rep,
                           int rep_hi, uint32_t rep_stride, int nrep, hipStream_t s) {
-    static const int wide = getenv("NGP_COARSE_WIDE") ? atoi(getenv("NGP_COARSE_WIDE")) : 0;  // (A/B)
-    static const int lpw = getenv("NGP_COARSE_LPW") ? atoi(getenv("NGP_COARSE_LPW")) : 8;     // (A/B)
-    if (lo == 0 && hi <= 8 && wide > 0) {
-#define NGP_WIDE(NGv, LPWv)                                                                                          \
-    if (wide == NGv && lpw == LPWv) {                                                                                \
-        NGP_TIMED(NGP_K_HASH_BWD_COARSE, s,                                                                          \
-                  (hash_bwd_wide_kernel<NGv, LPWv><<<persistent_blocks(n, 4 * 16 * NGv / (8 / LPWv), HASH_BWD_BLOCKS), \
-                                                     256, 0, s>>>(xyzs, n, n_dev, sample_idx, ga, denc, grad_table, hi, \
-                                                                  rep, rep_hi, rep_stride, nrep)));                  \
-        return;                                                                                                      \
-    }
-        NGP_WIDE(4, 8) NGP_WIDE(4, 2) NGP_WIDE(8, 2) NGP_WIDE(8, 1) NGP_WIDE(8, 4) NGP_WIDE(16, 2) NGP_WIDE(4, 4)
-#undef NGP_WIDE
-    }
     NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<persistent_blocks(n, 64, HASH_BWD_BLOCKS), 256, 0, s>>>(
         xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
 }

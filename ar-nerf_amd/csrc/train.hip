@@ -80,7 +80,9 @@ __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
 
 // One row of rays_a on one wave; returns the composited sample count
 // (vr_samples' share of this ray) and, in na_out, the samples that carry
-// gradient (up to and including the terminating one).
+// gradient (up to and including the terminating one).  DIST: the distortion
+// loss is on (lambda_dist != 0; its code and registers are left out otherwise).
+template <bool DIST>
 __device__ __forceinline__ int64_t composite_loss_ray(
     int64_t n, const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, const float* __restrict__ gt,
@@ -169,7 +171,7 @@ __device__ __forceinline__ int64_t composite_loss_ray(
     // Rows longer than two chunks park dL/dws in dL_dsig[s] (overwritten by
     // pass 2 after it is read).
     float gws_c[2] = {0.f, 0.f}, S_ws = 0.f;
-    if (la.lambda_dist != 0.f) {
+    if (DIST) {
         const float gd2 = (la.lambda_dist * la.inv_n_rays) * 2;
         float cw = 0.f, cwt = 0.f, ld = 0.f;
         auto dist_chunk = [&](int64_t k0, const Chunk& c) {
@@ -218,7 +220,7 @@ __device__ __forceinline__ int64_t composite_loss_ray(
         const float pr = rc + wave_incl_scan(w * c.cr, lane), pg = gc + wave_incl_scan(w * c.cg, lane);
         const float pb = bc + wave_incl_scan(w * c.cb, lane), pd = dc + wave_incl_scan(w * c.tt, lane);
         float ws_term = 0.f;
-        if (la.lambda_dist != 0.f) {  // + T g_ws - (S - prefix(g_ws ws)) (volumerendering.cu:138-146)
+        if (DIST) {  // + T g_ws - (S - prefix(g_ws ws)) (volumerendering.cu:138-146)
             const float pw = wc + wave_incl_scan(in ? gw * w : 0.f, lane);
             ws_term = Ta * gw - (S_ws - pw);
             wc = __shfl(pw, 63, 64);
@@ -240,7 +242,7 @@ __device__ __forceinline__ int64_t composite_loss_ray(
         float gw = 0.f;
         if (k0 + lane < na) {
             c.w = dL_drgbs[3 * s]; c.Ta = dL_drgbs[3 * s + 1];
-            if (la.lambda_dist != 0.f) gw = dL_dsig[s];
+            if (DIST) gw = dL_dsig[s];
         }
         bw_chunk(k0, c, gw);
     }
@@ -325,6 +327,7 @@ __device__ __forceinline__ void lookback_finish(LookbackWs* __restrict__ lb, uin
     }
 }
 
+template <bool DIST>
 __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
     const float* __restrict__ sigmas, const float* __restrict__ rgbs, const float* __restrict__ deltas,
     const float* __restrict__ ts, const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ gt,
@@ -344,7 +347,7 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
         const int64_t n = r0 + wid;
         int64_t na = 0, start = 0;
         if (n < n_rays) {
-            vr += composite_loss_ray(n, sigmas, rgbs, deltas, ts, rays_a, gt, bg, la, dL_dsig, dL_drgbs, out_rgb,
+            vr += composite_loss_ray<DIST>(n, sigmas, rgbs, deltas, ts, rays_a, gt, bg, la, dL_dsig, dL_drgbs, out_rgb,
                                      out_op, out_depth, out_loss, n_active, na);
             start = rays_a[3 * n + 1];
             rm += rays_a[3 * n + 2];
@@ -1268,9 +1271,15 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
                 lambda_distortion};
     // one row per wave: every row's dependent load chain in flight at once
     // (a few rows per wave serialised their memory latencies)
-    NGP_TIMED(NGP_K_COMPOSITE, as_stream(stream), composite_loss_wave_kernel<<<(unsigned)std::min<int64_t>((n_rays + 3) / 4, 1 << 20), 256, 0, as_stream(stream)>>>(
-        sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
-        out_depth, out_loss, n_active, sample_idx, (unsigned long long*)alloc_ws, n_active_total, stats));
+    const unsigned nb = (unsigned)std::min<int64_t>((n_rays + 3) / 4, 1 << 20);
+    if (la.lambda_dist != 0.f)
+        NGP_TIMED(NGP_K_COMPOSITE, as_stream(stream), composite_loss_wave_kernel<true><<<nb, 256, 0, as_stream(stream)>>>(
+            sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
+            out_depth, out_loss, n_active, sample_idx, (unsigned long long*)alloc_ws, n_active_total, stats));
+    else
+        NGP_TIMED(NGP_K_COMPOSITE, as_stream(stream), composite_loss_wave_kernel<false><<<nb, 256, 0, as_stream(stream)>>>(
+            sigmas, rgbs, deltas, ts, rays_a, n_rays, rgb_gt, bg, la, dL_dsigmas, dL_drgbs, out_rgb, out_opacity,
+            out_depth, out_loss, n_active, sample_idx, (unsigned long long*)alloc_ws, n_active_total, stats));
     return ngp_launch_status();
 }
 

@@ -154,6 +154,39 @@ def test_march_train_bit_exact(scale, esf, n_rays, max_samples):
         assert torch.equal(a.cpu(), b)
 
 
+@pytest.mark.parametrize("occ,scale,max_samples", [("scene", 0.5, 1024), ("rand0.01", 0.5, 1024),
+                                                   ("rand0.2", 0.5, 1024), ("rand0.7", 0.5, 1024),
+                                                   ("scene", 0.25, 1024), ("rand0.05", 0.3, 1024),
+                                                   ("scene", 0.5, 40), ("blocks", 0.5, 1024)])
+def test_march_train_occupancy_patterns_bit_exact(occ, scale, max_samples):
+    """The training march (the wave-per-ray lattice walk) equals the oracle's serial
+    walk bit for bit -- counts, rays_a, xyz, dirs, t, dt -- on the scene's shell, on
+    random bitfields of several densities (many short empty / occupied runs: the
+    walk's chain through a window alternates between steps and jumps), on sparse
+    Morton-aligned 4^3 blocks (the summary's early out), at scales whose mip bound
+    is below 0.5 and with a max_samples cut."""
+    n_rays = 4096
+    sc, o, d, _, _ = _scene_rays(n_rays, scale=scale, W=400)
+    ht = _hits(o, d, scale)
+    noise = torch.rand(n_rays, generator=torch.Generator().manual_seed(5))
+    g = torch.Generator().manual_seed(7)
+    if occ == "scene":
+        bf = sc.bitfield
+    elif occ == "blocks":  # whole Morton-aligned 4^3 blocks (64-bit words) on or off
+        words = (torch.rand(128 ** 3 // 64, generator=g) < 0.03)
+        bf = words.repeat_interleave(8).to(torch.uint8) * 255
+    else:
+        frac = float(occ[4:])
+        bits = (torch.rand(128 ** 3, generator=g) < frac).to(torch.uint8)
+        bf = (bits.view(-1, 8) << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    ref = O.raymarching_train(o, d, ht, bf, 1, scale, 0.0, noise, 128, max_samples)
+    out = vren.raymarching_train(o.to(DEV), d.to(DEV), ht.to(DEV), bf.to(DEV), 1, scale, 0.0, noise.to(DEV), 128,
+                                 max_samples)
+    assert int(out[5][0]) == int(ref[5][0])
+    for a, b in zip(out[:5], ref[:5]):
+        assert torch.equal(a.cpu(), b)
+
+
 def test_march_train_empty_and_misses():
     o = torch.tensor([[5.0, 5.0, 5.0]]); d = torch.tensor([[1.0, 0.0, 0.0]])
     ht = torch.tensor([[-1.0, -1.0]])
