@@ -971,11 +971,14 @@ __device__ __forceinline__ void load_bwd_weights_direct(const _Float16* __restri
 
 __device__ __forceinline__ float max4(f4 v) { return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))); }
 // Per-sample power-of-two scales of the data chain: a gradient tile travels in
-// fp16 as value x 2^E, E per sample (the same in its four lanes), chosen from
-// the sample's largest |value| so that it lands in [2^13, 2^14): a full 11-bit
-// mantissa for everything within 2^27 of it.  A layer's MFMA output is in
-// units of the previous E; the next E follows from its max, and one
-// power-of-two factor 2^(E_new - E_prev) re-scales it (exact).
+// fp16 as value x 2^E, E per sample (the same in its four lanes).  At the
+// chain's two inputs (dL/drgb through the sigmoid, dL/dh with TruncExp's dL/dsigma)
+// E comes from the sample's largest |value| so that it lands in [2^13, 2^14): a
+// full 11-bit mantissa for everything within 2^27 of it.  A layer's MFMA output
+// is in units of the previous E; after W^T the next E is the previous one minus
+// the block's bound exponent of W^T (colsum_exp: the output stays below 2^14, no
+// per-sample max), and one power-of-two factor 2^(E_new - E_prev) re-scales it
+// (exact).
 constexpr int E_MIN = -100, E_MAX = 100;
 __device__ __forceinline__ int fexp(float m) {  // m = f 2^e, f in [0.5, 1) (0 -> 0)
     int e;
@@ -1021,21 +1024,6 @@ __device__ __forceinline__ h4 scale_h4(h4 v, int k) {
     const float f = ldexpf(1.0f, k);
     return h4{(_Float16)((float)v[0] * f), (_Float16)((float)v[1] * f), (_Float16)((float)v[2] * f),
               (_Float16)((float)v[3] * f)};
-}
-// max |c| over the units whose activation is nonzero (the ReLU' mask the
-// gradient tile gets; act = relu_h's fp16 output): the per-sample exponent
-// follows the values that are kept, not those of inactive units
-#ifndef NGP_BWD_MASKED
-#define NGP_BWD_MASKED 1  // 0: the exponent from all units (rounds 1-3)
-#endif
-__device__ __forceinline__ float max4_act(f4 c, h4 act) {
-#if !NGP_BWD_MASKED
-    return max4(c);
-#endif
-    const uint2 a = __builtin_bit_cast(uint2, act);
-    const float m0 = (a.x & 0xffffu) ? fabsf(c[0]) : 0.f, m1 = (a.x >> 16) ? fabsf(c[1]) : 0.f;
-    const float m2 = (a.y & 0xffffu) ? fabsf(c[2]) : 0.f, m3 = (a.y >> 16) ? fabsf(c[3]) : 0.f;
-    return fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
 }
 // min over the wave's 16 samples of a per-sample int (lanes 0-15 hold samples 0-15)
 __device__ __forceinline__ int samples_min(int v) {
@@ -1130,6 +1118,23 @@ __device__ __forceinline__ float sample_max(float v) {
     v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
     const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+
+// ceil(log2(max_i sum_o |W^T[i][o]|)) of a transposed weight image (rows of nout halfs,
+// pitch rt, nin rows; one row per lane, max over the wave): |W^T x| < 2^k max|x| for
+// every x, so a gradient tile scaled below 2^14 stays below 2^14 after W^T and a
+// re-scale by 2^-k (the inner layers' exponents without per-sample maxima: only the
+// chain's two inputs, dL/drgb and dL/dsigma, set a per-sample exponent).  Whole wave,
+// uniform result.
+__device__ __forceinline__ int colsum_exp(const _Float16* img, int nin, int nout, int rt, int lane) {
+    float a = 0.f;
+    if (lane < nin)
+        for (int o = 0; o < nout; ++o) a += fabsf((float)img[lane * rt + o]);
+    for (int off = 32; off > 0; off >>= 1) a = fmaxf(a, __shfl_xor(a, off, 64));
+    int e = 0;
+    const float m = frexpf(a, &e);
+    e = a == 0.f ? -30 : (m == 0.5f ? e - 1 : e);  // ceil(log2(a)) (a = 2^(e-1) exactly: e - 1)
+    return __builtin_amdgcn_readfirstlane(e);
 }
 
 // output tile k (acc_tile_info order) -> operand tile ids (G, H) in its phase's region
@@ -1251,6 +1256,10 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     int32_t i_next = row_index(j0 + stride);
     load_bwd_weights_direct(mlp, sw);
     __syncthreads();
+    // per-block bounds of W5^T, W4^T, W2^T: the inner layers' exponents follow from their input's
+    // (round 5; rounds 3-4 took a per-sample max after every layer: 12 % more VALU, 6 % longer)
+    const int k5 = colsum_exp(sw + BT5, 64, 16, RT16, lane), k4 = colsum_exp(sw + BT4, 64, 64, RT64, lane);
+    const int k2 = colsum_exp(sw + BT2, 64, 16, RT16, lane);
     NGP_BWD_EDGE(1);
     int par = 0;
     // block-uniform trip count: every wave reaches every barrier
@@ -1292,15 +1301,11 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         }
         const int Eo = next_exp(sample_max(max4(dout)), 0);
         const h4 do_h = cvt4(dout, ldexpf(1.0f, Eo));
-        // ---- dL/da4 = ReLU'(W5^T do)   (MFMA output in units of 2^Eo)
+        // ---- dL/da4 = ReLU'(W5^T do)   (MFMA output in units of 2^Eo; |.| < 2^(14 + k5))
         f4 c4[4];
-        float m = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            c4[t] = mfma16(lds4(sw + BT5 + (16 * t + s) * RT16 + 4 * g), do_h, z);
-            m = fmaxf(m, max4_act(c4[t], h4v[t]));
-        }
-        const int E4 = next_exp(sample_max(m), Eo);
+        for (int t = 0; t < 4; ++t) c4[t] = mfma16(lds4(sw + BT5 + (16 * t + s) * RT16 + 4 * g), do_h, z);
+        const int E4 = max(Eo - k5, E_MIN);
         h4 da4h[4];
         {
             const float r = ldexpf(1.0f, E4 - Eo);
@@ -1309,16 +1314,14 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         }
         // ---- dL/da3 = ReLU'(W4^T da4)
         f4 c3[4];
-        m = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             f4 c = z;
 #pragma unroll
             for (int kt = 0; kt < 4; ++kt) c = mfma16(lds4(sw + BT4 + (16 * t + s) * RT64 + 16 * kt + 4 * g), da4h[kt], c);
             c3[t] = c;
-            m = fmaxf(m, max4_act(c, h3[t]));
         }
-        const int E3 = next_exp(sample_max(m), E4);
+        const int E3 = max(E4 - k4, E_MIN);
         h4 da3h[4];
         {
             const float r = ldexpf(1.0f, E3 - E4);
@@ -1335,13 +1338,9 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         const h4 dhh = cvt4(dh, ldexpf(1.0f, Eh));
         // ---- dL/da1 = ReLU'(W2^T dh)
         f4 c1[4];
-        m = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            c1[t] = mfma16(lds4(sw + BT2 + (16 * t + s) * RT16 + 4 * g), dhh, z);
-            m = fmaxf(m, max4_act(c1[t], h1[t]));
-        }
-        const int E1 = next_exp(sample_max(m), Eh);
+        for (int t = 0; t < 4; ++t) c1[t] = mfma16(lds4(sw + BT2 + (16 * t + s) * RT16 + 4 * g), dhh, z);
+        const int E1 = max(Eh - k2, E_MIN);
         h4 da1h[4];
         {
             const float r = ldexpf(1.0f, E1 - Eh);

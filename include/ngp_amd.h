@@ -378,7 +378,8 @@ int ngp_rays_nonempty(const int64_t* rays_a, int64_t n_rays, int32_t* rows, int6
  * start + 64 .. start + N of every row with rc > 0, appended at ranges
  * reserved on *total2 (zero at the launch; its final value = the list's
  * length): rows in no fixed order, each row's samples contiguous and
- * ascending.  *evaluated (nullable) += the samples evaluated here plus, with
+ * ascending; list2 holds n entries (writes past it are dropped, and readers
+ * of a device count clamp it to their capacity).  *evaluated (nullable) += the samples evaluated here plus, with
  * list2, the listed ones.  With ngp_rays_nonempty's list: one wave per
  * non-empty row.
  * Replaces, for the model(xyzs, dirs) call of __render_rays_train

@@ -239,9 +239,11 @@ def test_field_backward_parity(table_init):
 def test_field_backward_per_sample_scales():
     """dL/denc per sample when the per-sample gradient magnitudes span nine
     decades (composited weights of a batch do): the MLP backward scales each
-    sample's gradient column by its own power of two before the fp16 cast,
-    so small-gradient samples keep full precision beside large ones.  Oracle:
-    fp32 autograd through the oracle's MLP from the same fp16 encoding."""
+    sample's gradient column by its own power of two before the fp16 cast (at
+    the chain's inputs; after each inner layer the exponent drops by the block's
+    bound exponent of W^T, round 5), so small-gradient samples keep full
+    precision beside large ones.  Oracle: fp32 autograd through the oracle's MLP
+    from the same fp16 encoding."""
     f, flat = _oracle_and_params(0.5)
     x, d = _points(20000, 0.5, seed=3)
     g = torch.Generator().manual_seed(11)
