@@ -1007,8 +1007,9 @@ class NGPTrainer:
         self._ev("composite_loss", 1)
         cs = torch.cuda.current_stream()
         hybrid = self.hash_backward != "atomic"
+        binned = hybrid and self.bin_level_lo < self.grid.n_levels  # (hybrid at bin_level_lo == L: all atomic)
         bs = self.bwd_stream
-        if hybrid:  # bucket plan of the binned fine levels (xyzs / sample_idx only) beside the MLP backward
+        if binned:  # bucket plan of the binned fine levels (xyzs / sample_idx only) beside the MLP backward
             bs.wait_stream(cs)
             with torch.cuda.stream(bs):
                 vren._ok(HGL.ngp_hash_binned_plan(_p(self.xyzs), self.cap, _p(self.n_active_total),
@@ -1051,25 +1052,26 @@ class NGPTrainer:
                 self._ev("hash_bwd_coarse", 1)
                 if adam_split:
                     self._adam(0, split, vren._stream(), rep=fold_in_adam)
-            cs.wait_event(planned)
             self._ev("hash_binned_apply", 0)
             t = HG.MLP_PARAMS
-            if fused:  # + FusedAdam of the binned levels inside the accumulation
-                vren._ok(HGL.ngp_hash_binned_apply_adam(
-                    _p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
-                    HG.ctypes.byref(self.grid.desc), _p(self.denc), _p(self.grad[t:]), _p(self.bin_ws),
-                    self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi, _p(self.params[t:]),
-                    _p(self.exp_avg[t:]), _p(self.exp_avg_sq[t:]), _p(self.params16[t:]), _p(self.lr_dev),
-                    ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
-                    ctypes_float(1.0 / self.world), s), "hash_binned_apply_adam")
-            else:
-                vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
-                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
-                                                   _p(self.denc), _p(self.grad[t:]), _p(self.bin_ws),
-                                                   self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi, s),
-                         "hash_binned_apply")
-                if adam_split:
-                    self._adam(split, self.n_params, s)
+            if binned:  # (none at bin_level_lo == L: the side stream took every level and its Adam)
+                cs.wait_event(planned)
+                if fused:  # + FusedAdam of the binned levels inside the accumulation
+                    vren._ok(HGL.ngp_hash_binned_apply_adam(
+                        _p(self.xyzs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
+                        HG.ctypes.byref(self.grid.desc), _p(self.denc), _p(self.grad[t:]), _p(self.bin_ws),
+                        self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi, _p(self.params[t:]),
+                        _p(self.exp_avg[t:]), _p(self.exp_avg_sq[t:]), _p(self.params16[t:]), _p(self.lr_dev),
+                        ctypes_float(0.9), ctypes_float(0.999), ctypes_float(1e-15), _p(self.dctr),
+                        ctypes_float(1.0 / self.world), s), "hash_binned_apply_adam")
+                else:
+                    vren._ok(HGL.ngp_hash_binned_apply(_p(self.xyzs), self.cap, _p(self.n_active_total),
+                                                       _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
+                                                       _p(self.denc), _p(self.grad[t:]), _p(self.bin_ws),
+                                                       self.bin_max_samples, self.bin_level_lo, self.bin_merge_hi, s),
+                             "hash_binned_apply")
+                    if adam_split:
+                        self._adam(split, self.n_params, s)
             self._ev("hash_binned_apply", 1)
             cs.wait_stream(bs)
             if adam_split:
