@@ -410,6 +410,21 @@ def pmc_traffic(members):
     return round(sum(t[m]["bytes_per_launch"] for m in members))
 
 
+def transplant_state(src, dst):
+    """Training state of trainer src into dst (same scene and model shape): parameters, fp16 shadow,
+    Adam moments, occupancy grid / bitfield / threshold, device counters and the host step count."""
+    n = src.params.numel()
+    with torch.no_grad():
+        dst.params[:n].copy_(src.params)
+        dst.params16[:n].copy_(src.params16)
+        dst.exp_avg[:n].copy_(src.exp_avg[:n])
+        dst.exp_avg_sq[:n].copy_(src.exp_avg_sq[:n])
+        for name in ("density_grid", "density_bitfield", "threshold", "dctr"):
+            getattr(dst, name).copy_(getattr(src, name))
+    dst.global_step = src.global_step
+    dst._updated_for = src._updated_for
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)  # local: this rank's device index
@@ -445,7 +460,24 @@ def main():
         return int(trainer.dctr[0].item())
 
     t0 = time.time()
-    run(args.pretrain)
+    if args.emulate_dp:
+        # One emulated rank updates only its shards (the other ranks' updates never arrive), so it
+        # would train a different model with different work per step: the setup steps run on a
+        # single-process trainer and its whole state moves into the emulated rank before timing.
+        pre = NGPTrainer(scale=args.scale, batch_size=args.batch, device=dev, hash_backward=args.hash_backward,
+                         bin_level_lo=args.bin_level_lo, bin_samples_per_ray=args.bin_samples_per_ray, erode=erode,
+                         bin_merge_hi=args.bin_merge_hi, pair_steps=not args.no_pair_steps,
+                         **({} if args.chunk_first is None else {"chunk_first": args.chunk_first}))
+        pre.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
+        for i in range(args.pretrain):
+            pre.train_step(gt_images, directions, poses, allow_pair=i < args.pretrain - 1)
+        pre.drain()
+        torch.cuda.synchronize()
+        transplant_state(pre, trainer)
+        del pre
+        torch.cuda.empty_cache()
+    else:
+        run(args.pretrain)
     torch.cuda.synchronize()
     log(rank, f"[bench] pretrain {args.pretrain} steps in {time.time() - t0:.1f}s, "
               f"samples last batch {int(trainer.n_samples.item())}")
