@@ -539,7 +539,10 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         // the records are summed, so its HBM latency hides behind the LDS
         // accumulation instead of following it (the flush then only computes
         // and stores).  PF x blockDim.x covers a whole bucket at ACC_T threads.
-        constexpr int PF = 4;
+#ifndef NGP_ACC_PF
+#define NGP_ACC_PF 4
+#endif
+        constexpr int PF = NGP_ACC_PF;
         const uint32_t ng = 2 * ne / 4;  // float4 groups of the range
         float4 pP[PF], pM[PF], pV[PF];
         if (fz) {

@@ -403,6 +403,11 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
 // lr_dev / step_dev (nullable): learning rate and the 0-based count of steps
 // already taken read from device memory (graph replays), bias corrections
 // for step *step_dev + 1 computed here (same fp32 powf as the host path).
+// (A/B builds: NGP_ADAM_RB replica loads in flight per lane -- a slim Adam whose waves fit beside the
+// accumulation's whole-CU blocks)
+#ifndef NGP_ADAM_RB
+#define NGP_ADAM_RB 8
+#endif
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ grad, float* __restrict__ m,
                                                    float* __restrict__ v, _Float16* __restrict__ p16, int64_t n4,
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2,
@@ -420,7 +425,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         if (rep && j >= 0 && j < rep4) {  // gradient replicas (ngp_hash_backward_levels_rep), folded in order
             // (the first 8 replicas' loads all issued before any is summed or cleared: one round trip)
             float4* r4 = reinterpret_cast<float4*>(rep);
-            constexpr int RB = 8;
+            constexpr int RB = NGP_ADAM_RB;
             float4 b[RB];
 #pragma unroll
             for (int r = 0; r < RB; ++r)
