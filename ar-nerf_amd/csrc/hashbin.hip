@@ -538,11 +538,13 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         // A fused bucket's Adam state (p, m, v of the range) is loaded before
         // the records are summed, so its HBM latency hides behind the LDS
         // accumulation instead of following it (the flush then only computes
-        // and stores).  PF x blockDim.x covers a whole bucket at ACC_T threads.
-#ifndef NGP_ACC_PF
-#define NGP_ACC_PF 4
-#endif
-        constexpr int PF = NGP_ACC_PF;
+        // and stores).  One float4 group per thread (PF x blockDim.x = a
+        // quarter of a bucket; the rest is read at the flush): 105 instead of
+        // 128 VGPRs, so one wave per SIMD of the MLP + coarse Adam fits beside
+        // these whole-CU blocks (round 5: +2.0 % end to end with the Adam's
+        // one-replica fold, profiles/r05/ab/round5_ab.txt r5bb / r5cc; four
+        // groups filled the register file and the Adam waited ~60 us).
+        constexpr int PF = 1;
         const uint32_t ng = 2 * ne / 4;  // float4 groups of the range
         float4 pP[PF], pM[PF], pV[PF];
         if (fz) {

@@ -403,11 +403,6 @@ __global__ void __launch_bounds__(256) composite_loss_wave_kernel(
 // lr_dev / step_dev (nullable): learning rate and the 0-based count of steps
 // already taken read from device memory (graph replays), bias corrections
 // for step *step_dev + 1 computed here (same fp32 powf as the host path).
-// (A/B builds: NGP_ADAM_RB replica loads in flight per lane -- a slim Adam whose waves fit beside the
-// accumulation's whole-CU blocks)
-#ifndef NGP_ADAM_RB
-#define NGP_ADAM_RB 8
-#endif
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ grad, float* __restrict__ m,
                                                    float* __restrict__ v, _Float16* __restrict__ p16, int64_t n4,
                                                    float lr, float b1, float b2, float eps, float bc1, float bc2,
@@ -423,20 +418,12 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         float4 M = reinterpret_cast<float4*>(m)[i], V = reinterpret_cast<float4*>(v)[i];
         const int64_t j = i - rep_lo4;
         if (rep && j >= 0 && j < rep4) {  // gradient replicas (ngp_hash_backward_levels_rep), folded in order
-            // (the first 8 replicas' loads all issued before any is summed or cleared: one round trip)
+            // One replica in flight per lane (round 5): the kernel's 60 VGPRs let one Adam wave per SIMD
+            // run beside the accumulation's 1024-thread blocks (105 VGPRs), where with all 8 replicas'
+            // loads issued first (round 3) it waited for those blocks to retire: +2.0 % end to end with
+            // the accumulation's prefetch at one group (profiles/r05/ab/round5_ab.txt r5bb / r5cc).
             float4* r4 = reinterpret_cast<float4*>(rep);
-            constexpr int RB = NGP_ADAM_RB;
-            float4 b[RB];
-#pragma unroll
-            for (int r = 0; r < RB; ++r)
-                if (r < nrep) b[r] = r4[r * rep4 + j];
-#pragma unroll
-            for (int r = 0; r < RB; ++r)
-                if (r < nrep) { Gd.x += b[r].x; Gd.y += b[r].y; Gd.z += b[r].z; Gd.w += b[r].w; }
-#pragma unroll
-            for (int r = 0; r < RB; ++r)
-                if (r < nrep) r4[r * rep4 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int r = RB; r < nrep; ++r) {
+            for (int r = 0; r < nrep; ++r) {
                 const float4 c = r4[r * rep4 + j];
                 Gd.x += c.x; Gd.y += c.y; Gd.z += c.z; Gd.w += c.w;
                 r4[r * rep4 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
