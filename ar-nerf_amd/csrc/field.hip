@@ -596,6 +596,8 @@ __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
 #define NGP_FEM_REMAT 1
 #endif
 constexpr int FEM2_WAVES = NGP_FEM2_WAVES, FEM_LPR = NGP_FEM_LPR;
+constexpr int PRE_LEVELS = 8;  // coarse levels round 1 may find pre-encoded (encode_coarse_first_kernel)
+static_assert(PRE_LEVELS % FEM_LPR == 0 && PRE_LEVELS % 2 == 0, "pre-encoded levels: whole rounds and pairs");
 static_assert(L % FEM_LPR == 0, "levels per round");
 template <bool COLOR>
 __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_mlp_reg_kernel(
@@ -703,12 +705,14 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
 // Encode + MLPs of the 64-sample chunk [i0, i0 + cnt) on one wave (lane =
 // sample i0 + lane): field_encode_mlp_reg_kernel's body for a contiguous
 // chunk; returns this lane's sigma (0 past cnt) for a transmittance epilogue.
+// pre (0 or PRE_LEVELS): levels [0, pre) are already in enc_pm (written by
+// encode_coarse_first_kernel with the same arithmetic) and only read back.
 template <bool COLOR>
 __device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs, const float* __restrict__ dirs,
                                                   int64_t i0, int cnt, int64_t n, const GridArgs& ga,
                                                   const LevelLds& lv, const uint32_t* __restrict__ table,
                                                   const _Float16* sw, _Float16* __restrict__ enc_pm,
-                                                  float* __restrict__ sigmas, float* __restrict__ rgbs) {
+                                                  float* __restrict__ sigmas, float* __restrict__ rgbs, int pre = 0) {
     int lane_l = threadIdx.x & 63;  // (opaque: lane-derived addresses are rematerialised, not held)
     asm volatile("" : "+v"(lane_l));
     const int s = lane_l & 15, g = lane_l >> 4;
@@ -717,8 +721,17 @@ __device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs
     float in[3];
     load_x01(xyzs, i, valid, ga, in);
     uint32_t E[16];
+    if (pre) {
+        // after pre / FEM_LPR rounds the chain holds levels [0, pre) at the top of E
+#pragma unroll
+        for (int pr = 0; pr < PRE_LEVELS / 2; ++pr) {
+            const uint2 q = valid ? *reinterpret_cast<const uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) : make_uint2(0u, 0u);
+            E[16 - PRE_LEVELS + 2 * pr] = q.x;
+            E[16 - PRE_LEVELS + 2 * pr + 1] = q.y;
+        }
+    }
 #pragma unroll 1
-    for (int rr = 0; rr < L / FEM_LPR; ++rr) {
+    for (int rr = pre / FEM_LPR; rr < L / FEM_LPR; ++rr) {
         uint32_t v[FEM_LPR][8];
 #pragma unroll
         for (int q = 0; q < FEM_LPR; ++q) gather_level_loads(in, level_u(lv, FEM_LPR * rr + q), table, v[q]);
@@ -730,7 +743,8 @@ __device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs
     if (valid && enc_pm) {
 #pragma unroll
         for (int pr = 0; pr < 8; ++pr)
-            *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(E[2 * pr], E[2 * pr + 1]);
+            if (2 * pr >= pre)
+                *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(E[2 * pr], E[2 * pr + 1]);
     }
     transpose_rows4(E);
     float sg = 0.f;
@@ -788,13 +802,13 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
     int64_t n_rows, int64_t n, float T_thr, GridArgs ga, const uint32_t* __restrict__ table,
     const _Float16* __restrict__ mlp, _Float16* __restrict__ enc_pm, float* __restrict__ sigmas,
     float* __restrict__ rgbs, int32_t* __restrict__ rest, int32_t* __restrict__ list2, int64_t* __restrict__ total2,
-    int64_t* __restrict__ evaluated) {
+    int64_t* __restrict__ evaluated, int pre) {
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ LevelLds lv;
     __shared__ unsigned long long blk_eval;
     NGP_PROBE_BEGIN(NGP_P_FIRST_CHUNK);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t NR = n_rows_dev ? *n_rows_dev : n_rows;
+    const int64_t NR = n_rows_dev ? min(*n_rows_dev, n_rows) : n_rows;  // (a device count never past the capacity)
     const int64_t G = gridDim.x, stride = (int64_t)FEM2_WAVES * G;
     int64_t j = (int64_t)wv * G + blockIdx.x;  // the wave's first row (wave-uniform)
     // its row (list -> rays_a: dependent round trips) requested before the weight image is built
@@ -814,7 +828,8 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
         int32_t rc = 0;
         if (cnt > 0) {
             const float dl = lane < cnt ? deltas[start + lane] : 0.f;
-            const float sg = encode_mlp_chunk<COLOR>(xyzs, dirs, start, cnt, n, ga, lv, table, sw, enc_pm, sigmas, rgbs);
+            const float sg = encode_mlp_chunk<COLOR>(xyzs, dirs, start, cnt, n, ga, lv, table, sw, enc_pm, sigmas, rgbs,
+                                                     pre);
             const float om = 1.0f - (1.0f - __expf(-sg * dl));  // chunk_segments_kernel's expression
             const ChunkT ct = chunk_transmittance(om, cnt, 1.0f, T_thr, lane);
             rc = (!ct.hit && N > 64) ? (int32_t)(N - 64) : 0;
@@ -839,6 +854,53 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
     __syncthreads();
     if (threadIdx.x == 0 && evaluated && blk_eval) atomicAdd((unsigned long long*)evaluated, blk_eval);
     NGP_PROBE_END();
+}
+
+// Levels [0, PRE_LEVELS) of round 1's encoding, ahead of time: for the rows
+// rows[j], j < *n_rows_dev, of the NEXT batch (its march and row list are
+// done beside the current step), the first min(N, 64) samples' coarse-level
+// features, written to the pair-major enc_pm (pairs [0, PRE_LEVELS / 2)) with
+// encode_mlp_chunk's arithmetic.  Those levels' parameters are final once the
+// MLP + coarse levels' Adam of the current step has run, ~a bucket
+// accumulation before the step ends, so this runs beside the binned levels'
+// accumulation and round 1 of the next step (field_first_chunk_kernel with
+// pre = PRE_LEVELS) gathers only the fine levels: half its dependent gather
+// rounds leave the critical path.
+__global__ void __launch_bounds__(256) encode_coarse_first_kernel(
+    const float* __restrict__ xyzs, const int64_t* __restrict__ rays_a, const int32_t* __restrict__ rows,
+    const int64_t* __restrict__ n_rows_dev, int64_t n_rows, int64_t n, GridArgs ga,
+    const uint32_t* __restrict__ table, _Float16* __restrict__ enc_pm) {
+    __shared__ LevelLds lv;
+    load_levels(ga, lv);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t NR = n_rows_dev ? min(*n_rows_dev, n_rows) : n_rows;  // (a device count never past the capacity)
+    const int64_t stride = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < NR; j += stride) {
+        const int64_t r = rows ? (int64_t)rows[j] : j;
+        const int64_t start = rays_a[3 * r + 1], N = rays_a[3 * r + 2];
+        const bool valid = lane < N;
+        const int64_t i = start + lane;
+        float in[3];
+        load_x01(xyzs, i, valid, ga, in);
+        uint32_t E[PRE_LEVELS];
+#pragma unroll 1
+        for (int rr = 0; rr < PRE_LEVELS / FEM_LPR; ++rr) {
+            uint32_t v[FEM_LPR][8];
+#pragma unroll
+            for (int q = 0; q < FEM_LPR; ++q) gather_level_loads(in, level_u(lv, FEM_LPR * rr + q), table, v[q]);
+#pragma unroll
+            for (int q = 0; q < PRE_LEVELS - FEM_LPR; ++q) E[q] = E[q + FEM_LPR];
+#pragma unroll
+            for (int q = 0; q < FEM_LPR; ++q)
+                E[PRE_LEVELS - FEM_LPR + q] = level_sum_h2(in, level_u(lv, FEM_LPR * rr + q), v[q]);
+        }
+        if (valid) {
+#pragma unroll
+            for (int pr = 0; pr < PRE_LEVELS / 2; ++pr)
+                *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(E[2 * pr], E[2 * pr + 1]);
+        }
+    }
 }
 
 // One level of the coarse (atomic) hash backward for the wave's 16 consecutive
@@ -1511,7 +1573,12 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
     NGP_PROBE_END();
 }
 
-constexpr unsigned HASH_BWD_BLOCKS = 8192;  // grid cap of hash_bwd_kernel (2048 measured slower)
+constexpr unsigned HASH_BWD_BLOCKS = 8192;  // grid cap of hash_bwd_kernel, all-level API path (2048 measured slower)
+// grid cap of the training step's coarse levels (launch_coarse): 2048 waves, two per SIMD.  Round 5: its
+// atomics spread over a longer span beside the record write, now that the coarse levels' Adam runs beside
+// the accumulation and no longer waits on it -- with the prefetch-free accumulation +1.2-1.3 %,
+// profiles/r05/ab/round5_ab.txt r5ee / r5ff (rounds 2-4: 8192, when a longer coarse kernel delayed that Adam)
+constexpr unsigned COARSE_BLOCKS = 512;
 
 // grad[i] += sum_r rep[r][i]; rep[r][i] = 0 (i < n4 float4 groups), replicas
 // summed in order r = 0..nrep-1; all of a lane's loads are issued first
@@ -1657,11 +1724,12 @@ int ngp_field_encode_mlp(const float* xyzs, const float* dirs, int64_t n, const 
     return ngp_launch_status();
 }
 
-int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
-                            const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
-                            float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
-                            void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int32_t* list2,
-                            int64_t* total2, int64_t* evaluated, void* stream) {
+int ngp_field_forward_first_pre(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
+                                const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
+                                float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16,
+                                const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs, int32_t* rest,
+                                int32_t* list2, int64_t* total2, int64_t* evaluated, int pre_levels, void* stream) {
+    NGP_CHECK_ARG(pre_levels == 0 || (pre_levels == PRE_LEVELS && enc_pm));
     GridArgs ga;
     int st = grid_args(grid, ga);
     if (st) return st;
@@ -1677,7 +1745,35 @@ int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* d
     const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + FEM2_WAVES - 1) / FEM2_WAVES)));
     NGP_TIMED(NGP_K_HASH_ENCODE, s, field_first_chunk_kernel<true><<<blocks, 64 * FEM2_WAVES, 0, s>>>(
         xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
-        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, list2, total2, evaluated));
+        (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, list2, total2, evaluated, pre_levels));
+    return ngp_launch_status();
+}
+
+int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
+                            const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
+                            float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
+                            void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int32_t* list2,
+                            int64_t* total2, int64_t* evaluated, void* stream) {
+    return ngp_field_forward_first_pre(xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, grid,
+                                       table_f16, mlp_f16, enc_pm, sigmas, rgbs, rest, list2, total2, evaluated, 0,
+                                       stream);
+}
+
+int ngp_field_encode_first_coarse(const float* xyzs, const int64_t* rays_a, const int32_t* rows,
+                                  const int64_t* n_rows_dev, int64_t n_rows, int64_t n, const ngp_hashgrid_t* grid,
+                                  const void* table_f16, void* enc_pm, void* stream) {
+    GridArgs ga;
+    int st = grid_args(grid, ga);
+    if (st) return st;
+    NGP_CHECK_ARG(n_rows >= 0 && n >= 0);
+    if (n_rows == 0) return NGP_OK;
+    NGP_CHECK_ARG(xyzs && rays_a && table_f16 && enc_pm && ((uintptr_t)table_f16 & 15) == 0 &&
+                  ((uintptr_t)enc_pm & 7) == 0);
+    hipStream_t s = as_stream(stream);
+    static const unsigned cap = resident_blocks(encode_coarse_first_kernel, 256, 0);
+    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + 3) / 4)));
+    encode_coarse_first_kernel<<<blocks, 256, 0, s>>>(xyzs, rays_a, rows, n_rows_dev, n_rows, n, ga,
+                                                      (const uint32_t*)table_f16, (_Float16*)enc_pm);
     return ngp_launch_status();
 }
 
@@ -1734,7 +1830,7 @@ int ngp_hash_backward(const float* xyzs, int64_t n, const int64_t* n_dev, const 
 static void launch_coarse(const float* xyzs, int64_t n, const int64_t* n_dev, const int32_t* sample_idx,
                           const GridArgs& ga, const float* denc, float* grad_table, int lo, int hi, float* rep,
                           int rep_hi, uint32_t rep_stride, int nrep, hipStream_t s) {
-    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<persistent_blocks(n, 64, HASH_BWD_BLOCKS), 256, 0, s>>>(
+    NGP_TIMED(NGP_K_HASH_BWD_COARSE, s, hash_bwd_kernel<<<persistent_blocks(n, 64, COARSE_BLOCKS), 256, 0, s>>>(
         xyzs, n, n_dev, sample_idx, ga, denc, grad_table, lo, hi, rep, rep_hi, rep_stride, nrep));
 }
 

@@ -535,29 +535,7 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
         const bool fz = FUSED && nch == 1 && !overflow;  // fused_bucket
         const bool flagged = ws.fb[b] != 0;               // direct adds in the range
         NGP_ACC_PHASE(1);
-        // A fused bucket's Adam state (p, m, v of the range) is loaded before
-        // the records are summed, so its HBM latency hides behind the LDS
-        // accumulation instead of following it (the flush then only computes
-        // and stores).  One float4 group per thread (PF x blockDim.x = a
-        // quarter of a bucket; the rest is read at the flush): 105 instead of
-        // 128 VGPRs, so one wave per SIMD of the MLP + coarse Adam fits beside
-        // these whole-CU blocks (round 5: +2.0 % end to end with the Adam's
-        // one-replica fold, profiles/r05/ab/round5_ab.txt r5bb / r5cc; four
-        // groups filled the register file and the Adam waited ~60 us).
-        constexpr int PF = 1;
         const uint32_t ng = 2 * ne / 4;  // float4 groups of the range
-        float4 pP[PF], pM[PF], pV[PF];
-        if (fz) {
-#pragma unroll
-            for (int k = 0; k < PF; ++k) {
-                const uint32_t e = t + k * blockDim.x;
-                if (e < ng) {
-                    pP[k] = reinterpret_cast<const float4*>(adam.p + gbase)[e];
-                    pM[k] = reinterpret_cast<const float4*>(adam.m + gbase)[e];
-                    pV[k] = reinterpret_cast<const float4*>(adam.v + gbase)[e];
-                }
-            }
-        }
         for (uint32_t e = t; e < 2 * BENT / 2; e += blockDim.x)
             reinterpret_cast<double2*>(img)[e] = make_double2(0.0, 0.0);
         __syncthreads();
@@ -643,16 +621,14 @@ __global__ void __launch_bounds__(ACC_T) hash_accum_kernel(GridArgs ga, BinArgs 
             const float sc = adam.grad_scale;
             return make_float4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
         };
-        uint32_t e0 = t;
-        if (fz) {
-#pragma unroll
-            for (int k = 0; k < PF; ++k, e0 += blockDim.x) {
-                if (e0 >= ng) break;
-                adam4_regs(adam, gbase, e0, fused_grad(e0), pP[k], pM[k], pV[k], lr, bc1, bc2);
-            }
-        }
-        for (uint32_t e = e0; e < ng; e += blockDim.x) {
-            if (fz) {  // (blocks narrower than PF x the range: the rest from memory)
+        // A fused bucket's Adam state (p, m, v) is read here, at the flush, not
+        // prefetched before the records (rounds 3-5 held one to four float4
+        // groups of it per thread across the record phase): 93 instead of 105-128
+        // VGPRs, so beside these whole-CU blocks (4 waves per SIMD) there is room
+        // for the MLP + coarse Adam's and the next batch's round-1 pre-encode's
+        // waves (round 5, profiles/r05/ab/round5_ab.txt r5dd-r5ff).
+        for (uint32_t e = t; e < ng; e += blockDim.x) {
+            if (fz) {
                 adam4(adam, gbase, e, fused_grad(e), lr, bc1, bc2);
                 continue;
             }

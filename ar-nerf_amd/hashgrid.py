@@ -51,6 +51,9 @@ def _lib():
         L.ngp_field_encode_mlp.argtypes = [vp, vp, c_int64, vp, vp, P, vp, vp, vp, vp, vp, vp, vp]
         L.ngp_field_forward_first.argtypes = [vp, vp, vp, vp, vp, vp, c_int64, c_int64, c_float, P, vp, vp, vp, vp, vp,
                                               vp, vp, vp, vp, vp]
+        L.ngp_field_forward_first_pre.argtypes = [vp, vp, vp, vp, vp, vp, c_int64, c_int64, c_float, P, vp, vp, vp,
+                                                  vp, vp, vp, vp, vp, vp, c_int, vp]
+        L.ngp_field_encode_first_coarse.argtypes = [vp, vp, vp, vp, c_int64, c_int64, P, vp, vp, vp]
         L.ngp_hash_backward.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp]
         L.ngp_hash_backward_binned.argtypes = [vp, c_int64, vp, vp, P, vp, vp, vp, c_int64, c_int, c_int, vp]
         L.ngp_hash_backward_levels.argtypes = [vp, c_int64, vp, vp, P, vp, vp, c_int, c_int, vp]

@@ -229,6 +229,10 @@ class NGPTrainer:
         # beside the MLP backward slows it 1.7x (garden-shaped: -6 %, profiles/r04/ab/garden_r4.txt);
         # NGP_MARCH_AT = start | r1 | fwd | mlp overrides
         self.march_at = os.environ.get("NGP_MARCH_AT", "r1" if self.cascades == 1 else "start")
+        # round 1's coarse levels 0-7 encoded ahead (the next batch's first chunks, once the MLP + coarse
+        # levels' Adam of this step has run, beside the binned levels' accumulation): round 1 then gathers
+        # only levels 8-15 (NGP_PRE_COARSE=0: off)
+        self.pre_coarse = os.environ.get("NGP_PRE_COARSE", "1") == "1"
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -289,6 +293,7 @@ class NGPTrainer:
         # HIP graphs of the steady-state step, one per buffer set (see train_step)
         self.use_graphs = bool(use_graphs)
         self._graphs = {}
+        self._graph_post = {}
         self.L = vren.lib()
         HG._lib()
         # {"field_fwd"|"mlp_bwd"|"hash_bwd"|stage: (start, end) torch.cuda.Event} (eager diagnostics)
@@ -320,7 +325,10 @@ class NGPTrainer:
                     # row-forward round 1: the non-empty rows (built by the march), the round-2 counts
                     rows_ne=torch.empty(R, dtype=torch.int32, device=dev),
                     n_rows_ne=torch.zeros(1, dtype=torch.int64, device=dev),
-                    eval_total2=torch.zeros(1, dtype=torch.int64, device=dev))
+                    eval_total2=torch.zeros(1, dtype=torch.int64, device=dev),
+                    # round 1's coarse levels 0-7 already in self.enc for this set's first chunks
+                    # (ngp_field_encode_first_coarse, run by the previous step beside its accumulation)
+                    pre_ready=False)
 
     def _bind(self, m):
         for k, v in m.items():
@@ -457,6 +465,7 @@ class NGPTrainer:
         ground truth, noise from Philox keyed by (seed, batch counter + add),
         the counter in device memory so a replayed graph draws fresh batches)."""
         m = self.msets[k]
+        m["pre_ready"] = False  # (the set's coarse-level round-1 encoding is stale from here on)
         L, R = self.L, self.batch_size
         side = stream is self.march_stream
         with torch.cuda.stream(stream):
@@ -662,7 +671,8 @@ class NGPTrainer:
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
         self._set_lr()
-        key = (k, bool(update_after), gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype)
+        key = (k, bool(update_after), gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype,
+               self.msets[k]["pre_ready"])
         if not self.dp:
             self._run_graph(key, lambda: self._graph_body(k, gt, directions, poses, update_after))
         else:
@@ -744,7 +754,8 @@ class NGPTrainer:
         if ev is not None:
             torch.cuda.current_stream().wait_event(ev)
         self._set_lr()
-        key = ("pair", k, gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype)
+        key = ("pair", k, gt.data_ptr(), directions.data_ptr(), poses.data_ptr(), gt.shape, gt.dtype,
+               self.msets[k]["pre_ready"])
 
         def body():
             self._graph_body(k, gt, directions, poses, False)
@@ -756,7 +767,7 @@ class NGPTrainer:
         self.n_prefetched += 2
         self.global_step += 1
         self._ran_ahead = True
-        self._pair_key = key[2:]
+        self._pair_key = key[2:7]
         return self.out_loss
 
     def _run_graph(self, key, body):
@@ -777,8 +788,13 @@ class NGPTrainer:
             finally:
                 if tm is not None:
                     tm.disarm()
+            # host-side state the body leaves (which buffer set has its round-1 coarse levels
+            # encoded ahead): a replay does not run the body, so it restores this instead
+            self._graph_post[key] = tuple(m["pre_ready"] for m in self.msets)
             self._graphs[key] = g
         self._graphs[key].replay()
+        for m, f in zip(self.msets, self._graph_post[key]):
+            m["pre_ready"] = f
 
     def _segment_compute(self, k, gt, directions, poses, update_after):
         """world > 1, first segment: the step up to the gradient (and the next
@@ -944,13 +960,16 @@ class NGPTrainer:
             # deciding the row's round 2, whose samples it appends to the round-2 list itself (no
             # list pass); round 2: the field over that list
             self._ev("hash_encode", 0)
-            vren._ok(HGL.ngp_field_forward_first(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a),
-                                                 _p(self.rows_ne), _p(self.n_rows_ne), R, self.cap,
-                                                 ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
-                                                 _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16),
-                                                 _p(self.enc), _p(self.sigmas), _p(self.rgbs), None,
-                                                 _p(self.eval_idx), _p(self.eval_total2), _p(self.eval_stats),
-                                                 s), "field_forward_first")
+            m = self.msets[self.cur]
+            pre = 8 if m["pre_ready"] else 0
+            m["pre_ready"] = False
+            vren._ok(HGL.ngp_field_forward_first_pre(_p(self.xyzs), _p(self.dirs), _p(self.deltas), _p(self.rays_a),
+                                                     _p(self.rows_ne), _p(self.n_rows_ne), R, self.cap,
+                                                     ctypes_float(1e-4), HG.ctypes.byref(self.grid.desc),
+                                                     _p(self.params16[HG.MLP_PARAMS:]), _p(self.params16),
+                                                     _p(self.enc), _p(self.sigmas), _p(self.rgbs), None,
+                                                     _p(self.eval_idx), _p(self.eval_total2), _p(self.eval_stats),
+                                                     pre, s), "field_forward_first")
             self._ev("hash_encode", 1)
             if fork is not None and at == "r1":
                 fork()
@@ -1052,6 +1071,15 @@ class NGPTrainer:
                 self._ev("hash_bwd_coarse", 1)
                 if adam_split:
                     self._adam(0, split, vren._stream(), rep=fold_in_adam)
+                    if self.pre_coarse and fork is not None and at == "r1" and self._rows_fwd(self.chunk_first):
+                        # the next batch (marched beside this step) gets its round-1 coarse levels now
+                        nx = self.msets[1 - self.cur]
+                        bs.wait_stream(self.march_stream)
+                        vren._ok(HGL.ngp_field_encode_first_coarse(
+                            _p(nx["xyzs"]), _p(nx["rays_a"]), _p(nx["rows_ne"]), _p(nx["n_rows_ne"]), R, self.cap,
+                            HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc),
+                            vren._stream()), "encode_first_coarse")
+                        nx["pre_ready"] = True
             self._ev("hash_binned_apply", 0)
             t = HG.MLP_PARAMS
             if binned:  # (none at bin_level_lo == L: the side stream took every level and its Adam)

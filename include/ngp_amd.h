@@ -390,6 +390,23 @@ int ngp_field_forward_first(const float* xyzs, const float* dirs, const float* d
                             float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16, const void* mlp_f16,
                             void* enc_pm, float* sigmas, float* rgbs, int32_t* rest, int32_t* list2,
                             int64_t* total2, int64_t* evaluated, void* stream);
+/* ngp_field_forward_first whose levels [0, pre_levels) (pre_levels 0 or 8) are
+ * already in enc_pm for the first-chunk samples (ngp_field_encode_first_coarse
+ * with the same rows and parameters): read back instead of gathered, and not
+ * rewritten.  Same outputs bit for bit. */
+int ngp_field_forward_first_pre(const float* xyzs, const float* dirs, const float* deltas, const int64_t* rays_a,
+                                const int32_t* rows, const int64_t* n_rows_dev, int64_t n_rows, int64_t n,
+                                float T_threshold, const ngp_hashgrid_t* grid, const void* table_f16,
+                                const void* mlp_f16, void* enc_pm, float* sigmas, float* rgbs, int32_t* rest,
+                                int32_t* list2, int64_t* total2, int64_t* evaluated, int pre_levels, void* stream);
+/* The coarse levels 0-7 of ngp_field_forward_first's encoding, ahead of time:
+ * for the rows rows[j], j < *n_rows_dev (as there), the first min(N, 64)
+ * samples' level features written to enc_pm pairs 0-3 (plane stride n).  The
+ * training step runs it for the NEXT batch once the coarse levels' Adam has
+ * run, beside the binned levels' accumulation. */
+int ngp_field_encode_first_coarse(const float* xyzs, const int64_t* rays_a, const int32_t* rows,
+                                  const int64_t* n_rows_dev, int64_t n_rows, int64_t n, const ngp_hashgrid_t* grid,
+                                  const void* table_f16, void* enc_pm, void* stream);
 int ngp_field_mlp_forward(const void* enc_pm, const float* dirs, int64_t n, const int64_t* n_dev,
                           const int32_t* sample_idx, const void* mlp_f16, float* sigmas, float* rgbs, void* h_f16,
                           void* stream);

@@ -347,6 +347,63 @@ def test_hash_backward_binned_matches_atomic(scale, level_cap, level_lo, merge_h
     torch.testing.assert_close(out.cpu(), ref.cpu(), rtol=1e-4, atol=1e-6 * float(d_ref.abs().max()))
 
 
+def test_forward_first_with_preencoded_coarse_levels_is_bit_identical():
+    """ngp_field_encode_first_coarse (levels 0-7 of the first chunks, ahead of
+    time) + ngp_field_forward_first_pre(pre_levels = 8) == ngp_field_forward_first:
+    the encoding, sigma, rgb, round-2 counts and evaluated count bit for bit;
+    the pre-encode touches only pairs 0-3 of the first-chunk samples."""
+    import ctypes
+    _, flat = _oracle_and_params(scale=0.5)
+    x, d = _points(20000, 0.5)
+    n = x.shape[0]
+    grid = HG.HashGrid(0.5)
+    p16 = flat.to(DEV).half()
+    x, d = x.to(DEV), d.to(DEV)
+    g = torch.Generator().manual_seed(7)
+    R = 400
+    N = torch.randint(1, 150, (R,), generator=g)
+    N[torch.rand(R, generator=g) < 0.4] = 0
+    while int(N.sum()) > n:
+        N = N // 2
+    start = torch.cumsum(N, 0) - N
+    rays_a = torch.stack([torch.arange(R), start, N], 1).to(DEV)
+    deltas = ((torch.rand(n, generator=g) + 0.5) * 1e-2).to(DEV)
+    L, Lv = HG._lib(), vren.lib()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    rows = torch.empty(R, dtype=torch.int32, device=DEV)
+    n_ne = torch.zeros(1, dtype=torch.int64, device=DEV)
+    vren._ok(Lv.ngp_rays_nonempty(vp(rays_a), R, vp(rows), vp(n_ne), None, None, vren._stream()), "nonempty")
+    first = torch.cat([torch.arange(int(s), int(s) + min(int(k), 64)) for s, k in zip(start, N)]).to(DEV)
+    outs = []
+    for pre in (0, 8):
+        enc_pm = torch.full((8, n, 4), 7.0, dtype=torch.float16, device=DEV)
+        sig, rgb = torch.full((n,), -1.0, device=DEV), torch.full((n, 3), -1.0, device=DEV)
+        rest = torch.full((R,), -9, dtype=torch.int32, device=DEV)
+        ev = torch.zeros(1, dtype=torch.int64, device=DEV)
+        if pre:
+            vren._ok(L.ngp_field_encode_first_coarse(vp(x), vp(rays_a), vp(rows), vp(n_ne), R, n,
+                                                     ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:]), vp(enc_pm),
+                                                     vren._stream()), "encode_first_coarse")
+            torch.cuda.synchronize()
+            rows_enc = enc_pm.permute(1, 0, 2).reshape(n, 32)
+            touched = torch.zeros(n, dtype=torch.bool, device=DEV)
+            touched[first] = True
+            assert bool((rows_enc[~touched] == 7.0).all()) and bool((rows_enc[touched][:, 16:] == 7.0).all())
+        vren._ok(L.ngp_field_forward_first_pre(vp(x), vp(d), vp(deltas), vp(rays_a), vp(rows), vp(n_ne), R, n,
+                                               ctypes.c_float(1e-4), ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:]),
+                                               vp(p16), vp(enc_pm), vp(sig), vp(rgb), vp(rest), None, None, vp(ev),
+                                               pre, vren._stream()), "forward_first_pre")
+        torch.cuda.synchronize()
+        outs.append((enc_pm.clone(), sig.clone(), rgb.clone(), rest.clone(), int(ev)))
+    (e0, s0, r0, c0, v0), (e1, s1, r1, c1, v1) = outs
+    assert torch.equal(e0.view(torch.int16), e1.view(torch.int16))
+    assert torch.equal(s0, s1) and torch.equal(r0, r1) and torch.equal(c0, c1) and v0 == v1 == first.numel()
+    assert L.ngp_field_forward_first_pre(vp(x), vp(d), vp(deltas), vp(rays_a), vp(rows), vp(n_ne), R, n,
+                                         ctypes.c_float(1e-4), ctypes.byref(grid.desc), vp(p16[HG.MLP_PARAMS:]),
+                                         vp(p16), vp(enc_pm), vp(sig), vp(rgb), vp(rest), None, None, vp(ev), 4,
+                                         vren._stream()) == -1
+
+
 @pytest.mark.parametrize("layout", ["rays", "scattered"])
 def test_coarse_scatter_matches_oracle(layout):
     """ngp_hash_backward_levels(_rep) over levels 0-7 (runs merged per wave,

@@ -359,3 +359,34 @@ def test_pair_step_replays_match_single_steps():
           f"losses {la:.5f} {lb:.5f} {lp:.5f}")
     assert float((pp - pa).norm()) <= 3 * noise + 1e-3 * float(pa.norm())
     assert abs(lp - la) <= 0.1 * abs(la) + 3 * abs(lb - la)
+
+
+def test_preencoded_round1_trains_like_the_plain_forward():
+    """Round 1's coarse levels encoded ahead beside the previous step's
+    accumulation (NGPTrainer.pre_coarse, the default) train like the plain
+    row forward: same schedule from the same seed, the pre-encode run is as
+    close to a plain run as a second plain run is (float-atomic order noise),
+    the losses agree, graphs with the pre-encoded round 1 were replayed, and
+    the host-side flag follows the replays (a replayed graph restores the
+    state its capture left)."""
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    outs = []
+    for pre in (False, False, True):
+        tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, warmup_steps=16, pair_steps=True)
+        tr.pre_coarse = pre
+        tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
+        losses = []
+        for _ in range(120):
+            losses.append(float(tr.train_step(gt_img, dirs, poses).mean()))
+        tr.drain()
+        torch.cuda.synchronize()
+        n_pre = sum(1 for k in tr._graphs if k[-1] is True or (len(k) > 7 and k[7] is True))
+        outs.append((tr.params.clone(), sum(losses[-20:]) / 20, n_pre))
+    (pa, la, na), (pb, lb, nb), (pp, lp, npre) = outs
+    assert na == nb == 0 and npre >= 1
+    noise = float((pb - pa).norm())
+    print(f"pre vs plain {float((pp - pa).norm()):.3f}, plain vs plain {noise:.3f}; losses {la:.5f} {lb:.5f} {lp:.5f}")
+    assert float((pp - pa).norm()) <= 3 * noise + 1e-3 * float(pa.norm())
+    assert abs(lp - la) <= 0.1 * abs(la) + 3 * abs(lb - la)
