@@ -871,6 +871,7 @@ __global__ void __launch_bounds__(256) encode_coarse_first_kernel(
     const int64_t* __restrict__ n_rows_dev, int64_t n_rows, int64_t n, GridArgs ga,
     const uint32_t* __restrict__ table, _Float16* __restrict__ enc_pm) {
     __shared__ LevelLds lv;
+    NGP_PROBE_BEGIN(NGP_P_PRE_ENCODE);
     load_levels(ga, lv);
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -901,6 +902,7 @@ __global__ void __launch_bounds__(256) encode_coarse_first_kernel(
                 *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(E[2 * pr], E[2 * pr + 1]);
         }
     }
+    NGP_PROBE_END();
 }
 
 // One level of the coarse (atomic) hash backward for the wave's 16 consecutive

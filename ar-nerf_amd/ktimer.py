@@ -124,7 +124,7 @@ class KernelTimer:
 # include/ngp_amd.h NGP_P_* order
 PROBES = ["march", "first_chunk", "field_encode_mlp", "composite_loss", "mlp_bwd", "hash_bwd_coarse", "hash_count",
           "hash_write", "hash_accum", "adam", "segments", "rays_nonempty", "counters_inc", "hash_plan", "adam_residual",
-          "march_compact", "sample_batch"]
+          "march_compact", "sample_batch", "pre_encode"]
 
 
 class ProbeTimer:

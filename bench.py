@@ -70,7 +70,7 @@ _MLP_BWD = (2 * (32 * 64 + 64 * 16 + 32 * 64 + 64 * 64 + 64 * 16)
             + 2 * (16 * 64 + 64 * 64 + 64 * 16 + 16 * 64 + 64 * 32)
             + 2 * (16 * 64 + 64 * 64 + 64 * 32 + 16 * 64 + 64 * 32))
 KERNEL_WORK = {  # name: (bound, [(work per unit, unit basis), ...], member probes)
-    "hash_encode": ("hbm", [(16 * 8 * 2 * 2 + 12 + 64, "evaluated")], ["first_chunk", "field_encode_mlp"]),
+    "hash_encode": ("hbm", [(16 * 8 * 2 * 2 + 12 + 64, "evaluated")], ["first_chunk", "field_encode_mlp", "pre_encode"]),
     "mlp_bwd": ("mfma", [(_MLP_BWD, "active")], ["mlp_bwd"]),
     "hash_bwd_coarse": ("atomic", [(8 * 8 * 2 * 4, "active")], ["hash_bwd_coarse"]),
     "hash_bwd_fine": ("hbm", [(32 + 12 + 2 * 8 * 8 * 2 * 2, "active"), (26, "fused_params")],
@@ -80,7 +80,7 @@ KERNEL_WORK = {  # name: (bound, [(work per unit, unit basis), ...], member prob
     "adam": ("hbm", [(34, "adam_params")], ["adam"]),  # params the Adam launches step
 }
 # PMC traffic (profiles/pmc_traffic.json) keys of each op's kernels
-PMC_KEYS = {"hash_bwd_fine": ["hash_write", "hash_accum"], "hash_encode": ["hash_encode_first", "hash_encode"],
+PMC_KEYS = {"hash_bwd_fine": ["hash_write", "hash_accum"], "hash_encode": ["hash_encode_first", "hash_encode", "hash_encode_pre"],
             "mlp_bwd": ["mlp_bwd"], "adam": ["adam"]}
 
 

@@ -72,7 +72,7 @@ double ngp_timing_tick_ns(void);
 enum {
     NGP_P_MARCH = 0, NGP_P_FIRST_CHUNK, NGP_P_FIELD_ENCODE_MLP, NGP_P_COMPOSITE, NGP_P_MLP_BWD, NGP_P_HASH_BWD_COARSE,
     NGP_P_HASH_COUNT, NGP_P_HASH_WRITE, NGP_P_HASH_ACCUM, NGP_P_ADAM, NGP_P_SEGMENTS, NGP_P_NONEMPTY, NGP_P_COUNTERS,
-    NGP_P_HASH_PLAN, NGP_P_RESIDUAL, NGP_P_COMPACT, NGP_P_SAMPLE_BATCH,
+    NGP_P_HASH_PLAN, NGP_P_RESIDUAL, NGP_P_COMPACT, NGP_P_SAMPLE_BATCH, NGP_P_PRE_ENCODE,
     NGP_P_COUNT
 };
 int ngp_probe_set(uint64_t* buf, const int64_t* step_dev, int64_t ring);

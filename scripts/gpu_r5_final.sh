@@ -22,6 +22,6 @@ python3 scripts/kstats.py $TR 200 > $OUT/kstats.txt 2>&1 || true
 python3 scripts/timeline.py $TR 20 10 > $OUT/timeline.txt 2>&1 || true
 cp $(find $OUT/prof -name 'run_kernel_stats.csv' | head -1) $OUT/rocprof_kernel_stats.csv || true
 rm -rf $OUT/prof
-bash scripts/pmc_bench.sh 'hash_write|hash_accum|hash_adam_residual|adam_kernel|field_|hash_bwd_kernel' $T "fetch write atom"
+bash scripts/pmc_bench.sh 'hash_write|hash_accum|hash_adam_residual|adam_kernel|field_|encode_coarse|hash_bwd_kernel' $T "fetch write atom"
 python3 scripts/pmc_traffic.py gpurun_out/pmc_$T $OUT/pmc_traffic.json > /dev/null
 python3 -c "import json,sys; d=json.load(open(sys.argv[1])); [print(k, v['bytes_per_launch'], v.get('dur_us_fetch_pass')) for k, v in d.items() if k[0] != '_']" $OUT/pmc_traffic.json

@@ -14,6 +14,7 @@ import sys
 NAMES = {"hash_bwd_kernel": "hash_bwd_coarse", "field_bwd_mlp_kernel": "mlp_bwd", "hash_encode_kernel": "hash_encode",
          "field_bwd_mlp_coop_kernel": "mlp_bwd", "field_encode_mlp_kernel": "hash_encode",
          "field_encode_mlp_reg_kernel": "hash_encode", "field_first_chunk_kernel": "hash_encode_first",
+         "encode_coarse_first_kernel": "hash_encode_pre",
          "field_rows_block_kernel": "hash_encode_rows",
          "hash_adam_residual_kernel": "adam",
          "adam_kernel": "adam", "field_fwd_kernel": "field_mlp", "hash_write_kernel": "hash_write",

@@ -23,6 +23,7 @@ KERNEL_OF = {
     "march": "march_slots_wave_kernel",
     "first_chunk": "field_first_chunk_kernel",
     "field_encode_mlp": ("field_encode_mlp_reg_kernel", ("ILb1E", "<true>")),
+    "pre_encode": "encode_coarse_first_kernel",
     "composite_loss": "composite_loss_wave_kernel",
     "mlp_bwd": "field_bwd_mlp_coop_kernel",
     "hash_bwd_coarse": ("hash_bwd_", ("hash_bwd_kernel", "hash_bwd_wide_kernel")),
