@@ -233,6 +233,7 @@ class NGPTrainer:
         # levels' Adam of this step has run, beside the binned levels' accumulation): round 1 then gathers
         # only levels 8-15 (NGP_PRE_COARSE=0: off)
         self.pre_coarse = os.environ.get("NGP_PRE_COARSE", "1") == "1"
+        self.pre_levels = 8  # (the kernel's PRE_LEVELS: levels 0-7, final once the side stream's Adam has run)
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -1071,7 +1072,10 @@ class NGPTrainer:
                 self._ev("hash_bwd_coarse", 1)
                 if adam_split:
                     self._adam(0, split, vren._stream(), rep=fold_in_adam)
-                    if self.pre_coarse and fork is not None and at == "r1" and self._rows_fwd(self.chunk_first):
+                    # (only while levels 0-7 are all stepped by that Adam: the binned levels' parameters
+                    # change inside the accumulation, after this launch)
+                    if self.pre_coarse and fork is not None and at == "r1" and self._rows_fwd(self.chunk_first) \
+                            and self.bin_level_lo >= self.pre_levels:
                         # the next batch (marched beside this step) gets its round-1 coarse levels now
                         nx = self.msets[1 - self.cur]
                         bs.wait_stream(self.march_stream)

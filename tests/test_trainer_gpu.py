@@ -390,3 +390,22 @@ def test_preencoded_round1_trains_like_the_plain_forward():
     print(f"pre vs plain {float((pp - pa).norm()):.3f}, plain vs plain {noise:.3f}; losses {la:.5f} {lb:.5f} {lp:.5f}")
     assert float((pp - pa).norm()) <= 3 * noise + 1e-3 * float(pa.norm())
     assert abs(lp - la) <= 0.1 * abs(la) + 3 * abs(lb - la)
+
+
+def test_preencode_only_when_levels_0_7_are_stepped_before_it():
+    """The pre-encode reads levels 0-7 right after the side stream's Adam; with
+    any of them binned (their Adam runs inside the accumulation, after it) it
+    must stay off: no graph replays a pre-encoded round 1."""
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    for kw in ({"hash_backward": "binned"}, {"bin_level_lo": 6}):
+        tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, warmup_steps=16, pair_steps=True, **kw)
+        assert tr.pre_coarse and tr.bin_level_lo < 8
+        tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
+        for _ in range(40):
+            tr.train_step(gt_img, dirs, poses)
+        tr.drain()
+        torch.cuda.synchronize()
+        assert not any(k[-1] is True or (len(k) > 7 and k[7] is True) for k in tr._graphs)
+        assert not any(m["pre_ready"] for m in tr.msets)
