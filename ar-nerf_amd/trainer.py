@@ -1065,20 +1065,27 @@ class NGPTrainer:
             self._adam_hi = split if fused else self.n_params
             fold_in_adam = adam_split and self.rep_buf is not None
 
+            # the next batch's round-1 pre-encode after the Adam below (only while levels 0-7 are all
+            # stepped by that Adam: the binned levels' parameters change inside the accumulation)
+            pre = (adam_split and self.pre_coarse and fork is not None and at == "r1"
+                   and self._rows_fwd(self.chunk_first) and self.bin_level_lo >= self.pre_levels)
             bs.wait_stream(cs)
+            if pre and os.environ.get("NGP_PRE_WAIT", "coarse") == "coarse":
+                # its dependency on the next batch's march (done long before) taken by the coarse
+                # kernel, which waits on the main stream anyway: a second cross-queue wait on the
+                # pre-encode itself delayed its start ~12 us past the Adam's end (r5tl)
+                bs.wait_stream(self.march_stream)
             with torch.cuda.stream(bs):
                 self._ev("hash_bwd_coarse", 0)
                 self._coarse_levels(fold=not fold_in_adam)
                 self._ev("hash_bwd_coarse", 1)
                 if adam_split:
                     self._adam(0, split, vren._stream(), rep=fold_in_adam)
-                    # (only while levels 0-7 are all stepped by that Adam: the binned levels' parameters
-                    # change inside the accumulation, after this launch)
-                    if self.pre_coarse and fork is not None and at == "r1" and self._rows_fwd(self.chunk_first) \
-                            and self.bin_level_lo >= self.pre_levels:
+                    if pre:
                         # the next batch (marched beside this step) gets its round-1 coarse levels now
                         nx = self.msets[1 - self.cur]
-                        bs.wait_stream(self.march_stream)
+                        if os.environ.get("NGP_PRE_WAIT", "coarse") != "coarse":
+                            bs.wait_stream(self.march_stream)
                         vren._ok(HGL.ngp_field_encode_first_coarse(
                             _p(nx["xyzs"]), _p(nx["rays_a"]), _p(nx["rows_ne"]), _p(nx["n_rows_ne"]), R, self.cap,
                             HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc),
