@@ -876,31 +876,26 @@ __global__ void __launch_bounds__(256) encode_coarse_first_kernel(
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t NR = n_rows_dev ? min(*n_rows_dev, n_rows) : n_rows;  // (a device count never past the capacity)
+    // a wave item = (row, level pair): one gather round per item, the row's PRE_LEVELS / 2 pairs
+    // on consecutive waves (one dependent round each instead of PRE_LEVELS / 2 per row: the rows
+    // are ~2.7 K, a third of the waves the chip holds)
+    constexpr int NP = PRE_LEVELS / 2;
     const int64_t stride = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t j = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < NR; j += stride) {
+    for (int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); q < NR * NP; q += stride) {
+        const int64_t j = q / NP;
+        const int pr = (int)(q - j * NP);
         const int64_t r = rows ? (int64_t)rows[j] : j;
         const int64_t start = rays_a[3 * r + 1], N = rays_a[3 * r + 2];
         const bool valid = lane < N;
         const int64_t i = start + lane;
         float in[3];
         load_x01(xyzs, i, valid, ga, in);
-        uint32_t E[PRE_LEVELS];
-#pragma unroll 1
-        for (int rr = 0; rr < PRE_LEVELS / FEM_LPR; ++rr) {
-            uint32_t v[FEM_LPR][8];
-#pragma unroll
-            for (int q = 0; q < FEM_LPR; ++q) gather_level_loads(in, level_u(lv, FEM_LPR * rr + q), table, v[q]);
-#pragma unroll
-            for (int q = 0; q < PRE_LEVELS - FEM_LPR; ++q) E[q] = E[q + FEM_LPR];
-#pragma unroll
-            for (int q = 0; q < FEM_LPR; ++q)
-                E[PRE_LEVELS - FEM_LPR + q] = level_sum_h2(in, level_u(lv, FEM_LPR * rr + q), v[q]);
-        }
-        if (valid) {
-#pragma unroll
-            for (int pr = 0; pr < PRE_LEVELS / 2; ++pr)
-                *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(E[2 * pr], E[2 * pr + 1]);
-        }
+        uint32_t v[2][8];
+        gather_level_loads(in, level_u(lv, 2 * pr), table, v[0]);
+        gather_level_loads(in, level_u(lv, 2 * pr + 1), table, v[1]);
+        const uint32_t e0 = level_sum_h2(in, level_u(lv, 2 * pr), v[0]);
+        const uint32_t e1 = level_sum_h2(in, level_u(lv, 2 * pr + 1), v[1]);
+        if (valid) *reinterpret_cast<uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) = make_uint2(e0, e1);
     }
     NGP_PROBE_END();
 }
@@ -1773,7 +1768,7 @@ int ngp_field_encode_first_coarse(const float* xyzs, const int64_t* rays_a, cons
                   ((uintptr_t)enc_pm & 7) == 0);
     hipStream_t s = as_stream(stream);
     static const unsigned cap = resident_blocks(encode_coarse_first_kernel, 256, 0);
-    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + 3) / 4)));
+    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows * (PRE_LEVELS / 2) + 3) / 4)));
     encode_coarse_first_kernel<<<blocks, 256, 0, s>>>(xyzs, rays_a, rows, n_rows_dev, n_rows, n, ga,
                                                       (const uint32_t*)table_f16, (_Float16*)enc_pm);
     return ngp_launch_status();

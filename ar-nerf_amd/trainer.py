@@ -1070,10 +1070,10 @@ class NGPTrainer:
             pre = (adam_split and self.pre_coarse and fork is not None and at == "r1"
                    and self._rows_fwd(self.chunk_first) and self.bin_level_lo >= self.pre_levels)
             bs.wait_stream(cs)
-            if pre and os.environ.get("NGP_PRE_WAIT", "coarse") == "coarse":
+            if pre:
                 # its dependency on the next batch's march (done long before) taken by the coarse
-                # kernel, which waits on the main stream anyway: a second cross-queue wait on the
-                # pre-encode itself delayed its start ~12 us past the Adam's end (r5tl)
+                # kernel, which waits on the main stream anyway (a second cross-queue wait on the
+                # pre-encode itself started it ~12 us after the Adam's end instead of ~7: r5tl / r5ii)
                 bs.wait_stream(self.march_stream)
             with torch.cuda.stream(bs):
                 self._ev("hash_bwd_coarse", 0)
@@ -1084,8 +1084,6 @@ class NGPTrainer:
                     if pre:
                         # the next batch (marched beside this step) gets its round-1 coarse levels now
                         nx = self.msets[1 - self.cur]
-                        if os.environ.get("NGP_PRE_WAIT", "coarse") != "coarse":
-                            bs.wait_stream(self.march_stream)
                         vren._ok(HGL.ngp_field_encode_first_coarse(
                             _p(nx["xyzs"]), _p(nx["rays_a"]), _p(nx["rows_ne"]), _p(nx["n_rows_ne"]), R, self.cap,
                             HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc),
