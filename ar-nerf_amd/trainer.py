@@ -1067,7 +1067,8 @@ class NGPTrainer:
 
             # the next batch's round-1 pre-encode after the Adam below (only while levels 0-7 are all
             # stepped by that Adam: the binned levels' parameters change inside the accumulation)
-            pre = (adam_split and self.pre_coarse and fork is not None and at == "r1"
+            # (any fork point: the next batch's march is captured before this point)
+            pre = (adam_split and self.pre_coarse and fork is not None
                    and self._rows_fwd(self.chunk_first) and self.bin_level_lo >= self.pre_levels)
             bs.wait_stream(cs)
             if pre:
