@@ -707,7 +707,7 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
 // chunk; returns this lane's sigma (0 past cnt) for a transmittance epilogue.
 // pre (0 or PRE_LEVELS): levels [0, pre) are already in enc_pm (written by
 // encode_coarse_first_kernel with the same arithmetic) and only read back.
-template <bool COLOR, int LPR = FEM_LPR>
+template <bool COLOR>
 __device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs, const float* __restrict__ dirs,
                                                   int64_t i0, int cnt, int64_t n, const GridArgs& ga,
                                                   const LevelLds& lv, const uint32_t* __restrict__ table,
@@ -722,7 +722,7 @@ __device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs
     load_x01(xyzs, i, valid, ga, in);
     uint32_t E[16];
     if (pre) {
-        // after pre / LPR rounds the chain holds levels [0, pre) at the top of E
+        // after pre / FEM_LPR rounds the chain holds levels [0, pre) at the top of E
 #pragma unroll
         for (int pr = 0; pr < PRE_LEVELS / 2; ++pr) {
             const uint2 q = valid ? *reinterpret_cast<const uint2*>(enc_pm + ((int64_t)pr * n + i) * 4) : make_uint2(0u, 0u);
@@ -730,16 +730,15 @@ __device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs
             E[16 - PRE_LEVELS + 2 * pr + 1] = q.y;
         }
     }
-    static_assert(L % LPR == 0 && PRE_LEVELS % LPR == 0, "levels per round");
 #pragma unroll 1
-    for (int rr = pre / LPR; rr < L / LPR; ++rr) {
-        uint32_t v[LPR][8];
+    for (int rr = pre / FEM_LPR; rr < L / FEM_LPR; ++rr) {
+        uint32_t v[FEM_LPR][8];
 #pragma unroll
-        for (int q = 0; q < LPR; ++q) gather_level_loads(in, level_u(lv, LPR * rr + q), table, v[q]);
+        for (int q = 0; q < FEM_LPR; ++q) gather_level_loads(in, level_u(lv, FEM_LPR * rr + q), table, v[q]);
 #pragma unroll
-        for (int q = 0; q < 16 - LPR; ++q) E[q] = E[q + LPR];
+        for (int q = 0; q < 16 - FEM_LPR; ++q) E[q] = E[q + FEM_LPR];
 #pragma unroll
-        for (int q = 0; q < LPR; ++q) E[16 - LPR + q] = level_sum_h2(in, level_u(lv, LPR * rr + q), v[q]);
+        for (int q = 0; q < FEM_LPR; ++q) E[16 - FEM_LPR + q] = level_sum_h2(in, level_u(lv, FEM_LPR * rr + q), v[q]);
     }
     if (valid && enc_pm) {
 #pragma unroll
@@ -796,22 +795,8 @@ __device__ __forceinline__ float encode_mlp_chunk(const float* __restrict__ xyzs
 // value); their count is added to *evaluated with the first chunks'.  A wave
 // per row rather than 64 packed list entries (~8 % idle lanes on this step's
 // rows); the sigmas never leave registers.
-// Round 1 runs alone on the chip with ~one row per wave (~2.7 K rows): its
-// rows fit the resident waves at 3 per SIMD, so it takes 4 levels per gather
-// round (two dependent rounds for levels 8-15 after the pre-encode, four
-// without) at <= 168 VGPRs, in 4-wave blocks (three per CU).
-#ifndef NGP_R1_WAVES
-#define NGP_R1_WAVES 4
-#endif
-#ifndef NGP_R1_LPR
-#define NGP_R1_LPR 4
-#endif
-#ifndef NGP_R1_WPS
-#define NGP_R1_WPS 3  // waves per SIMD the launch bound asks for
-#endif
-constexpr int R1_WAVES = NGP_R1_WAVES, R1_LPR = NGP_R1_LPR;
 template <bool COLOR>
-__global__ void __launch_bounds__(64 * R1_WAVES, NGP_R1_WPS) field_first_chunk_kernel(
+__global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_chunk_kernel(
     const float* __restrict__ xyzs, const float* __restrict__ dirs, const float* __restrict__ deltas,
     const int64_t* __restrict__ rays_a, const int32_t* __restrict__ rows, const int64_t* __restrict__ n_rows_dev,
     int64_t n_rows, int64_t n, float T_thr, GridArgs ga, const uint32_t* __restrict__ table,
@@ -824,7 +809,7 @@ __global__ void __launch_bounds__(64 * R1_WAVES, NGP_R1_WPS) field_first_chunk_k
     NGP_PROBE_BEGIN(NGP_P_FIRST_CHUNK);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t NR = n_rows_dev ? min(*n_rows_dev, n_rows) : n_rows;  // (a device count never past the capacity)
-    const int64_t G = gridDim.x, stride = (int64_t)R1_WAVES * G;
+    const int64_t G = gridDim.x, stride = (int64_t)FEM2_WAVES * G;
     int64_t j = (int64_t)wv * G + blockIdx.x;  // the wave's first row (wave-uniform)
     // its row (list -> rays_a: dependent round trips) requested before the weight image is built
     int64_t r = 0, start = 0, N = 0;
@@ -843,7 +828,7 @@ __global__ void __launch_bounds__(64 * R1_WAVES, NGP_R1_WPS) field_first_chunk_k
         int32_t rc = 0;
         if (cnt > 0) {
             const float dl = lane < cnt ? deltas[start + lane] : 0.f;
-            const float sg = encode_mlp_chunk<COLOR, R1_LPR>(xyzs, dirs, start, cnt, n, ga, lv, table, sw, enc_pm, sigmas, rgbs,
+            const float sg = encode_mlp_chunk<COLOR>(xyzs, dirs, start, cnt, n, ga, lv, table, sw, enc_pm, sigmas, rgbs,
                                                      pre);
             const float om = 1.0f - (1.0f - __expf(-sg * dl));  // chunk_segments_kernel's expression
             const ChunkT ct = chunk_transmittance(om, cnt, 1.0f, T_thr, lane);
@@ -1753,9 +1738,9 @@ int ngp_field_forward_first_pre(const float* xyzs, const float* dirs, const floa
                   ((uintptr_t)evaluated & 7) == 0);
     hipStream_t s = as_stream(stream);
     // grid = every resident block: the rows are dealt over all resident waves
-    static const unsigned cap = resident_blocks(field_first_chunk_kernel<true>, 64 * R1_WAVES, 0);
-    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + R1_WAVES - 1) / R1_WAVES)));
-    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_first_chunk_kernel<true><<<blocks, 64 * R1_WAVES, 0, s>>>(
+    static const unsigned cap = resident_blocks(field_first_chunk_kernel<true>, 64 * FEM2_WAVES, 0);
+    const unsigned blocks = std::max(1u, std::min(cap, (unsigned)((n_rows + FEM2_WAVES - 1) / FEM2_WAVES)));
+    NGP_TIMED(NGP_K_HASH_ENCODE, s, field_first_chunk_kernel<true><<<blocks, 64 * FEM2_WAVES, 0, s>>>(
         xyzs, dirs, deltas, rays_a, rows, n_rows_dev, n_rows, n, T_threshold, ga, (const uint32_t*)table_f16,
         (const _Float16*)mlp_f16, (_Float16*)enc_pm, sigmas, rgbs, rest, list2, total2, evaluated, pre_levels));
     return ngp_launch_status();
