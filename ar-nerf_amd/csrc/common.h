@@ -57,6 +57,34 @@ __device__ __forceinline__ unsigned long long* ngp_probe_slot(int id) {
 #define NGP_PROBE_END() \
     if (ngp_probe_ && (threadIdx.x & 63) == 0) ngp_probe_[1] = (unsigned long long)wall_clock64()
 
+// Capacity guards (ngp_guard_hits, host.hip): every translation unit counts
+// in its own device word and registers a reader/resetter at load time.  A
+// kernel that clamps a device-side count to the capacity its caller gave it
+// (so an overflow cannot write or read out of bounds) counts the clamp here:
+// the result is then truncated, and ngp_guard_hits() > 0 says so.
+static __device__ unsigned long long ngp_guard_tu;
+void ngp_guard_register(unsigned long long (*get)(int reset));
+static unsigned long long ngp_guard_get_tu(int reset) {
+    unsigned long long v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(ngp_guard_tu), sizeof v) != hipSuccess) return ~0ull;
+    if (reset) {
+        const unsigned long long z = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(ngp_guard_tu), &z, sizeof z);
+    }
+    return v;
+}
+static const int ngp_guard_registered = (ngp_guard_register(ngp_guard_get_tu), 0);
+__device__ __forceinline__ void ngp_guard_hit() { atomicAdd(&ngp_guard_tu, 1ull); }
+// *n_dev (a device-side count) clamped to the capacity n; a clamp counts one
+// guard hit (thread 0 of block 0 only: one per launch).  n_dev null: n.
+__device__ __forceinline__ int64_t ngp_capped_count(const int64_t* n_dev, int64_t n) {
+    if (!n_dev) return n;
+    const int64_t v = *n_dev;
+    if (v <= n) return v;
+    if (blockIdx.x == 0 && threadIdx.x == 0) ngp_guard_hit();
+    return n;
+}
+
 // Workgroups of `kernel` that fit on the whole device at once (occupancy x
 // CUs): the grid of a persistent kernel, so per-block prologues (LDS weight
 // images) are paid once per resident block, not once per tile.

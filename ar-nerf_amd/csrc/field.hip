@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(256) field_fwd_kernel(const float* __restrict_
     load_fwd_weights_direct(mlp, sw, COLOR);
     if constexpr (!ENC_IN) load_levels(ga, lv);
     __syncthreads();
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
+    const int64_t N = ngp_capped_count(n_dev, n);  // (a device count never past the capacity: a guard hit)
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16; base < N; base += nw * 16) {
@@ -519,7 +519,7 @@ __global__ void __launch_bounds__(256) hash_encode_kernel(const float* __restric
     __shared__ LevelLds lv;
     load_levels(ga, lv);
     __syncthreads();
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
+    const int64_t N = ngp_capped_count(n_dev, n);  // (a device count never past the capacity: a guard hit)
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < N; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = sidx ? (int64_t)sidx[j] : j;
         float in[3];
@@ -586,16 +586,9 @@ __device__ __forceinline__ uint32_t pack_h2(float a, float b) {
     return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)b) << 16);
 }
 
-#ifndef NGP_FEM_LPR
-#define NGP_FEM_LPR 2  // 4: the loads of 4 levels in flight need > 128 VGPRs (spills)
-#endif
-#ifndef NGP_FEM2_WAVES
-#define NGP_FEM2_WAVES 8
-#endif
-#ifndef NGP_FEM_REMAT
-#define NGP_FEM_REMAT 1
-#endif
-constexpr int FEM2_WAVES = NGP_FEM2_WAVES, FEM_LPR = NGP_FEM_LPR;
+// 8 waves per block; 2 levels per gather round (4: the loads of 4 levels in flight need > 128
+// VGPRs and spill, -3 %)
+constexpr int FEM2_WAVES = 8, FEM_LPR = 2;
 constexpr int PRE_LEVELS = 8;  // coarse levels round 1 may find pre-encoded (encode_coarse_first_kernel)
 static_assert(PRE_LEVELS % FEM_LPR == 0 && PRE_LEVELS % 2 == 0, "pre-encoded levels: whole rounds and pairs");
 static_assert(L % FEM_LPR == 0, "levels per round");
@@ -608,11 +601,8 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
     __shared__ __attribute__((aligned(16))) _Float16 sw[SWF];
     __shared__ LevelLds lv;
     NGP_PROBE_BEGIN(NGP_P_FIELD_ENCODE_MLP);
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
+    const int64_t N = ngp_capped_count(n_dev, n);  // (a device count never past the capacity: a guard hit)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#if !NGP_FEM_REMAT
-    const int s = lane & 15, g = lane >> 4;
-#endif
     const int64_t G = gridDim.x;
     const int64_t chunks = (N + 63) >> 6;
     int64_t k = (int64_t)wv * G + blockIdx.x;  // first chunk of this wave (wave-uniform)
@@ -631,14 +621,10 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_encode_
     __syncthreads();
     bool first = true;
     for (; k < chunks; k += (int64_t)FEM2_WAVES * G) {
-#if NGP_FEM_REMAT
         int lane_l = lane;  // (opaque per iteration: lane-derived addresses are not held across the loop)
         asm volatile("" : "+v"(lane_l));
         const int s = lane_l & 15, g = lane_l >> 4;
         const int64_t j = k * 64 + lane_l;
-#else
-        const int64_t j = k * 64 + lane;
-#endif
         const bool valid = j < N;
         int64_t i = i_first;
         float in[3] = {in_first[0], in_first[1], in_first[2]};
@@ -808,7 +794,7 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
     __shared__ unsigned long long blk_eval;
     NGP_PROBE_BEGIN(NGP_P_FIRST_CHUNK);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t NR = n_rows_dev ? min(*n_rows_dev, n_rows) : n_rows;  // (a device count never past the capacity)
+    const int64_t NR = ngp_capped_count(n_rows_dev, n_rows);  // (a device count never past the capacity: a guard hit)
     const int64_t G = gridDim.x, stride = (int64_t)FEM2_WAVES * G;
     int64_t j = (int64_t)wv * G + blockIdx.x;  // the wave's first row (wave-uniform)
     // its row (list -> rays_a: dependent round trips) requested before the weight image is built
@@ -840,7 +826,8 @@ __global__ void __launch_bounds__(64 * FEM2_WAVES, FEM2_WAVES / 2) field_first_c
             unsigned long long o = 0;
             if (lane == 0) o = atomicAdd((unsigned long long*)total2, (unsigned long long)rc);
             const int64_t o2 = (int64_t)__shfl(o, 0, 64);
-            for (int t = lane; t < rc && o2 + t < n; t += 64) list2[o2 + t] = (int32_t)(start + 64 + t);  // (bounded by the list's capacity n)
+            if (lane == 0 && o2 + rc > n) ngp_guard_hit();  // (past the list's capacity n: counted, then bounded)
+            for (int t = lane; t < rc && o2 + t < n; t += 64) list2[o2 + t] = (int32_t)(start + 64 + t);
             ev += rc;
         }
         const int64_t jn = j + stride;
@@ -875,7 +862,7 @@ __global__ void __launch_bounds__(256) encode_coarse_first_kernel(
     load_levels(ga, lv);
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t NR = n_rows_dev ? min(*n_rows_dev, n_rows) : n_rows;  // (a device count never past the capacity)
+    const int64_t NR = ngp_capped_count(n_rows_dev, n_rows);  // (a device count never past the capacity: a guard hit)
     // a wave item = (row, level pair): one gather round per item, the row's PRE_LEVELS / 2 pairs
     // on consecutive waves (one dependent round each instead of PRE_LEVELS / 2 per row: the rows
     // are ~2.7 K, a third of the waves the chip holds)
@@ -1153,13 +1140,9 @@ __device__ __forceinline__ void acc_tile_info(int k, int& ow, int& in_dim, int& 
 #define NGP_BWD_PHASE(k)
 #define NGP_BWD_EDGE(k)
 #endif
-#ifndef NGP_BWD_REMAT
-#define NGP_BWD_REMAT 1
-#endif
-#ifndef NGP_BWD_CW
-#define NGP_BWD_CW 8  // waves per block (CW / 4 per SIMD); 12 fits the LDS (161 KB) at <= 168 VGPRs
-#endif
-constexpr int CW = NGP_BWD_CW, NT1 = 19, NT2 = 11, CSCRW = NT1 * TTILE;
+// CW waves per block (CW / 4 per SIMD; 12 fit the LDS at <= 168 VGPRs but measured -3 %, DESIGN.md
+// section 9 round 4)
+constexpr int CW = 8, NT1 = 19, NT2 = 11, CSCRW = NT1 * TTILE;
 constexpr int COOP_LDS_HALFS = SCR + CW * CSCRW;
 static_assert(CW % 4 == 0, "waves per block: a multiple of 4");
 static_assert(NGP_MLP_PARAMS <= CW * CSCRW && NT2 <= NT1, "raw weight staging / phase-2 tiles exceed the scratch");
@@ -1270,7 +1253,7 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     _Float16* scr = smem + SCR;
     NGP_BWD_EDGE(0);
     NGP_PROBE_BEGIN(NGP_P_MLP_BWD);
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
+    const int64_t N = ngp_capped_count(n_dev, n);  // (a device count never past the capacity: a guard hit)
     const int lane = threadIdx.x & 63, s = lane & 15, g = lane >> 4;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     _Float16* mine = scr + wid * CSCRW;
@@ -1328,14 +1311,12 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
         load_in(i_next, nxt);
         i_next = row_index(base + s + 2 * stride);
         NGP_BWD_PHASE(0);
-#if NGP_BWD_REMAT
         // the lane's (sample, group) re-derived opaquely per iteration: the LDS / global
         // addresses built from them are recomputed here instead of held (or spilled) across the
         // loop as loop-invariant registers
         int lane_l = lane;
         asm volatile("" : "+v"(lane_l));
         const int s = lane_l & 15, g = lane_l >> 4;
-#endif
         const int64_t j = base + s;
         const bool valid = j < N;
         const h8 e = cur.e;
@@ -1539,7 +1520,7 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
     NGP_PROBE_BEGIN(NGP_P_HASH_BWD_COARSE);
     load_levels(ga, lv);
     __syncthreads();
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
+    const int64_t N = ngp_capped_count(n_dev, n);  // (a device count never past the capacity: a guard hit)
     const int lane = threadIdx.x & 63, s = lane >> 2, cx = (lane >> 1) & 1, f = lane & 1, wv = threadIdx.x >> 6;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + wv) * 16; base < N; base += nw * 16) {

@@ -54,10 +54,7 @@ namespace ngp {
 
 // entries per bucket (fp64 LDS image: 2 x BENT x 8 B = 128 KB, one accumulating workgroup per CU;
 // 4096-entry buckets at two per CU measured the same accumulation time and a slower count pass)
-#ifndef NGP_BSHIFT
-#define NGP_BSHIFT 13
-#endif
-constexpr int BSHIFT = NGP_BSHIFT, BENT = 1 << BSHIFT;
+constexpr int BSHIFT = 13, BENT = 1 << BSHIFT;
 constexpr int NBL = (1 << 19) / BENT;            // bucket slots per level (2^19 / BENT)
 // accumulation workgroup: 8192-entry buckets (128 KB LDS, one per CU) take
 // 1024 threads, 4096-entry buckets (64 KB, two per CU) 512, so that a
@@ -185,7 +182,7 @@ __global__ void __launch_bounds__(256) hash_count_kernel(const float* __restrict
     __shared__ uint32_t cnt[NSLOT];
     NGP_PROBE_BEGIN(NGP_P_HASH_COUNT);
     load_levels(ga, lv);
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
+    const int64_t N = ngp_capped_count(n_dev, n);  // (a device count never past the capacity: a guard hit)
     const int64_t ntiles = min((N + TILE - 1) / TILE, ba.tiles_cap);
     const int t = threadIdx.x, yz = t & 3, cy = yz & 1, cz = yz >> 1;
     const float2 g0 = make_float2(0.f, 0.f);
@@ -228,7 +225,7 @@ __global__ void __launch_bounds__(256) hash_scan_kernel(const int64_t* __restric
     __shared__ uint32_t wsum[4];
     const int slot = blockIdx.x, l = slot / NBL, lb = slot % NBL;
     if (lb >= (int)(ba.bbase[l + 1] - ba.bbase[l])) return;
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
+    const int64_t N = ngp_capped_count(n_dev, n);  // (a device count never past the capacity: a guard hit)
     const int64_t ntiles = min((N + TILE - 1) / TILE, ba.tiles_cap);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint32_t carry = 0;
@@ -305,7 +302,7 @@ __global__ void __launch_bounds__(256) hash_write_kernel(const float* __restrict
     static_assert(sizeof(stage) >= NSLOT * sizeof(uint32_t), "stage[] holds the per-level counters");
     NGP_PROBE_BEGIN(NGP_P_HASH_WRITE);
     load_levels(ga, lv);
-    const int64_t N = n_dev ? min(*n_dev, n) : n;  // (a device count never past the capacity)
+    const int64_t N = ngp_capped_count(n_dev, n);  // (a device count never past the capacity: a guard hit)
     const int64_t ntiles = (N + TILE - 1) / TILE;
     const int t = threadIdx.x, yz = t & 3, cy = yz & 1, cz = yz >> 1;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {

@@ -37,6 +37,13 @@ void ngp_probe_register(void (*set)(const ProbeCtl&)) {
     if (g_n_probe_setters < 16) g_probe_setters[g_n_probe_setters++] = set;
 }
 
+// capacity guards: each translation unit's counter reader (common.h)
+static unsigned long long (*g_guard_getters[16])(int);
+static int g_n_guard_getters = 0;
+void ngp_guard_register(unsigned long long (*get)(int)) {
+    if (g_n_guard_getters < 16) g_guard_getters[g_n_guard_getters++] = get;
+}
+
 // a kernel whose only purpose is its name in a dispatch trace (ngp_trace_marker)
 __global__ void trace_marker_kernel(int tag) {
     if (tag < 0) __builtin_trap();  // (never: keeps the argument live)
@@ -69,6 +76,22 @@ int ngp_probe_set(uint64_t* buf, const int64_t* step_dev, int64_t ring) {
 }
 
 int ngp_probe_count(void) { return NGP_P_COUNT; }
+
+unsigned long long ngp_guard_hits(void) {
+    unsigned long long s = 0;
+    for (int i = 0; i < g_n_guard_getters; ++i) {
+        const unsigned long long v = g_guard_getters[i](0);
+        if (v == ~0ull) return ~0ull;
+        s += v;
+    }
+    return s;
+}
+
+int ngp_guard_reset(void) {
+    for (int i = 0; i < g_n_guard_getters; ++i)
+        if (g_guard_getters[i](1) == ~0ull) return NGP_EINVAL;
+    return NGP_OK;
+}
 
 int ngp_trace_marker(int tag, void* stream) {
     NGP_CHECK_ARG(tag >= 0);

@@ -410,7 +410,7 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
     wc.dil = wc.sum ? wc.sum + p.n_sum32 : nullptr;
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // one ray per wave; a grid capped below the rays (NGP_MARCH_BLOCKS, A/B) strides over them
+    // one ray per wave (grid-stride: any grid covers every ray)
     for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < n_rays; r += (int64_t)gridDim.x * 4) {
         float o[3], d[3], dinv[3];
         load_ray(rays_o, rays_d, r, o, d, dinv);
@@ -612,11 +612,6 @@ __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict_
 using namespace ngp;
 
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
-// (A/B) a cap on the training march's grid (env NGP_MARCH_BLOCKS; 0 / unset: one 4-ray block per 4 rays)
-static inline unsigned march_blocks(unsigned b) {
-    static const unsigned cap = getenv("NGP_MARCH_BLOCKS") ? (unsigned)atoi(getenv("NGP_MARCH_BLOCKS")) : 0u;
-    return cap && cap < b ? cap : b;
-}
 
 extern "C" {
 
@@ -783,7 +778,7 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
         NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && slot_t && slot_dt);
         const size_t lds = march_summary_lds(p);
         if (march_simple(p))  // one cascade, esf 0: the wave-per-ray lattice walk
-            NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<march_blocks(nblk(n_rays, 4)), 256, lds, s>>>(
+            NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<nblk(n_rays, 4), 256, lds, s>>>(
                                           rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt));
         else
             NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false><<<nblk(n_rays, 4 * MARCH_RPW), 256, lds, s>>>(

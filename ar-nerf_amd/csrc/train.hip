@@ -19,9 +19,6 @@ __global__ void zero_words_kernel(unsigned long long* __restrict__ p, int n) {
     if ((int)threadIdx.x < n) p[threadIdx.x] = 0ull;
 }
 
-// Guard trips of the occupancy-list kernels (a reservation past the list's
-// capacity: only a corrupted count can cause one) -- ngp_guard_hits().
-__device__ unsigned long long g_guard_hits = 0ull;
 
 // ------------------------------------------------------ composite + loss
 // One wave per ray.  Pass 1 = composite_train_fw (volumerendering.cu:5-44),
@@ -293,13 +290,13 @@ __device__ __forceinline__ int64_t lookback_prefix(LookbackWs* __restrict__ lb, 
         unsigned long long wv = LB_INCL;  // (q < 0: before block 0, an inclusive 0)
         // bounded: a predecessor publishes its aggregate without waiting on anyone, so this
         // ends in microseconds; the bound only keeps a corrupted workspace from hanging the
-        // GPU (counted in g_guard_hits, the result is then wrong)
+        // GPU (counted as a guard hit, ngp_guard_hits: the result is then wrong)
         for (uint32_t spin = 0;; ++spin) {
             if (q >= 0) wv = __hip_atomic_load(&lb->status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const bool ok = q < 0 || ((uint32_t)(wv >> 42) == (gen & 0x3fffffu) && (wv & (3ull << 40)) != 0);
             if (__all(ok)) break;
             if (spin == (1u << 22)) {
-                if (lane == 0) atomicAdd(&g_guard_hits, 1ull);
+                if (lane == 0) ngp_guard_hit();
                 wv = LB_INCL;
                 break;
             }
@@ -548,7 +545,7 @@ __global__ void __launch_bounds__(OCC_T) occ_list_kernel(const float* __restrict
     // (the list holds at most n_cells entries: a base past that can only come
     // from corrupted counts -- dropped instead of written)
     if (base > (unsigned long long)n_cells) {
-        if (tid == 0) atomicAdd(&g_guard_hits, 1ull);
+        if (tid == 0) ngp_guard_hit();
         return;
     }
     int64_t pos = (int64_t)base + wcnt[wid] + incl - mine;
@@ -576,7 +573,8 @@ __global__ void __launch_bounds__(256) occ_sample_kernel(uint64_t seed, const in
         idx = (int32_t)morton3((uint32_t)uniform_index(v.x, G), (uint32_t)uniform_index(v.y, G),
                                (uint32_t)uniform_index(v.z, G));
     } else {  // a cell drawn from the occupied list
-        const unsigned long long cnt = min(*count, (unsigned long long)G * G * G);  // (guard: list capacity)
+        const unsigned long long cnt0 = *count, cnt = min(cnt0, (unsigned long long)G * G * G);  // (guard: list capacity)
+        if (cnt0 != cnt && i == (lo > M ? lo : M)) ngp_guard_hit();
         if (cnt == 0) {
             flat[o] = -1;
             xyzs[3 * o] = 0.f; xyzs[3 * o + 1] = 0.f; xyzs[3 * o + 2] = 0.f;
@@ -702,7 +700,8 @@ __global__ void __launch_bounds__(OSC_T) occ_sample_sorted_kernel(
     run += incl - loc;
     const double inv_tot = 1.0 / sums[2 * nb + half];
     const int64_t n_cells = (int64_t)G * G * G;
-    const unsigned long long cnt = half ? min(*count, (unsigned long long)n_cells) : 0ull;  // (guard: capacity)
+    const unsigned long long cnt0 = half ? *count : 0ull, cnt = min(cnt0, (unsigned long long)n_cells);  // (guard: capacity)
+    if (cnt0 != cnt && threadIdx.x == 0) ngp_guard_hit();
     const float gm1 = (float)(G - 1);
 #pragma unroll 1
     for (int j = 0; j < OSC_PER; ++j) {
@@ -811,7 +810,7 @@ __global__ void __launch_bounds__(256) scatter_kept_kernel(const int32_t* __rest
                                                            const int64_t* __restrict__ flat,
                                                            const float* __restrict__ sig, int64_t pos_base,
                                                            unsigned long long* __restrict__ key) {
-    const int64_t nk = min(*count, n_max);
+    const int64_t nk = ngp_capped_count(count, n_max);
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nk; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = list[j];
         const int64_t c = flat[i];
@@ -1140,10 +1139,8 @@ __global__ void __launch_bounds__(1024) rays_nonempty_kernel(const int64_t* __re
 // before it and publish their aggregate without waiting -- no deadlock at any
 // grid size.  The last block to finish resets the ticket and advances the
 // generation (stale status words of the previous launch never match).
-#ifndef NGP_CS_ROWS
-#define NGP_CS_ROWS 64
-#endif
-constexpr int CS_ROWS = NGP_CS_ROWS, CS_THREADS = 512, CS_RPW = CS_ROWS / (CS_THREADS / 64);
+// (64 rows per block: 32 / 16 measured slower, profiles/r03/ab/chunk_segments_rows.txt)
+constexpr int CS_ROWS = 64, CS_THREADS = 512, CS_RPW = CS_ROWS / (CS_THREADS / 64);
 constexpr int CS_LOG = CS_ROWS == 64 ? 6 : CS_ROWS == 32 ? 5 : 4;
 static_assert(CS_ROWS == 64 || CS_ROWS == 32 || CS_ROWS == 16, "row block");
 
@@ -1445,12 +1442,6 @@ int ngp_counters_inc(int64_t* counters, int n, void* stream) {
     NGP_CHECK_ARG(counters && n >= 1 && n <= 64);
     counters_inc_kernel<<<1, 64, 0, as_stream(stream)>>>(counters, n);
     return ngp_launch_status();
-}
-
-unsigned long long ngp_guard_hits(void) {
-    unsigned long long v = 0;
-    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_guard_hits), sizeof(v)) != hipSuccess) return ~0ull;
-    return v;
 }
 
 int ngp_density_scatter_last(const int64_t* indices, const float* sigmas, int64_t n, int64_t pos_base,

@@ -115,7 +115,7 @@ def all_gather_(full, shard, group=None):
 
 def allreduce_grad_(grad, group=None):
     """Sum the flat gradient over ranks (the mean is applied in Adam)."""
-    if world_info(group)[1] > 1:
+    if comm_active(group):
         if _gloo(group) and grad.is_cuda:
             g = grad.cpu()
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
@@ -130,7 +130,7 @@ def combine_density_tmp_(tmp, group=None):
     << 32 | sigma bits, 0 = unevaluated; ngp_density_scatter_last): the
     largest list position wins across ranks as within one, so the result
     equals a single process evaluating the whole list."""
-    if world_info(group)[1] > 1:
+    if comm_active(group):
         if _gloo(group) and tmp.is_cuda:
             t = tmp.cpu()
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
@@ -142,7 +142,7 @@ def combine_density_tmp_(tmp, group=None):
 
 def sync_threshold_(thr, group=None):
     """Broadcast rank 0's occupancy threshold so bitfields are identical."""
-    if world_info(group)[1] > 1:
+    if comm_active(group):
         src = dist.get_global_rank(group, 0) if group is not None else 0
         if _gloo(group) and thr.is_cuda:
             t = thr.cpu()

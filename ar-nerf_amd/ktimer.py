@@ -179,19 +179,27 @@ class ProbeTimer:
         """{probe: (avg ms per launch, launches counted)}"""
         return {k: (sum(m for _, m in v) / len(v), len(v)) for k, v in self.spans(skip_rows).items()}
 
-    def step_gaps(self, first="first_chunk", last="counters_inc"):
-        """[(row, us)]: from the end of row r's `last` kernel to the start of
-        row r + 1's `first` (the step boundary: inside a two-step graph, or
-        between two graph replays), over consecutive rows where both ran"""
+    def step_gaps(self, step0, n_steps, skip_steps=(), first="first_chunk", last="counters_inc"):
+        """[(step, us)]: from the end of step s's `last` kernel to the start of
+        step s + 1's `first` (the step boundary: inside a two-step graph, or
+        between two graph replays), for the consecutive steps s, s + 1 of the
+        window [step0, step0 + n_steps) (n_steps <= rows: rows are step % rows,
+        so only pairs inside the window are taken -- the row after the
+        window's last step holds its FIRST step) where neither is in
+        skip_steps (steps with an occupancy update launch extra kernels)"""
         b = self.buf
         big = torch.iinfo(torch.int64).max
         st = torch.where(b[..., 0] > 0, b[..., 0], torch.full_like(b[..., 0], big)).min(-1).values.cpu()
         en = b[..., 1].max(-1).values.cpu()
         f, l = PROBES.index(first), PROBES.index(last)
+        skip = set(skip_steps)
         out = []
-        for r in range(self.rows - 1):
-            if en[r, l] > 0 and st[r + 1, f] < big:
-                out.append((r, round(float(st[r + 1, f] - en[r, l]) * self.tick_ns * 1e-3, 1)))
+        for s in range(step0, step0 + min(n_steps, self.rows) - 1):
+            if s in skip or s + 1 in skip:
+                continue
+            r, r1 = s % self.rows, (s + 1) % self.rows
+            if en[r, l] > 0 and st[r1, f] < big:
+                out.append((s, round(float(st[r1, f] - en[r, l]) * self.tick_ns * 1e-3, 1)))
         return out
 
     def timeline(self, skip_rows=(), origin="first_chunk"):

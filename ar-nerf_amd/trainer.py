@@ -147,8 +147,9 @@ class NGPTrainer:
         self._occ_flat = torch.empty(M2, dtype=torch.int64, device=dev)
         self._occ_sig = torch.empty(M2, device=dev)
         # only the samples whose sigma the update keeps are evaluated (ngp_occupancy_keep:
-        # a cell's last draw; NGP_OCC_KEEP=0: all 2M, as the reference evaluates them)
-        self.occ_keep = os.environ.get("NGP_OCC_KEEP", "1") == "1"
+        # a cell's last draw; bit-identical grid, 362 -> 302 us per update; occ_keep = False
+        # (tests): all 2M, as the reference evaluates them)
+        self.occ_keep = True
         self._occ_mark = torch.empty((self.G ** 3 + 15) // 16, 4, dtype=torch.int32, device=dev)
         self._occ_kept = torch.empty(M2, dtype=torch.int32, device=dev)
         self._occ_kept_n = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -215,24 +216,24 @@ class NGPTrainer:
         # round-2 list in one launch (counts + look-back scan + map): its look-back workspace, zeroed once
         self._cs_ws = torch.zeros((vren.lib().ngp_chunk_segments_workspace(R) + 7) // 8, dtype=torch.int64,
                                   device=dev)
-        # row forward (NGP_ROW_FWD=1, the default since round 4: +2 %, 9 of 9 alternating pairs,
+        # row forward (the default since round 4: +2 %, 9 of 9 alternating pairs,
         # profiles/r04/ab/row_forward_variants.txt): round 1 one wave per non-empty row with the
         # row's transmittance in its epilogue, which appends the row's round-2 samples to the
-        # round-2 list itself (ngp_field_forward_first: no list launch); NGP_ROW_FWD=0: the
-        # two-round lists below
-        self.row_forward = int(os.environ.get("NGP_ROW_FWD", "1"))
+        # round-2 list itself (ngp_field_forward_first: no list launch); row_forward = 0 (tests)
+        # or chunk_first != 64: the two-round lists below
+        self.row_forward = 1
         assert self.row_forward in (0, 1)
         # where the next batch's march forks off the step: after the row forward's round 1 on the
         # single-cascade (Lego-shaped) scenes (round 1 runs alone, the march beside round 2 /
         # composite / MLP backward: +2.1 %, 6 of 6 pairs, profiles/r04/ab/march_fork_position.txt);
         # at the step's start on cascaded scenes, whose march is 3/4 of a forward-sized step and
         # beside the MLP backward slows it 1.7x (garden-shaped: -6 %, profiles/r04/ab/garden_r4.txt);
-        # NGP_MARCH_AT = start | r1 | fwd | mlp overrides
-        self.march_at = os.environ.get("NGP_MARCH_AT", "r1" if self.cascades == 1 else "start")
+        # (march_at = start | r1 | fwd | mlp: diagnostics, scripts/diag/skip_cost.py)
+        self.march_at = "r1" if self.cascades == 1 else "start"
         # round 1's coarse levels 0-7 encoded ahead (the next batch's first chunks, once the MLP + coarse
         # levels' Adam of this step has run, beside the binned levels' accumulation): round 1 then gathers
-        # only levels 8-15 (NGP_PRE_COARSE=0: off)
-        self.pre_coarse = os.environ.get("NGP_PRE_COARSE", "1") == "1"
+        # only levels 8-15 (pre_coarse = False, tests: off)
+        self.pre_coarse = True
         self.pre_levels = 8  # (the kernel's PRE_LEVELS: levels 0-7, final once the side stream's Adam has run)
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -546,7 +547,9 @@ class NGPTrainer:
         needs (the next batch's indices, the bitfield, the idle set's last
         readers = the previous step's backward) is already enqueued on the
         main stream, which one event captures.  (Callers that edit
-        density_bitfield between steps must not pass next_batch.)"""
+        density_bitfield between steps must not pass next_batch; callers that
+        edit params / params16 between steps call invalidate_pre_encode, or
+        use load_params.)"""
         if not self._can_prefetch():
             return False
         k = 1 - self.cur
@@ -559,6 +562,25 @@ class NGPTrainer:
         self._pending = (k, ev)
         self.n_prefetched += 1
         return True
+
+    def invalidate_pre_encode(self):
+        """Forget every buffer set's round-1 coarse-level encoding done ahead
+        (pre_ready): it was encoded from the parameters of its time, so any
+        write to params / params16 between steps (checkpoint load, state
+        transplant, hand edits) must call this (load_params does) -- the next
+        round 1 then gathers all 16 levels itself instead of mixing levels 0-7
+        of the old parameters with 8-15 of the new."""
+        for m in self.msets:
+            m["pre_ready"] = False
+
+    @torch.no_grad()
+    def load_params(self, params, params16=None):
+        """Overwrite the fp32 master (and the fp16 shadow: params16, or the
+        master rounded) between steps, invalidating the pre-encoded round 1."""
+        n = self.n_params
+        self.params.copy_(params[:n].to(self.params))
+        self.params16.copy_(params[:n].half() if params16 is None else params16[:n].to(self.params16))
+        self.invalidate_pre_encode()
 
     def drain(self):
         """Order the current stream after a batch marched ahead on the side
@@ -698,14 +720,22 @@ class NGPTrainer:
     def _capture_comm(self):
         """The data-parallel step's collectives captured into the step's graph
         (one replay per step, no segment boundaries): emulated worlds (local
-        copies) and RCCL process groups (RCCL supports stream capture); gloo
-        stages device tensors through the host and cannot be captured.
-        NGP_DP_CAPTURE=0 keeps the segments."""
-        if os.environ.get("NGP_DP_CAPTURE", "1") != "1":
+        copies) and a world-1 RCCL group (tests) by default.  A real world > 1
+        keeps the graph segments with eager RCCL calls between them unless
+        NGP_DP_CAPTURE=1 opts in (captured multi-rank RCCL
+        collectives, with the occupancy update's eager ones between the
+        replays, have not run on a multi-GPU node; the segmented step measured
+        ~4 % slower emulated).  gloo stages device tensors
+        through the host and cannot be captured.  NGP_DP_CAPTURE=0: segments
+        always."""
+        opt = os.environ.get("NGP_DP_CAPTURE", "")
+        if opt == "0":
             return False
         if not ddp.comm_active(self.pg):
             return True
-        return dist.get_backend(self.pg) == "nccl"
+        if dist.get_backend(self.pg) != "nccl":
+            return False
+        return self.world == 1 or opt == "1"
 
     def _dp_sequence(self, k, gt, directions, poses, update_after, run):
         """The data-parallel step (ZeRO-1, per-bucket pipeline): run(sub, fn)
@@ -808,6 +838,7 @@ class NGPTrainer:
             def fork():
                 self.march_stream.wait_stream(cs)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
+                return True
         self._segmented = True
         try:
             self._compute(self.rgb_gt, True, fork)
@@ -902,6 +933,7 @@ class NGPTrainer:
             def fork():
                 self.march_stream.wait_stream(cs)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
+                return True
 
             self._compute(self.rgb_gt, True, fork)
             cs.wait_stream(self.march_stream)
@@ -944,8 +976,9 @@ class NGPTrainer:
     def _compute(self, rgb_gt, apply_adam, fork):
         """Field forward (chunked), compositing + loss + its backward, field
         backward, [all-reduce], Adam -- on the current stream, no host sync.
-        fork() (nullable) launches the next batch's march on the side stream,
-        where self.march_at says: by default right after the row forward's
+        fork() (nullable) launches the next batch's march on the side stream
+        and returns whether it did (prefetch() declines before an occupancy
+        update or with no_prefetch), where self.march_at says: by default right after the row forward's
         round 1 (which then has the chip to itself; the march overlaps round
         2, the composite and the MLP backward: +2.1 %,
         profiles/r04/ab/march_fork_position.txt); before the row forward, at
@@ -953,8 +986,9 @@ class NGPTrainer:
         profiles/r02/ab/prefetch_at.txt)."""
         L, s, HGL, R = self.L, vren._stream(), HG._lib(), self.batch_size
         at = self.march_fork_point()
+        marched = False  # the next batch marched beside this step (fork() said so)
         if fork is not None and at == "start":
-            fork()
+            marched = bool(fork())
         self._ev("field_fwd", 0)
         if self._rows_fwd(self.chunk_first):
             # round 1: a wave per non-empty row (the list built by the march), its transmittance
@@ -973,7 +1007,7 @@ class NGPTrainer:
                                                      pre, s), "field_forward_first")
             self._ev("hash_encode", 1)
             if fork is not None and at == "r1":
-                fork()
+                marched = bool(fork())
             self._field_indexed(s, self.eval_idx, self.eval_total2)
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
             K = self.chunk_first
@@ -1004,7 +1038,7 @@ class NGPTrainer:
             self._ev("hash_encode", 1)
         self._ev("field_fwd", 1)
         if fork is not None and at == "fwd":
-            fork()
+            marched = bool(fork())
         bg = self.bg
         if self.random_bg:  # rendering.py:287-288, one colour per batch, drawn on device (graph-safe)
             bg = self._bg_rand
@@ -1044,7 +1078,7 @@ class NGPTrainer:
                                             _p(self.denc), _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
         if fork is not None and at == "mlp":
-            fork()
+            marched = bool(fork())
         if self._segmented and hybrid:
             # (world > 1 graph segments: the hash backward runs as two more
             # graphs -- coarse levels on the side stream, binned levels here --
@@ -1068,7 +1102,7 @@ class NGPTrainer:
             # the next batch's round-1 pre-encode after the Adam below (only while levels 0-7 are all
             # stepped by that Adam: the binned levels' parameters change inside the accumulation)
             # (any fork point: the next batch's march is captured before this point)
-            pre = (adam_split and self.pre_coarse and fork is not None
+            pre = (adam_split and self.pre_coarse and marched
                    and self._rows_fwd(self.chunk_first) and self.bin_level_lo >= self.pre_levels)
             bs.wait_stream(cs)
             if pre:

@@ -111,6 +111,8 @@ def _declare(L):
     L.ngp_render_test_capacity.restype = c_int64
     L.ngp_guard_hits.argtypes = []
     L.ngp_guard_hits.restype = ctypes.c_ulonglong
+    L.ngp_guard_reset.argtypes = []
+    L.ngp_guard_reset.restype = c_int
     # measurement hook (ktimer.py)
     L.ngp_timing_set.argtypes = [vp, vp, c_int64, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64]
     L.ngp_timing_set.restype = c_int

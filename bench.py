@@ -423,6 +423,7 @@ def transplant_state(src, dst):
             getattr(dst, name).copy_(getattr(src, name))
     dst.global_step = src.global_step
     dst._updated_for = src._updated_for
+    dst.invalidate_pre_encode()
 
 
 def main():
@@ -571,7 +572,8 @@ def main():
                                                  if st % probes.rows == r)]
     pr_summary = probes.summary(skip_rows=skip)
     pr_timeline = probes.timeline(skip_rows=skip)
-    pr_gaps = probes.step_gaps()
+    upd_steps = [st for st in range(s_rf, s_rf + ran_rf) if st % ui == 0]
+    pr_gaps = probes.step_gaps(s_rf, ran_rf, skip_steps=upd_steps)
     m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         e_rf = m_rf
@@ -667,10 +669,17 @@ def main():
     oracle_q = None
     if rank == 0 and world == 1 and not args.no_oracle_quality:
         oracle_q = oracle_quality()
+    # capacity guards (ngp_guard_hits): a device count clamped to its buffer's capacity anywhere in
+    # this run -- samples dropped -- would make the line's work smaller than the step's
+    guard_hits = int(vren.lib().ngp_guard_hits())
+    if guard_hits:
+        print(f"[bench] WARNING: {guard_hits} capacity guard hits (a device count clamped: work truncated)",
+              file=sys.stderr)
+    ms_step = t_el / args.steps * 1e3
     if rank == 0:
         out = {
             "metric": BASELINE["metric"], "value": round(value, 1), "unit": "rays/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_el / args.steps * 1e3, 4),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp16 field (MLP forward, backward and weight gradients on fp16 MFMA operands, fp32 accumulate) / fp32 march, composite, Adam",
             "data": "synthetic (analytic sphere+box scene, 100 views 800x800, Lego intrinsics; random-init weights "
@@ -699,9 +708,15 @@ def main():
             "probe_step_gaps_us": {"gaps": [g for _, g in pr_gaps],
                                    "mean": round(sum(g for _, g in pr_gaps) / max(1, len(pr_gaps)), 1),
                                    "note": "end of a step's counters_inc to the next step's round 1, per "
-                                           "consecutive step pair of the probe window (two steps per graph "
-                                           "replay: alternately inside a graph and across a replay boundary)"},
+                                           "consecutive step pair inside the probe window (pairs touching a step "
+                                           "with an occupancy update left out; two steps per graph replay: "
+                                           "alternately inside a graph and across a replay boundary)"},
             "step_bound": step_bound,
+            # the timed window's step time per unit of its own work (the work per step follows the
+            # training state, so these compare runs whose windows landed on different phases)
+            "ns_per_composited_sample": round(ms_step * 1e6 / max(units["composited"], 1e-9), 4),
+            "ns_per_marched_sample": round(ms_step * 1e6 / max(units["marched"], 1e-9), 4),
+            "guard_hits": guard_hits,
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "breakdown_note": (f"ops / kernels: wall-clock stamps around every kernel inside the captured graphs "
                                f"over {bd_steps} replayed steps ({t_bd * 1e3:.3f} ms/step with all stamps); timeline_us: "

@@ -644,11 +644,16 @@ int ngp_counters_inc(int64_t* counters, int n, void* stream);
  * Python), threshold_out[1] = the mean; feed threshold_out to ngp_packbits'
  * threshold_dev.  sum_cnt_ws: 16 bytes of scratch (two fp64 accumulators, 8-byte
  * aligned; the mean is taken in fp64). */
-/* Number of times the occupancy-list kernel found a block's list position
- * past the list's capacity and dropped the block instead of writing out of
- * bounds (nonzero only after memory corruption: tests assert 0;
- * synchronises the device). */
+/* Capacity guards: the number of times a kernel found a device-side count
+ * past the capacity its caller gave it and clamped it (the result is then
+ * truncated: samples, rows or cells dropped instead of read or written out of
+ * bounds) -- every n_dev / n_rows_dev / count argument of the field, hash
+ * backward and occupancy kernels, the row forward's round-2 list, the
+ * occupancy list and the bounded look-back spin.  Nonzero only after a
+ * capacity overflow or memory corruption (tests assert 0, bench.py reports
+ * it).  Synchronises the device.  ngp_guard_reset zeroes the counters. */
 unsigned long long ngp_guard_hits(void);
+int ngp_guard_reset(void);
 int ngp_density_scatter_last(const int64_t* indices, const float* sigmas, int64_t n, int64_t pos_base,
                              uint64_t* grid_key, void* stream);
 int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, float decay,
@@ -693,7 +698,7 @@ int ngp_occupancy_samples_sorted(uint64_t seed, const int64_t* counter_dev, int 
  * only a cell the occupied half does not draw.  Lists the kept positions of
  * [lo, hi) (ascending within each 8192-position block, blocks in any order)
  * and *count = their number (device, 8-byte aligned).  cell_base = cascade *
- * n_cells; mark_ws: n_cells bytes of scratch, 16-byte aligned.  Evaluating
+ * n_cells; mark_ws: round_up(n_cells, 16) bytes of scratch, 16-byte aligned (cleared in 16-byte words).  Evaluating
  * only these (ngp_field_encode_mlp with sample_idx = list) and scattering them
  * with ngp_density_scatter_kept leaves the same key grid as evaluating and
  * scattering all of [lo, hi). */

@@ -282,13 +282,13 @@ def test_segmented_replay_reduces_the_whole_gradient_when_every_level_is_binned(
     assert worst < 1e-3
 
 
-def _emu_trainer(use_graphs, k=2, lo=None):
+def _emu_trainer(use_graphs, k=2, lo=None, update_interval=10 ** 6, emulate_dp=1):
     import synthetic as S
     from trainer import NGPTrainer
     sc = S.AnalyticScene(W=100, H=100, n_images=10)
     dev = torch.device("cuda", 0)
-    tr = NGPTrainer(scale=0.5, batch_size=R, device=dev, seed=3, warmup_steps=0, update_interval=10 ** 6,
-                    emulate_dp=1, use_graphs=use_graphs, dp_fine_buckets=k,
+    tr = NGPTrainer(scale=0.5, batch_size=R, device=dev, seed=3, warmup_steps=0, update_interval=update_interval,
+                    emulate_dp=emulate_dp, use_graphs=use_graphs, dp_fine_buckets=k,
                     **({} if lo is None else {"bin_level_lo": lo}))
     with torch.no_grad():
         g = torch.Generator().manual_seed(11)
@@ -404,3 +404,76 @@ def test_rccl_world1_segmented_replay_matches_the_unsegmented_step(k):
         worst = max(worst, float((dA[a:b].double() - ref).norm() / ref.norm()))
     print(f"RCCL world-1 captured step vs unsegmented step ({len(buckets)} buckets, {calls}): worst rel L2 {worst:.2e}")
     assert worst < 2e-2
+
+
+def test_rccl_world1_occupancy_update_runs_through_rccl_between_captured_replays():
+    """VERDICT r5 #2 / ADVICE r5: the data-parallel step's occupancy update --
+    the int64 MAX all-reduce of the cell keys and the threshold broadcast
+    (ddp.combine_density_tmp_ / sync_threshold_, which honour
+    ddp.FORCE_COLLECTIVES like the bucket collectives) -- issued EAGERLY on a
+    world-1 RCCL group every 16 steps between replays of step graphs that hold
+    captured RCCL reduce-scatters / all-gathers (trainer._replay,
+    update_after), over 40 steps.  Then, from one state, the data-parallel
+    trainer's update through RCCL and a single-process trainer's update give
+    the identical grid, threshold and bitfield."""
+    import ddp
+    import vren
+    from trainer import NGPTrainer
+    assert not dist.is_initialized()
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    calls = {"all_reduce": 0, "broadcast": 0, "rs": 0}
+    ar0, bc0, rs0 = dist.all_reduce, dist.broadcast, dist.reduce_scatter_tensor
+
+    def ar(*a, **kw):
+        calls["all_reduce"] += 1
+        return ar0(*a, **kw)
+
+    def bc(*a, **kw):
+        calls["broadcast"] += 1
+        return bc0(*a, **kw)
+
+    def rs(*a, **kw):
+        calls["rs"] += 1
+        return rs0(*a, **kw)
+    ddp.FORCE_COLLECTIVES = True
+    dist.all_reduce, dist.broadcast, dist.reduce_scatter_tensor = ar, bc, rs
+    try:
+        tr, sc = _emu_trainer(True, update_interval=16)
+        assert tr.dp and tr._capture_comm()
+        gt, dirs, poses = sc.gt_images(device="cuda"), sc.directions.cuda(), sc.poses.cuda()
+        for _ in range(40):
+            tr.train_step(gt, dirs, poses)
+        tr.drain()
+        torch.cuda.synchronize()
+        assert tr.global_step == 41
+        assert any("whole" in g for g in tr._graphs)  # the step graphs held the captured collectives
+        assert calls["all_reduce"] >= 2 and calls["broadcast"] >= 2, calls  # updates at steps 16 and 32
+        assert torch.isfinite(tr.params).all()
+        # the bitfield is the packed grid at the broadcast threshold
+        bf = torch.empty_like(tr.density_bitfield)
+        vren.packbits(tr.density_grid, tr.threshold[:1], bf)
+        assert torch.equal(tr.density_bitfield, bf), "bitfield vs packbits at the broadcast threshold"
+        # one more update from this state: data-parallel (RCCL) vs single process
+        solo = NGPTrainer(scale=0.5, batch_size=R, device=tr.dev, seed=3, warmup_steps=0, update_interval=16)
+        with torch.no_grad():
+            solo.load_params(tr.params, tr.params16)
+            for name in ("density_grid", "density_bitfield", "threshold", "dctr"):
+                getattr(solo, name).copy_(getattr(tr, name))
+        n_ar = calls["all_reduce"]
+        tr.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
+        ddp.FORCE_COLLECTIVES = False  # (the single process: no collective at all)
+        solo.update_density_grid(0.01 * 1024 / 3 ** 0.5, warmup=False)
+        ddp.FORCE_COLLECTIVES = True
+        torch.cuda.synchronize()
+        assert calls["all_reduce"] == n_ar + 1  # the DP trainer's keys went through RCCL; the solo one's did not
+        assert torch.equal(tr.density_grid, solo.density_grid)
+        assert torch.equal(tr.threshold, solo.threshold)
+        assert torch.equal(tr.density_bitfield, solo.density_bitfield)
+        occ = int(np.unpackbits(tr.density_bitfield.cpu().numpy()).sum())
+        print(f"RCCL world-1 occupancy updates between captured replays: {calls}; occupied cells {occ}")
+    finally:
+        dist.all_reduce, dist.broadcast, dist.reduce_scatter_tensor = ar0, bc0, rs0
+        ddp.FORCE_COLLECTIVES = False
+        dist.destroy_process_group()
