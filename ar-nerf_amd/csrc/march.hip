@@ -395,7 +395,63 @@ __global__ void __launch_bounds__(256) march_slots_kernel(const float* __restric
 
 // (lattice helpers LatSeg / lat_build / lat_jump: march.h)
 
-__global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __restrict__ rays_o,
+// The serial walk of one ray on lane 0 (a lattice whose segment table
+// overflows: dt below half an ulp of t, or more than LSEG binades -- never on
+// the object scenes; kept out of line so its registers do not count against
+// the lattice loop's).
+__device__ __forceinline__ int march_serial_lane(const float o[3], const float d[3], const float dinv[3], float t,
+                                              float t2, const MarchParams& p, WordCache& wc, float* st, float* sd) {
+    float x, y, z, dts;
+    int N = 0;
+    while (0 <= t && t < t2 && N < p.max_samples) {
+        const float tc = t;
+        if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) { st[N] = tc; sd[N] = dts; N++; }
+    }
+    return N;
+}
+
+// first j > k with t_j >= T, for lane point k with value tk: inside the
+// window's segment [Kq, Kn) (value Tq, increment Iq, its reciprocal invIq, in
+// registers) from one estimate and exact fix-ups; a jump that would leave the
+// segment steps on serially, t_{j+1} = fl(t_j + dt) -- the lattice's own
+// definition (march_step's `do t += dt while (t < t_target)`), exact across
+// any binade boundary.  The first index with t_j >= T is unique, so the
+// estimate only sets the cost.
+__device__ __forceinline__ int lat_jump_seg(int k, float tk, float T, float dt, int k_end, int Kq, int Kn, float Tq,
+                                            float Iq, float invIq) {
+    int j = k + 1;
+    if (j < Kn) {
+        if (fmaf((float)(j - Kq), Iq, Tq) >= T) return j;
+        const float need = (T - fmaf((float)(j - Kq), Iq, Tq)) * invIq;
+        int jj = min(j + (need < 4096.f ? max(1, (int)need) : 4096), Kn);
+        while (jj > j + 1 && fmaf((float)(jj - 1 - Kq), Iq, Tq) >= T) --jj;
+        if (jj < Kn) {
+            while (jj < Kn && fmaf((float)(jj - Kq), Iq, Tq) < T) ++jj;
+            if (jj < Kn) return jj;
+        }
+        // every point of the segment from j on lies below T: continue from its last one
+        j = Kn;
+        tk = fmaf((float)(Kn - 1 - Kq), Iq, Tq);
+    }
+    float t = tk;
+    j -= 1;  // (t = t_j)
+    do {
+        t = t + dt;
+        ++j;
+    } while (t < T && j < k_end);
+    return min(j, k_end);
+}
+
+// a wave-uniform fp32 value moved to a scalar register (VALU results are
+// per-lane VGPRs even when every lane holds the same value)
+__device__ __forceinline__ float uniform_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+#ifndef NGP_MARCH_WAVES
+#define NGP_MARCH_WAVES 8
+#endif
+__global__ void __launch_bounds__(256, NGP_MARCH_WAVES) march_slots_wave_kernel(const float* __restrict__ rays_o,
                                                                const float* __restrict__ rays_d,
                                                                const float* __restrict__ hits_t, int64_t n_rays,
                                                                const float* __restrict__ noise, MarchParams p,
@@ -409,13 +465,16 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
     wc.sum = load_summary(p, ssum);
     wc.dil = wc.sum ? wc.sum + p.n_sum32 : nullptr;
     __syncthreads();
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // one ray per wave (grid-stride: any grid covers every ray)
-    for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < n_rays; r += (int64_t)gridDim.x * 4) {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (wave-uniform: the ray's setup is scalar)
+    // one ray per wave (the launch has a wave per ray; no loop: no per-ray invariants held across rays)
+    for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < n_rays; r = n_rays) {
         float o[3], d[3], dinv[3];
         load_ray(rays_o, rays_d, r, o, d, dinv);
-        const float t2 = hits_t[2 * r + 1];
-        const float t0 = start_t(hits_t, noise, r, p);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { o[i] = uniform_f(o[i]); d[i] = uniform_f(d[i]); dinv[i] = uniform_f(dinv[i]); }
+        const float t2 = uniform_f(hits_t[2 * r + 1]);
+        const float t0 = uniform_f(start_t(hits_t, noise, r, p));
         const float dt = NGP_SQRT3 / p.max_samples;
         float* st = slot_t + r * (int64_t)p.max_samples;
         float* sd = slot_dt + r * (int64_t)p.max_samples;
@@ -461,57 +520,59 @@ __global__ void __launch_bounds__(256) march_slots_wave_kernel(const float* __re
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (k_end < 0) {  // segment table overflow: the serial walk on lane 0
-            if (lane == 0) {
-                float t = t0, x, y, z, dts;
-                int N = 0;
-                while (0 <= t && t < t2 && N < p.max_samples)
-                {
-                    const float tc = t;
-                    if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) { st[N] = tc; sd[N] = dts; N++; }
-                }
-                counts[r] = N;
-            }
+            if (lane == 0) counts[r] = march_serial_lane(o, d, dinv, t0, t2, p, wc, st, sd);
             continue;
         }
-        int c = 0, N = 0, q0 = 0;  // window start (a visited point), samples, its segment
+        // the window's segment q0 = [Kq, Kn) in registers (re-read when the window passes Kn)
+        int c = 0, N = 0, q0 = 0;
+        int Kq = 0, Kn = -1;
+        float Tq = 0.f, Iq = 0.f, invIq = 0.f;
         while (c < k_end && N < p.max_samples) {
-            while (q0 + 1 < nseg && c >= sg.K[q0 + 1]) ++q0;
+            if (c >= Kn) {
+                while (q0 + 1 < nseg && c >= sg.K[q0 + 1]) ++q0;
+                Kq = sg.K[q0];
+                Kn = q0 + 1 < nseg ? sg.K[q0 + 1] : k_end;
+                Tq = uniform_f(sg.T[q0]);
+                Iq = uniform_f(sg.I[q0]);
+                invIq = uniform_f(1.0f / Iq);
+            }
             const int k = c + lane;
-            int q = q0;
-            while (q + 1 < nseg && k >= sg.K[q + 1]) ++q;
             const bool live = k < k_end;
-            const float tk = live ? lat_t(sg, q, k) : 0.f;
             bool occ = false;
             int nxt = k_end;
+            float tk = 0.f;
             if (live) {
+                if (k < Kn) {
+                    tk = fmaf((float)(k - Kq), Iq, Tq);
+                } else {  // past the window's segment (the window straddles a binade): step on from its last point
+                    float t = fmaf((float)(Kn - 1 - Kq), Iq, Tq);
+                    for (int i = Kn; i <= k; ++i) t = t + dt;
+                    tk = t;
+                }
                 float x, y, z, dts, T;
                 occ = march_probe<true>(tk, o, d, dinv, p, x, y, z, dts, wc, T);
-                nxt = occ ? k + 1 : lat_jump(sg, nseg, q, k, T, k_end);
+                nxt = occ ? k + 1 : lat_jump_seg(k, tk, T, dt, k_end, Kq, Kn, Tq, Iq, invIq);
             }
-            const uint64_t occm = __ballot(occ && live);
-            // The walk's chain through the window, in parallel: J_b(i) = the
-            // 2^b-th successor of window point i (64 = out of the window),
-            // built by pointer doubling; every lane then climbs from point 0
-            // with binary lifting to the last chain point <= itself -- it is
-            // on the chain iff that is itself.  (Successors only move forward.)
-            int J[6];
-            J[0] = live ? min(nxt - c, 64) : 64;
-    #pragma unroll
-            for (int b = 1; b < 6; ++b) {
-                const int prev = J[b - 1];
-                const int v = __builtin_amdgcn_ds_bpermute(min(prev, 63) << 2, prev);
-                J[b] = prev >= 64 ? 64 : v;
+            const uint64_t occm = __ballot(occ);
+            const uint64_t livem = __ballot(live);
+            // The walk's chain through the window (wave-uniform, scalar): from a chain
+            // point cur, the walk visits every point of the occupied run starting there
+            // (successor k + 1), then the run's first unoccupied point e; from an empty e
+            // it jumps to nxt(e).  One hop per empty chain point: ~1 per cell in empty
+            // space, none across occupied cells.
+            uint64_t vis = 0ull;
+            int cur = 0, pnt;
+            while (true) {
+                const uint64_t from = ~occm & (~0ull << cur);
+                const int e = from ? (int)__builtin_ctzll(from) : 64;
+                vis |= (e >= 64 ? ~0ull : ((1ull << e) - 1ull)) & (~0ull << cur);
+                if (e >= 64) { pnt = c + 64; break; }           // lane 63 occupied: successor c + 64
+                if (!((livem >> e) & 1ull)) { pnt = k_end; break; }  // past the walk's stop
+                vis |= 1ull << e;
+                const int nx = __builtin_amdgcn_readlane(nxt, e);
+                if (nx >= c + 64) { pnt = nx; break; }
+                cur = nx - c;
             }
-            int cur = 0;
-    #pragma unroll
-            for (int b = 5; b >= 0; --b) {
-                const int v = __builtin_amdgcn_ds_bpermute(min(cur, 63) << 2, J[b]);
-                const int to = cur >= 64 ? 64 : v;
-                if (to <= lane) cur = to;
-            }
-            uint64_t vis = __ballot(cur == lane);
-            const int last = 63 - __builtin_clzll(vis);  // the chain's last point in the window
-            const int pnt = __builtin_amdgcn_readlane(nxt, last);   // k_end if it ends the walk
             vis &= occm;
             // emit the chain's occupied points, at most up to max_samples
             const int room = p.max_samples - N;
