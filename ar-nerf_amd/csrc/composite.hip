@@ -1,8 +1,9 @@
 // Volume-rendering compositing (forward, backward, test-time) for gfx950.
 // Replaces models/csrc/volumerendering.cu of the reference.
 //
-// One lane per ray (64-lane workgroups), front-to-back, with the same
-// early-termination rule (T <= T_threshold breaks BEFORE the count
+// One wave per ray (training fw / bw: lanes load a chunk, the serial chain
+// runs on scalar copies) or one lane per ray (test time), front-to-back,
+// with the same early-termination rule (T <= T_threshold breaks BEFORE the count
 // increments, volumerendering.cu:40-41).  Unlike the reference, the kernels
 // write every output element themselves (zeros past termination), so the
 // caller never needs a zero-fill, and the backward keeps the running prefix
@@ -14,79 +15,131 @@
 
 namespace ngp {
 
-__global__ void __launch_bounds__(64) composite_fw_kernel(const float* __restrict__ sigmas,
-                                                          const float* __restrict__ rgbs,
-                                                          const float* __restrict__ deltas,
-                                                          const float* __restrict__ ts,
-                                                          const int64_t* __restrict__ rays_a, int64_t n_rays,
-                                                          float T_thr, int64_t* __restrict__ total_samples,
-                                                          float* __restrict__ opacity, float* __restrict__ depth,
-                                                          float* __restrict__ rgb, float* __restrict__ ws) {
-    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// fp32 lane value j of a wave, in a scalar register
+__device__ __forceinline__ float lane_f(float v, int j) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
+}
+
+// volumerendering.cu:5-44 with one wave per ray: the lanes load a 64-sample
+// chunk (coalesced) and compute each sample's alpha, then the ray's serial
+// chain -- T, the left folds of rgb / depth / opacity, the break before the
+// count -- runs in the reference's order on scalar copies of lane j's values:
+// the same fp32 operations in the same order as the per-lane serial loop
+// (bit-identical), with the memory latency paid once per chunk instead of per
+// sample and 64x the waves in flight.
+__global__ void __launch_bounds__(256) composite_fw_kernel(const float* __restrict__ sigmas,
+                                                           const float* __restrict__ rgbs,
+                                                           const float* __restrict__ deltas,
+                                                           const float* __restrict__ ts,
+                                                           const int64_t* __restrict__ rays_a, int64_t n_rays,
+                                                           float T_thr, int64_t* __restrict__ total_samples,
+                                                           float* __restrict__ opacity, float* __restrict__ depth,
+                                                           float* __restrict__ rgb, float* __restrict__ ws) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (n >= n_rays) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
     float T = 1.0f, r = 0.f, g = 0.f, b = 0.f, d = 0.f, op = 0.f;
     int64_t samples = 0;
-    while (samples < N) {
-        const int64_t s = start + samples;
-        const float a = 1.0f - __expf(-sigmas[s] * deltas[s]);
-        const float w = a * T;
-        r += w * rgbs[3 * s]; g += w * rgbs[3 * s + 1]; b += w * rgbs[3 * s + 2];
-        d += w * ts[s];
-        op += w;
-        ws[s] = w;
-        T *= 1.0f - a;
-        if (T <= T_thr) break;
-        samples++;
+    bool done = false;
+    for (int64_t k0 = 0; k0 < N; k0 += 64) {
+        const int64_t s = start + k0 + lane;
+        const int cnt = (int)(N - k0 < 64 ? N - k0 : 64);
+        const bool in = lane < cnt;
+        if (done) {  // past the termination: ws = 0 (the reference's tail loop)
+            if (in) ws[s] = 0.f;
+            continue;
+        }
+        float a = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, tt = 0.f;
+        if (in) {
+            a = 1.0f - __expf(-sigmas[s] * deltas[s]);
+            cr = rgbs[3 * s]; cg = rgbs[3 * s + 1]; cb = rgbs[3 * s + 2];
+            tt = ts[s];
+        }
+        float wl = 0.f;  // lane j's ws
+        for (int j = 0; j < cnt; ++j) {
+            const float aj = lane_f(a, j);
+            const float w = aj * T;
+            r += w * lane_f(cr, j); g += w * lane_f(cg, j); b += w * lane_f(cb, j);
+            d += w * lane_f(tt, j);
+            op += w;
+            if (lane == j) wl = w;
+            T *= 1.0f - aj;
+            if (T <= T_thr) { done = true; samples = k0 + j; break; }
+        }
+        if (!done) samples = k0 + cnt;
+        if (in) ws[s] = wl;  // (0 past the terminating sample)
     }
-    for (int64_t k = samples + 1; k < N; ++k) ws[start + k] = 0.f;
-    rgb[3 * ray] = r; rgb[3 * ray + 1] = g; rgb[3 * ray + 2] = b;
-    depth[ray] = d;
-    opacity[ray] = op;
-    total_samples[ray] = samples;
+    if (lane == 0) {
+        rgb[3 * ray] = r; rgb[3 * ray + 1] = g; rgb[3 * ray + 2] = b;
+        depth[ray] = d;
+        opacity[ray] = op;
+        total_samples[ray] = samples;
+    }
 }
 
-__global__ void __launch_bounds__(64) composite_bw_kernel(
+// volumerendering.cu:86-150, one wave per ray as composite_fw_kernel: the
+// total of dL_dws * ws (the reference's inclusive scan's last value) as a
+// serial left fold, then the serial pass in the reference's order, each
+// sample's gradient put back into its lane and stored per chunk.
+__global__ void __launch_bounds__(256) composite_bw_kernel(
     const float* __restrict__ dL_dop, const float* __restrict__ dL_ddep, const float* __restrict__ dL_drgb,
     const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ rgbs,
     const float* __restrict__ ws, const float* __restrict__ deltas, const float* __restrict__ ts,
     const int64_t* __restrict__ rays_a, int64_t n_rays, const float* __restrict__ opacity,
     const float* __restrict__ depth, const float* __restrict__ rgb, float T_thr, float* __restrict__ dL_dsig,
     float* __restrict__ dL_drgbs) {
-    const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (n >= n_rays) return;
     const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
     if (N <= 0) return;
-    // total of the inclusive scan of dL_dws*ws (volumerendering.cu:118-122)
     float S = 0.f;
-    for (int64_t k = 0; k < N; ++k) S += dL_dws[start + k] * ws[start + k];
+    for (int64_t k0 = 0; k0 < N; k0 += 64) {
+        const int cnt = (int)(N - k0 < 64 ? N - k0 : 64);
+        const float pk = lane < cnt ? dL_dws[start + k0 + lane] * ws[start + k0 + lane] : 0.f;
+        for (int j = 0; j < cnt; ++j) S += lane_f(pk, j);
+    }
     const float R = rgb[3 * ray], G = rgb[3 * ray + 1], B = rgb[3 * ray + 2];
     const float O = opacity[ray], D = depth[ray];
     const float gr = dL_drgb[3 * ray], gg = dL_drgb[3 * ray + 1], gb = dL_drgb[3 * ray + 2];
     const float gop = dL_dop[ray], gdep = dL_ddep[ray];
     float T = 1.0f, r = 0.f, g = 0.f, b = 0.f, d = 0.f, pre = 0.f;
-    int64_t samples = 0;
-    while (samples < N) {
-        const int64_t s = start + samples;
-        const float a = 1.0f - __expf(-sigmas[s] * deltas[s]);
-        const float w = a * T;
-        r += w * rgbs[3 * s]; g += w * rgbs[3 * s + 1]; b += w * rgbs[3 * s + 2];
-        d += w * ts[s];
-        T *= 1.0f - a;
-        pre += dL_dws[s] * ws[s];
-        dL_drgbs[3 * s] = gr * w;
-        dL_drgbs[3 * s + 1] = gg * w;
-        dL_drgbs[3 * s + 2] = gb * w;
-        dL_dsig[s] = deltas[s] * (gr * (rgbs[3 * s] * T - (R - r)) + gg * (rgbs[3 * s + 1] * T - (G - g)) +
-                                  gb * (rgbs[3 * s + 2] * T - (B - b)) + gop * (1 - O) +
-                                  gdep * (ts[s] * T - (D - d)) + T * dL_dws[s] - (S - pre));
-        if (T <= T_thr) break;
-        samples++;
-    }
-    for (int64_t k = samples + 1; k < N; ++k) {
-        const int64_t s = start + k;
-        dL_dsig[s] = 0.f;
-        dL_drgbs[3 * s] = 0.f; dL_drgbs[3 * s + 1] = 0.f; dL_drgbs[3 * s + 2] = 0.f;
+    bool done = false;
+    for (int64_t k0 = 0; k0 < N; k0 += 64) {
+        const int64_t s = start + k0 + lane;
+        const int cnt = (int)(N - k0 < 64 ? N - k0 : 64);
+        const bool in = lane < cnt;
+        float gs = 0.f, gw = 0.f;  // lane j's dL/dsigma and ws (0 past the termination)
+        if (!done) {
+            float a = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, tt = 0.f, dl = 0.f, dw = 0.f, pk = 0.f;
+            if (in) {
+                dl = deltas[s];
+                a = 1.0f - __expf(-sigmas[s] * dl);
+                cr = rgbs[3 * s]; cg = rgbs[3 * s + 1]; cb = rgbs[3 * s + 2];
+                tt = ts[s];
+                dw = dL_dws[s];
+                pk = dw * ws[s];
+            }
+            for (int j = 0; j < cnt; ++j) {
+                const float aj = lane_f(a, j), crj = lane_f(cr, j), cgj = lane_f(cg, j), cbj = lane_f(cb, j);
+                const float ttj = lane_f(tt, j);
+                const float w = aj * T;
+                r += w * crj; g += w * cgj; b += w * cbj;
+                d += w * ttj;
+                T *= 1.0f - aj;
+                pre += lane_f(pk, j);
+                const float gsj = lane_f(dl, j) * (gr * (crj * T - (R - r)) + gg * (cgj * T - (G - g)) +
+                                                   gb * (cbj * T - (B - b)) + gop * (1 - O) +
+                                                   gdep * (ttj * T - (D - d)) + T * lane_f(dw, j) - (S - pre));
+                if (lane == j) { gs = gsj; gw = w; }
+                if (T <= T_thr) { done = true; break; }
+            }
+        }
+        if (in) {
+            dL_dsig[s] = gs;
+            dL_drgbs[3 * s] = gr * gw; dL_drgbs[3 * s + 1] = gg * gw; dL_drgbs[3 * s + 2] = gb * gw;
+        }
     }
 }
 
@@ -188,7 +241,7 @@ int ngp_composite_train_fw(const float* sigmas, const float* rgbs, const float* 
     NGP_CHECK_ARG(n_rays >= 0);
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(rays_a && total_samples && opacity && depth && rgb);
-    composite_fw_kernel<<<nblk(n_rays, 64), 64, 0, as_stream(stream)>>>(sigmas, rgbs, deltas, ts, rays_a, n_rays,
+    composite_fw_kernel<<<nblk(n_rays, 4), 256, 0, as_stream(stream)>>>(sigmas, rgbs, deltas, ts, rays_a, n_rays,
                                                                        T_threshold, total_samples, opacity, depth,
                                                                        rgb, ws);
     return ngp_launch_status();
@@ -202,7 +255,7 @@ int ngp_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, con
     NGP_CHECK_ARG(n_rays >= 0);
     if (n_rays == 0) return NGP_OK;
     NGP_CHECK_ARG(dL_dopacity && dL_ddepth && dL_drgb && rays_a && opacity && depth && rgb);
-    composite_bw_kernel<<<nblk(n_rays, 64), 64, 0, as_stream(stream)>>>(
+    composite_bw_kernel<<<nblk(n_rays, 4), 256, 0, as_stream(stream)>>>(
         dL_dopacity, dL_ddepth, dL_drgb, dL_dws, sigmas, rgbs, ws, deltas, ts, rays_a, n_rays, opacity, depth, rgb,
         T_threshold, dL_dsigmas, dL_drgbs);
     return ngp_launch_status();

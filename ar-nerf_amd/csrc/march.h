@@ -88,6 +88,51 @@ __device__ __forceinline__ bool march_probe(float t, const float o[3], const flo
     return false;
 }
 
+// march_probe<true>'s per-launch constants, computed once (the wave march
+// keeps them in scalar registers: uniform VALU results would otherwise sit in
+// VGPRs for the whole kernel)
+struct ProbeConsts {
+    float mip_bound, mip_bound_inv, grid_f, grid_size_inv, gm1;
+};
+__device__ __forceinline__ float uniform_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ ProbeConsts probe_consts(const MarchParams& p) {
+    ProbeConsts c;
+    c.mip_bound = uniform_f(fminf(0.5f, p.scale));
+    c.mip_bound_inv = uniform_f(1 / c.mip_bound);
+    c.grid_f = uniform_f((float)p.grid_size);
+    c.grid_size_inv = uniform_f(1.0f / p.grid_size);
+    c.gm1 = uniform_f(p.grid_size - 1.0f);
+    return c;
+}
+// march_probe<true> with the constants precomputed: the same expressions,
+// operand for operand (bit-identical)
+__device__ __forceinline__ bool march_probe_simple(float t, const float o[3], const float d[3], const float dinv[3],
+                                                   const MarchParams& p, const ProbeConsts& k, WordCache& wc,
+                                                   float& t_target) {
+    const uint32_t G = (uint32_t)p.grid_size;
+    const float x = o[0] + t * d[0], y = o[1] + t * d[1], z = o[2] + t * d[2];
+    const int nx = (int)clampf(0.5f * (x * k.mip_bound_inv + 1) * k.grid_f, 0.0f, k.gm1);
+    const int ny = (int)clampf(0.5f * (y * k.mip_bound_inv + 1) * k.grid_f, 0.0f, k.gm1);
+    const int nz = (int)clampf(0.5f * (z * k.mip_bound_inv + 1) * k.grid_f, 0.0f, k.gm1);
+    (void)G;
+    const uint32_t idx = morton3((uint32_t)nx, (uint32_t)ny, (uint32_t)nz);
+    const uint32_t wi = idx >> 6;
+    if (wi != wc.idx) {
+        const bool any = !wc.sum || ((wc.sum[wi >> 5] >> (wi & 31u)) & 1u);
+        wc.word = any ? reinterpret_cast<const uint64_t*>(p.bitfield)[wi] : 0ull;
+        wc.idx = wi;
+    }
+    const bool occ = (wc.word >> (idx & 63u)) & 1ull;
+    if (occ) return true;
+    const float tx = (((nx + 0.5f + 0.5f * copysignf(1.0f, d[0])) * k.grid_size_inv * 2 - 1) * k.mip_bound - x) * dinv[0];
+    const float ty = (((ny + 0.5f + 0.5f * copysignf(1.0f, d[1])) * k.grid_size_inv * 2 - 1) * k.mip_bound - y) * dinv[1];
+    const float tz = (((nz + 0.5f + 0.5f * copysignf(1.0f, d[2])) * k.grid_size_inv * 2 - 1) * k.mip_bound - z) * dinv[2];
+    t_target = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+    return false;
+}
+
 template <bool SIMPLE>
 __device__ __forceinline__ bool march_step(float& t, const float o[3], const float d[3], const float dinv[3],
                                            const MarchParams& p, float& x, float& y, float& z, float& dt,

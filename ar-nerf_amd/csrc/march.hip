@@ -442,12 +442,9 @@ __device__ __forceinline__ int lat_jump_seg(int k, float tk, float T, float dt, 
     return min(j, k_end);
 }
 
-// a wave-uniform fp32 value moved to a scalar register (VALU results are
-// per-lane VGPRs even when every lane holds the same value)
-__device__ __forceinline__ float uniform_f(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
-}
-
+#ifndef NGP_MARCH_DOUBLING
+#define NGP_MARCH_DOUBLING 0
+#endif
 #ifndef NGP_MARCH_WAVES
 #define NGP_MARCH_WAVES 8
 #endif
@@ -467,6 +464,7 @@ __global__ void __launch_bounds__(256, NGP_MARCH_WAVES) march_slots_wave_kernel(
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (wave-uniform: the ray's setup is scalar)
+    const ProbeConsts pc = probe_consts(p);
     // one ray per wave (the launch has a wave per ray; no loop: no per-ray invariants held across rays)
     for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < n_rays; r = n_rays) {
         float o[3], d[3], dinv[3];
@@ -549,8 +547,8 @@ __global__ void __launch_bounds__(256, NGP_MARCH_WAVES) march_slots_wave_kernel(
                     for (int i = Kn; i <= k; ++i) t = t + dt;
                     tk = t;
                 }
-                float x, y, z, dts, T;
-                occ = march_probe<true>(tk, o, d, dinv, p, x, y, z, dts, wc, T);
+                float T;
+                occ = march_probe_simple(tk, o, d, dinv, p, pc, wc, T);
                 nxt = occ ? k + 1 : lat_jump_seg(k, tk, T, dt, k_end, Kq, Kn, Tq, Iq, invIq);
             }
             const uint64_t occm = __ballot(occ);
@@ -562,7 +560,31 @@ __global__ void __launch_bounds__(256, NGP_MARCH_WAVES) march_slots_wave_kernel(
             // space, none across occupied cells.
             uint64_t vis = 0ull;
             int cur = 0, pnt;
+#if NGP_MARCH_DOUBLING
+            {
+                int J[6];
+                J[0] = live ? min(nxt - c, 64) : 64;
+#pragma unroll
+                for (int b = 1; b < 6; ++b) {
+                    const int prev = J[b - 1];
+                    const int v = __builtin_amdgcn_ds_bpermute(min(prev, 63) << 2, prev);
+                    J[b] = prev >= 64 ? 64 : v;
+                }
+                int cu = 0;
+#pragma unroll
+                for (int b = 5; b >= 0; --b) {
+                    const int v = __builtin_amdgcn_ds_bpermute(min(cu, 63) << 2, J[b]);
+                    const int to = cu >= 64 ? 64 : v;
+                    if (to <= lane) cu = to;
+                }
+                vis = __ballot(cu == lane);
+                const int last = 63 - __builtin_clzll(vis);
+                pnt = __builtin_amdgcn_readlane(nxt, last);
+            }
+            while (false) {
+#else
             while (true) {
+#endif
                 const uint64_t from = ~occm & (~0ull << cur);
                 const int e = from ? (int)__builtin_ctzll(from) : 64;
                 vis |= (e >= 64 ? ~0ull : ((1ull << e) - 1ull)) & (~0ull << cur);

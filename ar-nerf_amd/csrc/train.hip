@@ -1552,6 +1552,46 @@ int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, flo
     return ngp_launch_status();
 }
 
+}  // extern "C"
+
+// The rows of (dL/dsigma, dL/drgb) with a nonzero entry: the samples that
+// carry gradient (the compositing backward, volumerendering.cu:86-150, leaves
+// every sample past its ray's termination at exact zero, and a zero upstream
+// gradient adds exactly nothing to the parameters' gradient) -> idx[0..*count):
+// each wave's rows ascending, waves in reservation order (one atomic per wave).
+__global__ void __launch_bounds__(256) grad_rows_kernel(const float* __restrict__ dsig, const float* __restrict__ drgb,
+                                                        int64_t n, int32_t* __restrict__ idx,
+                                                        unsigned long long* __restrict__ count) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t i0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); i0 < n; i0 += (int64_t)gridDim.x * 256) {
+        const int64_t i = i0 + lane;
+        bool nz = false;
+        if (i < n) nz = dsig[i] != 0.f || drgb[3 * i] != 0.f || drgb[3 * i + 1] != 0.f || drgb[3 * i + 2] != 0.f;
+        const uint64_t m = __ballot(nz);
+        if (!m) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(count, (unsigned long long)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (nz) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+    }
+}
+
+extern "C" {
+
+int ngp_gradient_rows(const float* dL_dsigmas, const float* dL_drgbs, int64_t n, int32_t* idx, int64_t* count,
+                      void* stream) {
+    NGP_CHECK_ARG(n >= 0 && n < (1ll << 31) && count && ((uintptr_t)count & 7) == 0);
+    hipStream_t s = as_stream(stream);
+    zero_words_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(count), 1);
+    if (n > 0) {
+        NGP_CHECK_ARG(dL_dsigmas && dL_drgbs && idx);
+        const int64_t b = (n + 255) / 256;
+        grad_rows_kernel<<<(unsigned)(b < 4096 ? b : 4096), 256, 0, s>>>(
+            dL_dsigmas, dL_drgbs, n, idx, reinterpret_cast<unsigned long long*>(count));
+    }
+    return ngp_launch_status();
+}
+
 int ngp_active_samples(const int32_t* n_active, const int64_t* rays_a, int64_t n_rows, int64_t* act_start_ws,
                        int64_t* n_active_total, int32_t* sample_idx, void* stream) {
     NGP_CHECK_ARG(n_rows >= 0 && n_active_total);

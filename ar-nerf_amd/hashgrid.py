@@ -198,6 +198,51 @@ def field_backward(xyzs, dirs, grid: HashGrid, params16, enc, dL_dsig, dL_drgb, 
     vren._ok(st, "ngp_field_backward")
 
 
+BIN_LEVEL_LO, BIN_MERGE_HI = 8, 11  # the trainer's hybrid split on object scenes (trainer.NGPTrainer)
+BIN_WS_SAMPLES = 1 << 20  # binned workspace: gradient-carrying samples it holds (the rest: atomic path, exact)
+_bin_ws = {}
+
+
+def _binned_workspace(device):
+    """The binned hash backward's workspace (ngp_hash_backward_binned_workspace(BIN_WS_SAMPLES) bytes),
+    one per device, allocated on first use and reused by every drop-in backward."""
+    ws = _bin_ws.get(device)
+    if ws is None:
+        nbytes = _lib().ngp_hash_backward_binned_workspace(BIN_WS_SAMPLES)
+        ws = _bin_ws[device] = torch.empty((nbytes + 255) // 256, 64, dtype=torch.int32, device=device)
+    return ws
+
+
+def field_backward_sparse(xyzs, dirs, grid: HashGrid, params16, enc, dL_dsig, dL_drgb, grad):
+    """field_backward over the samples that carry gradient only, with the
+    training step's hybrid hash backward: the rows with a nonzero dL/dsigma or
+    dL/drgb are listed on the device (ngp_gradient_rows: no host sync) -- the
+    compositing backward leaves every sample past its ray's termination at
+    exact zero, and a zero row adds exactly nothing -- then the MLP backward,
+    the atomic coarse levels [0, 8) and the binned levels [8, 16) over that list
+    (the same gradient as field_backward up to fp32 summation order)."""
+    n = xyzs.shape[0]
+    _check(grad, "grad", torch.float32, grid.n_params)
+    _check(enc, "enc", torch.float16)
+    _check(dL_dsig, "dL_dsigmas", torch.float32); _check(dL_drgb, "dL_drgbs", torch.float32)
+    if n == 0:
+        return
+    dev = xyzs.device
+    L, s = _lib(), vren._stream()
+    idx = torch.empty(n, dtype=torch.int32, device=dev)
+    cnt = torch.empty(1, dtype=torch.int64, device=dev)
+    vren._ok(vren.lib().ngp_gradient_rows(_ptr(dL_dsig), _ptr(dL_drgb), n, _ptr(idx), _ptr(cnt), s), "gradient_rows")
+    denc = torch.empty(n, 32, device=dev)
+    vren._ok(L.ngp_field_backward_mlp(_ptr(dirs), n, _ptr(cnt), _ptr(idx), _ptr(enc), 0, _ptr(params16),
+                                      _ptr(dL_dsig), _ptr(dL_drgb), _ptr(denc), _ptr(grad), s), "field_backward_mlp")
+    gt = grad[MLP_PARAMS:]
+    vren._ok(L.ngp_hash_backward_levels(_ptr(xyzs), n, _ptr(cnt), _ptr(idx), ctypes.byref(grid.desc), _ptr(denc),
+                                        _ptr(gt), 0, BIN_LEVEL_LO, s), "hash_backward_levels")
+    vren._ok(L.ngp_hash_backward_binned(_ptr(xyzs), n, _ptr(cnt), _ptr(idx), ctypes.byref(grid.desc), _ptr(denc),
+                                        _ptr(gt), _ptr(_binned_workspace(dev)), BIN_WS_SAMPLES, BIN_LEVEL_LO,
+                                        BIN_MERGE_HI, s), "hash_backward_binned")
+
+
 class FP16Shadow:
     """fp16 copy of an fp32 master parameter, refreshed when the master changes."""
 
@@ -230,7 +275,7 @@ class _FieldFn(torch.autograd.Function):
         dsig = torch.zeros(xyzs.shape[0], device=xyzs.device) if dsig is None else dsig.float().contiguous()
         drgb = torch.zeros(xyzs.shape[0], 3, device=xyzs.device) if drgb is None else drgb.float().contiguous()
         grad = torch.zeros(grid.n_params, device=xyzs.device)
-        field_backward(xyzs.contiguous(), dirs.contiguous(), grid, ctx.p16, enc, dsig, drgb, grad)
+        field_backward_sparse(xyzs.contiguous(), dirs.contiguous(), grid, ctx.p16, enc, dsig, drgb, grad)
         return None, None, grad, None, None
 
 

@@ -547,6 +547,17 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
                        int32_t* sample_idx, void* alloc_ws, int64_t* n_active_total, int64_t* stats,
                        void* stream);
 
+/* The samples that carry gradient in the drop-in backward: rows i < n with
+ * dL_dsigmas[i] != 0 or any dL_drgbs[i][*] != 0 (the compositing backward,
+ * volumerendering.cu:86-150, leaves every sample past its ray's termination at
+ * exact zero) -> idx[0..*count) (device count, 8-byte aligned, zeroed by the
+ * call; rows ascending within each 64-row group, groups in any order).  The
+ * field backward over that list (ngp_field_backward_mlp / ngp_hash_backward*
+ * with sample_idx = idx, n_dev = count) adds exactly what it adds over all n
+ * rows.  Replaces nothing in the reference: it lets models.custom_functions'
+ * autograd surface skip the zero rows the reference's tcnn backward walks. */
+int ngp_gradient_rows(const float* dL_dsigmas, const float* dL_drgbs, int64_t n, int32_t* idx, int64_t* count,
+                      void* stream);
 /* Compacted list of the gradient-carrying samples: act_start_ws (n_rows) i64
  * scratch, n_active_total (1) i64, sample_idx (>= total) i32 with
  * sample_idx[act_start[r] + k] = rays_a[r].start + k, k < n_active[r]. */

@@ -18,3 +18,11 @@ for lib in lib_base lib; do
   echo $lib; tail -1 $OUT/skip_$lib.txt
 done
 bash scripts/ab_lib.sh $T/ab 2 "lib_base::" "lib_m7::" "::"
+# the drop-in loop: wall time, host-side op profile, and a rocprofv3 kernel trace of its steps
+timeout -k 10 300 python -u scripts/diag/dropin_profile.py 2000 40 --torch-profile > $OUT/dropin.json 2> $OUT/dropin_torchprof.txt
+cat $OUT/dropin.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/dprof -o run -f csv -- python3 scripts/diag/dropin_profile.py 2000 40 > $OUT/dropin_prof.json 2> $OUT/dropin_prof.err
+TR=$(find $OUT/dprof -name 'run_kernel_trace.csv' | head -1)
+python3 scripts/kstats.py $TR 40 > $OUT/dropin_kstats.txt 2>&1 || true
+head -30 $OUT/dropin_kstats.txt
+rm -rf $OUT/dprof
