@@ -442,11 +442,8 @@ __device__ __forceinline__ int lat_jump_seg(int k, float tk, float T, float dt, 
     return min(j, k_end);
 }
 
-#ifndef NGP_MARCH_DOUBLING
-#define NGP_MARCH_DOUBLING 0
-#endif
 #ifndef NGP_MARCH_WAVES
-#define NGP_MARCH_WAVES 8
+#define NGP_MARCH_WAVES 1
 #endif
 __global__ void __launch_bounds__(256, NGP_MARCH_WAVES) march_slots_wave_kernel(const float* __restrict__ rays_o,
                                                                const float* __restrict__ rays_d,
@@ -553,15 +550,21 @@ __global__ void __launch_bounds__(256, NGP_MARCH_WAVES) march_slots_wave_kernel(
             }
             const uint64_t occm = __ballot(occ);
             const uint64_t livem = __ballot(live);
-            // The walk's chain through the window (wave-uniform, scalar): from a chain
-            // point cur, the walk visits every point of the occupied run starting there
-            // (successor k + 1), then the run's first unoccupied point e; from an empty e
-            // it jumps to nxt(e).  One hop per empty chain point: ~1 per cell in empty
-            // space, none across occupied cells.
-            uint64_t vis = 0ull;
-            int cur = 0, pnt;
-#if NGP_MARCH_DOUBLING
-            {
+            // The walk's chain through the window.  A window whose live points are all
+            // occupied is visited whole (successor k + 1 throughout).  Otherwise, in
+            // parallel: J_b(i) = the 2^b-th successor of window point i (64 = out of the
+            // window), built by pointer doubling; every lane then climbs from point 0 with
+            // binary lifting to the last chain point <= itself -- it is on the chain iff
+            // that is itself (successors only move forward).  (A scalar hop per empty
+            // chain point instead: ~14 hops per window in empty space, 30 SALU
+            // instructions and 3 branches each, the kernel 1.6x slower with every wave
+            // resident -- the CU's scalar unit is shared, profiles/r06/march_variants.txt.)
+            uint64_t vis;
+            int pnt;
+            if (occm == livem) {
+                vis = livem;
+                pnt = (livem >> 63) ? c + 64 : k_end;
+            } else {
                 int J[6];
                 J[0] = live ? min(nxt - c, 64) : 64;
 #pragma unroll
@@ -578,22 +581,8 @@ __global__ void __launch_bounds__(256, NGP_MARCH_WAVES) march_slots_wave_kernel(
                     if (to <= lane) cu = to;
                 }
                 vis = __ballot(cu == lane);
-                const int last = 63 - __builtin_clzll(vis);
-                pnt = __builtin_amdgcn_readlane(nxt, last);
-            }
-            while (false) {
-#else
-            while (true) {
-#endif
-                const uint64_t from = ~occm & (~0ull << cur);
-                const int e = from ? (int)__builtin_ctzll(from) : 64;
-                vis |= (e >= 64 ? ~0ull : ((1ull << e) - 1ull)) & (~0ull << cur);
-                if (e >= 64) { pnt = c + 64; break; }           // lane 63 occupied: successor c + 64
-                if (!((livem >> e) & 1ull)) { pnt = k_end; break; }  // past the walk's stop
-                vis |= 1ull << e;
-                const int nx = __builtin_amdgcn_readlane(nxt, e);
-                if (nx >= c + 64) { pnt = nx; break; }
-                cur = nx - c;
+                const int last = 63 - __builtin_clzll(vis);  // the chain's last point in the window
+                pnt = __builtin_amdgcn_readlane(nxt, last);  // k_end if it ends the walk
             }
             vis &= occm;
             // emit the chain's occupied points, at most up to max_samples

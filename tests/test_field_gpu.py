@@ -609,8 +609,9 @@ def test_sparse_field_backward_matches_the_dense_one():
     idx = torch.empty(x.shape[0], dtype=torch.int32, device=DEV)
     cnt = torch.empty(1, dtype=torch.int64, device=DEV)
     import vren
-    vren._ok(vren.lib().ngp_gradient_rows(HG._ptr(dsig.to(DEV).contiguous()), HG._ptr(drgb.to(DEV).contiguous()),
-                                          x.shape[0], HG._ptr(idx), HG._ptr(cnt), vren._stream()), "gradient_rows")
+    dsd, drd = dsig.to(DEV).contiguous(), drgb.to(DEV).contiguous()  # (held: the launch reads them later)
+    vren._ok(vren.lib().ngp_gradient_rows(HG._ptr(dsd), HG._ptr(drd), x.shape[0], HG._ptr(idx), HG._ptr(cnt),
+                                          vren._stream()), "gradient_rows")
     n = int(cnt)
     nz = torch.nonzero((dsig != 0) | (drgb != 0).any(1))[:, 0]
     assert n == nz.numel() and torch.equal(torch.sort(idx[:n].cpu().long())[0], nz)
