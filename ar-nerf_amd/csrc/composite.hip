@@ -20,13 +20,35 @@ __device__ __forceinline__ float lane_f(float v, int j) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
 }
 
+// The reference's serial transmittance chain over one 64-sample chunk
+// (T *= 1 - a, in order): lane j gets T before (Tb) and after (Ta) its
+// sample.  Only the product is serial (one multiply per sample, no branch:
+// the walk's break is found afterwards as the first lane whose T after its
+// sample is <= thr -- the values up to there are exactly the serial loop's).
+struct ChainT {
+    float Tb, Ta, T;  // per lane; T: the chain's value after the chunk's last sample (uniform)
+};
+__device__ __forceinline__ ChainT serial_transmittance(float om, int cnt, float T, int lane) {
+    ChainT c;
+    c.Tb = c.Ta = 0.f;
+    for (int j = 0; j < cnt; ++j) {
+        const bool me = lane == j;
+        if (me) c.Tb = T;
+        T *= lane_f(om, j);
+        if (me) c.Ta = T;
+    }
+    c.T = T;
+    return c;
+}
+
 // volumerendering.cu:5-44 with one wave per ray: the lanes load a 64-sample
-// chunk (coalesced) and compute each sample's alpha, then the ray's serial
-// chain -- T, the left folds of rgb / depth / opacity, the break before the
-// count -- runs in the reference's order on scalar copies of lane j's values:
-// the same fp32 operations in the same order as the per-lane serial loop
-// (bit-identical), with the memory latency paid once per chunk instead of per
-// sample and 64x the waves in flight.
+// chunk (coalesced) and compute each sample's alpha; the chunk's serial
+// transmittance chain (serial_transmittance) gives every lane its T; each
+// sample's weight w = a T and its products with rgb / t are formed per lane;
+// then the ray's left folds of rgb / depth / opacity add them in order up to
+// the terminating sample (independent chains, no branch per sample).  The
+// same fp32 operations in the same order as the per-lane serial loop
+// (bit-identical), the memory latency paid once per chunk, a wave per ray.
 __global__ void __launch_bounds__(256) composite_fw_kernel(const float* __restrict__ sigmas,
                                                            const float* __restrict__ rgbs,
                                                            const float* __restrict__ deltas,
@@ -56,19 +78,24 @@ __global__ void __launch_bounds__(256) composite_fw_kernel(const float* __restri
             cr = rgbs[3 * s]; cg = rgbs[3 * s + 1]; cb = rgbs[3 * s + 2];
             tt = ts[s];
         }
-        float wl = 0.f;  // lane j's ws
-        for (int j = 0; j < cnt; ++j) {
-            const float aj = lane_f(a, j);
-            const float w = aj * T;
-            r += w * lane_f(cr, j); g += w * lane_f(cg, j); b += w * lane_f(cb, j);
-            d += w * lane_f(tt, j);
-            op += w;
-            if (lane == j) wl = w;
-            T *= 1.0f - aj;
-            if (T <= T_thr) { done = true; samples = k0 + j; break; }
+        const ChainT ch = serial_transmittance(1.0f - a, cnt, T, lane);
+        const uint64_t hit = __ballot(in && ch.Ta <= T_thr);
+        const int last = hit ? __ffsll((unsigned long long)hit) - 1 : cnt - 1;  // the chunk's last composited sample
+        const float w = a * ch.Tb;
+        const float pr = w * cr, pg = w * cg, pb = w * cb, pd = w * tt;
+        for (int j = 0; j <= last; ++j) {
+            r += lane_f(pr, j); g += lane_f(pg, j); b += lane_f(pb, j);
+            d += lane_f(pd, j);
+            op += lane_f(w, j);
         }
-        if (!done) samples = k0 + cnt;
-        if (in) ws[s] = wl;  // (0 past the terminating sample)
+        if (in) ws[s] = lane <= last ? w : 0.f;
+        if (hit) {
+            done = true;
+            samples = k0 + last;  // (the break comes before the count)
+        } else {
+            samples = k0 + cnt;
+            T = ch.T;
+        }
     }
     if (lane == 0) {
         rgb[3 * ray] = r; rgb[3 * ray + 1] = g; rgb[3 * ray + 2] = b;
@@ -79,9 +106,11 @@ __global__ void __launch_bounds__(256) composite_fw_kernel(const float* __restri
 }
 
 // volumerendering.cu:86-150, one wave per ray as composite_fw_kernel: the
-// total of dL_dws * ws (the reference's inclusive scan's last value) as a
-// serial left fold, then the serial pass in the reference's order, each
-// sample's gradient put back into its lane and stored per chunk.
+// total S of dL_dws * ws (the reference's inclusive scan's last value) as a
+// serial left fold; per chunk the serial transmittance chain, then the left
+// folds of rgb / depth / dL_dws * ws, each fold's running value handed back
+// to its sample's lane, and every sample's gradient formed in its lane from
+// those (the reference's expression, operand for operand).
 __global__ void __launch_bounds__(256) composite_bw_kernel(
     const float* __restrict__ dL_dop, const float* __restrict__ dL_ddep, const float* __restrict__ dL_drgb,
     const float* __restrict__ dL_dws, const float* __restrict__ sigmas, const float* __restrict__ rgbs,
@@ -110,7 +139,7 @@ __global__ void __launch_bounds__(256) composite_bw_kernel(
         const int64_t s = start + k0 + lane;
         const int cnt = (int)(N - k0 < 64 ? N - k0 : 64);
         const bool in = lane < cnt;
-        float gs = 0.f, gw = 0.f;  // lane j's dL/dsigma and ws (0 past the termination)
+        float gs = 0.f, gw = 0.f;  // this lane's dL/dsigma and ws (0 past the termination)
         if (!done) {
             float a = 0.f, cr = 0.f, cg = 0.f, cb = 0.f, tt = 0.f, dl = 0.f, dw = 0.f, pk = 0.f;
             if (in) {
@@ -121,20 +150,26 @@ __global__ void __launch_bounds__(256) composite_bw_kernel(
                 dw = dL_dws[s];
                 pk = dw * ws[s];
             }
-            for (int j = 0; j < cnt; ++j) {
-                const float aj = lane_f(a, j), crj = lane_f(cr, j), cgj = lane_f(cg, j), cbj = lane_f(cb, j);
-                const float ttj = lane_f(tt, j);
-                const float w = aj * T;
-                r += w * crj; g += w * cgj; b += w * cbj;
-                d += w * ttj;
-                T *= 1.0f - aj;
+            const ChainT ch = serial_transmittance(1.0f - a, cnt, T, lane);
+            const uint64_t hit = __ballot(in && ch.Ta <= T_thr);
+            const int last = hit ? __ffsll((unsigned long long)hit) - 1 : cnt - 1;
+            const float w = a * ch.Tb;
+            const float pr = w * cr, pg = w * cg, pb = w * cb, pd = w * tt;
+            float rj = 0.f, gj = 0.f, bj = 0.f, dj = 0.f, prej = 0.f;  // the folds' values after this lane's sample
+            for (int j = 0; j <= last; ++j) {
+                r += lane_f(pr, j); g += lane_f(pg, j); b += lane_f(pb, j);
+                d += lane_f(pd, j);
                 pre += lane_f(pk, j);
-                const float gsj = lane_f(dl, j) * (gr * (crj * T - (R - r)) + gg * (cgj * T - (G - g)) +
-                                                   gb * (cbj * T - (B - b)) + gop * (1 - O) +
-                                                   gdep * (ttj * T - (D - d)) + T * lane_f(dw, j) - (S - pre));
-                if (lane == j) { gs = gsj; gw = w; }
-                if (T <= T_thr) { done = true; break; }
+                if (lane == j) { rj = r; gj = g; bj = b; dj = d; prej = pre; }
             }
+            const float Ta = ch.Ta;
+            if (lane <= last) {
+                gs = dl * (gr * (cr * Ta - (R - rj)) + gg * (cg * Ta - (G - gj)) + gb * (cb * Ta - (B - bj)) +
+                           gop * (1 - O) + gdep * (tt * Ta - (D - dj)) + Ta * dw - (S - prej));
+                gw = w;
+            }
+            if (hit) done = true;
+            else T = ch.T;
         }
         if (in) {
             dL_dsig[s] = gs;

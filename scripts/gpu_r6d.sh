@@ -6,6 +6,8 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 T=${1:-r6d}
 OUT=gpurun_out/$T; mkdir -p $OUT
+timeout -k 10 120 python -u scripts/diag/composite_libs.py ar-nerf_amd/lib_serial/libngp_amd.so ar-nerf_amd/lib/libngp_amd.so > $OUT/composite_libs.json 2> $OUT/composite_libs.err || { tail -20 $OUT/composite_libs.err; exit 1; }
+cat $OUT/composite_libs.json
 timeout -k 10 400 python -u -m pytest tests/test_vren_gpu.py tests/test_field_gpu.py tests/test_dropin_gpu.py tests/test_golden_gpu.py tests/test_renderer_gpu.py -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -60 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 timeout -k 10 300 python -u scripts/diag/march_libs.py 1500 ar-nerf_amd/lib_base/libngp_amd.so ar-nerf_amd/lib/libngp_amd.so ar-nerf_amd/lib_w8/libngp_amd.so > $OUT/march_libs.txt 2> $OUT/march_libs.err || { tail -20 $OUT/march_libs.err; exit 1; }

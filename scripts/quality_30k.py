@@ -47,10 +47,30 @@ def run(steps=30000, res=400, n_train=100, n_test=10, seed=4, root=None):
             "train_rays_per_s_exact": exact["train_rays_per_s"]}
 
 
+def run_seeds(seeds, steps=30000, res=400):
+    """run() for several seeds (model init, batches, occupancy draws) on one written scene: per-seed PSNRs
+    of both modes, their means and the mean / spread of the per-seed difference (VERDICT r5 #9)."""
+    import synthetic as S
+    with tempfile.TemporaryDirectory() as tmp:
+        scene = os.path.join(tmp, "Synthetic_NeRF", "Analytic")
+        S.write_nsvf_scene(scene, res=res, n_train=100, n_test=10)
+        per = [run(steps, res, seed=sd, root=scene) for sd in seeds]
+    d = [p["delta_db"] for p in per]
+    mean = lambda v: round(sum(v) / len(v), 3)  # noqa: E731
+    return {"steps": steps, "seeds": list(seeds), "psnr_default": [p["psnr_default"] for p in per],
+            "psnr_exact": [p["psnr_exact"] for p in per], "mean_default": mean([p["psnr_default"] for p in per]),
+            "mean_exact": mean([p["psnr_exact"] for p in per]), "delta_db": d, "mean_delta_db": mean(d),
+            "delta_range_db": [min(d), max(d)], "scene": per[0]["scene"]}
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30000)
     ap.add_argument("--res", type=int, default=400)
     ap.add_argument("--root", default=None, help="an existing NSVF scene instead of the synthetic one")
+    ap.add_argument("--seeds", default=None, help="comma-separated seeds: run_seeds (both modes per seed)")
     a = ap.parse_args()
-    print(json.dumps(run(a.steps, a.res, root=a.root)))
+    if a.seeds:
+        print(json.dumps(run_seeds([int(x) for x in a.seeds.split(",")], a.steps, a.res)))
+    else:
+        print(json.dumps(run(a.steps, a.res, root=a.root)))
