@@ -442,10 +442,10 @@ __device__ __forceinline__ int lat_jump_seg(int k, float tk, float T, float dt, 
     return min(j, k_end);
 }
 
-#ifndef NGP_MARCH_WAVES
-#define NGP_MARCH_WAVES 1
-#endif
-__global__ void __launch_bounds__(256, NGP_MARCH_WAVES) march_slots_wave_kernel(const float* __restrict__ rays_o,
+// 8 waves per SIMD (64 VGPRs): every wave of an 8192-ray batch resident at once, no second
+// dispatch round (73 -> 57 us alone; 7 waves at 65 VGPRs measured 58 us and -0.8 % end to end,
+// profiles/r06/march_variants.txt)
+__global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* __restrict__ rays_o,
                                                                const float* __restrict__ rays_d,
                                                                const float* __restrict__ hits_t, int64_t n_rays,
                                                                const float* __restrict__ noise, MarchParams p,

@@ -1557,22 +1557,44 @@ int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, flo
 // The rows of (dL/dsigma, dL/drgb) with a nonzero entry: the samples that
 // carry gradient (the compositing backward, volumerendering.cu:86-150, leaves
 // every sample past its ray's termination at exact zero, and a zero upstream
-// gradient adds exactly nothing to the parameters' gradient) -> idx[0..*count):
-// each wave's rows ascending, waves in reservation order (one atomic per wave).
+// gradient adds exactly nothing to the parameters' gradient) -> idx[0..*count).
+// A block takes 1024 consecutive rows (a wave 256 of them), counts them per wave,
+// reserves its range with ONE atomic (a per-wave atomic on the one counter
+// serialised ~9 K reservations: 57 us per launch) and writes the rows in
+// order; blocks land in reservation order.
 __global__ void __launch_bounds__(256) grad_rows_kernel(const float* __restrict__ dsig, const float* __restrict__ drgb,
                                                         int64_t n, int32_t* __restrict__ idx,
                                                         unsigned long long* __restrict__ count) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t i0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); i0 < n; i0 += (int64_t)gridDim.x * 256) {
-        const int64_t i = i0 + lane;
-        bool nz = false;
-        if (i < n) nz = dsig[i] != 0.f || drgb[3 * i] != 0.f || drgb[3 * i + 1] != 0.f || drgb[3 * i + 2] != 0.f;
-        const uint64_t m = __ballot(nz);
-        if (!m) continue;
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(count, (unsigned long long)__popcll(m));
-        base = __shfl(base, 0, 64);
-        if (nz) idx[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+    __shared__ uint32_t wcnt[4];
+    __shared__ unsigned long long base_s;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t b0 = (int64_t)blockIdx.x * 1024; b0 < n; b0 += (int64_t)gridDim.x * 1024) {
+        uint64_t m[4];
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // wave w takes rows b0 + 256 w .. + 255, 64 per step
+            const int64_t i = b0 + 256 * w + 64 * q + lane;
+            bool nz = false;
+            if (i < n) nz = dsig[i] != 0.f || drgb[3 * i] != 0.f || drgb[3 * i + 1] != 0.f || drgb[3 * i + 2] != 0.f;
+            m[q] = __ballot(nz);
+            c += (uint32_t)__popcll(m[q]);
+        }
+        if (lane == 0) wcnt[w] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+            base_s = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+        }
+        __syncthreads();
+        unsigned long long o = base_s;
+        for (int v = 0; v < w; ++v) o += wcnt[v];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if ((m[q] >> lane) & 1ull)
+                idx[o + __popcll(m[q] & ((1ull << lane) - 1ull))] = (int32_t)(b0 + 256 * w + 64 * q + lane);
+            o += __popcll(m[q]);
+        }
+        __syncthreads();  // wcnt / base_s are rewritten next round
     }
 }
 
@@ -1585,7 +1607,7 @@ int ngp_gradient_rows(const float* dL_dsigmas, const float* dL_drgbs, int64_t n,
     zero_words_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(count), 1);
     if (n > 0) {
         NGP_CHECK_ARG(dL_dsigmas && dL_drgbs && idx);
-        const int64_t b = (n + 255) / 256;
+        const int64_t b = (n + 1023) / 1024;
         grad_rows_kernel<<<(unsigned)(b < 4096 ? b : 4096), 256, 0, s>>>(
             dL_dsigmas, dL_drgbs, n, idx, reinterpret_cast<unsigned long long*>(count));
     }

@@ -200,7 +200,9 @@ def field_backward(xyzs, dirs, grid: HashGrid, params16, enc, dL_dsig, dL_drgb, 
 
 BIN_LEVEL_LO, BIN_MERGE_HI = 8, 11  # the trainer's hybrid split on object scenes (trainer.NGPTrainer)
 BIN_WS_SAMPLES = 1 << 20  # binned workspace: gradient-carrying samples it holds (the rest: atomic path, exact)
+COARSE_REP, COARSE_REP_LEVELS = 8, 4  # the trainer's gradient replicas of the coarsest atomic levels
 _bin_ws = {}
+_rep_bufs = {}
 
 
 def _binned_workspace(device):
@@ -213,13 +215,24 @@ def _binned_workspace(device):
     return ws
 
 
+def _rep_buffer(grid, device):
+    """Replicas of the coarse levels' gradient (ngp_hash_backward_levels_rep; zero between calls)."""
+    key = (device, tuple(grid.offsets))
+    rep = _rep_bufs.get(key)
+    if rep is None:
+        nrep = _lib().ngp_hash_backward_rep_floats(ctypes.byref(grid.desc), COARSE_REP_LEVELS, COARSE_REP)
+        rep = _rep_bufs[key] = torch.zeros(nrep, device=device)
+    return rep
+
+
 def field_backward_sparse(xyzs, dirs, grid: HashGrid, params16, enc, dL_dsig, dL_drgb, grad):
     """field_backward over the samples that carry gradient only, with the
     training step's hybrid hash backward: the rows with a nonzero dL/dsigma or
     dL/drgb are listed on the device (ngp_gradient_rows: no host sync) -- the
     compositing backward leaves every sample past its ray's termination at
     exact zero, and a zero row adds exactly nothing -- then the MLP backward,
-    the atomic coarse levels [0, 8) and the binned levels [8, 16) over that list
+    the atomic coarse levels [0, 8) (levels 0-3 into 8 gradient replicas, folded
+    after) and the binned levels [8, 16) over that list
     (the same gradient as field_backward up to fp32 summation order)."""
     n = xyzs.shape[0]
     _check(grad, "grad", torch.float32, grid.n_params)
@@ -236,8 +249,9 @@ def field_backward_sparse(xyzs, dirs, grid: HashGrid, params16, enc, dL_dsig, dL
     vren._ok(L.ngp_field_backward_mlp(_ptr(dirs), n, _ptr(cnt), _ptr(idx), _ptr(enc), 0, _ptr(params16),
                                       _ptr(dL_dsig), _ptr(dL_drgb), _ptr(denc), _ptr(grad), s), "field_backward_mlp")
     gt = grad[MLP_PARAMS:]
-    vren._ok(L.ngp_hash_backward_levels(_ptr(xyzs), n, _ptr(cnt), _ptr(idx), ctypes.byref(grid.desc), _ptr(denc),
-                                        _ptr(gt), 0, BIN_LEVEL_LO, s), "hash_backward_levels")
+    vren._ok(L.ngp_hash_backward_levels_rep(_ptr(xyzs), n, _ptr(cnt), _ptr(idx), ctypes.byref(grid.desc), _ptr(denc),
+                                            _ptr(gt), 0, BIN_LEVEL_LO, _ptr(_rep_buffer(grid, dev)),
+                                            COARSE_REP_LEVELS, COARSE_REP, 1, s), "hash_backward_levels_rep")
     vren._ok(L.ngp_hash_backward_binned(_ptr(xyzs), n, _ptr(cnt), _ptr(idx), ctypes.byref(grid.desc), _ptr(denc),
                                         _ptr(gt), _ptr(_binned_workspace(dev)), BIN_WS_SAMPLES, BIN_LEVEL_LO,
                                         BIN_MERGE_HI, s), "hash_backward_binned")

@@ -16,7 +16,10 @@ def render(model, rays_o, rays_d, **kwargs):
     rays_o = rays_o.contiguous()
     rays_d = rays_d.contiguous()
     _, hits_t, _ = RayAABBIntersector.apply(rays_o, rays_d, model.center, model.half_size, 1)
-    hits_t[(hits_t[:, 0, 0] >= 0) & (hits_t[:, 0, 0] < NEAR_DISTANCE), 0, 0] = NEAR_DISTANCE
+    # (the reference's boolean-mask assignment, as a select: a mask index_put lists the mask's
+    # nonzeros first, which waits for the device every call)
+    h0 = hits_t[:, 0, 0]
+    hits_t[:, 0, 0] = torch.where((h0 >= 0) & (h0 < NEAR_DISTANCE), torch.full_like(h0, NEAR_DISTANCE), h0)
     render_func = __render_rays_test if kwargs.get('test_time', False) else __render_rays_train
     mesh_depth_map = kwargs.get('mesh_depth_map', None)
     if mesh_depth_map is not None:  # rendering.py:38-44

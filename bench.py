@@ -287,7 +287,7 @@ class DropinLoop:
         loss = sum(lo.mean() for lo in loss_d.values())
         loss.backward()
         self.opt.step()
-        self.opt.zero_grad(set_to_none=False)
+        self.opt.zero_grad()  # (torch's default, set_to_none=True: the next backward assigns the gradient)
         self.global_step += 1
         return loss, results
 

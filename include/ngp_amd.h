@@ -551,7 +551,7 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
  * dL_dsigmas[i] != 0 or any dL_drgbs[i][*] != 0 (the compositing backward,
  * volumerendering.cu:86-150, leaves every sample past its ray's termination at
  * exact zero) -> idx[0..*count) (device count, 8-byte aligned, zeroed by the
- * call; rows ascending within each 64-row group, groups in any order).  The
+ * call; rows ascending within each 1024-row block, blocks in any order).  The
  * field backward over that list (ngp_field_backward_mlp / ngp_hash_backward*
  * with sample_idx = idx, n_dev = count) adds exactly what it adds over all n
  * rows.  Replaces nothing in the reference: it lets models.custom_functions'
