@@ -399,16 +399,10 @@ __global__ void __launch_bounds__(256) march_slots_kernel(const float* __restric
 // overflows: dt below half an ulp of t, or more than LSEG binades -- never on
 // the object scenes; kept out of line so its registers do not count against
 // the lattice loop's).
+struct MarchDirect;
 __device__ __forceinline__ int march_serial_lane(const float o[3], const float d[3], const float dinv[3], float t,
-                                              float t2, const MarchParams& p, WordCache& wc, float* st, float* sd) {
-    float x, y, z, dts;
-    int N = 0;
-    while (0 <= t && t < t2 && N < p.max_samples) {
-        const float tc = t;
-        if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) { st[N] = tc; sd[N] = dts; N++; }
-    }
-    return N;
-}
+                                              float t2, const MarchParams& p, WordCache& wc, float* st, float* sd,
+                                              const MarchDirect& md, int64_t r);
 
 // first j > k with t_j >= T, for lane point k with value tk: inside the
 // window's segment [Kq, Kn) (value Tq, increment Iq, its reciprocal invIq, in
@@ -442,6 +436,63 @@ __device__ __forceinline__ int lat_jump_seg(int k, float tk, float T, float dt, 
     return min(j, k_end);
 }
 
+// Direct training layout (ngp_march_train_direct; xyzs == nullptr: the slot
+// mode of ngp_march_train_slots): ray r's samples are written straight to
+// slots [r * max_samples, r * max_samples + N_r) of xyzs / dirs / ts /
+// deltas (the compaction's expressions: xyz = o + t d, no contraction --
+// bit-identical values), rays_a[r] = (r, r * max_samples, N_r), a ray with
+// samples appends r to rows (rows in completion order) and adds N_r to
+// *total.  The training step reads samples only through rays_a and index
+// lists, so the slot layout needs no scan and no compaction pass.
+struct MarchDirect {
+    float* xyzs;
+    float* dirs;
+    float* ts;
+    float* deltas;
+    int64_t* rays_a;
+    int32_t* rows;
+    unsigned long long* n_rows;
+    unsigned long long* total;
+};
+__device__ __forceinline__ void march_direct_finish(const MarchDirect& md, int64_t r, int max_samples, int N,
+                                                    int lane) {
+    if (lane == 0) {
+        md.rays_a[3 * r] = r;
+        md.rays_a[3 * r + 1] = r * (int64_t)max_samples;
+        md.rays_a[3 * r + 2] = N;
+        if (N > 0) {
+            md.rows[atomicAdd(md.n_rows, 1ull)] = (int32_t)r;
+            atomicAdd(md.total, (unsigned long long)N);
+        }
+    }
+}
+
+// (lane 0: the ray's samples into its slot_t / slot_dt range, or, direct, its xyzs / dirs / ts / deltas slots)
+__device__ __forceinline__ int march_serial_lane(const float o[3], const float d[3], const float dinv[3], float t,
+                                              float t2, const MarchParams& p, WordCache& wc, float* st, float* sd,
+                                              const MarchDirect& md, int64_t r) {
+    float x, y, z, dts;
+    int N = 0;
+    const int64_t base = r * (int64_t)p.max_samples;
+    while (0 <= t && t < t2 && N < p.max_samples) {
+        const float tc = t;
+        if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) {
+            if (md.xyzs) {
+                const int64_t q = base + N;
+                md.xyzs[3 * q] = x; md.xyzs[3 * q + 1] = y; md.xyzs[3 * q + 2] = z;
+                md.dirs[3 * q] = d[0]; md.dirs[3 * q + 1] = d[1]; md.dirs[3 * q + 2] = d[2];
+                md.ts[q] = tc;
+                md.deltas[q] = dts;
+            } else {
+                st[N] = tc;
+                sd[N] = dts;
+            }
+            N++;
+        }
+    }
+    return N;
+}
+
 // 8 waves per SIMD (64 VGPRs): every wave of an 8192-ray batch resident at once, no second
 // dispatch round (73 -> 57 us alone; 7 waves at 65 VGPRs measured 58 us and -0.8 % end to end,
 // profiles/r06/march_variants.txt)
@@ -451,7 +502,7 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
                                                                const float* __restrict__ noise, MarchParams p,
                                                                int32_t* __restrict__ counts,
                                                                float* __restrict__ slot_t,
-                                                               float* __restrict__ slot_dt) {
+                                                               float* __restrict__ slot_dt, MarchDirect md) {
     extern __shared__ uint32_t ssum[];
     __shared__ LatSeg segs[4];
     WordCache wc;
@@ -475,6 +526,7 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
         float* sd = slot_dt + r * (int64_t)p.max_samples;
         if (!(0 <= t0) || !(t0 < t2)) {
             if (lane == 0) counts[r] = 0;
+            if (md.xyzs) march_direct_finish(md, r, p.max_samples, 0, lane);
             continue;
         }
         // Conservative early out (exact): points every half 4^3-block along
@@ -505,6 +557,7 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
             }
             if (!near) {
                 if (lane == 0) counts[r] = 0;
+                if (md.xyzs) march_direct_finish(md, r, p.max_samples, 0, lane);
                 continue;
             }
         }
@@ -515,7 +568,9 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (k_end < 0) {  // segment table overflow: the serial walk on lane 0
-            if (lane == 0) counts[r] = march_serial_lane(o, d, dinv, t0, t2, p, wc, st, sd);
+            int Ns = 0;
+            if (lane == 0) counts[r] = Ns = march_serial_lane(o, d, dinv, t0, t2, p, wc, st, sd, md, r);
+            if (md.xyzs) march_direct_finish(md, r, p.max_samples, Ns, lane);
             continue;
         }
         // the window's segment q0 = [Kq, Kn) in registers (re-read when the window passes Kn)
@@ -591,14 +646,25 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
             if ((vis >> lane) & 1ull) {
                 const int rank = __builtin_popcountll(vis & ((1ull << lane) - 1ull));
                 if (rank < room) {
-                    st[N + rank] = tk;
-                    sd[N + rank] = dt;
+                    if (md.xyzs) {  // (direct: the compaction's values, in the ray's slots)
+                        const int64_t q = r * (int64_t)p.max_samples + N + rank;
+                        md.xyzs[3 * q] = o[0] + tk * d[0];
+                        md.xyzs[3 * q + 1] = o[1] + tk * d[1];
+                        md.xyzs[3 * q + 2] = o[2] + tk * d[2];
+                        md.dirs[3 * q] = d[0]; md.dirs[3 * q + 1] = d[1]; md.dirs[3 * q + 2] = d[2];
+                        md.ts[q] = tk;
+                        md.deltas[q] = dt;
+                    } else {
+                        st[N + rank] = tk;
+                        sd[N + rank] = dt;
+                    }
                 }
             }
             N += min(nv, room);
             c = pnt;
         }
         if (lane == 0) counts[r] = N;
+        if (md.xyzs) march_direct_finish(md, r, p.max_samples, N, lane);
     }
     NGP_PROBE_END();
 }
@@ -684,6 +750,14 @@ __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict_
 using namespace ngp;
 
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+// the direct march's counters zeroed in stream order (a kernel node: captured memsets were not
+// reliably ordered before their reader, train.hip zero_words_kernel)
+__global__ void zero3_kernel(unsigned long long* a, unsigned long long* b, unsigned long long* c) {
+    if (threadIdx.x == 0) *a = 0ull;
+    if (threadIdx.x == 1) *b = 0ull;
+    if (threadIdx.x == 2 && c) *c = 0ull;
+}
 
 extern "C" {
 
@@ -851,7 +925,8 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
         const size_t lds = march_summary_lds(p);
         if (march_simple(p))  // one cascade, esf 0: the wave-per-ray lattice walk
             NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<nblk(n_rays, 4), 256, lds, s>>>(
-                                          rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt));
+                                          rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt,
+                                          MarchDirect{}));
         else
             NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false><<<nblk(n_rays, 4 * MARCH_RPW), 256, lds, s>>>(
                                           rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt));
@@ -868,6 +943,36 @@ int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int6
     NGP_CHECK_ARG(rays_o && rays_d && rays_a && slot_t && slot_dt && xyzs && dirs && deltas && ts);
     NGP_TIMED(NGP_K_COMPACT, as_stream(stream), march_compact_kernel<<<nblk(n_rays, 4), 256, 0, as_stream(stream)>>>(rays_o, rays_d, rays_a, n_rays, slot_t,
                                                                         slot_dt, max_samples, xyzs, dirs, deltas, ts));
+    return ngp_launch_status();
+}
+
+int ngp_march_train_direct(const float* rays_o, const float* rays_d, const float* hits_t, int64_t n_rays,
+                           const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
+                           const float* noise, int max_samples, int32_t* counts, float* slot_t, float* slot_dt,
+                           const uint32_t* occ_summary, float* xyzs, float* dirs, float* deltas, float* ts,
+                           int64_t* rays_a, int32_t* rows, int64_t* n_rows, int64_t* total, int64_t* zero,
+                           void* stream) {
+    MarchParams p;
+    int st = march_params(bitfield, cascades, grid_size, scale, exp_step_factor, max_samples, p);
+    if (st) return st;
+    st = march_attach_summary(p, occ_summary);
+    if (st) return st;
+    NGP_CHECK_ARG(march_simple(p));  // the wave-per-ray lattice walk (one cascade, esf 0) only
+    NGP_CHECK_ARG(n_rays >= 0 && n_rays <= 0x7fffffff && n_rows && total && ((uintptr_t)n_rows & 7) == 0 &&
+                  ((uintptr_t)total & 7) == 0 && (!zero || ((uintptr_t)zero & 7) == 0));
+    NGP_CHECK_ARG(n_rays * (int64_t)max_samples < (1ll << 31));  // slot indices are int32 in the index lists
+    hipStream_t s = as_stream(stream);
+    zero3_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(n_rows),
+                                  reinterpret_cast<unsigned long long*>(total),
+                                  reinterpret_cast<unsigned long long*>(zero));
+    if (n_rays > 0) {
+        NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && counts && slot_t && slot_dt && xyzs && dirs && deltas &&
+                      ts && rays_a && rows);
+        const MarchDirect md{xyzs, dirs, ts, deltas, rays_a, rows, reinterpret_cast<unsigned long long*>(n_rows),
+                             reinterpret_cast<unsigned long long*>(total)};
+        NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<nblk(n_rays, 4), 256, march_summary_lds(p), s>>>(
+                                      rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, md));
+    }
     return ngp_launch_status();
 }
 
