@@ -26,7 +26,9 @@ def _train(args):
     process, as in training; the GPU state of one run cannot touch the next)"""
     out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "train_scene.py")] + args,
                          check=True, stdout=subprocess.PIPE, text=True).stdout
-    return json.loads(out.strip().splitlines()[-1])
+    r = json.loads(out.strip().splitlines()[-1])
+    print(f"[quality_30k] {' '.join(args[-3:])}: {json.dumps(r)[:200]}", file=sys.stderr, flush=True)  # (progress)
+    return r
 
 
 def run(steps=30000, res=400, n_train=100, n_test=10, seed=4, root=None):
