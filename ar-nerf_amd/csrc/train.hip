@@ -1554,6 +1554,90 @@ int ngp_density_grid_ema(float* density_grid, uint64_t* grid_key, int64_t n, flo
 
 }  // extern "C"
 
+// NeRFLoss (losses.py:41-82) of the drop-in surface in one launch each way:
+// the per-ray terms {rgb (3), opacity, depth} the reference builds from ~15
+// elementwise torch ops, and their backward, one lane per ray, each op of the
+// reference's expression rounded in fp32 in its order (x.detach() in the rgb
+// denominator carries no gradient; division by the grid scale is torch's
+// multiplication by its reciprocal; clip's gradient is 0 where it clips).
+// loss_type 0 raw, 2 log, 3 tanh (the reference's set).
+__device__ __forceinline__ float nerf_rgb_term(int type, float x, float y, float& dtdx) {
+    if (type == 0) {
+        const float den = x + 1e-3f;
+        dtdx = 1.0f / den;  // (only used as grad / den below)
+        return (x - y) / den;
+    }
+    if (type == 2) {
+        const float a = 0.2935f + x;
+        dtdx = a;
+        return logf(a / (0.2935f + y)) * 0.7607f;
+    }
+    const float tx = tanhf(x);
+    dtdx = tx;
+    return tx - tanhf(y);
+}
+
+__global__ void __launch_bounds__(256) nerf_loss_fw_kernel(const float* __restrict__ rgb, const float* __restrict__ gt,
+                                                           const float* __restrict__ opacity,
+                                                           const float* __restrict__ depth, int64_t n, int type,
+                                                           float lam_op, float neg_lam_depth, float inv_scale,
+                                                           float* __restrict__ l_rgb, float* __restrict__ l_op,
+                                                           float* __restrict__ l_dep) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float dd;
+        const float t = nerf_rgb_term(type, rgb[3 * i + c], gt[3 * i + c], dd);
+        l_rgb[3 * i + c] = t * t;
+    }
+    const float o = opacity[i] + 1e-10f;
+    l_op[i] = lam_op * (-o * logf(o));
+    const float v = fminf(depth[i] * inv_scale + 1e-10f, 1.0f);
+    l_dep[i] = neg_lam_depth * logf(v);
+}
+
+// (g_*: dL/d of each loss term; null = no gradient flows into that term)
+__global__ void __launch_bounds__(256) nerf_loss_bw_kernel(const float* __restrict__ rgb, const float* __restrict__ gt,
+                                                           const float* __restrict__ opacity,
+                                                           const float* __restrict__ depth, int64_t n, int type,
+                                                           float lam_op, float neg_lam_depth, float inv_scale,
+                                                           const float* __restrict__ g_rgb,
+                                                           const float* __restrict__ g_op,
+                                                           const float* __restrict__ g_dep, float* __restrict__ d_rgb,
+                                                           float* __restrict__ d_op, float* __restrict__ d_dep) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float g = 0.f;
+        if (g_rgb) {
+            const float x = rgb[3 * i + c];
+            float dd;
+            const float t = nerf_rgb_term(type, x, gt[3 * i + c], dd);
+            const float gt2 = g_rgb[3 * i + c] * (2.0f * t);  // PowBackward: grad * (2 t)
+            if (type == 0) g = gt2 / (x + 1e-3f);              // DivBackward (the denominator detached)
+            else if (type == 2) g = (gt2 * 0.7607f) / dd;       // MulBackward, LogBackward of (a / b): 1 / a
+            else g = gt2 * (1.0f - dd * dd);                    // TanhBackward
+        }
+        d_rgb[3 * i + c] = g;
+    }
+    float go = 0.f;
+    if (g_op) {
+        const float o = opacity[i] + 1e-10f, lo = logf(o);
+        const float gl = g_op[i] * lam_op;  // MulBackward of lam * f
+        // f = (-o) * log(o): d/d(-o) = gl * log(o) -> d/do = -(gl * log(o)); d/dlog = gl * (-o) -> / o
+        go = -(gl * lo) + (gl * (-o)) / o;
+    }
+    d_op[i] = go;
+    float gd = 0.f;
+    if (g_dep) {
+        const float v = depth[i] * inv_scale + 1e-10f;
+        if (v <= 1.0f) gd = ((g_dep[i] * neg_lam_depth) / fminf(v, 1.0f)) * inv_scale;
+    }
+    d_dep[i] = gd;
+}
+
 // The rows of (dL/dsigma, dL/drgb) with a nonzero entry: the samples that
 // carry gradient (the compositing backward, volumerendering.cu:86-150, leaves
 // every sample past its ray's termination at exact zero, and a zero upstream
@@ -1599,6 +1683,31 @@ __global__ void __launch_bounds__(256) grad_rows_kernel(const float* __restrict_
 }
 
 extern "C" {
+
+int ngp_nerf_loss_fw(const float* rgb, const float* rgb_gt, const float* opacity, const float* depth, int64_t n,
+                     int loss_type, float lambda_opacity, float lambda_depth, float grid_scale, float* loss_rgb,
+                     float* loss_opacity, float* loss_depth, void* stream) {
+    NGP_CHECK_ARG(n >= 0 && (loss_type == 0 || loss_type == 2 || loss_type == 3) && grid_scale > 0.f);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(rgb && rgb_gt && opacity && depth && loss_rgb && loss_opacity && loss_depth);
+    nerf_loss_fw_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(
+        rgb, rgb_gt, opacity, depth, n, loss_type, lambda_opacity, -lambda_depth, 1.0f / grid_scale, loss_rgb,
+        loss_opacity, loss_depth);
+    return ngp_launch_status();
+}
+
+int ngp_nerf_loss_bw(const float* rgb, const float* rgb_gt, const float* opacity, const float* depth, int64_t n,
+                     int loss_type, float lambda_opacity, float lambda_depth, float grid_scale, const float* g_rgb,
+                     const float* g_opacity, const float* g_depth, float* d_rgb, float* d_opacity, float* d_depth,
+                     void* stream) {
+    NGP_CHECK_ARG(n >= 0 && (loss_type == 0 || loss_type == 2 || loss_type == 3) && grid_scale > 0.f);
+    if (n == 0) return NGP_OK;
+    NGP_CHECK_ARG(rgb && rgb_gt && opacity && depth && d_rgb && d_opacity && d_depth);
+    nerf_loss_bw_kernel<<<(unsigned)((n + 255) / 256), 256, 0, as_stream(stream)>>>(
+        rgb, rgb_gt, opacity, depth, n, loss_type, lambda_opacity, -lambda_depth, 1.0f / grid_scale, g_rgb,
+        g_opacity, g_depth, d_rgb, d_opacity, d_depth);
+    return ngp_launch_status();
+}
 
 int ngp_gradient_rows(const float* dL_dsigmas, const float* dL_drgbs, int64_t n, int32_t* idx, int64_t* count,
                       void* stream) {

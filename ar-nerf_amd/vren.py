@@ -77,6 +77,8 @@ def _declare(L):
                                vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_active_samples": [vp, vp, c_int64, vp, vp, vp, vp],
         "ngp_gradient_rows": [vp, vp, c_int64, vp, vp, vp],
+        "ngp_nerf_loss_fw": [vp, vp, vp, vp, c_int64, c_int, c_float, c_float, c_float, vp, vp, vp, vp],
+        "ngp_nerf_loss_bw": [vp, vp, vp, vp, c_int64, c_int, c_float, c_float, c_float, vp, vp, vp, vp, vp, vp, vp],
         "ngp_chunk_counts": [vp, c_int64, c_int, vp, vp, c_float, vp, vp],
         "ngp_chunk_counts_range": [vp, c_int64, c_int, c_int, vp, vp, c_float, vp, vp],
         "ngp_ray_segments": [vp, vp, c_int64, c_int, vp, vp, vp, vp, vp],

@@ -565,6 +565,21 @@ int ngp_composite_loss(const float* sigmas, const float* rgbs, const float* delt
                        int32_t* sample_idx, void* alloc_ws, int64_t* n_active_total, int64_t* stats,
                        void* stream);
 
+/* NeRFLoss (losses.py:41-82) of the drop-in surface: per ray the rgb term
+ * (loss_type 0 raw ((x - y) / (x + 1e-3))^2 with the denominator detached, 2
+ * log, 3 tanh; (n,3)), the opacity term lambda_opacity * (-o log o), o =
+ * opacity + 1e-10, and the depth term -lambda_depth * log(min(depth /
+ * grid_scale + 1e-10, 1)) -- one launch; _bw: their gradients w.r.t. rgb,
+ * opacity and depth from the terms' upstream gradients (each nullable: no
+ * gradient into that term), the derivative of each torch op in order.
+ * Replaces ~15 elementwise torch ops and their autograd nodes. */
+int ngp_nerf_loss_fw(const float* rgb, const float* rgb_gt, const float* opacity, const float* depth, int64_t n,
+                     int loss_type, float lambda_opacity, float lambda_depth, float grid_scale, float* loss_rgb,
+                     float* loss_opacity, float* loss_depth, void* stream);
+int ngp_nerf_loss_bw(const float* rgb, const float* rgb_gt, const float* opacity, const float* depth, int64_t n,
+                     int loss_type, float lambda_opacity, float lambda_depth, float grid_scale, const float* g_rgb,
+                     const float* g_opacity, const float* g_depth, float* d_rgb, float* d_opacity, float* d_depth,
+                     void* stream);
 /* The samples that carry gradient in the drop-in backward: rows i < n with
  * dL_dsigmas[i] != 0 or any dL_drgbs[i][*] != 0 (the compositing backward,
  * volumerendering.cu:86-150, leaves every sample past its ray's termination at

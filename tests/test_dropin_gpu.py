@@ -77,3 +77,36 @@ def test_dropin_loop_trains():
     assert sum(losses[-10:]) < 1.5 * sum(losses[:10])
     assert float((loop.model.params.detach() - p0).abs().max()) > 0
     assert int(res["rm_samples"]) > 0 and int(res["vr_samples"]) > 0
+
+
+@pytest.mark.parametrize("loss_set", ["raw", "log", "tanh"])
+def test_fused_nerf_loss_matches_the_reference_expressions(loss_set):
+    """losses.NeRFLoss on CUDA tensors (one ngp_nerf_loss_fw / _bw launch) against
+    the reference's torch expressions (losses.py:63-76, run here on the same
+    tensors): every term within fp32 rounding of the op-by-op values, and the
+    gradients w.r.t. rgb, opacity and depth through autograd the same, with
+    the depth clip's zero gradient where it clips."""
+    from losses import NeRFLoss
+    g = torch.Generator().manual_seed(3)
+    n = 5000
+    rgb = torch.rand(n, 3, generator=g).to(DEV).requires_grad_(True)
+    gt = torch.rand(n, 3, generator=g).to(DEV)
+    op = (torch.rand(n, generator=g) * 0.999 + 1e-4).to(DEV).requires_grad_(True)
+    dep = (torch.rand(n, generator=g) * 1.2).to(DEV).requires_grad_(True)  # some past the clip at depth / scale = 1
+    L = NeRFLoss(30, loss_set, 1.0, 1e-2, lambda_opacity=1e-3)
+    d = L({"rgb": rgb, "opacity": op, "depth": dep}, {"rgb": gt})
+    loss = sum(v.mean() for v in d.values())
+    gr = torch.autograd.grad(loss, (rgb, op, dep))
+    rr, oo, dd = rgb.detach().clone().requires_grad_(True), op.detach().clone().requires_grad_(True), \
+        dep.detach().clone().requires_grad_(True)
+    ref = {"rgb": L.rgb_loss(rr, gt) ** 2}
+    o = oo + 1e-10
+    ref["opacity"] = L.lambda_opacity * (-o * torch.log(o))
+    ref["depth"] = -L.lambda_depth * torch.log((dd / L.grid_scale + 1e-10).clip(max=1.0))
+    lref = sum(v.mean() for v in ref.values())
+    gref = torch.autograd.grad(lref, (rr, oo, dd))
+    for k in ("rgb", "opacity", "depth"):
+        torch.testing.assert_close(d[k], ref[k], rtol=2e-6, atol=1e-9)
+    for a, b in zip(gr, gref):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=1e-12)
+    assert int((gr[2] == 0).sum()) == int((dep.detach() / 1.0 + 1e-10 > 1.0).sum())
