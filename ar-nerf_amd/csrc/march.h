@@ -142,11 +142,19 @@ __device__ __forceinline__ bool march_step(float& t, const float o[3], const flo
         t += dt;
         return true;
     }
+    // (t past 2^24 steps of dt: t + dt == t, the reference's loop would never end -- only a
+    // degenerate ray (huge t2) gets there; it ends the ray instead and counts a guard hit)
     if constexpr (SIMPLE) {
-        do { t += dt; } while (t < t_target);
+        do {
+            const float tn = t + dt;
+            if (!(tn > t)) { t = INFINITY; ngp_guard_hit(); break; }
+            t = tn;
+        } while (t < t_target);
     } else {
         do {
-            t += calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
+            const float tn = t + calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
+            if (!(tn > t)) { t = INFINITY; ngp_guard_hit(); break; }
+            t = tn;
         } while (t < t_target);
     }
     return false;

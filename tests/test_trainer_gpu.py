@@ -429,7 +429,8 @@ def test_direct_march_matches_the_compacted_march():
     m = tr.msets[0]
     dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
     p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    vren._ok(tr.L.ngp_raygen_aabb(p(dirs), p(poses), p(img.to(DEV)), p(pix.to(DEV)), R, p(tr.center), p(tr.half_size),
+    img_d, pix_d = img.to(DEV), pix.to(DEV)  # (held: the launch reads them after this line)
+    vren._ok(tr.L.ngp_raygen_aabb(p(dirs), p(poses), p(img_d), p(pix_d), R, p(tr.center), p(tr.half_size),
                                   ctypes.c_float(0.01), p(m["rays_o"]), p(m["rays_d"]), p(m["hits_t"]), vren._stream()),
              "raygen")
     m["noise"].copy_(noise.to(DEV))

@@ -464,3 +464,35 @@ def test_rays_nonempty_lists_rows_and_zeroes_empty_counts(n_rows):
     assert int(n_ne) == ref.numel()
     assert torch.equal(rows[:ref.numel()].cpu().long(), ref)
     assert torch.equal(rest.cpu(), torch.where(N > 0, 7, 0).int()) and int(z) == 0
+
+
+@pytest.mark.timeout(60)
+def test_march_ends_a_degenerate_ray_instead_of_spinning():
+    """A ray whose t is so large that t + dt == t in fp32 (camera 4e4 units away:
+    ulp(t) > 2 dt) never advances in the reference's `do t += dt while (t <
+    t_target)` -- an endless loop.  The marcher ends such a ray (counted as a
+    guard hit) and every other ray of the batch is marched as usual."""
+    import vren as V
+    sc, o, d, _, _ = _scene_rays(256, W=64)
+    o = o.clone()
+    o[0] = torch.tensor([4.0e4, 0.0, 0.0])
+    d = d.clone()
+    d[0] = torch.tensor([-1.0, 0.0, 0.0])
+    ht = _hits(o, d, 0.5)
+    noise = torch.rand(256, generator=torch.Generator().manual_seed(2))
+    # one occupied cell, at the centre: the far ray passes within a block of it (no early out),
+    # and its first probe at the box's face is empty -- the jump that never advances
+    bf = torch.zeros(128 ** 3 // 8, dtype=torch.uint8)
+    c = int(vren.morton3D(torch.tensor([[64, 64, 64]], dtype=torch.int32, device=DEV))[0])
+    bf[c // 8] = 1 << (c % 8)
+    L = V.lib()
+    assert L.ngp_guard_reset() == 0
+    try:
+        out = vren.raymarching_train(o.to(DEV), d.to(DEV), ht.to(DEV), bf.to(DEV), 1, 0.5, 0.0,
+                                     noise.to(DEV), 128, 1024)
+        torch.cuda.synchronize()
+        assert int(out[0][0, 2]) == 0 and int(L.ngp_guard_hits()) >= 1
+        ref = O.raymarching_train(o[1:], d[1:], ht[1:], bf, 1, 0.5, 0.0, noise[1:], 128, 1024)
+        assert torch.equal(out[0][1:, 2].cpu(), ref[0][:, 2])
+    finally:
+        assert L.ngp_guard_reset() == 0
