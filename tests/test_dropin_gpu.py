@@ -93,7 +93,7 @@ def test_fused_nerf_loss_matches_the_reference_expressions(loss_set):
     gt = torch.rand(n, 3, generator=g).to(DEV)
     op = (torch.rand(n, generator=g) * 0.999 + 1e-4).to(DEV).requires_grad_(True)
     dep = (torch.rand(n, generator=g) * 1.2).to(DEV).requires_grad_(True)  # some past the clip at depth / scale = 1
-    L = NeRFLoss(30, loss_set, 1.0, 1e-2, lambda_opacity=1e-3)
+    L = NeRFLoss(30, loss_set, 1.0, 1e-2, lambda_opacity=1e-3, lambda_distortion=0.0)
     d = L({"rgb": rgb, "opacity": op, "depth": dep}, {"rgb": gt})
     loss = sum(v.mean() for v in d.values())
     gr = torch.autograd.grad(loss, (rgb, op, dep))
