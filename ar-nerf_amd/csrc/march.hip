@@ -399,10 +399,7 @@ __global__ void __launch_bounds__(256) march_slots_kernel(const float* __restric
 // overflows: dt below half an ulp of t, or more than LSEG binades -- never on
 // the object scenes; kept out of line so its registers do not count against
 // the lattice loop's).
-struct MarchDirect;
-__device__ __forceinline__ int march_serial_lane(const float o[3], const float d[3], const float dinv[3], float t,
-                                              float t2, const MarchParams& p, WordCache& wc, float* st, float* sd,
-                                              const MarchDirect& md, int64_t r);
+
 
 // first j > k with t_j >= T, for lane point k with value tk: inside the
 // window's segment [Kq, Kn) (value Tq, increment Iq, its reciprocal invIq, in
@@ -436,14 +433,16 @@ __device__ __forceinline__ int lat_jump_seg(int k, float tk, float T, float dt, 
     return min(j, k_end);
 }
 
-// Direct training layout (ngp_march_train_direct; xyzs == nullptr: the slot
-// mode of ngp_march_train_slots): ray r's samples are written straight to
-// slots [r * max_samples, r * max_samples + N_r) of xyzs / dirs / ts /
-// deltas (the compaction's expressions: xyz = o + t d, no contraction --
-// bit-identical values), rays_a[r] = (r, r * max_samples, N_r), a ray with
-// samples appends r to rows (rows in completion order) and adds N_r to
-// *total.  The training step reads samples only through rays_a and index
-// lists, so the slot layout needs no scan and no compaction pass.
+// Packed training layout (ngp_march_train_direct; xyzs == nullptr: the slot
+// mode of ngp_march_train_slots + its scan and compaction): once a ray's walk
+// is done, its wave reserves the ray's range of the packed arrays with one
+// atomic on *total and copies its slots there itself -- xyzs / dirs / ts /
+// deltas with the compaction's expressions (xyz = o + t d, no contraction:
+// bit-identical values) -- then rays_a[r] = (r, start_r, N_r), and a ray with
+// samples appends r to rows.  Rays land in completion order, each ray's
+// samples contiguous and in order: readers that take samples through rays_a
+// and index lists see the same batch, with no scan, compaction or row-list
+// launch behind the march.
 struct MarchDirect {
     float* xyzs;
     float* dirs;
@@ -454,41 +453,41 @@ struct MarchDirect {
     unsigned long long* n_rows;
     unsigned long long* total;
 };
-__device__ __forceinline__ void march_direct_finish(const MarchDirect& md, int64_t r, int max_samples, int N,
-                                                    int lane) {
+__device__ __forceinline__ void march_direct_finish(const MarchDirect& md, int64_t r, int N, const float o[3],
+                                                    const float d[3], const float* st, const float* sd, int lane) {
+    unsigned long long base = 0;
+    if (lane == 0 && N > 0) {
+        base = atomicAdd(md.total, (unsigned long long)N);
+        md.rows[atomicAdd(md.n_rows, 1ull)] = (int32_t)r;
+    }
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    const int64_t start = (int64_t)(((unsigned long long)hi << 32) | lo);
     if (lane == 0) {
         md.rays_a[3 * r] = r;
-        md.rays_a[3 * r + 1] = r * (int64_t)max_samples;
+        md.rays_a[3 * r + 1] = start;
         md.rays_a[3 * r + 2] = N;
-        if (N > 0) {
-            md.rows[atomicAdd(md.n_rows, 1ull)] = (int32_t)r;
-            atomicAdd(md.total, (unsigned long long)N);
-        }
+    }
+    // the slots were stored by this wave's lanes: wavefront-scope ordering before the reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int k = lane; k < N; k += 64) {
+        const float t = st[k];
+        const int64_t q = start + k;
+        md.xyzs[3 * q] = o[0] + t * d[0]; md.xyzs[3 * q + 1] = o[1] + t * d[1]; md.xyzs[3 * q + 2] = o[2] + t * d[2];
+        md.dirs[3 * q] = d[0]; md.dirs[3 * q + 1] = d[1]; md.dirs[3 * q + 2] = d[2];
+        md.ts[q] = t;
+        md.deltas[q] = sd[k];
     }
 }
 
-// (lane 0: the ray's samples into its slot_t / slot_dt range, or, direct, its xyzs / dirs / ts / deltas slots)
+// (lane 0: the ray's samples into its slot_t / slot_dt range)
 __device__ __forceinline__ int march_serial_lane(const float o[3], const float d[3], const float dinv[3], float t,
-                                              float t2, const MarchParams& p, WordCache& wc, float* st, float* sd,
-                                              const MarchDirect& md, int64_t r) {
+                                              float t2, const MarchParams& p, WordCache& wc, float* st, float* sd) {
     float x, y, z, dts;
     int N = 0;
-    const int64_t base = r * (int64_t)p.max_samples;
     while (0 <= t && t < t2 && N < p.max_samples) {
         const float tc = t;
-        if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) {
-            if (md.xyzs) {
-                const int64_t q = base + N;
-                md.xyzs[3 * q] = x; md.xyzs[3 * q + 1] = y; md.xyzs[3 * q + 2] = z;
-                md.dirs[3 * q] = d[0]; md.dirs[3 * q + 1] = d[1]; md.dirs[3 * q + 2] = d[2];
-                md.ts[q] = tc;
-                md.deltas[q] = dts;
-            } else {
-                st[N] = tc;
-                sd[N] = dts;
-            }
-            N++;
-        }
+        if (march_step<true>(t, o, d, dinv, p, x, y, z, dts, wc)) { st[N] = tc; sd[N] = dts; N++; }
     }
     return N;
 }
@@ -526,7 +525,7 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
         float* sd = slot_dt + r * (int64_t)p.max_samples;
         if (!(0 <= t0) || !(t0 < t2)) {
             if (lane == 0) counts[r] = 0;
-            if (md.xyzs) march_direct_finish(md, r, p.max_samples, 0, lane);
+            if (md.xyzs) march_direct_finish(md, r, 0, o, d, st, sd, lane);
             continue;
         }
         // Conservative early out (exact): points every half 4^3-block along
@@ -557,7 +556,7 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
             }
             if (!near) {
                 if (lane == 0) counts[r] = 0;
-                if (md.xyzs) march_direct_finish(md, r, p.max_samples, 0, lane);
+                if (md.xyzs) march_direct_finish(md, r, 0, o, d, st, sd, lane);
                 continue;
             }
         }
@@ -569,8 +568,8 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (k_end < 0) {  // segment table overflow: the serial walk on lane 0
             int Ns = 0;
-            if (lane == 0) counts[r] = Ns = march_serial_lane(o, d, dinv, t0, t2, p, wc, st, sd, md, r);
-            if (md.xyzs) march_direct_finish(md, r, p.max_samples, Ns, lane);
+            if (lane == 0) counts[r] = Ns = march_serial_lane(o, d, dinv, t0, t2, p, wc, st, sd);
+            if (md.xyzs) march_direct_finish(md, r, __builtin_amdgcn_readfirstlane(Ns), o, d, st, sd, lane);
             continue;
         }
         // the window's segment q0 = [Kq, Kn) in registers (re-read when the window passes Kn)
@@ -646,25 +645,15 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
             if ((vis >> lane) & 1ull) {
                 const int rank = __builtin_popcountll(vis & ((1ull << lane) - 1ull));
                 if (rank < room) {
-                    if (md.xyzs) {  // (direct: the compaction's values, in the ray's slots)
-                        const int64_t q = r * (int64_t)p.max_samples + N + rank;
-                        md.xyzs[3 * q] = o[0] + tk * d[0];
-                        md.xyzs[3 * q + 1] = o[1] + tk * d[1];
-                        md.xyzs[3 * q + 2] = o[2] + tk * d[2];
-                        md.dirs[3 * q] = d[0]; md.dirs[3 * q + 1] = d[1]; md.dirs[3 * q + 2] = d[2];
-                        md.ts[q] = tk;
-                        md.deltas[q] = dt;
-                    } else {
-                        st[N + rank] = tk;
-                        sd[N + rank] = dt;
-                    }
+                    st[N + rank] = tk;
+                    sd[N + rank] = dt;
                 }
             }
             N += min(nv, room);
             c = pnt;
         }
         if (lane == 0) counts[r] = N;
-        if (md.xyzs) march_direct_finish(md, r, p.max_samples, N, lane);
+        if (md.xyzs) march_direct_finish(md, r, N, o, d, st, sd, lane);
     }
     NGP_PROBE_END();
 }

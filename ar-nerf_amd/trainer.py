@@ -235,8 +235,8 @@ class NGPTrainer:
         # only levels 8-15 (pre_coarse = False, tests: off)
         self.pre_coarse = True
         self.pre_levels = 8  # (the kernel's PRE_LEVELS: levels 0-7, final once the side stream's Adam has run)
-        # the row forward's batches in the slot layout (ngp_march_train_direct: the march writes each
-        # ray's samples at r * max_samples + k; no scan, compaction or row-list launch)
+        # the row forward's batches from ngp_march_train_direct (each ray's wave packs its own samples
+        # at a range reserved by one atomic; no scan, compaction or row-list launch)
         self.direct_march = True
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -331,7 +331,8 @@ class NGPTrainer:
                     rows_ne=torch.empty(R, dtype=torch.int32, device=dev),
                     n_rows_ne=torch.zeros(1, dtype=torch.int64, device=dev),
                     eval_total2=torch.zeros(1, dtype=torch.int64, device=dev),
-                    # dense (compacted) sample layout; False: the slot layout of ngp_march_train_direct
+                    # ray-ordered dense layout (rays_a starts ascending); False: ngp_march_train_direct's
+                    # packed completion order (each ray contiguous)
                     dense=True,
                     # round 1's coarse levels 0-7 already in self.enc for this set's first chunks
                     # (ngp_field_encode_first_coarse, run by the previous step beside its accumulation)
@@ -503,8 +504,9 @@ class NGPTrainer:
             # density_bitfield (update_density_grid, tests, tools) stays valid
             vren.bitfield_summary(self.density_bitfield, self.G, out=m["occ_summary"])
             if self._direct_layout():
-                # the slot layout: samples written by the march itself at r * max_samples + k, rays_a
-                # and the non-empty rows from the same launch (no scan / compaction / row-list pass)
+                # the packed layout from the march launch itself: each ray's wave reserves its range and
+                # copies its slots there, rays_a and the non-empty rows from the same launch (no scan /
+                # compaction / row-list pass; rays in completion order, each ray contiguous)
                 m["dense"], m["eval1_K"] = False, 0
                 vren._ok(L.ngp_march_train_direct(
                     _p(m["rays_o"]), _p(m["rays_d"]), _p(m["hits_t"]), R, _p(self.density_bitfield), self.cascades,
@@ -542,9 +544,10 @@ class NGPTrainer:
                 self._ev("march_side", 1, stream)
 
     def _direct_layout(self):
-        """Batches marched in the slot layout (ngp_march_train_direct): the row forward's step on
-        single-cascade scenes (esf 0), which reads its samples only through rays_a and index
-        lists; the dense compacted layout otherwise (direct_march = False keeps it always)."""
+        """Batches marched by ngp_march_train_direct (the packed layout in completion order, from the
+        march launch alone): the row forward's step on single-cascade scenes (esf 0), which reads its
+        samples only through rays_a and index lists; the ray-ordered compaction otherwise
+        (direct_march = False keeps it always)."""
         return (self.direct_march and self.cascades == 1 and self.esf == 0 and self.row_forward == 1
                 and self._rows_fwd(self.chunk_first))
 
@@ -1056,9 +1059,6 @@ class NGPTrainer:
                      "chunk_segments")
             self._field_indexed(s)
         else:  # encode + MLPs in one launch over every marched sample
-            if not self.msets[self.cur]["dense"]:
-                raise RuntimeError("chunk_first = 0 needs the dense sample layout: this batch was marched in the slot "
-                                   "layout (set chunk_first / row_forward before the batch is marched)")
             self._ev("hash_encode", 0)
             vren._ok(HGL.ngp_field_encode_mlp(_p(self.xyzs), _p(self.dirs), self.cap, _p(self.n_samples), None,
                                               HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),

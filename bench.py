@@ -142,8 +142,9 @@ def parse():
     ap.add_argument("--dropin-steps", type=int, default=50,
                     help="timed steps of the reference's loop on the drop-in surface (DropinLoop; 0: skip)")
     ap.add_argument("--dense-march", action="store_true",
-                    help="march into the dense compacted layout (march + scan + compaction + row list) instead of "
-                         "the slot layout (ngp_march_train_direct, the default on single-cascade scenes)")
+                    help="march with the separate scan + compaction + row-list launches (ray-ordered layout) instead "
+                         "of ngp_march_train_direct (the march packs its own samples; the default on single-cascade "
+                         "scenes)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="world > 1 process group (nccl = RCCL; gloo only to rehearse the path with ranks sharing a GPU)")
     return ap.parse_args()
@@ -702,7 +703,7 @@ def main():
                        "chunk_first": trainer.chunk_first,
                        "row_forward": trainer.row_forward if trainer._rows_fwd(trainer.chunk_first) else 0,
                        "march_fork": trainer.march_fork_point(),
-                       "march_layout": "slot" if trainer._direct_layout() else "dense",
+                       "march_layout": "packed (march_train_direct)" if trainer._direct_layout() else "ray-ordered",
                        "parallelism": f"dp{world}" + (f" (data-parallel step of world {args.emulate_dp} emulated: collectives as local copies)" if args.emulate_dp else ""), "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
                        "bin_merge_hi": trainer.bin_merge_hi,

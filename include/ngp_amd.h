@@ -174,18 +174,19 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
 int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int64_t* rays_a,
                             int64_t n_rays, const float* slot_t, const float* slot_dt, int max_samples,
                             float* xyzs, float* dirs, float* deltas, float* ts, void* stream);
-/* The training step's march in the slot layout (raymarching.cu:166-332 as
- * ngp_march_train_slots; one cascade, exp_step_factor 0 -- the wave-per-ray
- * lattice walk -- only): ray r's samples written straight to rows
- * [r * max_samples, r * max_samples + N_r) of xyzs (n_rays*max_samples,3) /
- * dirs / deltas / ts, with the values ngp_march_train_compact would write
- * there (bit-identical); rays_a[r] = (r, r * max_samples, N_r); counts[r] =
- * N_r; the rays with N_r > 0 appended to rows[0..*n_rows) (completion
- * order); *total = sum N_r; *zero (nullable) = 0.  n_rows / total / zero
- * 8-byte aligned, zeroed by the call (a kernel node: graph-capturable).
- * slot_t / slot_dt: scratch for the rare serial fallback (as
- * ngp_march_train_slots).  No scan and no compaction pass: readers that
- * take samples through rays_a / index lists see the same batch. */
+/* The training step's march with its compaction inside (raymarching.cu:166-332
+ * as ngp_march_train_slots; one cascade, exp_step_factor 0 -- the
+ * wave-per-ray lattice walk -- only): each ray's wave walks into its
+ * slot_t / slot_dt range, then reserves the ray's range of the packed
+ * xyzs / dirs / deltas / ts (capacity n_rays*max_samples) with one atomic on
+ * *total and writes its samples there with the values
+ * ngp_march_train_compact would write (bit-identical); rays_a[r] = (r,
+ * start_r, N_r) -- rays in completion order, each ray's samples contiguous
+ * and in order; counts[r] = N_r; the rays with N_r > 0 appended to
+ * rows[0..*n_rows); *total = sum N_r; *zero (nullable) = 0.  n_rows / total /
+ * zero 8-byte aligned, zeroed by the call (a kernel node: graph-capturable).
+ * No scan, compaction or row-list launch: readers that take samples through
+ * rays_a / index lists see the same batch. */
 int ngp_march_train_direct(const float* rays_o, const float* rays_d, const float* hits_t, int64_t n_rays,
                            const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
                            const float* noise, int max_samples, int32_t* counts, float* slot_t, float* slot_dt,

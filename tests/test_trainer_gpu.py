@@ -61,9 +61,12 @@ def test_training_step_matches_oracle():
     ra, ra_ref = tr.rays_a.cpu(), ot.last["rays_a"]
     if tr.msets[tr.cur]["dense"]:
         assert torch.equal(ra, ra_ref)
-    else:  # the slot layout (ngp_march_train_direct): ray r's samples start at r * max_samples
+    else:  # ngp_march_train_direct's packed layout: rays in completion order, each contiguous
         assert torch.equal(ra[:, [0, 2]], ra_ref[:, [0, 2]])
-        assert torch.equal(ra[:, 1], torch.arange(R, dtype=torch.int64) * tr.max_samples)
+        ne = ra[:, 2] > 0
+        st = ra[ne, 1]
+        o = torch.argsort(st)
+        assert torch.equal(st[o][1:], (st[o] + ra[ne, 2][o])[:-1]) and int(st.min()) == 0  # a partition of [0, N)
     l_gpu = float(loss.sum())
     assert abs(l_gpu - l_ref) <= 2e-3 * abs(l_ref)
     torch.testing.assert_close(tr.out_rgb.cpu(), ot.last["rgb"], atol=1e-3, rtol=0)
@@ -417,11 +420,12 @@ def test_preencode_only_when_levels_0_7_are_stepped_before_it():
 
 
 def test_direct_march_matches_the_compacted_march():
-    """ngp_march_train_direct (the training step's slot layout: ray r's samples
-    written by the march at r * max_samples + k) against the API march
-    (vren.raymarching_train: ngp_march_train_slots + the compaction) on the same
-    rays: per ray the same count and bit-identical xyz / dir / t / dt, rays_a
-    (r, r * max_samples, N_r), the non-empty rows listed once each, the total."""
+    """ngp_march_train_direct (the training step's march: each ray's wave packs
+    its own samples at a range reserved by one atomic) against the API march
+    (vren.raymarching_train: ngp_march_train_slots + the scan + the compaction)
+    on the same rays: per ray the same count and bit-identical xyz / dir / t /
+    dt, the ranges a partition of [0, total), the non-empty rows listed once
+    each."""
     import ctypes
     import vren
     sc, tr, img, pix, noise = _setup(R=4096)
@@ -447,15 +451,16 @@ def test_direct_march_matches_the_compacted_march():
     ra_ref, xyz_ref, dir_ref, dl_ref, t_ref = [x.cpu() for x in ref[:5]]
     ra = m["rays_a"].cpu()
     assert torch.equal(ra[:, 0], ra_ref[:, 0]) and torch.equal(ra[:, 2], ra_ref[:, 2])
-    assert torch.equal(ra[:, 1], torch.arange(R, dtype=torch.int64) * M)
-    assert int(m["n_samples"]) == int(ref[5][0]) and int(m["eval_total2"]) == 0
-    # the slots of every ray, gathered in ray order, are the compacted arrays
+    total = int(m["n_samples"])
+    assert total == int(ref[5][0]) and int(m["eval_total2"]) == 0
     cnt = ra[:, 2]
+    # each ray's range, gathered in ray order, is the ray-ordered compaction
     idx = torch.repeat_interleave(ra[:, 1], cnt) + (torch.arange(int(cnt.sum())) -
                                                       torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt))
+    assert torch.equal(torch.sort(idx)[0], torch.arange(total))  # the ranges partition [0, total)
     for a, b in ((m["xyzs"], xyz_ref), (m["dirs"], dir_ref), (m["deltas"], dl_ref), (m["ts"], t_ref)):
         assert torch.equal(a.cpu()[idx], b)
     nr = int(m["n_rows_ne"])
     rows = torch.sort(m["rows_ne"][:nr].cpu().long())[0]
     assert torch.equal(rows, torch.nonzero(cnt > 0)[:, 0])
-    print(f"direct march: {nr} non-empty rows of {R}, {int(cnt.sum())} samples, slots bit-identical")
+    print(f"direct march: {nr} non-empty rows of {R}, {total} samples packed, bit-identical to the compaction")
