@@ -132,7 +132,9 @@ def test_prefetched_march_matches_inline():
     assert p0 == 0 and p1 >= 15
     upd = 16 - 1  # global_step starts at 1: step index 15 runs the occupancy update
     assert c0[:upd] == c1[:upd]
-    assert all(torch.equal(x, y) for x, y in zip(a0[:upd], a1[:upd]))
+    # (the rays' counts; their start offsets are the packing order of ngp_march_train_direct, which
+    # follows the march's completion order)
+    assert all(torch.equal(x[:, [0, 2]], y[:, [0, 2]]) for x, y in zip(a0[:upd], a1[:upd]))
     for x, y in zip(l0, l1):
         assert abs(x - y) <= 2e-2 * abs(x)
 
