@@ -433,53 +433,6 @@ __device__ __forceinline__ int lat_jump_seg(int k, float tk, float T, float dt, 
     return min(j, k_end);
 }
 
-// Packed training layout (ngp_march_train_direct; xyzs == nullptr: the slot
-// mode of ngp_march_train_slots + its scan and compaction): once a ray's walk
-// is done, its wave reserves the ray's range of the packed arrays with one
-// atomic on *total and copies its slots there itself -- xyzs / dirs / ts /
-// deltas with the compaction's expressions (xyz = o + t d, no contraction:
-// bit-identical values) -- then rays_a[r] = (r, start_r, N_r), and a ray with
-// samples appends r to rows.  Rays land in completion order, each ray's
-// samples contiguous and in order: readers that take samples through rays_a
-// and index lists see the same batch, with no scan, compaction or row-list
-// launch behind the march.
-struct MarchDirect {
-    float* xyzs;
-    float* dirs;
-    float* ts;
-    float* deltas;
-    int64_t* rays_a;
-    int32_t* rows;
-    unsigned long long* n_rows;
-    unsigned long long* total;
-};
-__device__ __forceinline__ void march_direct_finish(const MarchDirect& md, int64_t r, int N, const float o[3],
-                                                    const float d[3], const float* st, const float* sd, int lane) {
-    unsigned long long base = 0;
-    if (lane == 0 && N > 0) {
-        base = atomicAdd(md.total, (unsigned long long)N);
-        md.rows[atomicAdd(md.n_rows, 1ull)] = (int32_t)r;
-    }
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base), hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-    const int64_t start = (int64_t)(((unsigned long long)hi << 32) | lo);
-    if (lane == 0) {
-        md.rays_a[3 * r] = r;
-        md.rays_a[3 * r + 1] = start;
-        md.rays_a[3 * r + 2] = N;
-    }
-    // the slots were stored by this wave's lanes: wavefront-scope ordering before the reads
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int k = lane; k < N; k += 64) {
-        const float t = st[k];
-        const int64_t q = start + k;
-        md.xyzs[3 * q] = o[0] + t * d[0]; md.xyzs[3 * q + 1] = o[1] + t * d[1]; md.xyzs[3 * q + 2] = o[2] + t * d[2];
-        md.dirs[3 * q] = d[0]; md.dirs[3 * q + 1] = d[1]; md.dirs[3 * q + 2] = d[2];
-        md.ts[q] = t;
-        md.deltas[q] = sd[k];
-    }
-}
-
 // (lane 0: the ray's samples into its slot_t / slot_dt range)
 __device__ __forceinline__ int march_serial_lane(const float o[3], const float d[3], const float dinv[3], float t,
                                               float t2, const MarchParams& p, WordCache& wc, float* st, float* sd) {
@@ -501,7 +454,7 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
                                                                const float* __restrict__ noise, MarchParams p,
                                                                int32_t* __restrict__ counts,
                                                                float* __restrict__ slot_t,
-                                                               float* __restrict__ slot_dt, MarchDirect md) {
+                                                               float* __restrict__ slot_dt) {
     extern __shared__ uint32_t ssum[];
     __shared__ LatSeg segs[4];
     WordCache wc;
@@ -525,7 +478,6 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
         float* sd = slot_dt + r * (int64_t)p.max_samples;
         if (!(0 <= t0) || !(t0 < t2)) {
             if (lane == 0) counts[r] = 0;
-            if (md.xyzs) march_direct_finish(md, r, 0, o, d, st, sd, lane);
             continue;
         }
         // Conservative early out (exact): points every half 4^3-block along
@@ -556,8 +508,7 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
             }
             if (!near) {
                 if (lane == 0) counts[r] = 0;
-                if (md.xyzs) march_direct_finish(md, r, 0, o, d, st, sd, lane);
-                continue;
+                    continue;
             }
         }
         LatSeg& sg = segs[w];
@@ -567,9 +518,7 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (k_end < 0) {  // segment table overflow: the serial walk on lane 0
-            int Ns = 0;
-            if (lane == 0) counts[r] = Ns = march_serial_lane(o, d, dinv, t0, t2, p, wc, st, sd);
-            if (md.xyzs) march_direct_finish(md, r, __builtin_amdgcn_readfirstlane(Ns), o, d, st, sd, lane);
+            if (lane == 0) counts[r] = march_serial_lane(o, d, dinv, t0, t2, p, wc, st, sd);
             continue;
         }
         // the window's segment q0 = [Kq, Kn) in registers (re-read when the window passes Kn)
@@ -653,7 +602,6 @@ __global__ void __launch_bounds__(256, 8) march_slots_wave_kernel(const float* _
             c = pnt;
         }
         if (lane == 0) counts[r] = N;
-        if (md.xyzs) march_direct_finish(md, r, N, o, d, st, sd, lane);
     }
     NGP_PROBE_END();
 }
@@ -739,14 +687,6 @@ __global__ void __launch_bounds__(64) march_test_kernel(const float* __restrict_
 using namespace ngp;
 
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
-
-// the direct march's counters zeroed in stream order (a kernel node: captured memsets were not
-// reliably ordered before their reader, train.hip zero_words_kernel)
-__global__ void zero3_kernel(unsigned long long* a, unsigned long long* b, unsigned long long* c) {
-    if (threadIdx.x == 0) *a = 0ull;
-    if (threadIdx.x == 1) *b = 0ull;
-    if (threadIdx.x == 2 && c) *c = 0ull;
-}
 
 extern "C" {
 
@@ -914,8 +854,7 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
         const size_t lds = march_summary_lds(p);
         if (march_simple(p))  // one cascade, esf 0: the wave-per-ray lattice walk
             NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<nblk(n_rays, 4), 256, lds, s>>>(
-                                          rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt,
-                                          MarchDirect{}));
+                                          rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt));
         else
             NGP_TIMED(NGP_K_MARCH, s, march_slots_kernel<false><<<nblk(n_rays, 4 * MARCH_RPW), 256, lds, s>>>(
                                           rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt));
@@ -932,36 +871,6 @@ int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int6
     NGP_CHECK_ARG(rays_o && rays_d && rays_a && slot_t && slot_dt && xyzs && dirs && deltas && ts);
     NGP_TIMED(NGP_K_COMPACT, as_stream(stream), march_compact_kernel<<<nblk(n_rays, 4), 256, 0, as_stream(stream)>>>(rays_o, rays_d, rays_a, n_rays, slot_t,
                                                                         slot_dt, max_samples, xyzs, dirs, deltas, ts));
-    return ngp_launch_status();
-}
-
-int ngp_march_train_direct(const float* rays_o, const float* rays_d, const float* hits_t, int64_t n_rays,
-                           const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
-                           const float* noise, int max_samples, int32_t* counts, float* slot_t, float* slot_dt,
-                           const uint32_t* occ_summary, float* xyzs, float* dirs, float* deltas, float* ts,
-                           int64_t* rays_a, int32_t* rows, int64_t* n_rows, int64_t* total, int64_t* zero,
-                           void* stream) {
-    MarchParams p;
-    int st = march_params(bitfield, cascades, grid_size, scale, exp_step_factor, max_samples, p);
-    if (st) return st;
-    st = march_attach_summary(p, occ_summary);
-    if (st) return st;
-    NGP_CHECK_ARG(march_simple(p));  // the wave-per-ray lattice walk (one cascade, esf 0) only
-    NGP_CHECK_ARG(n_rays >= 0 && n_rays <= 0x7fffffff && n_rows && total && ((uintptr_t)n_rows & 7) == 0 &&
-                  ((uintptr_t)total & 7) == 0 && (!zero || ((uintptr_t)zero & 7) == 0));
-    NGP_CHECK_ARG(n_rays * (int64_t)max_samples < (1ll << 31));  // slot indices are int32 in the index lists
-    hipStream_t s = as_stream(stream);
-    zero3_kernel<<<1, 64, 0, s>>>(reinterpret_cast<unsigned long long*>(n_rows),
-                                  reinterpret_cast<unsigned long long*>(total),
-                                  reinterpret_cast<unsigned long long*>(zero));
-    if (n_rays > 0) {
-        NGP_CHECK_ARG(rays_o && rays_d && hits_t && noise && counts && slot_t && slot_dt && xyzs && dirs && deltas &&
-                      ts && rays_a && rows);
-        const MarchDirect md{xyzs, dirs, ts, deltas, rays_a, rows, reinterpret_cast<unsigned long long*>(n_rows),
-                             reinterpret_cast<unsigned long long*>(total)};
-        NGP_TIMED(NGP_K_MARCH, s, march_slots_wave_kernel<<<nblk(n_rays, 4), 256, march_summary_lds(p), s>>>(
-                                      rays_o, rays_d, hits_t, n_rays, noise, p, counts, slot_t, slot_dt, md));
-    }
     return ngp_launch_status();
 }
 

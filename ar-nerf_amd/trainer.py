@@ -235,9 +235,6 @@ class NGPTrainer:
         # only levels 8-15 (pre_coarse = False, tests: off)
         self.pre_coarse = True
         self.pre_levels = 8  # (the kernel's PRE_LEVELS: levels 0-7, final once the side stream's Adam has run)
-        # the row forward's batches from ngp_march_train_direct (each ray's wave packs its own samples
-        # at a range reserved by one atomic; no scan, compaction or row-list launch)
-        self.direct_march = True
         assert self.march_at in ("start", "r1", "fwd", "mlp")
         self.eval_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.eval_idx = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -331,9 +328,6 @@ class NGPTrainer:
                     rows_ne=torch.empty(R, dtype=torch.int32, device=dev),
                     n_rows_ne=torch.zeros(1, dtype=torch.int64, device=dev),
                     eval_total2=torch.zeros(1, dtype=torch.int64, device=dev),
-                    # ray-ordered dense layout (rays_a starts ascending); False: ngp_march_train_direct's
-                    # packed completion order (each ray contiguous)
-                    dense=True,
                     # round 1's coarse levels 0-7 already in self.enc for this set's first chunks
                     # (ngp_field_encode_first_coarse, run by the previous step beside its accumulation)
                     pre_ready=False)
@@ -503,21 +497,6 @@ class NGPTrainer:
             # the bitfield's block summary, rebuilt per march: any writer of
             # density_bitfield (update_density_grid, tests, tools) stays valid
             vren.bitfield_summary(self.density_bitfield, self.G, out=m["occ_summary"])
-            if self._direct_layout():
-                # the packed layout from the march launch itself: each ray's wave reserves its range and
-                # copies its slots there, rays_a and the non-empty rows from the same launch (no scan /
-                # compaction / row-list pass; rays in completion order, each ray contiguous)
-                m["dense"], m["eval1_K"] = False, 0
-                vren._ok(L.ngp_march_train_direct(
-                    _p(m["rays_o"]), _p(m["rays_d"]), _p(m["hits_t"]), R, _p(self.density_bitfield), self.cascades,
-                    self.G, ctypes_float(self.scale), ctypes_float(self.esf), _p(m["noise"]), self.max_samples,
-                    _p(m["counts"]), _p(m["slot_t"]), _p(m["slot_dt"]), _p(m["occ_summary"]), _p(m["xyzs"]),
-                    _p(m["dirs"]), _p(m["deltas"]), _p(m["ts"]), _p(m["rays_a"]), _p(m["rows_ne"]),
-                    _p(m["n_rows_ne"]), _p(m["n_samples"]), _p(m["eval_total2"]), s), "march_train_direct")
-                if side:
-                    self._ev("march_side", 1, stream)
-                return
-            m["dense"] = True
             vren._ok(L.ngp_march_train_slots(_p(m["rays_o"]), _p(m["rays_d"]), _p(m["hits_t"]), R,
                                              _p(self.density_bitfield), self.cascades, self.G,
                                              ctypes_float(self.scale), ctypes_float(self.esf), _p(m["noise"]),
@@ -542,14 +521,6 @@ class NGPTrainer:
                                              _p(m["eval_total2"]), s), "rays_nonempty")
             if side:
                 self._ev("march_side", 1, stream)
-
-    def _direct_layout(self):
-        """Batches marched by ngp_march_train_direct (the packed layout in completion order, from the
-        march launch alone): the row forward's step on single-cascade scenes (esf 0), which reads its
-        samples only through rays_a and index lists; the ray-ordered compaction otherwise
-        (direct_march = False keeps it always)."""
-        return (self.direct_march and self.cascades == 1 and self.esf == 0 and self.row_forward == 1
-                and self._rows_fwd(self.chunk_first))
 
     def _rows_fwd(self, K):
         """The row forward runs the chunked evaluation (its first chunk is one

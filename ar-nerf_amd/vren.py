@@ -65,8 +65,6 @@ def _declare(L):
                                   vp, vp, vp],
         "ngp_bitfield_summary": [vp, c_int64, c_int, vp, vp],
         "ngp_march_train_compact": [vp, vp, vp, c_int64, vp, vp, c_int, vp, vp, vp, vp, vp],
-        "ngp_march_train_direct": [vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, vp, c_int, vp, vp, vp, vp,
-                                   vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
         "ngp_march_test": [vp, vp, vp, vp, c_int64, vp, c_int, c_int, c_float, c_float, c_int, c_int, vp, vp, vp, vp,
                            vp, vp, vp],
         "ngp_composite_train_fw": [vp, vp, vp, vp, vp, c_int64, c_float, vp, vp, vp, vp, vp, vp],

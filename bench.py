@@ -141,10 +141,6 @@ def parse():
     ap.add_argument("--infer-res", type=int, default=800)
     ap.add_argument("--dropin-steps", type=int, default=50,
                     help="timed steps of the reference's loop on the drop-in surface (DropinLoop; 0: skip)")
-    ap.add_argument("--dense-march", action="store_true",
-                    help="march with the separate scan + compaction + row-list launches (ray-ordered layout) instead "
-                         "of ngp_march_train_direct (the march packs its own samples; the default on single-cascade "
-                         "scenes)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="world > 1 process group (nccl = RCCL; gloo only to rehearse the path with ranks sharing a GPU)")
     return ap.parse_args()
@@ -449,8 +445,6 @@ def main():
                          **({} if args.dp_fine_buckets is None else {"dp_fine_buckets": args.dp_fine_buckets}),
                          **({} if args.chunk_first is None else {"chunk_first": args.chunk_first}))
     trainer.mark_invisible_cells(scene.K, scene.poses, (scene.W, scene.H))
-    if args.dense_march:
-        trainer.direct_march = False
     WORK = KERNEL_WORK
     R = args.batch
 
@@ -703,7 +697,6 @@ def main():
                        "chunk_first": trainer.chunk_first,
                        "row_forward": trainer.row_forward if trainer._rows_fwd(trainer.chunk_first) else 0,
                        "march_fork": trainer.march_fork_point(),
-                       "march_layout": "packed (march_train_direct)" if trainer._direct_layout() else "ray-ordered",
                        "parallelism": f"dp{world}" + (f" (data-parallel step of world {args.emulate_dp} emulated: collectives as local copies)" if args.emulate_dp else ""), "last_loss": round(loss, 5),
                        "hash_backward": args.hash_backward, "bin_level_lo": trainer.bin_level_lo,
                        "bin_merge_hi": trainer.bin_merge_hi,

@@ -174,25 +174,6 @@ int ngp_march_train_slots(const float* rays_o, const float* rays_d, const float*
 int ngp_march_train_compact(const float* rays_o, const float* rays_d, const int64_t* rays_a,
                             int64_t n_rays, const float* slot_t, const float* slot_dt, int max_samples,
                             float* xyzs, float* dirs, float* deltas, float* ts, void* stream);
-/* The training step's march with its compaction inside (raymarching.cu:166-332
- * as ngp_march_train_slots; one cascade, exp_step_factor 0 -- the
- * wave-per-ray lattice walk -- only): each ray's wave walks into its
- * slot_t / slot_dt range, then reserves the ray's range of the packed
- * xyzs / dirs / deltas / ts (capacity n_rays*max_samples) with one atomic on
- * *total and writes its samples there with the values
- * ngp_march_train_compact would write (bit-identical); rays_a[r] = (r,
- * start_r, N_r) -- rays in completion order, each ray's samples contiguous
- * and in order; counts[r] = N_r; the rays with N_r > 0 appended to
- * rows[0..*n_rows); *total = sum N_r; *zero (nullable) = 0.  n_rows / total /
- * zero 8-byte aligned, zeroed by the call (a kernel node: graph-capturable).
- * No scan, compaction or row-list launch: readers that take samples through
- * rays_a / index lists see the same batch. */
-int ngp_march_train_direct(const float* rays_o, const float* rays_d, const float* hits_t, int64_t n_rays,
-                           const uint8_t* bitfield, int cascades, int grid_size, float scale, float exp_step_factor,
-                           const float* noise, int max_samples, int32_t* counts, float* slot_t, float* slot_dt,
-                           const uint32_t* occ_summary, float* xyzs, float* dirs, float* deltas, float* ts,
-                           int64_t* rays_a, int32_t* rows, int64_t* n_rows, int64_t* total, int64_t* zero,
-                           void* stream);
 
 /* Replaces vren.raymarching_test (binding.cpp:70-88 -> raymarching.cu:335-454).
  * hits_t (n_rays_total,2) updated in place; alive (n_alive) i64.  Out:

@@ -58,15 +58,7 @@ def test_training_step_matches_oracle():
     ot = O.OracleTrainer(p0, 0.5, tr.density_bitfield.cpu(), 1)
     l_ref, n_ref = ot.step(rays_o, rays_d, hits_t, gt, noise, torch.ones(3), apply_adam=False)
     assert int(tr.n_samples.item()) == n_ref  # marching: bit-exact sample count
-    ra, ra_ref = tr.rays_a.cpu(), ot.last["rays_a"]
-    if tr.msets[tr.cur]["dense"]:
-        assert torch.equal(ra, ra_ref)
-    else:  # ngp_march_train_direct's packed layout: rays in completion order, each contiguous
-        assert torch.equal(ra[:, [0, 2]], ra_ref[:, [0, 2]])
-        ne = ra[:, 2] > 0
-        st = ra[ne, 1]
-        o = torch.argsort(st)
-        assert torch.equal(st[o][1:], (st[o] + ra[ne, 2][o])[:-1]) and int(st.min()) == 0  # a partition of [0, N)
+    assert torch.equal(tr.rays_a.cpu(), ot.last["rays_a"])
     l_gpu = float(loss.sum())
     assert abs(l_gpu - l_ref) <= 2e-3 * abs(l_ref)
     torch.testing.assert_close(tr.out_rgb.cpu(), ot.last["rgb"], atol=1e-3, rtol=0)
@@ -132,9 +124,7 @@ def test_prefetched_march_matches_inline():
     assert p0 == 0 and p1 >= 15
     upd = 16 - 1  # global_step starts at 1: step index 15 runs the occupancy update
     assert c0[:upd] == c1[:upd]
-    # (the rays' counts; their start offsets are the packing order of ngp_march_train_direct, which
-    # follows the march's completion order)
-    assert all(torch.equal(x[:, [0, 2]], y[:, [0, 2]]) for x, y in zip(a0[:upd], a1[:upd]))
+    assert all(torch.equal(x, y) for x, y in zip(a0[:upd], a1[:upd]))
     for x, y in zip(l0, l1):
         assert abs(x - y) <= 2e-2 * abs(x)
 
@@ -420,49 +410,3 @@ def test_preencode_only_when_levels_0_7_are_stepped_before_it():
         assert not any(k[-1] is True or (len(k) > 7 and k[7] is True) for k in tr._graphs)
         assert not any(m["pre_ready"] for m in tr.msets)
 
-
-def test_direct_march_matches_the_compacted_march():
-    """ngp_march_train_direct (the training step's march: each ray's wave packs
-    its own samples at a range reserved by one atomic) against the API march
-    (vren.raymarching_train: ngp_march_train_slots + the scan + the compaction)
-    on the same rays: per ray the same count and bit-identical xyz / dir / t /
-    dt, the ranges a partition of [0, total), the non-empty rows listed once
-    each."""
-    import ctypes
-    import vren
-    sc, tr, img, pix, noise = _setup(R=4096)
-    R, M = 4096, tr.max_samples
-    m = tr.msets[0]
-    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
-    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    img_d, pix_d = img.to(DEV), pix.to(DEV)  # (held: the launch reads them after this line)
-    vren._ok(tr.L.ngp_raygen_aabb(p(dirs), p(poses), p(img_d), p(pix_d), R, p(tr.center), p(tr.half_size),
-                                  ctypes.c_float(0.01), p(m["rays_o"]), p(m["rays_d"]), p(m["hits_t"]), vren._stream()),
-             "raygen")
-    m["noise"].copy_(noise.to(DEV))
-    vren.bitfield_summary(tr.density_bitfield, tr.G, out=m["occ_summary"])
-    m["n_rows_ne"].fill_(12345)
-    vren._ok(tr.L.ngp_march_train_direct(
-        p(m["rays_o"]), p(m["rays_d"]), p(m["hits_t"]), R, p(tr.density_bitfield), 1, tr.G, ctypes.c_float(0.5),
-        ctypes.c_float(0.0), p(m["noise"]), M, p(m["counts"]), p(m["slot_t"]), p(m["slot_dt"]), p(m["occ_summary"]),
-        p(m["xyzs"]), p(m["dirs"]), p(m["deltas"]), p(m["ts"]), p(m["rays_a"]), p(m["rows_ne"]), p(m["n_rows_ne"]),
-        p(m["n_samples"]), p(m["eval_total2"]), vren._stream()), "march_train_direct")
-    ref = vren.raymarching_train(m["rays_o"], m["rays_d"], m["hits_t"], tr.density_bitfield, 1, 0.5, 0.0, m["noise"],
-                                 tr.G, M)
-    torch.cuda.synchronize()
-    ra_ref, xyz_ref, dir_ref, dl_ref, t_ref = [x.cpu() for x in ref[:5]]
-    ra = m["rays_a"].cpu()
-    assert torch.equal(ra[:, 0], ra_ref[:, 0]) and torch.equal(ra[:, 2], ra_ref[:, 2])
-    total = int(m["n_samples"])
-    assert total == int(ref[5][0]) and int(m["eval_total2"]) == 0
-    cnt = ra[:, 2]
-    # each ray's range, gathered in ray order, is the ray-ordered compaction
-    idx = torch.repeat_interleave(ra[:, 1], cnt) + (torch.arange(int(cnt.sum())) -
-                                                      torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt))
-    assert torch.equal(torch.sort(idx)[0], torch.arange(total))  # the ranges partition [0, total)
-    for a, b in ((m["xyzs"], xyz_ref), (m["dirs"], dir_ref), (m["deltas"], dl_ref), (m["ts"], t_ref)):
-        assert torch.equal(a.cpu()[idx], b)
-    nr = int(m["n_rows_ne"])
-    rows = torch.sort(m["rows_ne"][:nr].cpu().long())[0]
-    assert torch.equal(rows, torch.nonzero(cnt > 0)[:, 0])
-    print(f"direct march: {nr} non-empty rows of {R}, {total} samples packed, bit-identical to the compaction")
