@@ -187,13 +187,20 @@ __global__ void __launch_bounds__(256) bitfield_summary_kernel(const uint64_t* _
             const int64_t c0 = (w / blocks_per_cascade) * blocks_per_cascade;
             const uint32_t local = (uint32_t)(w - c0);
             const int bx = (int)compact3(local), by = (int)compact3(local >> 1), bz = (int)compact3(local >> 2);
-            for (int dz = -1; dz <= 1 && !dl; ++dz)
-                for (int dy = -1; dy <= 1 && !dl; ++dy)
-                    for (int dx = -1; dx <= 1 && !dl; ++dx) {
+            // all 27 loads independent and in flight together (an early exit on the first
+            // occupied neighbour made them 27 dependent round trips: 9-20 us per launch)
+            uint64_t any = 0;
+#pragma unroll
+            for (int dz = -1; dz <= 1; ++dz)
+#pragma unroll
+                for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; ++dx) {
                         const int x = bx + dx, y = by + dy, z = bz + dz;
                         if (x < 0 || y < 0 || z < 0 || x >= bside || y >= bside || z >= bside) continue;
-                        dl = words[c0 + morton3((uint32_t)x, (uint32_t)y, (uint32_t)z)] != 0ull;
+                        any |= words[c0 + morton3((uint32_t)x, (uint32_t)y, (uint32_t)z)];
                     }
+            dl = any != 0ull;
         }
     }
     const uint64_t bs = __ballot(s), bd = __ballot(dl);

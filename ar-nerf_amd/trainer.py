@@ -540,7 +540,7 @@ class NGPTrainer:
         return (self._pending is None and (self.global_step + 1) % self.update_interval != 0
                 and not self.no_prefetch)
 
-    def prefetch(self, src, directions, poses):
+    def prefetch(self, src, directions, poses, after=None):
         """March the NEXT batch into the idle buffer set on the side stream so
         it overlaps the current step's field / loss / backward / Adam.  Called
         by step() once the current set is bound: everything the side stream
@@ -553,8 +553,10 @@ class NGPTrainer:
         if not self._can_prefetch():
             return False
         k = 1 - self.cur
-        ready = torch.cuda.Event()
-        ready.record(torch.cuda.current_stream())
+        ready = after
+        if ready is None:  # (else: an event the caller recorded on the main stream earlier)
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream())
         self.march_stream.wait_event(ready)
         self._march(k, src, directions, poses, self.march_stream)
         ev = torch.cuda.Event()
@@ -835,8 +837,11 @@ class NGPTrainer:
         cs = torch.cuda.current_stream()
         fork = None
         if not update_after:
-            def fork():
-                self.march_stream.wait_stream(cs)
+            def fork(after=None):
+                if after is None:
+                    self.march_stream.wait_stream(cs)
+                else:
+                    self.march_stream.wait_event(after)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
                 return True
         self._segmented = True
@@ -930,8 +935,11 @@ class NGPTrainer:
         self._bind(self.msets[k])
         cs = torch.cuda.current_stream()
         if not update_after:
-            def fork():
-                self.march_stream.wait_stream(cs)
+            def fork(after=None):
+                if after is None:
+                    self.march_stream.wait_stream(cs)
+                else:
+                    self.march_stream.wait_event(after)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
                 return True
 
@@ -964,7 +972,7 @@ class NGPTrainer:
         self._ev("raygen_march", 1)
         fork = None
         if next_src is not None and apply_adam:
-            fork = lambda: self.prefetch(next_src, directions, poses)  # noqa: E731
+            fork = lambda after=None: self.prefetch(next_src, directions, poses, after)  # noqa: E731
         if apply_adam:
             self._set_lr()
         out = self._compute(rgb_gt, apply_adam, fork)
@@ -1007,6 +1015,9 @@ class NGPTrainer:
                                                      pre, s), "field_forward_first")
             self._ev("hash_encode", 1)
             if fork is not None and at == "r1":
+                # (captured before round 2: round 2 captured first and the march forked from an event
+                # recorded after round 1 -- the same dependencies -- ran 27 % slower: the graph's
+                # queue assignment follows the capture order, profiles/r06/ab/capture_order.txt)
                 marched = bool(fork())
             self._field_indexed(s, self.eval_idx, self.eval_total2)
         elif self.chunk_first > 0:  # two rounds: first K samples per row, then the rest of unterminated rows
@@ -1063,20 +1074,35 @@ class NGPTrainer:
         hybrid = self.hash_backward != "atomic"
         binned = hybrid and self.bin_level_lo < self.grid.n_levels  # (hybrid at bin_level_lo == L: all atomic)
         bs = self.bwd_stream
-        if binned:  # bucket plan of the binned fine levels (xyzs / sample_idx only) beside the MLP backward
-            bs.wait_stream(cs)
+        def plan(after=None):  # bucket plan of the binned fine levels (xyzs / sample_idx only) beside the MLP backward
+            if after is None:
+                bs.wait_stream(cs)
+            else:
+                bs.wait_event(after)
             with torch.cuda.stream(bs):
                 vren._ok(HGL.ngp_hash_binned_plan(_p(self.xyzs), self.cap, _p(self.n_active_total),
                                                   _p(self.sample_idx), HG.ctypes.byref(self.grid.desc),
                                                   _p(self.bin_ws), self.bin_max_samples, self.bin_level_lo,
                                                   self.bin_merge_hi, vren._stream()), "hash_binned_plan")
-                planned = torch.cuda.Event()
-                planned.record(bs)
+                ev = torch.cuda.Event()
+                ev.record(bs)
+            return ev
+
+        # capture order (the graph's queue assignment follows it; dependencies unchanged): the MLP
+        # backward, then the plan forked from an event recorded before it; the binned accumulation, then
+        # the coarse branch forked from an event after the MLP backward -- +0.8 % against the reverse
+        # order (5 of 7 alternating pairs, profiles/r06/ab/capture_order.txt)
+        planned = seg_done = None
+        if binned:
+            seg_done = torch.cuda.Event()
+            seg_done.record(cs)
         self._ev("mlp_bwd", 0)
         vren._ok(HGL.ngp_field_backward_mlp(_p(self.dirs), self.cap, _p(self.n_active_total), _p(self.sample_idx),
                                             _p(self.enc), self.cap, _p(self.params16), _p(self.dsig), _p(self.drgb),
                                             _p(self.denc), _p(self.grad), s), "field_backward_mlp")
         self._ev("mlp_bwd", 1)
+        if seg_done is not None:
+            planned = plan(seg_done)
         if fork is not None and at == "mlp":
             marched = bool(fork())
         if self._segmented and hybrid:
@@ -1104,26 +1130,37 @@ class NGPTrainer:
             # (any fork point: the next batch's march is captured before this point)
             pre = (adam_split and self.pre_coarse and marched
                    and self._rows_fwd(self.chunk_first) and self.bin_level_lo >= self.pre_levels)
-            bs.wait_stream(cs)
-            if pre:
-                # its dependency on the next batch's march (done long before) taken by the coarse
-                # kernel, which waits on the main stream anyway (a second cross-queue wait on the
-                # pre-encode itself started it ~12 us after the Adam's end instead of ~7: r5tl / r5ii)
-                bs.wait_stream(self.march_stream)
-            with torch.cuda.stream(bs):
-                self._ev("hash_bwd_coarse", 0)
-                self._coarse_levels(fold=not fold_in_adam)
-                self._ev("hash_bwd_coarse", 1)
-                if adam_split:
-                    self._adam(0, split, vren._stream(), rep=fold_in_adam)
-                    if pre:
-                        # the next batch (marched beside this step) gets its round-1 coarse levels now
-                        nx = self.msets[1 - self.cur]
-                        vren._ok(HGL.ngp_field_encode_first_coarse(
-                            _p(nx["xyzs"]), _p(nx["rays_a"]), _p(nx["rows_ne"]), _p(nx["n_rows_ne"]), R, self.cap,
-                            HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]), _p(self.enc),
-                            vren._stream()), "encode_first_coarse")
-                        nx["pre_ready"] = True
+            def side(after=None):
+                if after is None:
+                    bs.wait_stream(cs)
+                else:
+                    bs.wait_event(after)
+                if pre:
+                    # its dependency on the next batch's march (done long before) taken by the coarse
+                    # kernel, which waits on the main stream anyway (a second cross-queue wait on the
+                    # pre-encode itself started it ~12 us after the Adam's end instead of ~7: r5tl / r5ii)
+                    bs.wait_stream(self.march_stream)
+                with torch.cuda.stream(bs):
+                    self._ev("hash_bwd_coarse", 0)
+                    self._coarse_levels(fold=not fold_in_adam)
+                    self._ev("hash_bwd_coarse", 1)
+                    if adam_split:
+                        self._adam(0, split, vren._stream(), rep=fold_in_adam)
+                        if pre:
+                            # the next batch (marched beside this step) gets its round-1 coarse levels now
+                            nx = self.msets[1 - self.cur]
+                            vren._ok(HGL.ngp_field_encode_first_coarse(
+                                _p(nx["xyzs"]), _p(nx["rays_a"]), _p(nx["rows_ne"]), _p(nx["n_rows_ne"]), R,
+                                self.cap, HG.ctypes.byref(self.grid.desc), _p(self.params16[HG.MLP_PARAMS:]),
+                                _p(self.enc), vren._stream()), "encode_first_coarse")
+                            nx["pre_ready"] = True
+
+            mlp_done = None
+            if binned:
+                mlp_done = torch.cuda.Event()
+                mlp_done.record(cs)
+            else:
+                side()
             self._ev("hash_binned_apply", 0)
             t = HG.MLP_PARAMS
             if binned:  # (none at bin_level_lo == L: the side stream took every level and its Adam)
@@ -1145,6 +1182,8 @@ class NGPTrainer:
                     if adam_split:
                         self._adam(split, self.n_params, s)
             self._ev("hash_binned_apply", 1)
+            if mlp_done is not None:
+                side(mlp_done)
             cs.wait_stream(bs)
             if adam_split:
                 self._ev("hash_bwd", 1)
