@@ -143,19 +143,31 @@ __device__ __forceinline__ bool march_step(float& t, const float o[3], const flo
         return true;
     }
     // (t past 2^24 steps of dt: t + dt == t, the reference's loop would never end -- only a
-    // degenerate ray (huge t2) gets there; it ends the ray instead and counts a guard hit)
+    // degenerate ray (huge t2) gets there; it ends the ray instead and counts a guard hit.)
+    // Every step advances t while dt exceeds half an ulp of each t the loop visits, i.e. when
+    // dt > 2^-24 max(|t|, |t_target|) (the general dt only grows along the ray): then the plain
+    // loop runs; a per-step check inside it cost the test-time march 20-26 % (r6m)
+    const bool advances = dt * 16777216.0f > fmaxf(fabsf(t), fabsf(t_target));
     if constexpr (SIMPLE) {
-        do {
-            const float tn = t + dt;
-            if (!(tn > t)) { t = INFINITY; ngp_guard_hit(); break; }
-            t = tn;
-        } while (t < t_target);
+        if (advances) {
+            do { t += dt; } while (t < t_target);
+        } else {
+            do {
+                const float tn = t + dt;
+                if (!(tn > t)) { t = INFINITY; ngp_guard_hit(); break; }
+                t = tn;
+            } while (t < t_target);
+        }
     } else {
-        do {
-            const float tn = t + calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
-            if (!(tn > t)) { t = INFINITY; ngp_guard_hit(); break; }
-            t = tn;
-        } while (t < t_target);
+        if (advances) {
+            do { t += calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale); } while (t < t_target);
+        } else {
+            do {
+                const float tn = t + calc_dt(t, p.esf, p.max_samples, p.grid_size, p.dt_scale);
+                if (!(tn > t)) { t = INFINITY; ngp_guard_hit(); break; }
+                t = tn;
+            } while (t < t_target);
+        }
     }
     return false;
 }
