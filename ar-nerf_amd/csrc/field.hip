@@ -1554,7 +1554,8 @@ __global__ void __launch_bounds__(256) hash_bwd_kernel(const float* __restrict__
 constexpr unsigned HASH_BWD_BLOCKS = 8192;  // grid cap of hash_bwd_kernel, all-level API path (2048 measured slower)
 // grid cap of the training step's coarse levels (launch_coarse): 2048 waves, two per SIMD.  Round 5: its
 // atomics spread over a longer span beside the record write, now that the coarse levels' Adam runs beside
-// the accumulation and no longer waits on it -- with the prefetch-free accumulation +1.2-1.3 %,
+// the accumulation and no longer waits on it -- with the prefetch-free accumulation +1.2-1.3 %; round 6
+// re-check: 256 / 1024 / 2048 blocks -3.2 / -0.5 / -1.2 %, profiles/r06/ab/coarse_grid.txt;
 // profiles/r05/ab/round5_ab.txt r5ee / r5ff (rounds 2-4: 8192, when a longer coarse kernel delayed that Adam)
 constexpr unsigned COARSE_BLOCKS = 512;
 
