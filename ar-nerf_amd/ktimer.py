@@ -202,6 +202,23 @@ class ProbeTimer:
                 out.append((s, round(float(st[r1, f] - en[r, l]) * self.tick_ns * 1e-3, 1)))
         return out
 
+    def step_periods(self, step0, n_steps, first="first_chunk"):
+        """[(step, us)]: from the start of step s's `first` kernel to the start
+        of step s + 1's, for the consecutive steps of the window [step0, step0 +
+        n_steps) (as step_gaps) -- a step's whole period, including the
+        occupancy update and the march that follow it when step s + 1 opens
+        with one"""
+        b = self.buf
+        big = torch.iinfo(torch.int64).max
+        st = torch.where(b[..., 0] > 0, b[..., 0], torch.full_like(b[..., 0], big)).min(-1).values.cpu()
+        f = PROBES.index(first)
+        out = []
+        for s in range(step0, step0 + min(n_steps, self.rows) - 1):
+            r, r1 = s % self.rows, (s + 1) % self.rows
+            if st[r, f] < big and st[r1, f] < big:
+                out.append((s, round(float(st[r1, f] - st[r, f]) * self.tick_ns * 1e-3, 1)))
+        return out
+
     def timeline(self, skip_rows=(), origin="first_chunk"):
         """{probe: (avg start us, avg end us)} relative to the start of `origin`
         in the same step row: the step's schedule as the kernels ran (no

@@ -376,7 +376,35 @@ class NGPTrainer:
         self._decay_for = 0.95
 
     @torch.no_grad()
-    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=None, jitter=None):
+    def _occ_draw(self, c, density_threshold, s):
+        """The parameter-independent head of a past-warmup update of cascade c:
+        the occupied-cell list from density_grid, the sorted draws, and (keep)
+        the kept draws -- launched on stream s.  Returns (lo, hi, M)."""
+        L, G = self.L, self.G
+        sc = min(2 ** (c - 1), self.scale)
+        half_grid_size = sc / G
+        M = G ** 3 // 4
+        vren._ok(L.ngp_occupied_cells(_p(self.density_grid[c]), G ** 3, ctypes_float(density_threshold),
+                                      _p(self._occ_list), _p(self._occ_count), _p(self._occ_list_ws), s),
+                 "occupied_cells")
+        lo, hi = ddp.shard_range(2 * M, self.rank, self.world)
+        # (keep: every rank draws the whole list, positions = list positions, so that
+        # the kept ones -- a cell's last draw -- are found over the whole list)
+        glo, ghi = (0, 2 * M) if self.occ_keep else (lo, hi)
+        args = (self.occ_seed, _p(self.dctr[2:]), c, G, M, ctypes_float(sc - half_grid_size),
+                ctypes_float(half_grid_size), _p(self._occ_list), _p(self._occ_count), glo, ghi)
+        # each half's cells drawn in ascending order: the density forward's waves
+        # stay cache-local (1.8x faster than draw order, scripts/diag/density_order.py)
+        vren._ok(L.ngp_occupancy_samples_sorted(*args, _p(self._occ_ws), _p(self._occ_xyz),
+                                                _p(self._occ_flat), s), "occupancy_samples_sorted")
+        if self.occ_keep:
+            vren._ok(L.ngp_occupancy_keep(_p(self._occ_flat), M, c * G ** 3, G ** 3, lo, hi,
+                                          _p(self._occ_mark), _p(self._occ_kept), _p(self._occ_kept_n), s),
+                     "occupancy_keep")
+        return lo, hi, M
+
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=None, jitter=None,
+                            drawn=False):
         """models/networks.py:252-281.  Past warmup the cells are drawn on device
         (ngp_occupied_cells + ngp_occupancy_samples: no host sync, so the update
         can sit inside a captured graph).  Multi-GPU: each rank evaluates its
@@ -385,7 +413,9 @@ class NGPTrainer:
         bitfield.  erode (default: the trainer's setting) decays each cell by
         clamp(decay**(1/count_grid), 0.1, 0.95) (networks.py:270-272).
         jitter (tests): the warm-up's U[0,1) jitter per cell (C, G^3, 3) in
-        grid_coords order instead of the trainer's own draw."""
+        grid_coords order instead of the trainer's own draw.  drawn (one
+        cascade, past warmup): _occ_draw already ran for this update (the
+        captured step launches it beside the step before the update)."""
         C, G = self.cascades, self.G
         erode = self.erode if erode is None else erode
         if erode and self.decay_cells is None:
@@ -412,25 +442,14 @@ class NGPTrainer:
                 flat = (indices + c * G ** 3).contiguous()
                 n = flat.shape[0]
             else:  # sample_uniform_and_occupied_cells (networks.py:181-207), on device
-                M = G ** 3 // 4
-                vren._ok(L.ngp_occupied_cells(_p(self.density_grid[c]), G ** 3, ctypes_float(density_threshold),
-                                              _p(self._occ_list), _p(self._occ_count), _p(self._occ_list_ws), s),
-                         "occupied_cells")
-                lo, hi = ddp.shard_range(2 * M, self.rank, self.world)
+                if drawn:
+                    assert C == 1, "update_density_grid(drawn=True) needs one cascade"
+                    M = G ** 3 // 4
+                    lo, hi = ddp.shard_range(2 * M, self.rank, self.world)
+                else:
+                    lo, hi, M = self._occ_draw(c, density_threshold, s)
                 n = hi - lo
-                # (keep: every rank draws the whole list, positions = list positions, so that
-                # the kept ones -- a cell's last draw -- are found over the whole list)
-                glo, ghi = (0, 2 * M) if self.occ_keep else (lo, hi)
-                args = (self.occ_seed, _p(self.dctr[2:]), c, G, M, ctypes_float(sc - half_grid_size),
-                        ctypes_float(half_grid_size), _p(self._occ_list), _p(self._occ_count), glo, ghi)
-                # each half's cells drawn in ascending order: the density forward's waves
-                # stay cache-local (1.8x faster than draw order, scripts/diag/density_order.py)
-                vren._ok(L.ngp_occupancy_samples_sorted(*args, _p(self._occ_ws), _p(self._occ_xyz),
-                                                        _p(self._occ_flat), s), "occupancy_samples_sorted")
                 if self.occ_keep:
-                    vren._ok(L.ngp_occupancy_keep(_p(self._occ_flat), M, c * G ** 3, G ** 3, lo, hi,
-                                                  _p(self._occ_mark), _p(self._occ_kept), _p(self._occ_kept_n), s),
-                             "occupancy_keep")
                     # encode + density net of the kept samples only (sigma written at their position)
                     vren._ok(HG._lib().ngp_field_encode_mlp(_p(self._occ_xyz), None, n, _p(self._occ_kept_n),
                                                             _p(self._occ_kept), HG.ctypes.byref(self.grid.desc),
@@ -947,9 +966,20 @@ class NGPTrainer:
             cs.wait_stream(self.march_stream)
             vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
         else:
+            thr = 0.01 * MAX_SAMPLES / 3 ** 0.5
+            drawn = self.cascades == 1
+            if drawn:
+                # the update's parameter-independent head (occupied cells, draws, kept draws: they
+                # read density_grid and the occupancy counter only) beside this step, on the march
+                # stream (idle: no prefetch before an update)
+                self.march_stream.wait_stream(cs)
+                with torch.cuda.stream(self.march_stream):
+                    self._occ_draw(0, thr, vren._stream())
             self._compute(self.rgb_gt, True, None)
             vren._ok(self.L.ngp_counters_inc(_p(self.dctr), 2, vren._stream()), "counters_inc")
-            self.update_density_grid(0.01 * MAX_SAMPLES / 3 ** 0.5, warmup=False)
+            if drawn:
+                cs.wait_stream(self.march_stream)
+            self.update_density_grid(thr, warmup=False, drawn=drawn)
             self._march(1 - k, ("sample", 0, gt), directions, poses, cs)
 
     def _step(self, src, rgb_gt, directions, poses, apply_adam, next_src):

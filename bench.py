@@ -577,6 +577,17 @@ def main():
     pr_timeline = probes.timeline(skip_rows=skip)
     upd_steps = [st for st in range(s_rf, s_rf + ran_rf) if st % ui == 0]
     pr_gaps = probes.step_gaps(s_rf, ran_rf, skip_steps=upd_steps)
+    # the 1-in-update_interval step: its period (first kernel to the next step's first kernel) holds
+    # the occupancy update and the next batch's march after it, against the median regular period
+    periods = probes.step_periods(s_rf, ran_rf)
+    p_upd = [us for st, us in periods if (st + 1) % ui == 0]
+    p_reg = sorted(us for st, us in periods if (st + 1) % ui != 0)
+    update_step = None
+    if p_upd and p_reg:
+        reg = p_reg[len(p_reg) // 2]
+        update_step = {"interval": ui, "period_us": round(sum(p_upd) / len(p_upd), 1), "regular_period_us": reg,
+                       "extra_us": round(sum(p_upd) / len(p_upd) - reg, 1), "n_update_steps": len(p_upd),
+                       "amortised_extra_us_per_step": round((sum(p_upd) / len(p_upd) - reg) / ui, 1)}
     m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         e_rf = m_rf
@@ -720,6 +731,7 @@ def main():
             "ns_per_composited_sample": round(ms_step * 1e6 / max(units["composited"], 1e-9), 4),
             "ns_per_marched_sample": round(ms_step * 1e6 / max(units["marched"], 1e-9), 4),
             "guard_hits": guard_hits,
+            "occupancy_update_step": update_step,
             "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "breakdown_note": (f"ops / kernels: wall-clock stamps around every kernel inside the captured graphs "
                                f"over {bd_steps} replayed steps ({t_bd * 1e3:.3f} ms/step with all stamps); timeline_us: "
