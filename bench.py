@@ -587,7 +587,8 @@ def main():
         reg = p_reg[len(p_reg) // 2]
         update_step = {"interval": ui, "period_us": round(sum(p_upd) / len(p_upd), 1), "regular_period_us": reg,
                        "extra_us": round(sum(p_upd) / len(p_upd) - reg, 1), "n_update_steps": len(p_upd),
-                       "amortised_extra_us_per_step": round((sum(p_upd) / len(p_upd) - reg) / ui, 1)}
+                       "amortised_extra_us_per_step": round((sum(p_upd) / len(p_upd) - reg) / ui, 1),
+                       "update_step_periods_us": [us for st, us in periods if (st + 1) % ui == 0]}
     m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
     if trainer.chunk_first <= 0:
         e_rf = m_rf
