@@ -577,19 +577,28 @@ def main():
     pr_timeline = probes.timeline(skip_rows=skip)
     upd_steps = [st for st in range(s_rf, s_rf + ran_rf) if st % ui == 0]
     pr_gaps = probes.step_gaps(s_rf, ran_rf, skip_steps=upd_steps)
-    # the 1-in-update_interval step: its period (first kernel to the next step's first kernel) holds
-    # the occupancy update and the next batch's march after it, against the median regular period
-    periods = probes.step_periods(s_rf, ran_rf)
-    p_upd = [us for st, us in periods if (st + 1) % ui == 0]
+    m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
+    # ---- the 1-in-update_interval step: a window of 4 update intervals with the probes armed (its own
+    # rows: one per step); a step's period (its first kernel to the next step's first kernel) holds the
+    # occupancy update and the next batch's march when an update follows it, against the median regular
+    # period
+    n_up = 4 * ui
+    pu = KT.ProbeTimer(trainer.dctr, rows=n_up)
+    s_up = adam_steps()
+    pu.arm()
+    run(n_up)
+    torch.cuda.synchronize()
+    pu.disarm()
+    periods = pu.step_periods(s_up, adam_steps() - s_up)
+    del pu
+    p_upd = sorted(us for st, us in periods if (st + 1) % ui == 0)
     p_reg = sorted(us for st, us in periods if (st + 1) % ui != 0)
     update_step = None
     if p_upd and p_reg:
-        reg = p_reg[len(p_reg) // 2]
-        update_step = {"interval": ui, "period_us": round(sum(p_upd) / len(p_upd), 1), "regular_period_us": reg,
-                       "extra_us": round(sum(p_upd) / len(p_upd) - reg, 1), "n_update_steps": len(p_upd),
-                       "amortised_extra_us_per_step": round((sum(p_upd) / len(p_upd) - reg) / ui, 1),
-                       "update_step_periods_us": [us for st, us in periods if (st + 1) % ui == 0]}
-    m_rf, c_rf, a_rf, e_rf = trainer.stat_totals()
+        reg, upd = p_reg[len(p_reg) // 2], p_upd[len(p_upd) // 2]
+        update_step = {"interval": ui, "period_us": upd, "regular_period_us": reg, "extra_us": round(upd - reg, 1),
+                       "amortised_extra_us_per_step": round((upd - reg) / ui, 1), "update_step_periods_us": p_upd,
+                       "measured": f"medians over a {n_up}-step window after the roofline window (device probes)"}
     if trainer.chunk_first <= 0:
         e_rf = m_rf
     nr = max(1, ran_rf)
