@@ -354,3 +354,37 @@ def test_trainer_update_with_kept_samples_is_bit_identical():
     print(f"kept {n_kept} of {M2} samples ({n_kept / M2:.3f})")
     assert 0 < n_kept < M2
     assert not torch.equal(outs[0][0], state[0])  # (the update did change the grid)
+
+
+def test_update_with_its_draws_beside_the_step_is_bit_identical():
+    """The captured step before an update draws the update's cells on the
+    march stream beside itself (NGPTrainer._occ_draw), and the update then
+    starts from those draws (update_density_grid(drawn=True)): the same grid,
+    bitfield and threshold bit for bit as the update drawing them itself, from
+    the same trained state."""
+    sc = S.AnalyticScene(W=100, H=100, n_images=10)
+    dirs, poses = sc.directions.to(DEV), sc.poses.to(DEV)
+    gt_img = sc.gt_images(device=DEV)
+    tr = NGPTrainer(scale=0.5, batch_size=4096, device=DEV, seed=3, warmup_steps=16)
+    tr.mark_invisible_cells(sc.K, sc.poses, (sc.W, sc.H))
+    for _ in range(60):
+        tr.train_step(gt_img, dirs, poses)
+    tr.drain()
+    torch.cuda.synchronize()
+    state = [t.clone() for t in (tr.density_grid, tr.density_bitfield, tr.dctr, tr.threshold)]
+    outs = []
+    for drawn in (False, True):
+        for t, v in zip((tr.density_grid, tr.density_bitfield, tr.dctr, tr.threshold), state):
+            t.copy_(v)
+        cs = torch.cuda.current_stream()
+        if drawn:
+            tr.march_stream.wait_stream(cs)
+            with torch.cuda.stream(tr.march_stream):
+                tr._occ_draw(0, THR, vren._stream())
+            cs.wait_stream(tr.march_stream)
+        tr.update_density_grid(THR, warmup=False, drawn=drawn)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (tr.density_grid, tr.density_bitfield, tr.threshold, tr.dctr)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert not torch.equal(outs[0][0], state[0])  # (the update did change the grid)
