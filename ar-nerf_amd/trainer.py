@@ -559,7 +559,7 @@ class NGPTrainer:
         return (self._pending is None and (self.global_step + 1) % self.update_interval != 0
                 and not self.no_prefetch)
 
-    def prefetch(self, src, directions, poses, after=None):
+    def prefetch(self, src, directions, poses):
         """March the NEXT batch into the idle buffer set on the side stream so
         it overlaps the current step's field / loss / backward / Adam.  Called
         by step() once the current set is bound: everything the side stream
@@ -572,10 +572,8 @@ class NGPTrainer:
         if not self._can_prefetch():
             return False
         k = 1 - self.cur
-        ready = after
-        if ready is None:  # (else: an event the caller recorded on the main stream earlier)
-            ready = torch.cuda.Event()
-            ready.record(torch.cuda.current_stream())
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream())
         self.march_stream.wait_event(ready)
         self._march(k, src, directions, poses, self.march_stream)
         ev = torch.cuda.Event()
@@ -856,11 +854,8 @@ class NGPTrainer:
         cs = torch.cuda.current_stream()
         fork = None
         if not update_after:
-            def fork(after=None):
-                if after is None:
-                    self.march_stream.wait_stream(cs)
-                else:
-                    self.march_stream.wait_event(after)
+            def fork():
+                self.march_stream.wait_stream(cs)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
                 return True
         self._segmented = True
@@ -954,11 +949,8 @@ class NGPTrainer:
         self._bind(self.msets[k])
         cs = torch.cuda.current_stream()
         if not update_after:
-            def fork(after=None):
-                if after is None:
-                    self.march_stream.wait_stream(cs)
-                else:
-                    self.march_stream.wait_event(after)
+            def fork():
+                self.march_stream.wait_stream(cs)
                 self._march(1 - k, ("sample", 1, gt), directions, poses, self.march_stream)
                 return True
 
@@ -1002,7 +994,7 @@ class NGPTrainer:
         self._ev("raygen_march", 1)
         fork = None
         if next_src is not None and apply_adam:
-            fork = lambda after=None: self.prefetch(next_src, directions, poses, after)  # noqa: E731
+            fork = lambda: self.prefetch(next_src, directions, poses)  # noqa: E731
         if apply_adam:
             self._set_lr()
         out = self._compute(rgb_gt, apply_adam, fork)
