@@ -1171,7 +1171,13 @@ __device__ __forceinline__ float sample_max(float v) {
 __device__ __forceinline__ int colsum_exp(const _Float16* img, int nin, int nout, int rt, int lane) {
     float a = 0.f;
     if (lane < nin)
-        for (int o = 0; o < nout; ++o) a += fabsf((float)img[lane * rt + o]);
+        for (int o = 0; o < nout; o += 4) {  // (8-byte row reads; the same sequential sum)
+            const h4 v = *reinterpret_cast<const h4*>(img + lane * rt + o);
+            a += fabsf((float)v[0]);
+            a += fabsf((float)v[1]);
+            a += fabsf((float)v[2]);
+            a += fabsf((float)v[3]);
+        }
     for (int off = 32; off > 0; off >>= 1) a = fmaxf(a, __shfl_xor(a, off, 64));
     int e = 0;
     const float m = frexpf(a, &e);
@@ -1299,9 +1305,17 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     load_bwd_weights_direct(mlp, sw);
     __syncthreads();
     // per-block bounds of W5^T, W4^T, W2^T: the inner layers' exponents follow from their input's
-    // (round 5; rounds 3-4 took a per-sample max after every layer: 12 % more VALU, 6 % longer)
-    const int k5 = colsum_exp(sw + BT5, 64, 16, RT16, lane), k4 = colsum_exp(sw + BT4, 64, 64, RT64, lane);
-    const int k2 = colsum_exp(sw + BT2, 64, 16, RT16, lane);
+    // (round 5; rounds 3-4 took a per-sample max after every layer: 12 % more VALU, 6 % longer);
+    // one wave per matrix (round 6: every wave computed all three, ~1.3 M VALU per launch)
+    __shared__ int kex[3];
+    if (wid < 3) {
+        const int e = wid == 0 ? colsum_exp(sw + BT5, 64, 16, RT16, lane)
+                    : wid == 1 ? colsum_exp(sw + BT4, 64, 64, RT64, lane) : colsum_exp(sw + BT2, 64, 16, RT16, lane);
+        if (lane == 0) kex[wid] = e;
+    }
+    __syncthreads();
+    const int k5 = __builtin_amdgcn_readfirstlane(kex[0]), k4 = __builtin_amdgcn_readfirstlane(kex[1]);
+    const int k2 = __builtin_amdgcn_readfirstlane(kex[2]);
     NGP_BWD_EDGE(1);
     int par = 0;
     // block-uniform trip count: every wave reaches every barrier
