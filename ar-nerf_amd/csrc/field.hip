@@ -1479,25 +1479,30 @@ __global__ void __launch_bounds__(64 * CW, CW / 4) field_bwd_mlp_coop_kernel(
     // the memory-side atomic unit: 12 -> 7 us per launch; per-block partial
     // rows + a reduction launch measured slower).
     NGP_BWD_EDGE(2);
-    const int n1 = coop_n1(wid), nadd = 4 * (n1 + coop_n2(wid));
+    const int n1 = coop_n1(wid), n2 = coop_n2(wid), nadd = 4 * (n1 + n2);
     const int rot = (int)(blockIdx.x % (unsigned)nadd);
-#pragma unroll 1
-    for (int q0 = 0; q0 < nadd; ++q0) {
-        const int q = (q0 + rot) % nadd, t = q >> 2, r = q & 3;
-        const int t2 = t - n1;  // tiles t < n1: phase 1, else phase 2
-        f4 a = acc1[0];
+    // (q = 4 t + r over the wave's tiles in order, taken from q = rot on: two passes over a fully
+    // unrolled tile loop, so each add's accumulator element and weight offset are static -- the
+    // dynamically indexed version spent ~1000 VALU per wave selecting them)
 #pragma unroll
-        for (int u = 1; u < KT1; ++u)
-            if (t == u) a = acc1[u];
+    for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-        for (int u = 0; u < KT2; ++u)
-            if (t2 == u) a = acc2[u];
-        const float v = r == 0 ? a[0] : r == 1 ? a[1] : r == 2 ? a[2] : a[3];
-        const int k = t2 < 0 ? coop_k1(wid, t) : coop_k2(wid, t2);
-        int ow, in_dim, o0, i0;
-        acc_tile_info(k, ow, in_dim, o0, i0);
-        const int w = ow + (o0 + 4 * g + r) * in_dim + i0 + s;
-        atomicAdd(&grad_mlp[w], v);
+        for (int t = 0; t < KT1 + KT2; ++t) {
+            const bool p1 = t < KT1;
+            const int tt = p1 ? t : t - KT1;
+            if (p1 ? tt >= n1 : tt >= n2) continue;
+            const int tflat = p1 ? tt : n1 + tt;
+            const f4 a = p1 ? acc1[p1 ? tt : 0] : acc2[p1 ? 0 : tt];
+            const int k = p1 ? coop_k1(wid, tt) : coop_k2(wid, tt);
+            int ow, in_dim, o0, i0;
+            acc_tile_info(k, ow, in_dim, o0, i0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int q = 4 * tflat + r;
+                if ((pass == 0) != (q >= rot)) continue;
+                atomicAdd(&grad_mlp[ow + (o0 + 4 * g + r) * in_dim + i0 + s], a[r]);
+            }
+        }
     }
     NGP_BWD_EDGE(3);
     NGP_PROBE_END();
