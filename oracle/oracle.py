@@ -295,6 +295,29 @@ class _RoundHalf(torch.autograd.Function):
 rh = _RoundHalf.apply
 
 
+class _RoundGrad16(torch.autograd.Function):
+    """Identity in the forward; in the backward the gradient rounded to fp16's
+    11 significant bits (round to nearest even) over an unbounded exponent
+    range.  This is where tcnn's fused MLP backward stores a layer's gradient
+    in fp16 (the pre-activation gradient of every layer, ReLU' applied), at a
+    power-of-two scale that keeps it in fp16's normal range -- a power-of-two
+    scale is exact, so the rounding is the mantissa's alone.  The product's
+    MLP backward (field.hip field_bwd_mlp_coop_kernel) rounds at the same five
+    points with per-sample power-of-two scales."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        m, e = torch.frexp(g)
+        return torch.ldexp(torch.round(m * 2048.0) / 2048.0, e.to(g.dtype))
+
+
+rg16 = _RoundGrad16.apply
+
+
 def mlp_layers(params, dims):
     """Split flat params into row-major [out][in] weight matrices."""
     Ws, o = [], 0
@@ -305,11 +328,14 @@ def mlp_layers(params, dims):
     return Ws, o
 
 
-def mlp_forward(x16, Ws, out_act=None):
-    """FullyFusedMLP: ReLU hidden, fp32 accumulate, fp16 at every layer output."""
+def mlp_forward(x16, Ws, out_act=None, grad16=False):
+    """FullyFusedMLP: ReLU hidden, fp32 accumulate, fp16 at every layer output.
+    grad16: the backward stores each layer's pre-activation gradient in fp16
+    (rg16), tcnn's backward storage points; default: fp32 autograd throughout."""
     h = x16.float()
     for i, W in enumerate(Ws):
-        h = rh(h @ rh(W).t())
+        z = h @ rh(W).t()
+        h = rh(rg16(z) if grad16 else z)
         if i < len(Ws) - 1:
             h = torch.relu(h)
     if out_act == "Sigmoid":
@@ -406,6 +432,7 @@ class OracleNGPField(torch.nn.Module):
         self.xyz_params = torch.nn.Parameter(torch.cat([dens, table]))
         self.rgb_params = torch.nn.Parameter(col)
         self.n_dens = dens.numel()
+        self.grad16 = False  # True: the MLP backward's fp16 gradient storage points (mlp_forward)
 
     def density_feat(self, x):
         Ws, _ = mlp_layers(self.xyz_params[:self.n_dens], self.dens_dims)
@@ -413,7 +440,7 @@ class OracleNGPField(torch.nn.Module):
         enc = _HashEncodeFn.apply(table, x, self.spec, self.xyz_min, self.xyz_max)
         if enc.shape[1] < self.n_in:  # tcnn pads the encoding to the MLP's input width with ones
             enc = torch.cat([enc, torch.ones(enc.shape[0], self.n_in - enc.shape[1], dtype=enc.dtype)], 1)
-        h = mlp_forward(enc, Ws)
+        h = mlp_forward(enc, Ws, grad16=self.grad16)
         return h
 
     def density(self, x, return_feat=False):
@@ -425,7 +452,7 @@ class OracleNGPField(torch.nn.Module):
         sig, h = self.density(x, return_feat=True)
         sh = sh4(d).float()
         Ws, _ = mlp_layers(self.rgb_params, self.color_dims)
-        out = mlp_forward(torch.cat([sh, h], 1), Ws)
+        out = mlp_forward(torch.cat([sh, h], 1), Ws, grad16=self.grad16)
         rgb = rh(torch.sigmoid(out[:, :3]))
         return sig, rgb
 

@@ -213,3 +213,27 @@ def test_mlp_weight_gradient_operand_rounding():
     print(f"dW operand rounding, relative L2 vs fp32 operands: fp16 (per-sample, then block scale) {e_hf:.2e}, "
           f"bf16 {e_bf:.2e}")
     assert e_hf < 1e-3 and e_bf < 5e-3
+
+
+def test_rg16_rounds_gradients_like_fp16_over_an_unbounded_exponent_range():
+    """oracle.rg16 (the MLP backward's fp16 gradient storage model): identity
+    forward; its backward equals a cast to fp16 wherever the value is in
+    fp16's normal range, and keeps 11 significant bits far outside it (the
+    power-of-two scales put every stored gradient in range)."""
+    import oracle as O
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4096, generator=g) * torch.exp2(torch.randint(-12, 14, (4096,), generator=g).float())
+    x = torch.cat([x, torch.tensor([0.0, -0.0, 1.0, 65504.0, 2.0 ** -14, 1 + 2.0 ** -11, 1 + 3 * 2.0 ** -11])])
+    t = torch.zeros_like(x, requires_grad=True)
+    y = O.rg16(t)
+    assert torch.equal(y, t)
+    y.backward(x)
+    normal = (x.abs() >= 2.0 ** -14) | (x == 0)
+    assert int(normal.sum()) > 3500
+    assert torch.equal(t.grad[normal], x[normal].half().float())
+    # far outside fp16's range: the same 11-bit mantissa, scaled
+    xn = x[normal]
+    big = xn * 2.0 ** 60
+    t2 = torch.zeros_like(big, requires_grad=True)
+    O.rg16(t2).backward(big)
+    assert torch.equal(t2.grad, xn.half().float() * 2.0 ** 60)
