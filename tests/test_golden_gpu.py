@@ -84,6 +84,9 @@ def test_product_train_step_matches_reference_glue(case):
     assert abs(float(loss) - float(fx["loss"])) <= 1e-2 * abs(float(fx["loss"]))
     loss.backward()
     g = model.params.grad.cpu()
+    print(f"{case}: gradient relative L2 vs the glue: density MLP {_rel(g[:3072], fx['grad_mlp_density']):.2e}, "
+          f"colour MLP {_rel(g[3072:10240], fx['grad_rgb_net']):.2e}, table (listed entries) "
+          f"{_rel(g[10240:][torch.from_numpy(fx['grad_table_idx'])], fx['grad_table_vals']):.2e}")
     assert _rel(g[:3072], fx["grad_mlp_density"]) < 3e-2
     assert _rel(g[3072:10240], fx["grad_rgb_net"]) < 3e-2
     gt_tab = g[10240:]

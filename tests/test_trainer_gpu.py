@@ -5,7 +5,8 @@ against the oracle running the reference's training-step math on the CPU
 FusedAdam), from the same state, rays and noise.
 
 Tolerances: loss within 2e-3 relative (fp16 MLP storage points); per-ray
-rgb/opacity within 1e-3; gradients relative L2 <= 2e-2 (fp16 MFMA backward);
+rgb/opacity within 1e-3; gradients relative L2 <= 1e-3 against fp32 autograd and
+<= 5e-4 against the oracle's fp16 gradient-storage model (oracle.rg16);
 Adam-updated params within 1e-5 absolute (|update| <= lr = 1e-2 per step,
 dominated by sign(g) for fresh moments)."""
 import ctypes
@@ -64,9 +65,18 @@ def test_training_step_matches_oracle():
     torch.testing.assert_close(tr.out_rgb.cpu(), ot.last["rgb"], atol=1e-3, rtol=0)
     torch.testing.assert_close(tr.out_op.cpu(), ot.last["opacity"], atol=1e-3, rtol=0)
     g_gpu, g_ref = tr.grad.cpu(), ot.flat_grad()
+    # (measured, profiles/r06/r6af_grad16_trainer.txt: 5.5e-6 / 1.1e-5 / 6.9e-5 against fp32 autograd,
+    # 3.0e-6 / 1.1e-5 / 3.7e-5 against the fp16 gradient-storage model; rounds 1-5 held this to 2e-2)
     for lo, hi in ((0, 3072), (3072, 10240), (10240, g_ref.numel())):
         rel = float((g_gpu[lo:hi] - g_ref[lo:hi]).norm() / g_ref[lo:hi].norm())
-        assert rel < 2e-2, (lo, hi, rel)
+        assert rel < 1e-3, (lo, hi, rel)
+    o16 = O.OracleTrainer(p0, 0.5, tr.density_bitfield.cpu(), 1)
+    o16.field.grad16 = True
+    o16.step(rays_o, rays_d, hits_t, gt, noise, torch.ones(3), apply_adam=False)
+    g16 = o16.flat_grad()
+    for lo, hi in ((0, 3072), (3072, 10240), (10240, g16.numel())):
+        rel = float((g_gpu[lo:hi] - g16[lo:hi]).norm() / g16[lo:hi].norm())
+        assert rel < 5e-4, (lo, hi, rel)
     # Adam on both sides from the same gradient
     tr.grad.copy_(g_ref.to(DEV))
     vren._ok(tr.L.ngp_adam_step(*[vren.c_void_p(t.data_ptr()) for t in (tr.params, tr.grad, tr.exp_avg,
