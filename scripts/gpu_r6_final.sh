@@ -9,6 +9,7 @@ T=${1:-r6final}
 OUT=gpurun_out/$T; mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -60 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
+timeout -k 10 300 python -u -m pytest tests/test_golden_gpu.py tests/test_field_gpu.py -q -s --timeout 120 --timeout-method thread -k "train or backward" > $OUT/pytest_prints.log 2>&1
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 tail -1 $OUT/smoke.log
 timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_driver_cmd.json 2> $OUT/bench_driver_cmd.err
