@@ -6,7 +6,7 @@ against the golden outputs of the REFERENCE glue (tests/golden/*.npz).
 Bit-exact: rays_a, deltas, ts, rm_samples (marching).  Within 2e-3: rgb,
 opacity, depth, ws (fp16 MLP storage points; the MFMA accumulation order can
 move an fp16 output by one ulp).  Loss within 1e-2 relative; gradients
-relative L2 <= 3e-2 (fp16 MFMA backward vs fp32 autograd)."""
+relative L2 <= 5e-3 (fp16 MFMA backward vs fp32 autograd; measured <= 8.6e-4)."""
 import numpy as np
 import pytest
 import torch
@@ -87,11 +87,15 @@ def test_product_train_step_matches_reference_glue(case):
     print(f"{case}: gradient relative L2 vs the glue: density MLP {_rel(g[:3072], fx['grad_mlp_density']):.2e}, "
           f"colour MLP {_rel(g[3072:10240], fx['grad_rgb_net']):.2e}, table (listed entries) "
           f"{_rel(g[10240:][torch.from_numpy(fx['grad_table_idx'])], fx['grad_table_vals']):.2e}")
-    assert _rel(g[:3072], fx["grad_mlp_density"]) < 3e-2
-    assert _rel(g[3072:10240], fx["grad_rgb_net"]) < 3e-2
+    # (measured, profiles/r06/r6s3_pytest_prints.log: lego 3.3e-4 / 3.1e-5 / 8.6e-4, garden 1.8e-4 / 4.0e-5 /
+    # 5.8e-4; rounds 1-5 held these to 3e-2)
+    assert _rel(g[:3072], fx["grad_mlp_density"]) < 5e-3
+    assert _rel(g[3072:10240], fx["grad_rgb_net"]) < 5e-3
     gt_tab = g[10240:]
-    assert _rel(gt_tab[torch.from_numpy(fx["grad_table_idx"])], fx["grad_table_vals"]) < 3e-2
-    assert abs(float(gt_tab.norm()) - float(fx["grad_table_norm"])) < 3e-2 * float(fx["grad_table_norm"])
+    assert _rel(gt_tab[torch.from_numpy(fx["grad_table_idx"])], fx["grad_table_vals"]) < 5e-3
+    dn = abs(float(gt_tab.norm()) - float(fx["grad_table_norm"])) / float(fx["grad_table_norm"])
+    print(f"{case}: table gradient norm {dn:.2e} relative to the glue's")
+    assert dn < 1e-3  # (measured 2.8e-5 / 3.8e-5)
 
 
 def test_product_test_render_matches_reference_glue():
