@@ -81,6 +81,8 @@ def test_product_train_step_matches_reference_glue(case):
     print(f"{case}: {flipped} of {rays_a.shape[0]} rays end one side of T_thr apart, all borderline")
     loss_d = NeRFLoss(30, "raw", float(fx["scale"]), 0.0, lambda_distortion=0.0)(res, {"rgb": gt})
     loss = sum(v.mean() for v in loss_d.values())
+    print(f"{case}: loss {float(loss):.6e} vs the glue's {float(fx['loss']):.6e}, relative "
+          f"{abs(float(loss) - float(fx['loss'])) / abs(float(fx['loss'])):.2e}")
     assert abs(float(loss) - float(fx["loss"])) <= 1e-2 * abs(float(fx["loss"]))
     loss.backward()
     g = model.params.grad.cpu()

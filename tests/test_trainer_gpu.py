@@ -61,6 +61,9 @@ def test_training_step_matches_oracle():
     assert int(tr.n_samples.item()) == n_ref  # marching: bit-exact sample count
     assert torch.equal(tr.rays_a.cpu(), ot.last["rays_a"])
     l_gpu = float(loss.sum())
+    print(f"loss {l_gpu:.6e} vs the oracle's {l_ref:.6e}, relative {abs(l_gpu - l_ref) / abs(l_ref):.2e}; "
+          f"rgb max |diff| {float((tr.out_rgb.cpu() - ot.last['rgb']).abs().max()):.2e}, opacity "
+          f"{float((tr.out_op.cpu() - ot.last['opacity']).abs().max()):.2e}")
     assert abs(l_gpu - l_ref) <= 2e-3 * abs(l_ref)
     torch.testing.assert_close(tr.out_rgb.cpu(), ot.last["rgb"], atol=1e-3, rtol=0)
     torch.testing.assert_close(tr.out_op.cpu(), ot.last["opacity"], atol=1e-3, rtol=0)
