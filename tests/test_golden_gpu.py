@@ -5,7 +5,7 @@ against the golden outputs of the REFERENCE glue (tests/golden/*.npz).
 
 Bit-exact: rays_a, deltas, ts, rm_samples (marching).  Within 2e-3: rgb,
 opacity, depth, ws (fp16 MLP storage points; the MFMA accumulation order can
-move an fp16 output by one ulp).  Loss within 1e-2 relative; gradients
+move an fp16 output by one ulp).  Loss within 1e-4 relative; gradients
 relative L2 <= 5e-3 (fp16 MFMA backward vs fp32 autograd; measured <= 8.6e-4)."""
 import numpy as np
 import pytest
@@ -49,6 +49,9 @@ def test_product_train_step_matches_reference_glue(case):
     for k in ("rays_a", "deltas", "ts"):
         assert torch.equal(res[k].cpu(), torch.from_numpy(fx[k])), k
     assert int(res["rm_samples"]) == int(fx["rm_samples"])
+    print(f"{case}: max |diff| vs the glue " + ", ".join(
+        f"{k} {float((res[k].detach().cpu() - torch.from_numpy(fx[k])).abs().max()):.2e}"
+        for k in ("rgb", "opacity", "depth", "ws")))
     for k in ("rgb", "opacity", "depth", "ws"):
         torch.testing.assert_close(res[k].detach().cpu(), torch.from_numpy(fx[k]), atol=2e-3, rtol=0)
     # composited count: the field's sigma differs from the oracle's within the
@@ -81,9 +84,11 @@ def test_product_train_step_matches_reference_glue(case):
     print(f"{case}: {flipped} of {rays_a.shape[0]} rays end one side of T_thr apart, all borderline")
     loss_d = NeRFLoss(30, "raw", float(fx["scale"]), 0.0, lambda_distortion=0.0)(res, {"rgb": gt})
     loss = sum(v.mean() for v in loss_d.values())
-    print(f"{case}: loss {float(loss):.6e} vs the glue's {float(fx['loss']):.6e}, relative "
-          f"{abs(float(loss) - float(fx['loss'])) / abs(float(fx['loss'])):.2e}")
-    assert abs(float(loss) - float(fx["loss"])) <= 1e-2 * abs(float(fx["loss"]))
+    lv = float(loss.detach())
+    print(f"{case}: loss {lv:.6e} vs the glue's {float(fx['loss']):.6e}, relative "
+          f"{abs(lv - float(fx['loss'])) / abs(float(fx['loss'])):.2e}")
+    # (measured, profiles/r06/r6al_pytest_loss.log: 4.1e-6 lego, 1.6e-7 garden; rounds 1-5: 1e-2)
+    assert abs(float(loss.detach()) - float(fx["loss"])) <= 1e-4 * abs(float(fx["loss"]))
     loss.backward()
     g = model.params.grad.cpu()
     print(f"{case}: gradient relative L2 vs the glue: density MLP {_rel(g[:3072], fx['grad_mlp_density']):.2e}, "
@@ -106,6 +111,8 @@ def test_product_test_render_matches_reference_glue():
     o, d = torch.from_numpy(fx["rays_o"]).to(DEV), torch.from_numpy(fx["rays_d"]).to(DEV)
     with torch.no_grad():
         res = render(model, o, d, test_time=True)
+    print("lego_test: max |diff| vs the glue " + ", ".join(
+        f"{k} {float((res[k].cpu() - torch.from_numpy(fx[k])).abs().max()):.2e}" for k in ("rgb", "opacity", "depth")))
     for k in ("rgb", "opacity", "depth"):
         torch.testing.assert_close(res[k].cpu(), torch.from_numpy(fx[k]), atol=2e-3, rtol=0)
     assert abs(int(res["total_samples"]) - int(fx["total_samples"])) <= 4

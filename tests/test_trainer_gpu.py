@@ -4,8 +4,8 @@ against the oracle running the reference's training-step math on the CPU
 (oracle.OracleTrainer: VolumeRenderer fw/bw, NeRFLoss 'raw', autograd,
 FusedAdam), from the same state, rays and noise.
 
-Tolerances: loss within 2e-3 relative (fp16 MLP storage points); per-ray
-rgb/opacity within 1e-3; gradients relative L2 <= 1e-3 against fp32 autograd and
+Tolerances: loss within 1e-5 relative (fp16 MLP storage points); per-ray
+rgb/opacity within 1e-5; gradients relative L2 <= 1e-3 against fp32 autograd and
 <= 5e-4 against the oracle's fp16 gradient-storage model (oracle.rg16);
 Adam-updated params within 1e-5 absolute (|update| <= lr = 1e-2 per step,
 dominated by sign(g) for fresh moments)."""
@@ -64,9 +64,11 @@ def test_training_step_matches_oracle():
     print(f"loss {l_gpu:.6e} vs the oracle's {l_ref:.6e}, relative {abs(l_gpu - l_ref) / abs(l_ref):.2e}; "
           f"rgb max |diff| {float((tr.out_rgb.cpu() - ot.last['rgb']).abs().max()):.2e}, opacity "
           f"{float((tr.out_op.cpu() - ot.last['opacity']).abs().max()):.2e}")
-    assert abs(l_gpu - l_ref) <= 2e-3 * abs(l_ref)
-    torch.testing.assert_close(tr.out_rgb.cpu(), ot.last["rgb"], atol=1e-3, rtol=0)
-    torch.testing.assert_close(tr.out_op.cpu(), ot.last["opacity"], atol=1e-3, rtol=0)
+    # (measured, profiles/r06/r6al_pytest_loss.log: loss 1.9e-7 relative, rgb 9.5e-7, opacity 9.8e-7; rounds 1-5
+    # held these to 2e-3 and 1e-3)
+    assert abs(l_gpu - l_ref) <= 1e-5 * abs(l_ref)
+    torch.testing.assert_close(tr.out_rgb.cpu(), ot.last["rgb"], atol=1e-5, rtol=0)
+    torch.testing.assert_close(tr.out_op.cpu(), ot.last["opacity"], atol=1e-5, rtol=0)
     g_gpu, g_ref = tr.grad.cpu(), ot.flat_grad()
     # (measured, profiles/r06/r6af_grad16_trainer.txt: 5.5e-6 / 1.1e-5 / 6.9e-5 against fp32 autograd,
     # 3.0e-6 / 1.1e-5 / 3.7e-5 against the fp16 gradient-storage model; rounds 1-5 held this to 2e-2)
