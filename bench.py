@@ -187,7 +187,7 @@ def psnr_eval(trainer, scene, n_views, res, seed=123):
     return sum(psnrs) / len(psnrs)
 
 
-def inference_bench(trainer, res, frames, world, rank):
+def inference_bench(trainer, res, frames, world, rank, iters_per_graph=24, iters_tail=4):
     """BASELINE config 5: full-frame test-time render (models/rendering.py:162-253)
     of the trained model, graph-captured (renderer.TestRenderer), `frames` poses
     per rank (frames are independent: replicas).  The host-driven loop
@@ -196,7 +196,8 @@ def inference_bench(trainer, res, frames, world, rank):
     sc = S.AnalyticScene(W=res, H=res, n_images=max(2, frames), scale=trainer.scale, seed=321 + rank)
     n = res * res
     rr = RD.TestRenderer(n, trainer.grid, trainer.params16, trainer.density_bitfield, trainer.cascades,
-                         trainer.scale, trainer.G, exp_step_factor=trainer.esf, iters_per_graph=16, iters_tail=8)
+                         trainer.scale, trainer.G, exp_step_factor=trainer.esf, iters_per_graph=iters_per_graph,
+                         iters_tail=iters_tail)
     rr.set_camera(sc.directions.cuda(), trainer.center, trainer.half_size)
     poses = sc.poses.cuda()
     for i in range(2):  # capture + warm
@@ -233,7 +234,8 @@ def inference_bench(trainer, res, frames, world, rank):
             "samples_per_s": round(world * samples / t),
             "host_loop_ms_per_frame": round(t_host * 1e3, 3), "host_loop_bit_exact": same,
             "workload": "full-frame test render of the trained model (black bg), march+field+composite per "
-                        "iteration in HIP graphs (16 iterations, then 8 per replay while rays remain), one host sync per graph"}
+                        f"iteration in HIP graphs ({iters_per_graph} iterations, then {iters_tail} per replay while rays "
+                        "remain), one host sync per graph"}
 
 
 class DropinLoop:
